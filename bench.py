@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Hyperion-MI355X headline benchmark: ResNet-50 bf16 training throughput (samples/s) and step time.
+
+BASELINE.json metric: "samples/sec + step-ms, ResNet-50 bf16 at 1/2/4/8 MI355X; fused-kernel
+speedup".  Config (weak scaling): batch 32 per GPU, 3x224x224 synthetic images, random-init
+ResNet-50, bf16 autocast (fp32 master weights), the reference step benchmark's loss/optimizer
+(``nn.MSELoss`` vs random (32,1000) targets, ``Adam(lr=1e-3)``: ``Phase 1/baseline_performance.ipynb:
+252-358``), data-parallel over RCCL for N>1.  Every timed step does the full forward, backward,
+gradient all-reduce (N>1) and optimizer update.
+
+Reference number: 568.22 samples/s = 56.32 ms/step (ResNet-50, batch 32, fp32, 1x MI250X GCD;
+``Phase 1/results/benchmarks/Baseline/model_benchmarks.csv:2``).
+
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 run under
+``torch.distributed.run --nproc-per-node N``.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+BASELINE_SAMPLES_PER_S = 568.22  # BASELINE.md §2, ResNet-50 batch 32, 1x MI250X GCD
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description="Hyperion ResNet-50 training benchmark")
+    ap.add_argument("--gpus", type=int, default=None, help="number of GPUs (= WORLD_SIZE)")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "resnet18"])
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--kernels", default=None, choices=["hyperion", "torch"],
+                    help="hyperion = fused gfx950 kernels (default); torch = PyTorch eager ops (A/B)")
+    ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (1-GPU; N>1 see --graph-multi)")
+    ap.add_argument("--graph-multi", type=int, default=0, help="also capture when N>1")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--channels-last", type=int, default=1)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    if args.kernels:
+        os.environ["HYPERION_KERNELS"] = args.kernels
+    import torch
+    import torch.distributed as dist
+    import torch.nn as nn
+
+    import hyperion
+    from hyperion.models import resnet18, resnet50
+    from hyperion.ops import FusedAdam, _native
+    from hyperion.parallel import DDP, init_from_env
+    from hyperion.train.step import TrainStep
+    from hyperion.utils import seed_everything
+
+    env = init_from_env()
+    n_gpus = env.world_size
+    if args.gpus is not None and args.gpus != n_gpus and env.rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={n_gpus}; using WORLD_SIZE", file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    seed_everything(1234, env.rank)
+    torch.backends.cudnn.benchmark = True
+
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.precision]
+    model = (resnet50 if args.model == "resnet50" else resnet18)(num_classes=1000).to(dev)
+    mf = torch.channels_last if args.channels_last else torch.contiguous_format
+    model = model.to(memory_format=mf)
+    if n_gpus > 1:
+        model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
+                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None)
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    loss_fn = nn.MSELoss()
+
+    B = args.batch
+    x = torch.rand(B, 3, args.image, args.image, device=dev).to(memory_format=mf)
+    y = torch.rand(B, 1000, device=dev)
+    use_graph = bool(args.graph) and dev.type == "cuda" and (n_gpus == 1 or bool(args.graph_multi))
+    step = TrainStep(model, opt, loss_fn, amp_dtype=amp, graph=use_graph)
+
+    for _ in range(args.warmup):
+        step(x, y)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    if n_gpus > 1:
+        dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(x, y)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    if n_gpus > 1:
+        dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if n_gpus > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.float().item())
+    ms = elapsed / args.steps * 1e3
+    value = n_gpus * B * args.steps / elapsed
+    if env.rank == 0:
+        rec = {
+            "metric": "resnet50_train_samples_per_sec" if args.model == "resnet50" else "resnet18_train_samples_per_sec",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 3) if args.model == "resnet50" else None,
+            "dtype": args.precision,
+            "data": "synthetic (torch.rand images 3x224x224, rand targets; random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": B * n_gpus,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "image": args.image,
+                "parallelism": f"dp{n_gpus}",
+                "loss": "MSE vs rand(B,1000) (reference benchmark_model)",
+                "optimizer": "Adam lr=1e-3 (hyperion FusedAdam, multi-tensor)",
+                "hipgraph": use_graph,
+                "kernels": _native.backend(),
+                "native_so": _native.loaded_path(),
+                "channels_last": bool(args.channels_last),
+            },
+            "baseline": {"value": BASELINE_SAMPLES_PER_S, "ms_per_step": 56.32, "hw": "1x MI250X GCD, fp32"},
+            "final_loss": round(final_loss, 6),
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if n_gpus > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

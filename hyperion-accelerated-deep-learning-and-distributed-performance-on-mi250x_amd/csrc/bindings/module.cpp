@@ -1,0 +1,10 @@
+// hyperion._C module definition.
+#include <torch/extension.h>
+
+#include "bindings/registry.h"
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "Hyperion-MI355X native kernels (gfx950 HIP) and RCCL communicator";
+  m.attr("arch") = "gfx950";
+  hypbind::register_norm_ops(m);
+}

@@ -1,0 +1,134 @@
+// Torch bindings: fused BatchNorm(+res)(+ReLU), multi-tensor optimizer kernels, STREAM kernels.
+#include "bindings/common.h"
+#include "bindings/registry.h"
+
+namespace hypbind {
+namespace {
+
+// x: [N,C,H,W] channels-last or [M,C]; returns (y, save_mean, save_invstd)
+std::vector<at::Tensor> bn_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
+                               const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
+                               const c10::optional<at::Tensor>& running_mean,
+                               const c10::optional<at::Tensor>& running_var, double momentum, double eps, bool training,
+                               bool act) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(is_rows_by_channels(x), "bn_fwd: x must be channels-last 4D or contiguous 2D");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_fwd: C must be a multiple of 8");
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type(),
+                "bn_fwd: residual shape/dtype mismatch");
+    TORCH_CHECK(is_rows_by_channels(*residual), "bn_fwd: residual must be channels-last");
+  }
+  if (!training) TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BN needs running stats");
+  const c10::hip::HIPGuard guard(x.device());
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  int P = 1;
+  HYP_CHECK_HIP(hyp::bn_workspace_rows(M, (int)C, &P));
+  auto ws = at::empty({training ? 2 * P * C + 4 * C : 4 * C}, fopt);
+  float* base = ws.data_ptr<float>();
+  auto stats = at::empty({2, C}, fopt);
+  float* psum = training ? base + 4 * C : nullptr;
+  float* psq = training ? base + 4 * C + (int64_t)P * C : nullptr;
+  HYP_CHECK_HIP(hyp::bn_forward(dtype_code(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, (int)C,
+                                ptr_or_null<float>(weight), ptr_or_null<float>(bias), ptr_or_null<float>(running_mean),
+                                ptr_or_null<float>(running_var), (float)momentum, (float)eps, training ? 1 : 0,
+                                act ? 1 : 0, psum, psq, stats.data_ptr<float>(), stats.data_ptr<float>() + C, base,
+                                base + C, cur_stream()));
+  return {y, stats[0], stats[1]};
+}
+
+// returns (dx, dres or undefined, dweight, dbias)
+std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& y,
+                               const c10::optional<at::Tensor>& weight, const at::Tensor& save_mean,
+                               const at::Tensor& save_invstd, bool training, bool act, bool has_res) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd: dy shape mismatch");
+  at::Tensor dyc = is_rows_by_channels(dy) ? dy : (dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous());
+  if (act) TORCH_CHECK(y.has_value() && is_rows_by_channels(*y), "bn_bwd: act needs the forward output");
+  const c10::hip::HIPGuard guard(x.device());
+  auto dx = at::empty_like(x);
+  at::Tensor dres;
+  if (has_res) dres = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  int P = 1;
+  HYP_CHECK_HIP(hyp::bn_workspace_rows(M, (int)C, &P));
+  auto ws = at::empty({2 * (int64_t)P * C + 3 * C}, fopt);
+  float* base = ws.data_ptr<float>();
+  auto dwb = at::empty({2, C}, fopt);
+  HYP_CHECK_HIP(hyp::bn_backward(dtype_code(x), dyc.data_ptr(), x.data_ptr(), act ? y->data_ptr() : nullptr,
+                                 dx.data_ptr(), has_res ? dres.data_ptr() : nullptr, M, (int)C,
+                                 ptr_or_null<float>(weight), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                                 training ? 1 : 0, act ? 1 : 0, base + 3 * C, base + 3 * C + (int64_t)P * C,
+                                 dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, base, base + C, base + 2 * C,
+                                 cur_stream()));
+  return {dx, dres, dwb[0], dwb[1]};
+}
+
+// ---- multi-tensor optimizer ------------------------------------------------------------------
+void adam_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t T, int64_t chunk,
+             double lr, double b1, double b2, double eps, double wd, bool adamw, const c10::optional<at::Tensor>& lr_t,
+             const at::Tensor& step_t, const c10::optional<at::Tensor>& inv_scale,
+             const c10::optional<at::Tensor>& found_inf, int64_t grad_dtype) {
+  const c10::hip::HIPGuard guard(ptrs.device());
+  HYP_CHECK_HIP(hyp::adam_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
+                                       blocks.data_ptr<int>(), (int)blocks.size(0), (int)T, (int)chunk, (float)lr,
+                                       (float)b1, (float)b2, (float)eps, (float)wd, adamw ? 1 : 0,
+                                       ptr_or_null<float>(lr_t), step_t.data_ptr<float>(),
+                                       ptr_or_null<float>(inv_scale), ptr_or_null<float>(found_inf), cur_stream()));
+}
+
+void unscale_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,
+                const at::Tensor& inv_scale, const at::Tensor& found_inf, int64_t grad_dtype) {
+  const c10::hip::HIPGuard guard(ptrs.device());
+  HYP_CHECK_HIP(hyp::unscale_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
+                                          blocks.data_ptr<int>(), (int)blocks.size(0), (int)chunk,
+                                          inv_scale.data_ptr<float>(), found_inf.data_ptr<float>(), cur_stream()));
+}
+
+at::Tensor sumsq_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,
+                    int64_t grad_dtype) {
+  const c10::hip::HIPGuard guard(ptrs.device());
+  auto fopt = at::TensorOptions().device(ptrs.device()).dtype(at::kFloat);
+  auto part = at::empty({std::max<int64_t>(1, blocks.size(0))}, fopt);
+  auto out = at::empty({1}, fopt);
+  HYP_CHECK_HIP(hyp::sumsq_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
+                                        blocks.data_ptr<int>(), (int)blocks.size(0), (int)chunk, part.data_ptr<float>(),
+                                        out.data_ptr<float>(), cur_stream()));
+  return out;
+}
+
+void clip_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,
+             const at::Tensor& total_sq, double max_norm, int64_t grad_dtype) {
+  const c10::hip::HIPGuard guard(ptrs.device());
+  HYP_CHECK_HIP(hyp::clip_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
+                                       blocks.data_ptr<int>(), (int)blocks.size(0), (int)chunk,
+                                       total_sq.data_ptr<float>(), (float)max_norm, cur_stream()));
+}
+
+// ---- STREAM ----------------------------------------------------------------------------------
+void stream(int64_t op, const at::Tensor& a, const c10::optional<at::Tensor>& b, at::Tensor& c, double s,
+            bool nontemporal, int64_t blocks) {
+  TORCH_CHECK(a.scalar_type() == at::kFloat && c.scalar_type() == at::kFloat, "stream: fp32 only");
+  const c10::hip::HIPGuard guard(a.device());
+  HYP_CHECK_HIP(hyp::stream_op((int)op, a.data_ptr<float>(), ptr_or_null<float>(b), c.data_ptr<float>(), (float)s,
+                               a.numel(), nontemporal ? 1 : 0, (int)blocks, cur_stream()));
+}
+
+}  // namespace
+
+void register_norm_ops(pybind11::module& m) {
+  m.def("bn_fwd", &bn_fwd, "fused NHWC batch-norm (+residual)(+relu) forward");
+  m.def("bn_bwd", &bn_bwd, "fused NHWC batch-norm (+residual)(+relu) backward");
+  m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
+  m.def("unscale_mt", &unscale_mt, "multi-tensor unscale + non-finite check");
+  m.def("sumsq_mt", &sumsq_mt, "multi-tensor sum of squares");
+  m.def("clip_mt", &clip_mt, "multi-tensor clip by global norm (device scalar)");
+  m.def("stream", &stream, "STREAM copy/scale/add/triad");
+}
+
+}  // namespace hypbind

@@ -1,0 +1,7 @@
+// Registration hooks: each binding translation unit contributes its functions to hyperion._C.
+#pragma once
+#include <pybind11/pybind11.h>
+
+namespace hypbind {
+void register_norm_ops(pybind11::module& m);
+}  // namespace hypbind

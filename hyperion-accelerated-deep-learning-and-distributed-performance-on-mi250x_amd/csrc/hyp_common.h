@@ -1,0 +1,164 @@
+// Shared device helpers for the Hyperion gfx950 kernels.
+//
+// * dtype codes shared with the Python side (hyperion/ops/_native.py): 0=f32, 1=bf16, 2=f16
+// * 16-byte vector IO for 8 elements of a 2-byte type (Guideline 13: never scalar bf16 loads)
+// * wave64 reductions (wavefront = 64 lanes on CDNA; __shfl_xor spans all 64)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hyp {
+
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+constexpr int kWave = 64;
+
+typedef uint16_t bf16_t;  // storage type for bf16
+typedef _Float16 f16_t;
+
+__device__ __forceinline__ float bf16_to_float(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Plain cast: hipcc emits v_cvt_pk_bf16_f32 on gfx950 (RNE, NaN-preserving; MI355X_MICROARCH
+// "Correctness boundaries").
+__device__ __forceinline__ bf16_t float_to_bf16(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)float_to_bf16(lo) | ((uint32_t)float_to_bf16(hi) << 16);
+}
+
+__device__ __forceinline__ uint32_t pack_f16x2(float lo, float hi) {
+  f16_t a = (f16_t)lo, b = (f16_t)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+__device__ __forceinline__ float f16_lo(uint32_t w) { return (float)__builtin_bit_cast(f16_t, (uint16_t)(w & 0xffff)); }
+__device__ __forceinline__ float f16_hi(uint32_t w) { return (float)__builtin_bit_cast(f16_t, (uint16_t)(w >> 16)); }
+
+// ---- 8-wide vector IO -------------------------------------------------------------------
+template <typename T>
+struct Vec8;
+
+template <>
+struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* __restrict__ p, float (&v)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* __restrict__ p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <>
+struct Vec8<bf16_t> {
+  static __device__ __forceinline__ void load(const bf16_t* __restrict__ p, float (&v)[8]) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(bf16_t* __restrict__ p, const float (&v)[8]) {
+    uint4 r;
+    r.x = pack_bf16x2(v[0], v[1]);
+    r.y = pack_bf16x2(v[2], v[3]);
+    r.z = pack_bf16x2(v[4], v[5]);
+    r.w = pack_bf16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = r;
+  }
+};
+
+template <>
+struct Vec8<f16_t> {
+  static __device__ __forceinline__ void load(const f16_t* __restrict__ p, float (&v)[8]) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = f16_lo(w[i]);
+      v[2 * i + 1] = f16_hi(w[i]);
+    }
+  }
+  static __device__ __forceinline__ void store(f16_t* __restrict__ p, const float (&v)[8]) {
+    uint4 r;
+    r.x = pack_f16x2(v[0], v[1]);
+    r.y = pack_f16x2(v[2], v[3]);
+    r.z = pack_f16x2(v[4], v[5]);
+    r.w = pack_f16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = r;
+  }
+};
+
+// scalar load/store in float
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p);
+template <>
+__device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld1<bf16_t>(const bf16_t* p) { return bf16_to_float(*p); }
+template <>
+__device__ __forceinline__ float ld1<f16_t>(const f16_t* p) { return (float)*p; }
+
+template <typename T>
+__device__ __forceinline__ void st1(T* p, float v);
+template <>
+__device__ __forceinline__ void st1<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st1<bf16_t>(bf16_t* p, float v) { *p = float_to_bf16(v); }
+template <>
+__device__ __forceinline__ void st1<f16_t>(f16_t* p, float v) { *p = (f16_t)v; }
+
+// ---- wave / block reductions ------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `scratch` needs blockDim.x/64 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, scratch[i]);
+  return t;
+}
+
+// Dispatch a templated launcher over the three floating dtypes.
+#define HYP_DISPATCH_FLOAT(DT, T, ...)                 \
+  switch (DT) {                                        \
+    case ::hyp::kF32: { typedef float T; __VA_ARGS__; break; }   \
+    case ::hyp::kBF16: { typedef ::hyp::bf16_t T; __VA_ARGS__; break; } \
+    case ::hyp::kF16: { typedef ::hyp::f16_t T; __VA_ARGS__; break; }   \
+    default: return hipErrorInvalidValue;             \
+  }
+
+}  // namespace hyp

@@ -1,0 +1,36 @@
+// Host-side launcher declarations for every Hyperion gfx950 kernel.  Implementations live in
+// csrc/kernels/*.hip (pure HIP, no torch headers); csrc/bindings/*.cpp wraps them for Python.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hyp {
+
+// ---- bn_act.hip ----------------------------------------------------------------------------
+hipError_t bn_workspace_rows(int64_t M, int C, int* P_out);
+hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* weight,
+                      const float* bias, float* running_mean, float* running_var, float momentum, float eps,
+                      int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
+                      float* scale, float* shift, hipStream_t stream);
+hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
+                       const float* weight, const float* save_mean, const float* save_invstd, int training, int act,
+                       float* pdz, float* pdzx, float* dweight, float* dbias, float* kA, float* kB, float* kC,
+                       hipStream_t stream);
+
+// ---- adam.hip ------------------------------------------------------------------------------
+hipError_t adam_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
+                             int T, int chunk, float lr, float b1, float b2, float eps, float wd, int adamw,
+                             const float* lr_t, const float* step_t, const float* inv_scale, const float* found_inf,
+                             hipStream_t stream);
+hipError_t unscale_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks,
+                                int nblocks, int chunk, const float* inv_scale, float* found_inf, hipStream_t stream);
+hipError_t sumsq_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
+                              int chunk, float* partials, float* out, hipStream_t stream);
+hipError_t clip_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
+                             int chunk, const float* total_sq, float max_norm, hipStream_t stream);
+
+// ---- stream_bw.hip -------------------------------------------------------------------------
+hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, int64_t n, int nontemporal,
+                     int blocks, hipStream_t stream);
+
+}  // namespace hyp

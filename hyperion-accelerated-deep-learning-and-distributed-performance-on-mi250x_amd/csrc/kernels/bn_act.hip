@@ -1,0 +1,475 @@
+// Fused NHWC BatchNorm (+ residual add) (+ ReLU) for gfx950 — forward and backward.
+//
+// Replaces the reference's MIOpen batch-norm + separate ReLU + separate residual-add kernels in
+// every ResNet block (SURVEY §2.4 row "Convolution + BatchNorm + ReLU", §2.5 ResNet rows).
+//
+// Layout: x is channels-last, i.e. a row-major [M = N*H*W, C] matrix.  Each thread owns 8
+// consecutive channels (one 16-byte vector for bf16/f16, two for f32) and walks rows; a
+// 256-thread block covers `tpr` channel-vectors × `rpi` rows per iteration, so the per-channel
+// constants (scale/shift, or the backward coefficients) sit in registers for the whole loop.
+//
+// Forward (training):  stats_partial (deterministic per-block partial Σx, Σx²)
+//                      -> stats_finalize (fp64 combine, running-stat update, scale/shift)
+//                      -> apply   y = act(x*scale + shift [+ res])
+// Backward:            bwd_reduce (Σdz, Σdz·x with dz = dy·[y>0])
+//                      -> bwd_finalize (dγ, dβ, and dx = A·dz + B·x + C coefficients)
+//                      -> bwd_dx  dx = A·dz + B·x + C ; dres = dz
+#include "hyp_common.h"
+#include "hyp_kernels.h"
+
+namespace hyp {
+namespace {
+
+constexpr int kBlock = 256;
+
+struct BnGeom {
+  int tpr;   // threads per row (each owns 8 channels)
+  int rpi;   // rows per block-iteration
+  int gy;    // channel chunks (grid.y)
+  int P;     // row blocks (grid.x)
+  int64_t rows_per_block;
+};
+
+bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g) {
+  if (C % 8 != 0) return false;
+  const int cv = C / 8;
+  if (cv <= kBlock) {
+    g.tpr = cv;
+    g.gy = 1;
+  } else {
+    if (cv % kBlock != 0) return false;
+    g.tpr = kBlock;
+    g.gy = cv / kBlock;
+  }
+  g.rpi = kBlock / g.tpr;
+  int64_t want = (M + (int64_t)g.rpi * 4 - 1) / ((int64_t)g.rpi * 4);  // >= 4 row iterations/thread
+  int64_t cap = max_blocks / g.gy;
+  if (cap < 1) cap = 1;
+  int64_t P = want < cap ? want : cap;
+  if (P < 1) P = 1;
+  g.rows_per_block = (M + P - 1) / P;
+  g.P = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
+  if (g.P < 1) g.P = 1;
+  return true;
+}
+
+// ---------------------------------------------------------------- forward stats
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_stats_partial_k(const T* __restrict__ x, int64_t M, int C, int tpr,
+                                                             int rpi, int64_t rpb, float* __restrict__ psum,
+                                                             float* __restrict__ psq) {
+  __shared__ float ls[kBlock * 8];
+  __shared__ float lq[kBlock * 8];
+  const int tid = threadIdx.x;
+  const int r = tid / tpr, c8 = tid - r * tpr;
+  const int cbase = blockIdx.y * tpr * 8;
+  const int64_t row0 = (int64_t)blockIdx.x * rpb;
+  const int64_t row1 = min(M, row0 + rpb);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  if (r < rpi) {
+    const int64_t step = (int64_t)rpi * C;
+    const T* p = x + (row0 + r) * C + cbase + c8 * 8;
+    int64_t row = row0 + r;
+    for (; row + 3 * rpi < row1; row += 4 * rpi, p += 4 * step) {
+      float v0[8], v1[8], v2[8], v3[8];
+      Vec8<T>::load(p, v0);
+      Vec8<T>::load(p + step, v1);
+      Vec8<T>::load(p + 2 * step, v2);
+      Vec8<T>::load(p + 3 * step, v3);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += (v0[j] + v1[j]) + (v2[j] + v3[j]);
+        q[j] += (v0[j] * v0[j] + v1[j] * v1[j]) + (v2[j] * v2[j] + v3[j] * v3[j]);
+      }
+    }
+    for (; row < row1; row += rpi, p += step) {
+      float v[8];
+      Vec8<T>::load(p, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[j];
+        q[j] += v[j] * v[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ls[tid * 8 + j] = s[j];
+    lq[tid * 8 + j] = q[j];
+  }
+  __syncthreads();
+  const int nch = tpr * 8;
+  for (int ch = tid; ch < nch; ch += kBlock) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      a += ls[rr * nch + ch];
+      b += lq[rr * nch + ch];
+    }
+    psum[(int64_t)blockIdx.x * C + cbase + ch] = a;
+    psq[(int64_t)blockIdx.x * C + cbase + ch] = b;
+  }
+}
+
+// grid: ceil(C/64); block (64, 16)
+__global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restrict__ psum, const float* __restrict__ psq,
+                                                            int P, int C, int64_t M, const float* __restrict__ weight,
+                                                            const float* __restrict__ bias, float* running_mean,
+                                                            float* running_var, float momentum, float eps,
+                                                            float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                                            float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ double red_s[16][64];
+  __shared__ double red_q[16][64];
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int p = threadIdx.y; p < P; p += 16) {
+      a += (double)psum[(int64_t)p * C + c];
+      b += (double)psq[(int64_t)p * C + c];
+    }
+  }
+  red_s[threadIdx.y][threadIdx.x] = a;
+  red_q[threadIdx.y][threadIdx.x] = b;
+  __syncthreads();
+  if (threadIdx.y == 0 && c < C) {
+    for (int i = 1; i < 16; ++i) {
+      a += red_s[i][threadIdx.x];
+      b += red_q[i][threadIdx.x];
+    }
+    const double mean = a / (double)M;
+    double var = b / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[c] = (float)mean;
+    save_invstd[c] = invstd;
+    if (running_mean != nullptr) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+    }
+    const float w = weight ? weight[c] : 1.f;
+    const float bb = bias ? bias[c] : 0.f;
+    const float sc = w * invstd;
+    scale[c] = sc;
+    shift[c] = bb - (float)mean * sc;
+  }
+}
+
+// eval-mode constants from running stats
+__global__ void bn_eval_consts_k(int C, const float* __restrict__ weight, const float* __restrict__ bias,
+                                 const float* __restrict__ rm, const float* __restrict__ rv, float eps,
+                                 float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                 float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rv[c] + eps);
+  const float w = weight ? weight[c] : 1.f;
+  const float b = bias ? bias[c] : 0.f;
+  save_mean[c] = rm[c];
+  save_invstd[c] = invstd;
+  scale[c] = w * invstd;
+  shift[c] = b - rm[c] * w * invstd;
+}
+
+// ---------------------------------------------------------------- forward apply
+template <typename T, bool ACT, bool RES>
+__global__ __launch_bounds__(kBlock) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
+                                                     T* __restrict__ y, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, int64_t M, int C, int tpr,
+                                                     int rpi, int64_t rpb) {
+  const int tid = threadIdx.x;
+  const int r = tid / tpr, c8 = tid - r * tpr;
+  if (r >= rpi) return;
+  const int c0 = blockIdx.y * tpr * 8 + c8 * 8;
+  float sc[8], sh[8];
+  {
+    const float4 a = reinterpret_cast<const float4*>(scale + c0)[0];
+    const float4 b = reinterpret_cast<const float4*>(scale + c0)[1];
+    const float4 d = reinterpret_cast<const float4*>(shift + c0)[0];
+    const float4 e = reinterpret_cast<const float4*>(shift + c0)[1];
+    sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+    sh[0] = d.x; sh[1] = d.y; sh[2] = d.z; sh[3] = d.w; sh[4] = e.x; sh[5] = e.y; sh[6] = e.z; sh[7] = e.w;
+  }
+  const int64_t row0 = (int64_t)blockIdx.x * rpb;
+  const int64_t row1 = min(M, row0 + rpb);
+  const int64_t step = (int64_t)rpi * C;
+  int64_t off = (row0 + r) * C + c0;
+  int64_t row = row0 + r;
+  for (; row + rpi < row1; row += 2 * rpi, off += 2 * step) {
+    float v0[8], v1[8], r0[8], r1[8];
+    Vec8<T>::load(x + off, v0);
+    Vec8<T>::load(x + off + step, v1);
+    if (RES) {
+      Vec8<T>::load(res + off, r0);
+      Vec8<T>::load(res + off + step, r1);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = fmaf(v0[j], sc[j], sh[j]);
+      float b = fmaf(v1[j], sc[j], sh[j]);
+      if (RES) {
+        a += r0[j];
+        b += r1[j];
+      }
+      if (ACT) {
+        a = fmaxf(a, 0.f);
+        b = fmaxf(b, 0.f);
+      }
+      v0[j] = a;
+      v1[j] = b;
+    }
+    Vec8<T>::store(y + off, v0);
+    Vec8<T>::store(y + off + step, v1);
+  }
+  if (row < row1) {
+    float v[8], rr[8];
+    Vec8<T>::load(x + off, v);
+    if (RES) Vec8<T>::load(res + off, rr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = fmaf(v[j], sc[j], sh[j]);
+      if (RES) a += rr[j];
+      if (ACT) a = fmaxf(a, 0.f);
+      v[j] = a;
+    }
+    Vec8<T>::store(y + off, v);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+template <typename T, bool ACT>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ y, int64_t M, int C, int tpr, int rpi,
+                                                          int64_t rpb, float* __restrict__ pdz,
+                                                          float* __restrict__ pdzx) {
+  __shared__ float ls[kBlock * 8];
+  __shared__ float lq[kBlock * 8];
+  const int tid = threadIdx.x;
+  const int r = tid / tpr, c8 = tid - r * tpr;
+  const int cbase = blockIdx.y * tpr * 8;
+  const int64_t row0 = (int64_t)blockIdx.x * rpb;
+  const int64_t row1 = min(M, row0 + rpb);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  if (r < rpi) {
+    const int64_t step = (int64_t)rpi * C;
+    int64_t off = (row0 + r) * C + cbase + c8 * 8;
+    int64_t row = row0 + r;
+    for (; row + rpi < row1; row += 2 * rpi, off += 2 * step) {
+      float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
+      Vec8<T>::load(dy + off, g0);
+      Vec8<T>::load(dy + off + step, g1);
+      Vec8<T>::load(x + off, x0);
+      Vec8<T>::load(x + off + step, x1);
+      if (ACT) {
+        Vec8<T>::load(y + off, y0);
+        Vec8<T>::load(y + off + step, y1);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d0 = (!ACT || y0[j] > 0.f) ? g0[j] : 0.f;
+        const float d1 = (!ACT || y1[j] > 0.f) ? g1[j] : 0.f;
+        s[j] += d0 + d1;
+        q[j] += d0 * x0[j] + d1 * x1[j];
+      }
+    }
+    if (row < row1) {
+      float g[8], xv[8], yv[8];
+      Vec8<T>::load(dy + off, g);
+      Vec8<T>::load(x + off, xv);
+      if (ACT) Vec8<T>::load(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (!ACT || yv[j] > 0.f) ? g[j] : 0.f;
+        s[j] += d;
+        q[j] += d * xv[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ls[tid * 8 + j] = s[j];
+    lq[tid * 8 + j] = q[j];
+  }
+  __syncthreads();
+  const int nch = tpr * 8;
+  for (int ch = tid; ch < nch; ch += kBlock) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      a += ls[rr * nch + ch];
+      b += lq[rr * nch + ch];
+    }
+    pdz[(int64_t)blockIdx.x * C + cbase + ch] = a;
+    pdzx[(int64_t)blockIdx.x * C + cbase + ch] = b;
+  }
+}
+
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ pdz, const float* __restrict__ pdzx,
+                                                          int P, int C, int64_t M, const float* __restrict__ weight,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, int training,
+                                                          float* __restrict__ dweight, float* __restrict__ dbias,
+                                                          float* __restrict__ kA, float* __restrict__ kB,
+                                                          float* __restrict__ kC) {
+  __shared__ double red_s[16][64];
+  __shared__ double red_q[16][64];
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int p = threadIdx.y; p < P; p += 16) {
+      a += (double)pdz[(int64_t)p * C + c];
+      b += (double)pdzx[(int64_t)p * C + c];
+    }
+  }
+  red_s[threadIdx.y][threadIdx.x] = a;
+  red_q[threadIdx.y][threadIdx.x] = b;
+  __syncthreads();
+  if (threadIdx.y == 0 && c < C) {
+    for (int i = 1; i < 16; ++i) {
+      a += red_s[i][threadIdx.x];
+      b += red_q[i][threadIdx.x];
+    }
+    const double mu = mean[c], is = invstd[c];
+    const double sum_dz_xhat = is * (b - mu * a);
+    if (dweight) dweight[c] = (float)sum_dz_xhat;
+    if (dbias) dbias[c] = (float)a;
+    const double g = weight ? weight[c] : 1.0;
+    const double A = g * is;
+    if (training) {
+      const double Bc = -A * is * sum_dz_xhat / (double)M;
+      const double Cc = -A * a / (double)M - Bc * mu;
+      kA[c] = (float)A;
+      kB[c] = (float)Bc;
+      kC[c] = (float)Cc;
+    } else {
+      kA[c] = (float)A;
+      kB[c] = 0.f;
+      kC[c] = 0.f;
+    }
+  }
+}
+
+template <typename T, bool ACT, bool RES>
+__global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                      const T* __restrict__ y, T* __restrict__ dx,
+                                                      T* __restrict__ dres, const float* __restrict__ kA,
+                                                      const float* __restrict__ kB, const float* __restrict__ kC,
+                                                      int64_t M, int C, int tpr, int rpi, int64_t rpb) {
+  const int tid = threadIdx.x;
+  const int r = tid / tpr, c8 = tid - r * tpr;
+  if (r >= rpi) return;
+  const int c0 = blockIdx.y * tpr * 8 + c8 * 8;
+  float A[8], B[8], Cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A[j] = kA[c0 + j];
+    B[j] = kB[c0 + j];
+    Cc[j] = kC[c0 + j];
+  }
+  const int64_t row0 = (int64_t)blockIdx.x * rpb;
+  const int64_t row1 = min(M, row0 + rpb);
+  const int64_t step = (int64_t)rpi * C;
+  int64_t off = (row0 + r) * C + c0;
+  for (int64_t row = row0 + r; row < row1; row += rpi, off += step) {
+    float g[8], xv[8], yv[8];
+    Vec8<T>::load(dy + off, g);
+    Vec8<T>::load(x + off, xv);
+    if (ACT) Vec8<T>::load(y + off, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = (!ACT || yv[j] > 0.f) ? g[j] : 0.f;
+      g[j] = d;
+      xv[j] = fmaf(A[j], d, fmaf(B[j], xv[j], Cc[j]));
+    }
+    Vec8<T>::store(dx + off, xv);
+    if (RES) Vec8<T>::store(dres + off, g);
+  }
+}
+
+}  // namespace
+
+// ======================================================================== host launchers
+hipError_t bn_workspace_rows(int64_t M, int C, int* P_out) {
+  BnGeom g;
+  if (!bn_geom(M, C, 1024, g)) return hipErrorInvalidValue;
+  *P_out = g.P;
+  return hipSuccess;
+}
+
+hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* weight,
+                      const float* bias, float* running_mean, float* running_var, float momentum, float eps,
+                      int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
+                      float* scale, float* shift, hipStream_t stream) {
+  BnGeom gs, ga;
+  if (!bn_geom(M, C, 1024, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    const T* xt = static_cast<const T*>(x);
+    if (training) {
+      hipLaunchKernelGGL(bn_stats_partial_k<T>, dim3(gs.P, gs.gy), dim3(kBlock), 0, stream, xt, M, C, gs.tpr, gs.rpi,
+                         gs.rows_per_block, psum, psq);
+      hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + 63) / 64), dim3(64, 16), 0, stream, psum, psq, gs.P, C, M,
+                         weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+    } else {
+      hipLaunchKernelGGL(bn_eval_consts_k, dim3((C + 255) / 256), dim3(256), 0, stream, C, weight, bias, running_mean,
+                         running_var, eps, save_mean, save_invstd, scale, shift);
+    }
+    const dim3 grid(ga.P, ga.gy);
+    const T* rt = static_cast<const T*>(res);
+    T* yt = static_cast<T*>(y);
+    if (act && res)
+      hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+    else if (act)
+      hipLaunchKernelGGL((bn_apply_k<T, true, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+    else if (res)
+      hipLaunchKernelGGL((bn_apply_k<T, false, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+    else
+      hipLaunchKernelGGL((bn_apply_k<T, false, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+  });
+  return hipGetLastError();
+}
+
+hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
+                       const float* weight, const float* save_mean, const float* save_invstd, int training, int act,
+                       float* pdz, float* pdzx, float* dweight, float* dbias, float* kA, float* kB, float* kC,
+                       hipStream_t stream) {
+  BnGeom gs, ga;
+  if (!bn_geom(M, C, 1024, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    const T* dyt = static_cast<const T*>(dy);
+    const T* xt = static_cast<const T*>(x);
+    const T* yt = static_cast<const T*>(y);
+    const dim3 grs(gs.P, gs.gy);
+    if (act)
+      hipLaunchKernelGGL((bn_bwd_reduce_k<T, true>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr, gs.rpi,
+                         gs.rows_per_block, pdz, pdzx);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_k<T, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr, gs.rpi,
+                         gs.rows_per_block, pdz, pdzx);
+    hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(64, 16), 0, stream, pdz, pdzx, gs.P, C, M, weight,
+                       save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
+    const dim3 gra(ga.P, ga.gy);
+    T* dxt = static_cast<T*>(dx);
+    T* drt = static_cast<T*>(dres);
+    if (act && dres)
+      hipLaunchKernelGGL((bn_bwd_dx_k<T, true, true>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB, kC,
+                         M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+    else if (act)
+      hipLaunchKernelGGL((bn_bwd_dx_k<T, true, false>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB,
+                         kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+    else if (dres)
+      hipLaunchKernelGGL((bn_bwd_dx_k<T, false, true>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB,
+                         kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+    else
+      hipLaunchKernelGGL((bn_bwd_dx_k<T, false, false>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB,
+                         kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+  });
+  return hipGetLastError();
+}
+
+}  // namespace hyp

@@ -1,0 +1,153 @@
+"""Fused BatchNorm (+ residual add) (+ ReLU) — the conv epilogue of every ResNet block.
+
+Reference: torchvision ResNet blocks run ``conv -> bn -> relu`` and ``bn3 -> += identity ->
+relu`` as three or four separate kernels (MIOpen BN, elementwise add, ReLU) per block
+(``baseline_performance.ipynb:203-205``; SURVEY §2.4 "Convolution + BatchNorm + ReLU").
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` subclass (same parameters, buffers and
+state-dict keys) whose forward takes an optional ``residual`` and applies ReLU when
+``act=True``.  On GPU with channels-last activations it runs the gfx950 kernels in
+``csrc/kernels/bn_act.hip``: one stats pass + one apply pass forward (residual + ReLU folded into
+the apply), one reduce pass + one dx pass backward (ReLU mask from the saved output, residual
+gradient written by the same pass).  Elsewhere it runs the PyTorch reference composition, which
+is also the test oracle.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+
+def bn_act_reference(
+    x: torch.Tensor,
+    residual: Optional[torch.Tensor],
+    weight: Optional[torch.Tensor],
+    bias: Optional[torch.Tensor],
+    running_mean: Optional[torch.Tensor],
+    running_var: Optional[torch.Tensor],
+    training: bool,
+    momentum: float,
+    eps: float,
+    act: bool,
+) -> torch.Tensor:
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    if act:
+        y = F.relu(y)
+    return y
+
+
+def _native_ok(x: torch.Tensor) -> bool:
+    if not x.is_cuda or x.dtype not in _native.DTYPE_CODE:
+        return False
+    if x.dim() == 4:
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            return False
+    elif x.dim() != 2 or not x.is_contiguous():
+        return False
+    C = x.shape[1]
+    if C % 8:
+        return False
+    cv = C // 8
+    return cv <= 256 or cv % 256 == 0
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act):
+        C = _native.native()
+        if residual is not None and residual.dtype != x.dtype:
+            residual = residual.to(x.dtype)
+        if residual is not None and x.dim() == 4 and not residual.is_contiguous(memory_format=torch.channels_last):
+            residual = residual.contiguous(memory_format=torch.channels_last)
+        y, mean, invstd = C.bn_fwd(x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act)
+        ctx.act = act
+        ctx.training = training
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if act else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        need_res = ctx.has_res and ctx.needs_input_grad[1]
+        dx, dres, dw, db = _native.native().bn_bwd(
+            dy, x, y, weight, mean, invstd, ctx.training, ctx.act, need_res
+        )
+        return (
+            dx if ctx.needs_input_grad[0] else None,
+            dres if need_res else None,
+            dw if (weight is not None and ctx.needs_input_grad[2]) else None,
+            db if ctx.needs_input_grad[3] else None,
+            None, None, None, None, None, None,
+        )
+
+
+def bn_act(
+    x: torch.Tensor,
+    residual: Optional[torch.Tensor],
+    weight: Optional[torch.Tensor],
+    bias: Optional[torch.Tensor],
+    running_mean: Optional[torch.Tensor],
+    running_var: Optional[torch.Tensor],
+    training: bool,
+    momentum: float,
+    eps: float,
+    act: bool,
+) -> torch.Tensor:
+    """Functional fused BN(+res)(+ReLU); dispatches to HIP when possible."""
+    if (
+        _native.use_native(x)
+        and _native_ok(x)
+        and (weight is None or weight.dtype == torch.float32)
+        and (running_mean is None or running_mean.dtype == torch.float32)
+    ):
+        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act)
+    return bn_act_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, act)
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` + optional residual add + optional ReLU, fused on gfx950."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: Optional[float] = 0.1, act: bool = False,
+                 **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        self.act = act
+        self._host_batches = 0  # mirrors num_batches_tracked without a per-step device launch
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", act={self.act}"
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        if self.track_running_stats and self.num_batches_tracked is not None and self._host_batches:
+            with torch.no_grad():
+                self.num_batches_tracked.add_(self._host_batches)
+            self._host_batches = 0
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:  # type: ignore[override]
+        use_batch_stats = self.training or not self.track_running_stats
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats:
+            if self.momentum is None:  # cumulative moving average needs the true count every step
+                self.num_batches_tracked.add_(1)
+                momentum = 1.0 / float(self.num_batches_tracked.item())
+            else:
+                self._host_batches += 1
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        return bn_act(x, residual, self.weight, self.bias, rm, rv, use_batch_stats, momentum, self.eps, self.act)
+
+
+class BatchNormAct1d(BatchNormAct2d):
+    """[N, C] variant (same kernels; rows = batch)."""
+
+    def _check_input_dim(self, input):
+        if input.dim() != 2:
+            raise ValueError(f"expected 2D input (got {input.dim()}D input)")

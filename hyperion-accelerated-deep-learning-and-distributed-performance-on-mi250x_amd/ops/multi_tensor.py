@@ -1,0 +1,71 @@
+"""Multi-tensor launch tables for the gfx950 multi-tensor kernels (``csrc/kernels/adam.hip``).
+
+A table is built once per set of tensor pointers and reused while the pointers stay the same
+(always, inside a captured hipGraph).  Each row of the block table is (tensor id, chunk id); one
+256-thread block processes ``chunk`` elements.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+CHUNK = 8192  # elements per block (multiple of 4 for the float4 body)
+
+
+class MultiTensorTable:
+    def __init__(self, groups: Sequence[Sequence[torch.Tensor]], chunk: int = CHUNK):
+        """``groups``: K lists of T tensors each (e.g. [params, grads, exp_avg, exp_avg_sq])."""
+        assert groups and all(len(g) == len(groups[0]) for g in groups)
+        self.T = len(groups[0])
+        self.chunk = chunk
+        dev = groups[0][0].device
+        self.key = self.key_of(groups)
+        ptrs = [t.data_ptr() for g in groups for t in g]
+        for p in ptrs:
+            if p % 16:
+                raise ValueError("multi-tensor kernels need 16-byte aligned tensors")
+        sizes = [t.numel() for t in groups[0]]
+        blocks: List[int] = []
+        for i, n in enumerate(sizes):
+            for c in range((n + chunk - 1) // chunk):
+                blocks += [i, c]
+        self.nblocks = len(blocks) // 2
+        if not blocks:
+            blocks = [0, 0]
+        host = [
+            torch.tensor(ptrs, dtype=torch.int64),
+            torch.tensor(sizes, dtype=torch.int64),
+            torch.tensor(blocks, dtype=torch.int32).view(-1, 2),
+        ]
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            # inside hipGraph capture: copy from pinned host memory (a memcpy node that replays the
+            # same bytes); keep the pinned tensors alive as long as the table
+            self._pinned = [h.pin_memory() for h in host]
+            dev_t = [torch.empty_like(h, device=dev) for h in host]
+            for d, h in zip(dev_t, self._pinned):
+                d.copy_(h, non_blocking=True)
+        else:
+            dev_t = [h.to(dev) for h in host]
+        self.ptrs, self.sizes, self.blocks = dev_t
+        if self.nblocks == 0:
+            self.blocks = self.blocks[:0]
+
+    @staticmethod
+    def key_of(groups: Sequence[Sequence[torch.Tensor]]) -> Tuple[int, ...]:
+        return tuple(t.data_ptr() for g in groups for t in g)
+
+
+class TableCache:
+    """Keeps the most recent table per role; rebuilds when pointers change."""
+
+    def __init__(self):
+        self._tables: Dict[str, MultiTensorTable] = {}
+
+    def get(self, role: str, groups: Sequence[Sequence[torch.Tensor]]) -> MultiTensorTable:
+        key = MultiTensorTable.key_of(groups)
+        t = self._tables.get(role)
+        if t is None or t.key != key:
+            t = MultiTensorTable(groups)
+            self._tables[role] = t
+        return t

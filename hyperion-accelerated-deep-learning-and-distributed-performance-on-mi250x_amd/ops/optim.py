@@ -1,0 +1,186 @@
+"""Fused multi-tensor Adam / AdamW on gfx950 (one launch for every parameter).
+
+Reference optimizers: ``optim.Adam(lr=1e-3)`` in the baseline step benchmark
+(``baseline_performance.ipynb:282``) and ``AdamW`` in every trainer (``distributed_utils.py:161,
+232,334,503``).  torch's implementation launches a chain of ``_foreach_*`` kernels per parameter
+group chunk; ``FusedAdam`` runs ``adam_mt_k`` once, reading step / loss-scale / found-inf from
+device memory so the step can be captured in a hipGraph and skipped on overflow without a host
+sync (GradScaler semantics).
+
+Also provides multi-tensor global-norm clipping that takes the norm over *all* gradient shards
+(all-reduced when a process group is given) — the reference clipped only the local FSDP shard
+(``distributed_utils.py:351,522``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _native
+from .multi_tensor import TableCache
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(
+        self,
+        params: Iterable,
+        lr: float = 1e-3,
+        betas=(0.9, 0.999),
+        eps: float = 1e-8,
+        weight_decay: float = 0.0,
+        adamw: bool = False,
+    ):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=adamw)
+        super().__init__(params, defaults)
+        self._tables = TableCache()
+        self._step_t: Optional[torch.Tensor] = None
+        self._host_step = 0
+        # optional device scalars set by the AMP scaler
+        self.inv_scale: Optional[torch.Tensor] = None
+        self.found_inf: Optional[torch.Tensor] = None
+
+    def _group_tensors(self, group):
+        ps, gs, ms, vs = [], [], [], []
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            st = self.state[p]
+            if not st:
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            ps.append(p)
+            gs.append(p.grad)
+            ms.append(st["exp_avg"])
+            vs.append(st["exp_avg_sq"])
+        return ps, gs, ms, vs
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._host_step += 1
+        first = None
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    first = p
+                    break
+            if first is not None:
+                break
+        if first is None:
+            return loss
+        native = _native.use_native(first) and first.dtype == torch.float32
+        if native:
+            if self._step_t is None or self._step_t.device != first.device:
+                self._step_t = torch.zeros((), dtype=torch.float32, device=first.device)
+            self._step_t.add_(1.0)
+        for gi, group in enumerate(self.param_groups):
+            ps, gs, ms, vs = self._group_tensors(group)
+            if not ps:
+                continue
+            b1, b2 = group["betas"]
+            if native and all(g.dtype == gs[0].dtype for g in gs) and all(
+                p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous() for p, g in zip(ps, gs)
+            ):
+                tab = self._tables.get(f"adam{gi}", [ps, gs, ms, vs])
+                lr = group["lr"]
+                lr_t = lr if isinstance(lr, torch.Tensor) else None
+                _native.native().adam_mt(
+                    tab.ptrs, tab.sizes, tab.blocks, tab.T, tab.chunk,
+                    float(lr) if lr_t is None else 0.0, b1, b2, group["eps"], group["weight_decay"],
+                    bool(group["adamw"]), lr_t, self._step_t, self.inv_scale, self.found_inf,
+                    _native.DTYPE_CODE[gs[0].dtype],
+                )
+            else:
+                self._reference_step(group, ps, gs, ms, vs)
+        return loss
+
+    def _reference_step(self, group, ps, gs, ms, vs):
+        """PyTorch reference (CPU / fallback); identical math to the kernel."""
+        if self.found_inf is not None and float(self.found_inf) != 0.0:
+            return
+        b1, b2 = group["betas"]
+        lr = float(group["lr"])
+        wd = group["weight_decay"]
+        step = self._host_step
+        bc1 = 1 - b1**step
+        bc2_sqrt = math.sqrt(1 - b2**step)
+        inv = float(self.inv_scale) if self.inv_scale is not None else 1.0
+        for p, g, m, v in zip(ps, gs, ms, vs):
+            g = g.float() * inv
+            if group["adamw"]:
+                p.mul_(1 - lr * wd)
+            elif wd != 0:
+                g = g.add(p, alpha=wd)
+            m.mul_(b1).add_(g, alpha=1 - b1)
+            v.mul_(b2).addcmul_(g, g, value=1 - b2)
+            denom = (v.sqrt() / bc2_sqrt).add_(group["eps"])
+            p.addcdiv_(m, denom, value=-lr / bc1)
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["hyperion_step"] = self._host_step
+        return sd
+
+    def load_state_dict(self, state_dict):
+        state_dict = dict(state_dict)
+        self._host_step = int(state_dict.pop("hyperion_step", 0))
+        super().load_state_dict(state_dict)
+        self._step_t = None
+        if self._host_step:
+            for group in self.param_groups:
+                for p in group["params"]:
+                    if p.is_cuda:
+                        self._step_t = torch.full((), float(self._host_step), device=p.device)
+                        break
+                if self._step_t is not None:
+                    break
+
+
+def FusedAdamW(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+    return FusedAdam(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=True)
+
+
+_clip_tables = TableCache()
+
+
+@torch.no_grad()
+def clip_grad_norm_(
+    parameters: Iterable[torch.Tensor],
+    max_norm: float,
+    group: Optional["dist.ProcessGroup"] = None,
+    sharded: bool = False,
+) -> torch.Tensor:
+    """Clip by the global L2 norm.
+
+    ``sharded=True``: each rank holds a disjoint shard of the gradients (FSDP); the squared norm
+    is all-reduced over ``group`` before clipping — the reference's ``clip_grad_norm_`` on FSDP
+    modules skipped this and clipped by the local shard norm.
+    """
+    grads: List[torch.Tensor] = [p.grad for p in parameters if p.grad is not None]
+    if not grads:
+        return torch.zeros(())
+    dev = grads[0].device
+    native = _native.use_native(grads[0]) and all(g.is_contiguous() and g.dtype == grads[0].dtype for g in grads)
+    if native:
+        tab = _clip_tables.get("clip", [grads])
+        code = _native.DTYPE_CODE[grads[0].dtype]
+        total_sq = _native.native().sumsq_mt(tab.ptrs, tab.sizes, tab.blocks, tab.chunk, code)
+    else:
+        total_sq = torch.zeros(1, device=dev, dtype=torch.float32)
+        for g in grads:
+            total_sq += g.float().pow(2).sum()
+    if sharded and dist.is_available() and dist.is_initialized():
+        dist.all_reduce(total_sq, group=group)
+    if native:
+        _native.native().clip_mt(tab.ptrs, tab.sizes, tab.blocks, tab.chunk, total_sq, float(max_norm), code)
+    else:
+        coef = (max_norm / (total_sq.sqrt() + 1e-6)).clamp(max=1.0)
+        for g in grads:
+            g.mul_(coef.to(g.dtype))
+    return total_sq.sqrt().reshape(())

@@ -1,0 +1,216 @@
+"""Data-parallel training with bucketed gradient all-reduce overlapped with backward.
+
+Reference: ``torch.nn.parallel.DistributedDataParallel`` wrapped around every trainer model
+(``distributed_utils.py:159,229,475``; SURVEY §2.2 "DP: DDP", K2-K6).
+
+MI355X design:
+* gradients are packed (and pre-scaled by 1/world) into persistent flat buckets the moment each
+  parameter's gradient is final (``post_accumulate_grad`` hook), and a bucket's all-reduce is
+  issued as soon as it is complete — in bucket order on every rank — so RCCL traffic over xGMI
+  overlaps the rest of the backward pass;
+* bucket sizes default to 64 MiB (first bucket 4 MiB): with 288 GB HBM per GPU memory is no
+  constraint, and on a fully-connected 8-GPU xGMI mesh RCCL's ring/direct algorithms reach
+  their bus bandwidth only at tens of MiB per call, while a small first bucket
+  lets the first all-reduce start early in backward;
+* after backward, ``param.grad`` is re-pointed at its bucket slice, so the fused optimizer reads
+  the reduced gradient in place (no copy back) and its pointer table stays valid across steps;
+* ``comm_dtype=torch.bfloat16`` halves the bytes on the wire (the reduction runs in RCCL);
+* ``broadcast_buffers`` reproduces the reference's per-forward BN buffer broadcast (K5).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..utils.nvtx import range_push, range_pop
+
+
+def _flat_broadcast(tensors: List[torch.Tensor], src: int, group) -> None:
+    """Broadcast a list of tensors as one flat message per dtype."""
+    by_dtype: Dict[torch.dtype, List[torch.Tensor]] = {}
+    for t in tensors:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off : off + n].view_as(t))
+                off += n
+
+
+class _Bucket:
+    __slots__ = ("index", "params", "offsets", "buf", "ready", "got", "work", "launched")
+
+    def __init__(self, index: int, params: List[nn.Parameter], dtype: torch.dtype, device: torch.device):
+        self.index = index
+        self.params = params
+        self.offsets: List[int] = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += p.numel()
+        self.buf = torch.zeros(off, dtype=dtype, device=device)
+        self.ready = 0
+        self.got = [False] * len(params)
+        self.work = None
+        self.launched = False
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(
+        self,
+        module: nn.Module,
+        process_group=None,
+        bucket_cap_mb: float = 64.0,
+        first_bucket_mb: float = 4.0,
+        broadcast_buffers: bool = True,
+        comm_dtype: Optional[torch.dtype] = None,
+        device_ids=None,  # accepted for API compatibility with torch DDP
+        find_unused_parameters: bool = False,
+    ):
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self._sync = True
+        self._buckets: List[_Bucket] = []
+        self._where: Dict[nn.Parameter, Tuple[_Bucket, int]] = {}
+        self._next_launch = 0
+        self._callback_queued = False
+        self._hooks = []
+        if self.world > 1:
+            _flat_broadcast([p.data for p in module.parameters()] + list(module.buffers()), 0, process_group)
+            self._build_buckets(bucket_cap_mb, first_bucket_mb, comm_dtype)
+            for p in module.parameters():
+                if p.requires_grad:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._grad_ready))
+
+    # ------------------------------------------------------------------ buckets
+    def _build_buckets(self, cap_mb: float, first_mb: float, comm_dtype: Optional[torch.dtype]) -> None:
+        params = [p for p in self.module.parameters() if p.requires_grad]
+        params.reverse()  # gradients become ready roughly in reverse registration order
+        groups: List[Tuple[torch.dtype, torch.device, List[nn.Parameter]]] = []
+        cur: List[nn.Parameter] = []
+        cur_bytes = 0
+        cur_key = None
+        limit = first_mb * 2**20
+        for p in params:
+            dt = comm_dtype or p.dtype
+            key = (dt, p.device)
+            nbytes = p.numel() * torch.empty((), dtype=dt).element_size()
+            if cur and (key != cur_key or cur_bytes + nbytes > limit):
+                groups.append((cur_key[0], cur_key[1], cur))
+                cur, cur_bytes = [], 0
+                limit = cap_mb * 2**20
+            cur.append(p)
+            cur_bytes += nbytes
+            cur_key = key
+        if cur:
+            groups.append((cur_key[0], cur_key[1], cur))
+        for i, (dt, dev, ps) in enumerate(groups):
+            b = _Bucket(i, ps, dt, dev)
+            self._buckets.append(b)
+            for i, p in enumerate(ps):
+                self._where[p] = (b, i)
+
+    def bucket_sizes(self) -> List[int]:
+        return [b.buf.numel() for b in self._buckets]
+
+    # ------------------------------------------------------------------ hooks
+    def _grad_ready(self, p: nn.Parameter) -> None:
+        if not self._sync or p.grad is None:
+            return
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        b, i = self._where[p]
+        if b.got[i]:
+            return
+        off, n = b.offsets[i], p.numel()
+        slot = b.buf[off : off + n]
+        with torch.no_grad():
+            g = p.grad.reshape(-1)
+            if g.dtype == slot.dtype:
+                torch.mul(g, 1.0 / self.world, out=slot)  # pack + pre-scale in one pass
+            else:
+                slot.copy_(g * (1.0 / self.world))
+        b.got[i] = True
+        b.ready += 1
+        if b.ready == len(b.params):
+            self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next_launch < len(self._buckets):
+            b = self._buckets[self._next_launch]
+            if b.ready < len(b.params):
+                break
+            range_push(f"ddp_allreduce_b{b.index}")
+            b.work = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+            range_pop()
+            b.launched = True
+            self._next_launch += 1
+
+    def _finalize(self) -> None:
+        # parameters that got no gradient this step contribute zeros (find_unused_parameters)
+        for b in self._buckets[self._next_launch :]:
+            if b.ready < len(b.params):
+                with torch.no_grad():
+                    for i, (p, off) in enumerate(zip(b.params, b.offsets)):
+                        if not b.got[i]:
+                            b.buf[off : off + p.numel()].zero_()
+                            b.got[i] = True
+                b.ready = len(b.params)
+        self._launch_ready()
+        for b in self._buckets:
+            if b.work is not None:
+                b.work.wait()  # stream-ordered: the compute stream waits on RCCL, the host does not
+                b.work = None
+            for p, off in zip(b.params, b.offsets):
+                view = b.buf[off : off + p.numel()].view_as(p)
+                if view.dtype == p.dtype:
+                    p.grad = view
+                elif p.grad is not None:
+                    p.grad.copy_(view)
+                else:
+                    p.grad = view.to(p.dtype)
+            b.ready = 0
+            b.got = [False] * len(b.params)
+            b.launched = False
+        self._next_launch = 0
+        self._callback_queued = False
+
+    # ------------------------------------------------------------------ module API
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (no all-reduce) inside this context."""
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def forward(self, *args, **kwargs):
+        if self.world > 1 and self.broadcast_buffers:
+            bufs = [b for b in self.module.buffers() if b.numel() > 0]
+            if bufs:
+                _flat_broadcast(bufs, 0, self.process_group)
+        return self.module(*args, **kwargs)
+
+    def state_dict(self, *args, **kwargs):  # keep reference checkpoint keys (model.module.state_dict())
+        return self.module.state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        return self.module.load_state_dict(state_dict, strict=strict)
+
+
+DDP = DistributedDataParallel

@@ -1,0 +1,97 @@
+"""Training-step engine: eager or hipGraph-captured (fwd + bwd + optimizer as one graph).
+
+The reference amortized launch overhead with ``torch.compile(mode="reduce-overhead")`` /
+Inductor (``compilation_optimization.py:96-103``, C32).  Hyperion has no tracing compiler: the
+static-shape step is captured once into a hipGraph and replayed, so a ResNet-50 step (≈1,000
+kernels: convs, fused BN, fused optimizer) costs one graph launch on the host.
+
+Requirements for capture (all satisfied by Hyperion ops): no host syncs inside the step, no
+pageable H2D copies, device-side optimizer scalars (``FusedAdam`` keeps step count on device).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+
+
+def autocast_ctx(device: torch.device, dtype: Optional[torch.dtype]):
+    if dtype is None or dtype == torch.float32:
+        return contextlib.nullcontext()
+    return torch.autocast(device_type=device.type, dtype=dtype)
+
+
+class TrainStep:
+    """``loss = step(x, y)``; captures a hipGraph on GPU when ``graph=True``."""
+
+    def __init__(
+        self,
+        model: nn.Module,
+        optimizer: torch.optim.Optimizer,
+        loss_fn: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
+        amp_dtype: Optional[torch.dtype] = torch.bfloat16,
+        graph: bool = False,
+        warmup_iters: int = 3,
+        scaler=None,
+    ):
+        self.model = model
+        self.opt = optimizer
+        self.loss_fn = loss_fn
+        self.amp_dtype = amp_dtype
+        self.use_graph = graph and torch.cuda.is_available()
+        self.warmup_iters = warmup_iters
+        self.scaler = scaler
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.static_x: Optional[torch.Tensor] = None
+        self.static_y: Optional[torch.Tensor] = None
+        self.static_loss: Optional[torch.Tensor] = None
+
+    def _body(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        dev = x.device
+        with autocast_ctx(dev, self.amp_dtype):
+            out = self.model(x)
+            loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
+        if self.scaler is not None:
+            self.scaler.scale(loss).backward()
+            self.scaler.step(self.opt)
+            self.scaler.update()
+        else:
+            loss.backward()
+            self.opt.step()
+        return loss.detach()
+
+    def eager_step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        self.opt.zero_grad(set_to_none=True)
+        return self._body(x, y)
+
+    def _capture(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        self.static_x = x.clone()
+        self.static_y = y.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup_iters):
+                self.opt.zero_grad(set_to_none=True)
+                self._body(self.static_x, self.static_y)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.static_loss = self._body(self.static_x, self.static_y)
+        torch.cuda.synchronize()
+        self.graph = g
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if not self.use_graph:
+            return self.eager_step(x, y)
+        if self.graph is None:
+            self._capture(x, y)
+        if x.data_ptr() != self.static_x.data_ptr():
+            self.static_x.copy_(x, non_blocking=True)
+        if y.data_ptr() != self.static_y.data_ptr():
+            self.static_y.copy_(y, non_blocking=True)
+        self.graph.replay()
+        return self.static_loss

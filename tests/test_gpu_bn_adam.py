@@ -1,0 +1,138 @@
+"""GPU numerics: fused BN(+res)(+ReLU) and multi-tensor Adam vs PyTorch fp32 references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_bn(x, res, w, b, rm, rv, training, mom, eps, act):
+    y = F.batch_norm(x, rm, rv, w, b, training, mom, eps)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if act else y
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [64, 256, 2048])
+@pytest.mark.parametrize("act,use_res", [(True, False), (True, True), (False, False)])
+def test_bn_act_matches_reference(dtype, C, act, use_res):
+    from hyperion.ops import _native
+    from hyperion.ops.batchnorm import _BNActFn
+
+    assert _native.available(), "native extension must load on the GPU box"
+    torch.manual_seed(0)
+    N, H, W = 4, 7, 5
+    dev = "cuda"
+    x = (torch.randn(N, C, H, W, device=dev) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    res = torch.randn_like(x) if use_res else None
+    w = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm.clone(), rv.clone()
+
+    xr = x.detach().float().requires_grad_(True)
+    resr = res.detach().float().requires_grad_(True) if use_res else None
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = _ref_bn(xr, resr, wr, br, rm2, rv2, True, 0.1, 1e-5, act)
+
+    xn = x.detach().requires_grad_(True)
+    resn = res.detach().requires_grad_(True) if use_res else None
+    wn = w.clone().requires_grad_(True)
+    bn = b.clone().requires_grad_(True)
+    yn = _BNActFn.apply(xn, resn, wn, bn, rm, rv, 0.1, 1e-5, True, act)
+
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(yn.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(rv, rv2, atol=1e-4, rtol=1e-3)
+
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    yn.backward(gy.to(dtype).contiguous(memory_format=torch.channels_last))
+    gtol = 2e-4 if dtype == torch.float32 else 6e-2
+    torch.testing.assert_close(xn.grad.float(), xr.grad, atol=gtol, rtol=gtol)
+    torch.testing.assert_close(wn.grad, wr.grad, atol=gtol * C, rtol=gtol)
+    torch.testing.assert_close(bn.grad, br.grad, atol=gtol * C, rtol=gtol)
+    if use_res:
+        torch.testing.assert_close(resn.grad.float(), resr.grad, atol=gtol, rtol=gtol)
+
+
+def test_bn_eval_mode():
+    from hyperion.ops.batchnorm import BatchNormAct2d
+
+    torch.manual_seed(1)
+    m = BatchNormAct2d(128, act=True).cuda()
+    m.running_mean.uniform_(-1, 1)
+    m.running_var.uniform_(0.5, 2)
+    m.eval()
+    x = torch.randn(2, 128, 6, 6, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = m(x)
+    yr = F.relu(F.batch_norm(x, m.running_mean, m.running_var, m.weight, m.bias, False, 0.1, 1e-5))
+    torch.testing.assert_close(y, yr, atol=1e-5, rtol=1e-5)
+
+
+def test_fused_adam_matches_torch():
+    from hyperion.ops import FusedAdam
+
+    torch.manual_seed(0)
+    shapes = [(64, 3, 7, 7), (1000, 2048), (1000,), (3,), (8191,)]
+    ps = [torch.randn(s, device="cuda", requires_grad=True) for s in shapes]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    for adamw, wd in [(False, 0.0), (False, 1e-2), (True, 1e-2)]:
+        opt = FusedAdam(ps, lr=1e-3, weight_decay=wd, adamw=adamw)
+        ref = (torch.optim.AdamW if adamw else torch.optim.Adam)(qs, lr=1e-3, weight_decay=wd)
+        for _ in range(5):
+            for p, q in zip(ps, qs):
+                g = torch.randn_like(p)
+                p.grad = g.clone()
+                q.grad = g.clone()
+            opt.step()
+            ref.step()
+        for p, q in zip(ps, qs):
+            torch.testing.assert_close(p, q, atol=1e-5, rtol=1e-4)
+
+
+def test_stream_kernels():
+    from hyperion.ops import _native
+
+    C = _native.native()
+    n = 1 << 20
+    a = torch.randn(n, device="cuda")
+    b = torch.randn(n, device="cuda")
+    c = torch.empty_like(a)
+    C.stream(2, a, b, c, 0.0, False, 0)
+    torch.testing.assert_close(c, a + b)
+    C.stream(3, a, b, c, 3.0, True, 0)
+    torch.testing.assert_close(c, a + 3.0 * b)
+    C.stream(0, a, None, c, 0.0, False, 0)
+    torch.testing.assert_close(c, a)
+
+
+def test_resnet50_native_step_runs_and_matches_torch_path():
+    """One bf16 training step through the fused kernels vs the torch path on identical weights."""
+    import copy
+    import os
+
+    from hyperion.models import resnet50
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    m2 = copy.deepcopy(m)
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(x)
+    out.float().sum().backward()
+    os.environ["HYPERION_KERNELS"] = "torch"
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out2 = m2(x)
+        out2.float().sum().backward()
+    finally:
+        os.environ.pop("HYPERION_KERNELS", None)
+    torch.testing.assert_close(out.float(), out2.float(), atol=0.15, rtol=0.1)
+    g1 = m.conv1.weight.grad.float()
+    g2 = m2.conv1.weight.grad.float()
+    cos = F.cosine_similarity(g1.flatten(), g2.flatten(), dim=0)
+    assert cos > 0.98, cos
