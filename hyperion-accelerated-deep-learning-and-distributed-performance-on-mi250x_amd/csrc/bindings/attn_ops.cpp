@@ -1,0 +1,165 @@
+// Torch bindings: flash attention fwd/bwd and LayerNorm/RMSNorm fwd/bwd.
+#include "bindings/common.h"
+#include "bindings/registry.h"
+
+namespace hypbind {
+namespace {
+
+void check_bshd(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4, name, " must be a [B,S,H,D] GPU tensor");
+  TORCH_CHECK(t.stride(3) == 1, name, " must have a contiguous head dim");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
+              name, " strides must be multiples of 8 elements (16-byte vector loads)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
+                                 double scale, double p_drop, int64_t seed, const c10::optional<at::Tensor>& kpm,
+                                 bool need_lse) {
+  check_bshd(q, "q");
+  check_bshd(k, "k");
+  check_bshd(v, "v");
+  TORCH_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes(), "attn_fwd: self-attention shapes must match");
+  const int B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3);
+  const int dt = dtype_code(q);
+  TORCH_CHECK(hyp::attention_supported(dt, D), "attn_fwd: needs bf16/fp16 and head_dim 64 or 128");
+  const at::DeviceGuard guard(q.device());
+  auto o = at::empty({B, S, H, D}, q.options());
+  at::Tensor lse;
+  if (need_lse) lse = at::empty({B * H, S}, q.options().dtype(at::kFloat));
+  at::Tensor kpm_u8;
+  if (kpm.has_value() && kpm->defined()) {
+    kpm_u8 = kpm->to(at::kByte).contiguous();
+    TORCH_CHECK(kpm_u8.size(0) == B && kpm_u8.size(1) == S, "key_padding_mask must be [B, S]");
+  }
+  hyp::AttnParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr();
+  p.sqb = q.stride(0); p.sqs = q.stride(1); p.sqh = q.stride(2);
+  p.skb = k.stride(0); p.sks = k.stride(1); p.skh = k.stride(2);
+  p.svb = v.stride(0); p.svs = v.stride(1); p.svh = v.stride(2);
+  p.sob = o.stride(0); p.sos = o.stride(1); p.soh = o.stride(2);
+  p.lse = need_lse ? lse.data_ptr<float>() : nullptr;
+  p.kpm = kpm_u8.defined() ? kpm_u8.data_ptr<uint8_t>() : nullptr;
+  p.B = B; p.H = H; p.S = S; p.D = D;
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.causal = causal ? 1 : 0;
+  p.p_drop = (float)p_drop;
+  p.seed = (uint64_t)seed;
+  HYP_CHECK_HIP(hyp::attention_forward(dt, p, cur_stream()));
+  return {o, lse};
+}
+
+// grads are written into dq/dk/dv (any [B,S,H,D] strided views, e.g. slices of a packed dQKV)
+void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+              const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, double p_drop, int64_t seed,
+              const c10::optional<at::Tensor>& kpm, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
+  check_bshd(q, "q");
+  check_bshd(k, "k");
+  check_bshd(v, "v");
+  check_bshd(o, "o");
+  check_bshd(dq, "dq");
+  check_bshd(dk, "dk");
+  check_bshd(dv, "dv");
+  at::Tensor g = dout.stride(3) == 1 && dout.stride(0) % 8 == 0 && dout.stride(1) % 8 == 0 && dout.stride(2) % 8 == 0
+                     ? dout
+                     : dout.contiguous();
+  check_bshd(g, "dout");
+  const int B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3);
+  const int dt = dtype_code(q);
+  const at::DeviceGuard guard(q.device());
+  auto fopt = q.options().dtype(at::kFloat);
+  auto delta = at::empty({(int64_t)B * H * S}, fopt);
+  auto dq_acc = at::empty({(int64_t)B * H * S * D}, fopt);
+  at::Tensor kpm_u8;
+  if (kpm.has_value() && kpm->defined()) kpm_u8 = kpm->to(at::kByte).contiguous();
+  hyp::AttnBwdParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr(); p.dout = g.data_ptr();
+  p.dq = dq.data_ptr(); p.dk = dk.data_ptr(); p.dv = dv.data_ptr();
+  p.sqb = q.stride(0); p.sqs = q.stride(1); p.sqh = q.stride(2);
+  p.skb = k.stride(0); p.sks = k.stride(1); p.skh = k.stride(2);
+  p.svb = v.stride(0); p.svs = v.stride(1); p.svh = v.stride(2);
+  p.sob = o.stride(0); p.sos = o.stride(1); p.soh = o.stride(2);
+  p.sdob = g.stride(0); p.sdos = g.stride(1); p.sdoh = g.stride(2);
+  p.sdqb = dq.stride(0); p.sdqs = dq.stride(1); p.sdqh = dq.stride(2);
+  p.sdkb = dk.stride(0); p.sdks = dk.stride(1); p.sdkh = dk.stride(2);
+  p.sdvb = dv.stride(0); p.sdvs = dv.stride(1); p.sdvh = dv.stride(2);
+  p.lse = lse.data_ptr<float>();
+  p.delta = delta.data_ptr<float>();
+  p.dq_acc = dq_acc.data_ptr<float>();
+  p.kpm = kpm_u8.defined() ? kpm_u8.data_ptr<uint8_t>() : nullptr;
+  p.B = B; p.H = H; p.S = S; p.D = D;
+  p.scale = (float)scale;
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.causal = causal ? 1 : 0;
+  p.p_drop = (float)p_drop;
+  p.seed = (uint64_t)seed;
+  HYP_CHECK_HIP(hyp::attention_backward(dt, p, cur_stream()));
+}
+
+// ---- LayerNorm / RMSNorm ------------------------------------------------------------------
+// x: [..., d] contiguous; returns (y, s (fused residual stream or undefined), mean, rstd)
+std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
+                               const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
+                               double eps, bool rms) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.is_contiguous(), "ln_fwd: x must be contiguous");
+  const int d = x.size(-1);
+  TORCH_CHECK(hyp::layernorm_supported(d), "ln_fwd: unsupported hidden size ", d);
+  const int64_t rows = x.numel() / d;
+  const at::DeviceGuard guard(x.device());
+  auto y = at::empty_like(x);
+  at::Tensor s;
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res) {
+    TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes() &&
+                    residual->scalar_type() == x.scalar_type(),
+                "ln_fwd: residual mismatch");
+    s = at::empty_like(x);
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({rows}, fopt);
+  auto rstd = at::empty({rows}, fopt);
+  HYP_CHECK_HIP(hyp::layernorm_forward(dtype_code(x), rms ? 1 : 0, x.data_ptr(), has_res ? residual->data_ptr() : nullptr,
+                                       has_res ? s.data_ptr() : nullptr, y.data_ptr(), ptr_or_null<float>(weight),
+                                       ptr_or_null<float>(bias), rms ? nullptr : mean.data_ptr<float>(),
+                                       rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream()));
+  return {y, s, mean, rstd};
+}
+
+// returns (dx, dweight, dbias)
+std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, const c10::optional<at::Tensor>& weight,
+                               const at::Tensor& mean, const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                               bool need_dw, bool need_db, bool rms) {
+  const int d = xin.size(-1);
+  const int64_t rows = xin.numel() / d;
+  at::Tensor g = dy.is_contiguous() ? dy : dy.contiguous();
+  const at::DeviceGuard guard(xin.device());
+  auto dx = at::empty_like(xin);
+  int P = 1, rpw = 1;
+  hyp::layernorm_bwd_geom(rows, &P, &rpw);
+  auto fopt = xin.options().dtype(at::kFloat);
+  auto part = at::empty({2 * (int64_t)P * d}, fopt);
+  at::Tensor dw, db;
+  if (need_dw) dw = at::empty({d}, fopt);
+  if (need_db && !rms) db = at::empty({d}, fopt);
+  at::Tensor dr;
+  if (dres.has_value() && dres->defined()) dr = dres->is_contiguous() ? *dres : dres->contiguous();
+  HYP_CHECK_HIP(hyp::layernorm_backward(dtype_code(xin), rms ? 1 : 0, g.data_ptr(), xin.data_ptr(),
+                                        ptr_or_null<float>(weight), rms ? nullptr : mean.data_ptr<float>(),
+                                        rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(),
+                                        part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)P * d,
+                                        need_dw ? dw.data_ptr<float>() : nullptr,
+                                        db.defined() ? db.data_ptr<float>() : nullptr, rows, d, P, rpw, cur_stream()));
+  return {dx, dw, db};
+}
+
+}  // namespace
+
+void register_attn_ops(pybind11::module& m) {
+  m.def("attn_fwd", &attn_fwd, "flash attention forward (MFMA)");
+  m.def("attn_bwd", &attn_bwd, "flash attention backward (MFMA)");
+  m.def("ln_fwd", &ln_fwd, "LayerNorm/RMSNorm forward (+fused residual add)");
+  m.def("ln_bwd", &ln_bwd, "LayerNorm/RMSNorm backward");
+}
+
+}  // namespace hypbind

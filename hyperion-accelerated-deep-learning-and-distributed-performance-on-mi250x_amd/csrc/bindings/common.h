@@ -2,7 +2,7 @@
 #pragma once
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
 
 #include "hyp_common.h"
 #include "hyp_kernels.h"

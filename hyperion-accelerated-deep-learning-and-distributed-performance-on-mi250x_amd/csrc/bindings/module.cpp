@@ -7,4 +7,5 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "Hyperion-MI355X native kernels (gfx950 HIP) and RCCL communicator";
   m.attr("arch") = "gfx950";
   hypbind::register_norm_ops(m);
+  hypbind::register_attn_ops(m);
 }

@@ -22,7 +22,7 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, const c10::optional<at::Tens
     TORCH_CHECK(is_rows_by_channels(*residual), "bn_fwd: residual must be channels-last");
   }
   if (!training) TORCH_CHECK(running_mean.has_value() && running_var.has_value(), "eval BN needs running stats");
-  const c10::hip::HIPGuard guard(x.device());
+  const at::DeviceGuard guard(x.device());
   auto y = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   int P = 1;
@@ -50,7 +50,7 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const 
   TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd: dy shape mismatch");
   at::Tensor dyc = is_rows_by_channels(dy) ? dy : (dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous());
   if (act) TORCH_CHECK(y.has_value() && is_rows_by_channels(*y), "bn_bwd: act needs the forward output");
-  const c10::hip::HIPGuard guard(x.device());
+  const at::DeviceGuard guard(x.device());
   auto dx = at::empty_like(x);
   at::Tensor dres;
   if (has_res) dres = at::empty_like(x);
@@ -74,7 +74,7 @@ void adam_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& 
              double lr, double b1, double b2, double eps, double wd, bool adamw, const c10::optional<at::Tensor>& lr_t,
              const at::Tensor& step_t, const c10::optional<at::Tensor>& inv_scale,
              const c10::optional<at::Tensor>& found_inf, int64_t grad_dtype) {
-  const c10::hip::HIPGuard guard(ptrs.device());
+  const at::DeviceGuard guard(ptrs.device());
   HYP_CHECK_HIP(hyp::adam_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
                                        blocks.data_ptr<int>(), (int)blocks.size(0), (int)T, (int)chunk, (float)lr,
                                        (float)b1, (float)b2, (float)eps, (float)wd, adamw ? 1 : 0,
@@ -84,7 +84,7 @@ void adam_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& 
 
 void unscale_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,
                 const at::Tensor& inv_scale, const at::Tensor& found_inf, int64_t grad_dtype) {
-  const c10::hip::HIPGuard guard(ptrs.device());
+  const at::DeviceGuard guard(ptrs.device());
   HYP_CHECK_HIP(hyp::unscale_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
                                           blocks.data_ptr<int>(), (int)blocks.size(0), (int)chunk,
                                           inv_scale.data_ptr<float>(), found_inf.data_ptr<float>(), cur_stream()));
@@ -92,7 +92,7 @@ void unscale_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tenso
 
 at::Tensor sumsq_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,
                     int64_t grad_dtype) {
-  const c10::hip::HIPGuard guard(ptrs.device());
+  const at::DeviceGuard guard(ptrs.device());
   auto fopt = at::TensorOptions().device(ptrs.device()).dtype(at::kFloat);
   auto part = at::empty({std::max<int64_t>(1, blocks.size(0))}, fopt);
   auto out = at::empty({1}, fopt);
@@ -104,7 +104,7 @@ at::Tensor sumsq_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::T
 
 void clip_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,
              const at::Tensor& total_sq, double max_norm, int64_t grad_dtype) {
-  const c10::hip::HIPGuard guard(ptrs.device());
+  const at::DeviceGuard guard(ptrs.device());
   HYP_CHECK_HIP(hyp::clip_multi_tensor((int)grad_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
                                        blocks.data_ptr<int>(), (int)blocks.size(0), (int)chunk,
                                        total_sq.data_ptr<float>(), (float)max_norm, cur_stream()));
@@ -114,7 +114,7 @@ void clip_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& 
 void stream(int64_t op, const at::Tensor& a, const c10::optional<at::Tensor>& b, at::Tensor& c, double s,
             bool nontemporal, int64_t blocks) {
   TORCH_CHECK(a.scalar_type() == at::kFloat && c.scalar_type() == at::kFloat, "stream: fp32 only");
-  const c10::hip::HIPGuard guard(a.device());
+  const at::DeviceGuard guard(a.device());
   HYP_CHECK_HIP(hyp::stream_op((int)op, a.data_ptr<float>(), ptr_or_null<float>(b), c.data_ptr<float>(), (float)s,
                                a.numel(), nontemporal ? 1 : 0, (int)blocks, cur_stream()));
 }

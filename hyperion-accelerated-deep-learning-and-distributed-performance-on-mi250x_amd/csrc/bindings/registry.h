@@ -4,4 +4,5 @@
 
 namespace hypbind {
 void register_norm_ops(pybind11::module& m);
+void register_attn_ops(pybind11::module& m);
 }  // namespace hypbind

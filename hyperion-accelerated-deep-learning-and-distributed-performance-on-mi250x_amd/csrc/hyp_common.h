@@ -116,6 +116,16 @@ __device__ __forceinline__ void st1<bf16_t>(bf16_t* p, float v) { *p = float_to_
 template <>
 __device__ __forceinline__ void st1<f16_t>(f16_t* p, float v) { *p = (f16_t)v; }
 
+// round a float to T's precision and back (keeps fused outputs bit-consistent with stored ones)
+template <typename T>
+__device__ __forceinline__ float rnd(float v);
+template <>
+__device__ __forceinline__ float rnd<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ float rnd<bf16_t>(float v) { return bf16_to_float(float_to_bf16(v)); }
+template <>
+__device__ __forceinline__ float rnd<f16_t>(float v) { return (float)(f16_t)v; }
+
 // ---- wave / block reductions ------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -34,3 +34,46 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
                      int blocks, hipStream_t stream);
 
 }  // namespace hyp
+
+namespace hyp {
+// ---- layernorm.hip ---------------------------------------------------------------------------
+bool layernorm_supported(int d);
+void layernorm_bwd_geom(int64_t rows, int* P, int* rows_per_wave);
+hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
+                             const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
+                             hipStream_t st);
+hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
+                              const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, float* dw,
+                              float* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st);
+}  // namespace hyp
+
+namespace hyp {
+// ---- attention.hip ---------------------------------------------------------------------------
+struct AttnParams {
+  const void* q; const void* k; const void* v; void* o;
+  int64_t sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh;  // element strides (batch, seq, head)
+  float* lse;            // [B*H, S] log2-domain log-sum-exp (may be null in inference)
+  const uint8_t* kpm;    // [B, S] key padding mask, nonzero = ignore (may be null)
+  int B, H, S, D;
+  float scale_log2;      // softmax scale * log2(e)
+  int causal;
+  float p_drop;
+  uint64_t seed;
+};
+struct AttnBwdParams {
+  const void* q; const void* k; const void* v; const void* o; const void* dout;
+  void* dq; void* dk; void* dv;
+  int64_t sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh;
+  int64_t sdob, sdos, sdoh, sdqb, sdqs, sdqh, sdkb, sdks, sdkh, sdvb, sdvs, sdvh;
+  const float* lse; float* delta; float* dq_acc;  // delta [B*H*S], dq_acc [B*H*S*D] fp32 workspaces
+  const uint8_t* kpm;
+  int B, H, S, D;
+  float scale, scale_log2;
+  int causal;
+  float p_drop;
+  uint64_t seed;
+};
+bool attention_supported(int dtype, int D);
+hipError_t attention_forward(int dtype, const AttnParams& p, hipStream_t st);
+hipError_t attention_backward(int dtype, const AttnBwdParams& p, hipStream_t st);
+}  // namespace hyp

@@ -1,0 +1,115 @@
+"""LayerNorm / RMSNorm with an optional fused residual add (gfx950 kernels in ``layernorm.hip``).
+
+Reference users: the two post-norm LayerNorms in every ``nn.TransformerEncoderLayer``
+(SimpleTransformerLM ``distributed_utils.py:75-88``, LM-768 ``compilation_optimization.py:57-71``,
+CustomTransformer ``baseline_performance.ipynb:238-249``) and HF Llama's RMSNorm (C26).
+
+``layer_norm(x, weight, bias, eps, residual=r)`` computes ``LN(x + r)`` in one pass (post-norm:
+``norm(x + dropout(sublayer(x)))``); ``return_sum=True`` also returns ``x + r`` (pre-norm residual
+stream, Llama).  Modules keep ``nn.LayerNorm`` state-dict keys.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+_SUPPORTED_D = lambda d: d % 8 == 0 and d <= 4096 and ((d + 511) // 512 <= 4 or (d + 511) // 512 == 8)  # noqa: E731
+
+
+def _ref(x, residual, weight, bias, eps, rms):
+    s = x if residual is None else x + residual
+    if rms:
+        sf = s.float()
+        y = sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + eps)
+        if weight is not None:
+            y = y * weight.float()
+        y = y.to(s.dtype)
+    else:
+        y = F.layer_norm(s, (s.shape[-1],), weight, bias, eps)
+    return y, s
+
+
+class _LNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum):
+        C = _native.native()
+        x = x.contiguous()
+        if residual is not None:
+            residual = residual.contiguous().to(x.dtype)
+        y, s, mean, rstd = C.ln_fwd(x, residual, weight, bias, eps, rms)
+        xin = s if residual is not None else x
+        ctx.rms = rms
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(xin, weight, mean, rstd)
+        if return_sum:
+            return y, (s if residual is not None else x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, ds=None):
+        xin, weight, mean, rstd = ctx.saved_tensors
+        need_dw = weight is not None and ctx.needs_input_grad[2]
+        need_db = ctx.needs_input_grad[3]
+        dx, dw, db = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms)
+        return (
+            dx,
+            dx if ctx.has_res and ctx.needs_input_grad[1] else None,
+            dw if need_dw else None,
+            db if need_db else None,
+            None, None, None,
+        )
+
+
+def layer_norm(
+    x: torch.Tensor,
+    weight: Optional[torch.Tensor],
+    bias: Optional[torch.Tensor],
+    eps: float = 1e-5,
+    residual: Optional[torch.Tensor] = None,
+    rms: bool = False,
+    return_sum: bool = False,
+) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
+    d = x.shape[-1]
+    native = (
+        _native.use_native(x)
+        and x.dtype in _native.DTYPE_CODE
+        and _SUPPORTED_D(d)
+        and (weight is None or weight.dtype == torch.float32)
+        and (bias is None or bias.dtype == torch.float32)
+        and (residual is None or residual.shape == x.shape)
+    )
+    if native:
+        if x.dtype != torch.float32 and torch.is_autocast_enabled():
+            pass  # keep activation dtype; params stay fp32 inside the kernel
+        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum)
+    y, s = _ref(x, residual, weight, bias, eps, rms)
+    return (y, s) if return_sum else y
+
+
+class LayerNorm(nn.LayerNorm):
+    """``nn.LayerNorm`` (same keys) with an optional fused residual input."""
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:  # type: ignore[override]
+        if len(self.normalized_shape) != 1:
+            return super().forward(x if residual is None else x + residual)
+        if torch.is_autocast_enabled() and x.dtype == torch.float32 and residual is not None:
+            residual = residual.float()
+        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual)
+
+
+class RMSNorm(nn.Module):
+    """RMSNorm with HF Llama's parameter name (``weight``) and fp32 statistics."""
+
+    def __init__(self, hidden_size: int, eps: float = 1e-6):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(hidden_size))
+        self.variance_epsilon = eps
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, return_sum: bool = False):
+        return layer_norm(x, self.weight, None, self.variance_epsilon, residual=residual, rms=True,
+                          return_sum=return_sum)
