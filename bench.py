@@ -38,6 +38,8 @@ def parse(argv=None):
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "resnet18"])
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--amp", default="copies", choices=["copies", "autocast"],
+                    help="copies = bf16 weight copies + fp32 masters in the fused optimizer; autocast = torch autocast")
     ap.add_argument("--kernels", default=None, choices=["hyperion", "torch"],
                     help="hyperion = fused gfx950 kernels (default); torch = PyTorch eager ops (A/B)")
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (1-GPU; N>1 see --graph-multi)")
@@ -76,6 +78,11 @@ def main(argv=None) -> int:
     model = (resnet50 if args.model == "resnet50" else resnet18)(num_classes=1000).to(dev)
     mf = torch.channels_last if args.channels_last else torch.contiguous_format
     model = model.to(memory_format=mf)
+    copies = amp is not None and args.amp == "copies"
+    if copies:
+        from hyperion.train.amp import cast_for_compute
+
+        cast_for_compute(model, amp)
     if n_gpus > 1:
         model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                     comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None)
@@ -84,9 +91,11 @@ def main(argv=None) -> int:
 
     B = args.batch
     x = torch.rand(B, 3, args.image, args.image, device=dev).to(memory_format=mf)
+    if copies:
+        x = x.to(amp)
     y = torch.rand(B, 1000, device=dev)
     use_graph = bool(args.graph) and dev.type == "cuda" and (n_gpus == 1 or bool(args.graph_multi))
-    step = TrainStep(model, opt, loss_fn, amp_dtype=amp, graph=use_graph)
+    step = TrainStep(model, opt, loss_fn, amp_dtype=None if copies else amp, graph=use_graph)
 
     for _ in range(args.warmup):
         step(x, y)
@@ -137,6 +146,8 @@ def main(argv=None) -> int:
                 "loss": "MSE vs rand(B,1000) (reference benchmark_model)",
                 "optimizer": "Adam lr=1e-3 (hyperion FusedAdam, multi-tensor)",
                 "hipgraph": use_graph,
+                "amp": ("bf16 compute copies + fp32 master weights" if copies else
+                        ("torch.autocast " + args.precision if amp is not None else "none")),
                 "kernels": _native.backend(),
                 "native_so": _native.loaded_path(),
                 "channels_last": bool(args.channels_last),

@@ -18,10 +18,11 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
                        hipStream_t stream);
 
 // ---- adam.hip ------------------------------------------------------------------------------
-hipError_t adam_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
-                             int T, int chunk, float lr, float b1, float b2, float eps, float wd, int adamw,
-                             const float* lr_t, const float* step_t, const float* inv_scale, const float* found_inf,
-                             hipStream_t stream);
+// param_dtype kF32: ptrs = [param, grad, m, v]; kBF16/kF16: ptrs = [lowp param, grad, m, v, fp32 master]
+hipError_t adam_multi_tensor(int grad_dtype, int param_dtype, const int64_t* ptrs, const int64_t* sizes,
+                             const int* blocks, int nblocks, int T, int chunk, float lr, float b1, float b2, float eps,
+                             float wd, int adamw, const float* lr_t, const float* step_t, const float* inv_scale,
+                             const float* found_inf, hipStream_t stream);
 hipError_t unscale_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks,
                                 int nblocks, int chunk, const float* inv_scale, float* found_inf, hipStream_t stream);
 hipError_t sumsq_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,

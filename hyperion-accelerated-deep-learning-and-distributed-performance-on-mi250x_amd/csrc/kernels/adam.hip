@@ -55,8 +55,21 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p -= (lr / bc1) * (m / denom);
 }
 
+template <typename PL>
+__device__ __forceinline__ void store4(PL* p, const float4& v);
+template <>
+__device__ __forceinline__ void store4<bf16_t>(bf16_t* p, const float4& v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+}
+template <>
+__device__ __forceinline__ void store4<f16_t>(f16_t* p, const float4& v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_f16x2(v.x, v.y), pack_f16x2(v.z, v.w));
+}
+
 // ptrs: [4][T] int64 addresses (param f32, grad G, exp_avg f32, exp_avg_sq f32)
-template <typename G>
+// MASTER: [5][T] (param PL (bf16/f16 compute copy), grad G, exp_avg, exp_avg_sq, fp32 master);
+// the fp32 master is updated and the low-precision compute copy rewritten in the same pass.
+template <typename G, typename PL, bool MASTER>
 __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict__ ptrs, const int64_t* __restrict__ sizes,
                                                       const int* __restrict__ blocks, int T, int chunk, AdamArgs a,
                                                       const float* __restrict__ lr_t, const float* __restrict__ step_t,
@@ -65,7 +78,8 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
   if (found_inf != nullptr && *found_inf != 0.f) return;  // GradScaler: skip the step on inf/nan
   const int t = blocks[2 * blockIdx.x];
   const int ck = blocks[2 * blockIdx.x + 1];
-  float* __restrict__ p = reinterpret_cast<float*>(ptrs[t]);
+  float* __restrict__ p = reinterpret_cast<float*>(MASTER ? ptrs[4 * T + t] : ptrs[t]);
+  PL* __restrict__ pl = reinterpret_cast<PL*>(ptrs[t]);
   const G* __restrict__ g = reinterpret_cast<const G*>(ptrs[T + t]);
   float* __restrict__ m = reinterpret_cast<float*>(ptrs[2 * T + t]);
   float* __restrict__ v = reinterpret_cast<float*>(ptrs[3 * T + t]);
@@ -92,6 +106,7 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
     *reinterpret_cast<float4*>(p + i) = pv;
     *reinterpret_cast<float4*>(m + i) = mv;
     *reinterpret_cast<float4*>(v + i) = vv;
+    if (MASTER) store4<PL>(pl + i, pv);
   }
   for (int64_t i = nvec_end + threadIdx.x; i < end; i += kThreads) {
     float pp = p[i], mm = m[i], vv = v[i];
@@ -99,6 +114,7 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
+    if (MASTER) st1<PL>(pl + i, pp);
   }
 }
 
@@ -170,15 +186,22 @@ __global__ void sum_partials_k(const float* __restrict__ part, int n, float* __r
 
 }  // namespace
 
-hipError_t adam_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
-                             int T, int chunk, float lr, float b1, float b2, float eps, float wd, int adamw,
-                             const float* lr_t, const float* step_t, const float* inv_scale, const float* found_inf,
-                             hipStream_t stream) {
+hipError_t adam_multi_tensor(int grad_dtype, int param_dtype, const int64_t* ptrs, const int64_t* sizes,
+                             const int* blocks, int nblocks, int T, int chunk, float lr, float b1, float b2, float eps,
+                             float wd, int adamw, const float* lr_t, const float* step_t, const float* inv_scale,
+                             const float* found_inf, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   AdamArgs a{lr, b1, b2, eps, wd, adamw, 0};
   HYP_DISPATCH_FLOAT(grad_dtype, G, {
-    hipLaunchKernelGGL(adam_mt_k<G>, dim3(nblocks), dim3(kThreads), 0, stream, ptrs, sizes, blocks, T, chunk, a, lr_t,
-                       step_t, inv_scale, found_inf);
+    if (param_dtype == kF32)
+      hipLaunchKernelGGL((adam_mt_k<G, float, false>), dim3(nblocks), dim3(kThreads), 0, stream, ptrs, sizes, blocks,
+                         T, chunk, a, lr_t, step_t, inv_scale, found_inf);
+    else if (param_dtype == kBF16)
+      hipLaunchKernelGGL((adam_mt_k<G, bf16_t, true>), dim3(nblocks), dim3(kThreads), 0, stream, ptrs, sizes, blocks,
+                         T, chunk, a, lr_t, step_t, inv_scale, found_inf);
+    else
+      hipLaunchKernelGGL((adam_mt_k<G, f16_t, true>), dim3(nblocks), dim3(kThreads), 0, stream, ptrs, sizes, blocks,
+                         T, chunk, a, lr_t, step_t, inv_scale, found_inf);
   });
   return hipGetLastError();
 }

@@ -21,6 +21,7 @@ namespace hyp {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kStatsBlocks = 512;  // partial rows per reduction: keeps the combine pass short
 
 struct BnGeom {
   int tpr;   // threads per row (each owns 8 channels)
@@ -112,6 +113,29 @@ __global__ __launch_bounds__(kBlock) void bn_stats_partial_k(const T* __restrict
   }
 }
 
+// Sum partial rows p = threadIdx.y, +16, ... of column c with 8 independent loads in flight
+// (the loop is latency-bound; a rolled loop waits one L2 round trip per partial).
+__device__ __forceinline__ void combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int P,
+                                                 int C, int c, float& a, float& b) {
+  float sa[8], sb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.f;
+  int p = threadIdx.y;
+  for (; p + 16 * 7 < P; p += 16 * 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sa[i] += pa[(int64_t)(p + 16 * i) * C + c];
+      sb[i] += pb[(int64_t)(p + 16 * i) * C + c];
+    }
+  }
+  for (; p < P; p += 16) {
+    sa[0] += pa[(int64_t)p * C + c];
+    sb[0] += pb[(int64_t)p * C + c];
+  }
+  a = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
+  b = ((sb[0] + sb[1]) + (sb[2] + sb[3])) + ((sb[4] + sb[5]) + (sb[6] + sb[7]));
+}
+
 // grid: ceil(C/64); block (64, 16)
 __global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restrict__ psum, const float* __restrict__ psq,
                                                             int P, int C, int64_t M, const float* __restrict__ weight,
@@ -119,24 +143,21 @@ __global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restr
                                                             float* running_var, float momentum, float eps,
                                                             float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                             float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ double red_s[16][64];
-  __shared__ double red_q[16][64];
+  __shared__ float red_s[16][64];
+  __shared__ float red_q[16][64];
   const int c = blockIdx.x * 64 + threadIdx.x;
-  double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int p = threadIdx.y; p < P; p += 16) {
-      a += (double)psum[(int64_t)p * C + c];
-      b += (double)psq[(int64_t)p * C + c];
-    }
-  }
+  float a = 0.f, b = 0.f;
+  if (c < C) combine_partials(psum, psq, P, C, c, a, b);
   red_s[threadIdx.y][threadIdx.x] = a;
   red_q[threadIdx.y][threadIdx.x] = b;
   __syncthreads();
   if (threadIdx.y == 0 && c < C) {
+    double da = a, db = b;
     for (int i = 1; i < 16; ++i) {
-      a += red_s[i][threadIdx.x];
-      b += red_q[i][threadIdx.x];
+      da += red_s[i][threadIdx.x];
+      db += red_q[i][threadIdx.x];
     }
+    const double a = da, b = db;
     const double mean = a / (double)M;
     double var = b / (double)M - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -313,24 +334,21 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restric
                                                           float* __restrict__ dweight, float* __restrict__ dbias,
                                                           float* __restrict__ kA, float* __restrict__ kB,
                                                           float* __restrict__ kC) {
-  __shared__ double red_s[16][64];
-  __shared__ double red_q[16][64];
+  __shared__ float red_s[16][64];
+  __shared__ float red_q[16][64];
   const int c = blockIdx.x * 64 + threadIdx.x;
-  double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int p = threadIdx.y; p < P; p += 16) {
-      a += (double)pdz[(int64_t)p * C + c];
-      b += (double)pdzx[(int64_t)p * C + c];
-    }
-  }
+  float a = 0.f, b = 0.f;
+  if (c < C) combine_partials(pdz, pdzx, P, C, c, a, b);
   red_s[threadIdx.y][threadIdx.x] = a;
   red_q[threadIdx.y][threadIdx.x] = b;
   __syncthreads();
   if (threadIdx.y == 0 && c < C) {
+    double da = a, db = b;
     for (int i = 1; i < 16; ++i) {
-      a += red_s[i][threadIdx.x];
-      b += red_q[i][threadIdx.x];
+      da += red_s[i][threadIdx.x];
+      db += red_q[i][threadIdx.x];
     }
+    const double a = da, b = db;
     const double mu = mean[c], is = invstd[c];
     const double sum_dz_xhat = is * (b - mu * a);
     if (dweight) dweight[c] = (float)sum_dz_xhat;
@@ -393,7 +411,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, 
 // ======================================================================== host launchers
 hipError_t bn_workspace_rows(int64_t M, int C, int* P_out) {
   BnGeom g;
-  if (!bn_geom(M, C, 1024, g)) return hipErrorInvalidValue;
+  if (!bn_geom(M, C, kStatsBlocks, g)) return hipErrorInvalidValue;
   *P_out = g.P;
   return hipSuccess;
 }
@@ -403,7 +421,7 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
                       int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
                       float* scale, float* shift, hipStream_t stream) {
   BnGeom gs, ga;
-  if (!bn_geom(M, C, 1024, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  if (!bn_geom(M, C, kStatsBlocks, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     const T* xt = static_cast<const T*>(x);
     if (training) {
@@ -439,7 +457,7 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
                        float* pdz, float* pdzx, float* dweight, float* dbias, float* kA, float* kB, float* kC,
                        hipStream_t stream) {
   BnGeom gs, ga;
-  if (!bn_geom(M, C, 1024, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  if (!bn_geom(M, C, kStatsBlocks, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     const T* dyt = static_cast<const T*>(dy);
     const T* xt = static_cast<const T*>(x);

@@ -7,6 +7,11 @@ group chunk; ``FusedAdam`` runs ``adam_mt_k`` once, reading step / loss-scale / 
 device memory so the step can be captured in a hipGraph and skipped on overflow without a host
 sync (GradScaler semantics).
 
+Low-precision parameters (bf16/fp16 — "compute copies") get an fp32 master copy in the optimizer
+state; the kernel updates the master and rewrites the compute copy in the same pass.  This lets a
+model run its convolutions/GEMMs on bf16 weights directly (no per-forward autocast weight casts,
+no bf16→fp32 grad casts in backward) while the optimizer math stays in fp32.
+
 Also provides multi-tensor global-norm clipping that takes the norm over *all* gradient shards
 (all-reduced when a process group is given) — the reference clipped only the local FSDP shard
 (``distributed_utils.py:351,522``).
@@ -21,6 +26,10 @@ import torch.distributed as dist
 
 from . import _native
 from .multi_tensor import TableCache
+
+
+def _dense(t: torch.Tensor) -> bool:
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -42,20 +51,14 @@ class FusedAdam(torch.optim.Optimizer):
         self.inv_scale: Optional[torch.Tensor] = None
         self.found_inf: Optional[torch.Tensor] = None
 
-    def _group_tensors(self, group):
-        ps, gs, ms, vs = [], [], [], []
-        for p in group["params"]:
-            if p.grad is None:
-                continue
-            st = self.state[p]
-            if not st:
-                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            ps.append(p)
-            gs.append(p.grad)
-            ms.append(st["exp_avg"])
-            vs.append(st["exp_avg_sq"])
-        return ps, gs, ms, vs
+    def _state(self, p: torch.Tensor):
+        st = self.state[p]
+        if not st:
+            st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.preserve_format)
+            if p.dtype != torch.float32:
+                st["master"] = p.detach().to(torch.float32, memory_format=torch.preserve_format).clone()
+        return st
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -64,43 +67,50 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._host_step += 1
-        first = None
-        for group in self.param_groups:
-            for p in group["params"]:
-                if p.grad is not None:
-                    first = p
-                    break
-            if first is not None:
-                break
+        first = next((p for g in self.param_groups for p in g["params"] if p.grad is not None), None)
         if first is None:
             return loss
-        native = _native.use_native(first) and first.dtype == torch.float32
+        native = _native.use_native(first)
         if native:
             if self._step_t is None or self._step_t.device != first.device:
-                self._step_t = torch.zeros((), dtype=torch.float32, device=first.device)
+                self._step_t = torch.full((), float(self._host_step - 1), dtype=torch.float32, device=first.device)
             self._step_t.add_(1.0)
         for gi, group in enumerate(self.param_groups):
-            ps, gs, ms, vs = self._group_tensors(group)
-            if not ps:
-                continue
-            b1, b2 = group["betas"]
-            if native and all(g.dtype == gs[0].dtype for g in gs) and all(
-                p.dtype == torch.float32 and p.is_contiguous() and g.is_contiguous() for p, g in zip(ps, gs)
-            ):
-                tab = self._tables.get(f"adam{gi}", [ps, gs, ms, vs])
-                lr = group["lr"]
-                lr_t = lr if isinstance(lr, torch.Tensor) else None
-                _native.native().adam_mt(
-                    tab.ptrs, tab.sizes, tab.blocks, tab.T, tab.chunk,
-                    float(lr) if lr_t is None else 0.0, b1, b2, group["eps"], group["weight_decay"],
-                    bool(group["adamw"]), lr_t, self._step_t, self.inv_scale, self.found_inf,
-                    _native.DTYPE_CODE[gs[0].dtype],
+            params = [p for p in group["params"] if p.grad is not None]
+            # partition by (param dtype, grad dtype): one launch per partition
+            parts = {}
+            for p in params:
+                parts.setdefault((p.dtype, p.grad.dtype), []).append(p)
+            for (pdt, gdt), ps in parts.items():
+                sts = [self._state(p) for p in ps]
+                gs = [p.grad for p in ps]
+                ms = [s["exp_avg"] for s in sts]
+                vs = [s["exp_avg_sq"] for s in sts]
+                masters = [s["master"] for s in sts] if pdt != torch.float32 else None
+                ok = native and pdt in _native.DTYPE_CODE and gdt in _native.DTYPE_CODE and all(
+                    _dense(p) and p.stride() == g.stride() == m.stride() for p, g, m in zip(ps, gs, ms)
                 )
-            else:
-                self._reference_step(group, ps, gs, ms, vs)
+                if ok:
+                    groups = [ps, gs, ms, vs] + ([masters] if masters is not None else [])
+                    try:
+                        tab = self._tables.get(f"adam{gi}_{pdt}_{gdt}", groups)
+                    except ValueError:  # misaligned tensor -> reference path
+                        ok = False
+                if ok:
+                    lr = group["lr"]
+                    lr_t = lr if isinstance(lr, torch.Tensor) else None
+                    b1, b2 = group["betas"]
+                    _native.native().adam_mt(
+                        tab.ptrs, tab.sizes, tab.blocks, tab.T, tab.chunk,
+                        float(lr) if lr_t is None else 0.0, b1, b2, group["eps"], group["weight_decay"],
+                        bool(group["adamw"]), lr_t, self._step_t, self.inv_scale, self.found_inf,
+                        _native.DTYPE_CODE[gdt], _native.DTYPE_CODE[pdt],
+                    )
+                else:
+                    self._reference_step(group, ps, gs, ms, vs, masters)
         return loss
 
-    def _reference_step(self, group, ps, gs, ms, vs):
+    def _reference_step(self, group, ps, gs, ms, vs, masters=None):
         """PyTorch reference (CPU / fallback); identical math to the kernel."""
         if self.found_inf is not None and float(self.found_inf) != 0.0:
             return
@@ -111,16 +121,19 @@ class FusedAdam(torch.optim.Optimizer):
         bc1 = 1 - b1**step
         bc2_sqrt = math.sqrt(1 - b2**step)
         inv = float(self.inv_scale) if self.inv_scale is not None else 1.0
-        for p, g, m, v in zip(ps, gs, ms, vs):
+        for i, (p, g, m, v) in enumerate(zip(ps, gs, ms, vs)):
+            w = masters[i] if masters is not None else p
             g = g.float() * inv
             if group["adamw"]:
-                p.mul_(1 - lr * wd)
+                w.mul_(1 - lr * wd)
             elif wd != 0:
-                g = g.add(p, alpha=wd)
+                g = g.add(w, alpha=wd)
             m.mul_(b1).add_(g, alpha=1 - b1)
             v.mul_(b2).addcmul_(g, g, value=1 - b2)
             denom = (v.sqrt() / bc2_sqrt).add_(group["eps"])
-            p.addcdiv_(m, denom, value=-lr / bc1)
+            w.addcdiv_(m, denom, value=-lr / bc1)
+            if masters is not None:
+                p.copy_(w)
 
     def state_dict(self):
         sd = super().state_dict()
@@ -132,14 +145,7 @@ class FusedAdam(torch.optim.Optimizer):
         self._host_step = int(state_dict.pop("hyperion_step", 0))
         super().load_state_dict(state_dict)
         self._step_t = None
-        if self._host_step:
-            for group in self.param_groups:
-                for p in group["params"]:
-                    if p.is_cuda:
-                        self._step_t = torch.full((), float(self._host_step), device=p.device)
-                        break
-                if self._step_t is not None:
-                    break
+        self._tables = TableCache()
 
 
 def FusedAdamW(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
@@ -166,9 +172,13 @@ def clip_grad_norm_(
     if not grads:
         return torch.zeros(())
     dev = grads[0].device
-    native = _native.use_native(grads[0]) and all(g.is_contiguous() and g.dtype == grads[0].dtype for g in grads)
+    native = _native.use_native(grads[0]) and all(_dense(g) and g.dtype == grads[0].dtype for g in grads)
     if native:
-        tab = _clip_tables.get("clip", [grads])
+        try:
+            tab = _clip_tables.get("clip", [grads])
+        except ValueError:
+            native = False
+    if native:
         code = _native.DTYPE_CODE[grads[0].dtype]
         total_sq = _native.native().sumsq_mt(tab.ptrs, tab.sizes, tab.blocks, tab.chunk, code)
     else:

@@ -84,12 +84,12 @@ def test_layernorm(dtype, d, fused):
     r = torch.randn_like(x) if fused else None
     w = torch.rand(d, device="cuda") + 0.5
     b = torch.randn(d, device="cuda")
-    xr = x.float().requires_grad_(True)
-    rr = r.float().requires_grad_(True) if fused else None
+    xr = x.detach().float().clone().requires_grad_(True)
+    rr = r.detach().float().clone().requires_grad_(True) if fused else None
     wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
     yr = F.layer_norm(xr + rr if fused else xr, (d,), wr, br, 1e-5)
-    xn = x.clone().requires_grad_(True)
-    rn = r.clone().requires_grad_(True) if fused else None
+    xn = x.detach().clone().requires_grad_(True)
+    rn = r.detach().clone().requires_grad_(True) if fused else None
     wn, bn = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
     yn = _LNFn.apply(xn, rn, wn, bn, 1e-5, False, False)
     tol = 1e-4 if dtype == torch.float32 else 3e-2

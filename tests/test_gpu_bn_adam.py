@@ -136,3 +136,37 @@ def test_resnet50_native_step_runs_and_matches_torch_path():
     g2 = m2.conv1.weight.grad.float()
     cos = F.cosine_similarity(g1.flatten(), g2.flatten(), dim=0)
     assert cos > 0.98, cos
+
+
+def test_fused_adam_master_weights_bf16():
+    """bf16 compute copies + fp32 masters: master tracks fp32 Adam exactly; copy = rounded master."""
+    from hyperion.ops import FusedAdam
+
+    torch.manual_seed(0)
+    shapes = [(256, 64, 1, 1), (1000, 2048), (1000,)]
+    ref = [torch.randn(s, device="cuda").bfloat16().float().requires_grad_(True) for s in shapes]
+    lowp = [r.detach().bfloat16().requires_grad_(True) for r in ref]
+    opt = FusedAdam(lowp, lr=1e-3)
+    ropt = torch.optim.Adam(ref, lr=1e-3)
+    for _ in range(4):
+        for p, r in zip(lowp, ref):
+            g = torch.randn_like(r)
+            p.grad = g.bfloat16()
+            r.grad = g.bfloat16().float()
+        opt.step()
+        ropt.step()
+    for p, r in zip(lowp, ref):
+        torch.testing.assert_close(opt.state[p]["master"], r.detach(), atol=1e-5, rtol=1e-4)
+        torch.testing.assert_close(p.detach(), r.detach().bfloat16(), atol=0, rtol=0)
+
+
+def test_fused_adam_channels_last_params_take_native_path():
+    from hyperion.models import resnet18
+    from hyperion.ops import FusedAdam
+
+    m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    opt = FusedAdam(m.parameters())
+    x = torch.randn(2, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    m(x).sum().backward()
+    opt.step()
+    assert opt._tables._tables, "channels-last params must use the multi-tensor kernel"
