@@ -22,6 +22,8 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kStatsBlocks = 512;  // partial rows per reduction: keeps the combine pass short
+constexpr int kFinCh = 8;          // finalize block: 8 channels x 32 partial-row groups
+constexpr int kFinGr = 32;
 
 struct BnGeom {
   int tpr;   // threads per row (each owns 8 channels)
@@ -43,7 +45,12 @@ bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g) {
     g.gy = cv / kBlock;
   }
   g.rpi = kBlock / g.tpr;
-  int64_t want = (M + (int64_t)g.rpi * 4 - 1) / ((int64_t)g.rpi * 4);  // >= 4 row iterations/thread
+  // >= 4 row iterations per thread, and >= 16K elements per block so partial rows stay a tiny
+  // fraction of the data (the combine pass reads P*C partials)
+  int64_t min_rows = (int64_t)g.rpi * 4;
+  const int64_t by_size = (16384 + C - 1) / C;
+  if (max_blocks <= kStatsBlocks && by_size > min_rows) min_rows = by_size;
+  int64_t want = (M + min_rows - 1) / min_rows;
   int64_t cap = max_blocks / g.gy;
   if (cap < 1) cap = 1;
   int64_t P = want < cap ? want : cap;
@@ -121,14 +128,14 @@ __device__ __forceinline__ void combine_partials(const float* __restrict__ pa, c
 #pragma unroll
   for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.f;
   int p = threadIdx.y;
-  for (; p + 16 * 7 < P; p += 16 * 8) {
+  for (; p + kFinGr * 7 < P; p += kFinGr * 8) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      sa[i] += pa[(int64_t)(p + 16 * i) * C + c];
-      sb[i] += pb[(int64_t)(p + 16 * i) * C + c];
+      sa[i] += pa[(int64_t)(p + kFinGr * i) * C + c];
+      sb[i] += pb[(int64_t)(p + kFinGr * i) * C + c];
     }
   }
-  for (; p < P; p += 16) {
+  for (; p < P; p += kFinGr) {
     sa[0] += pa[(int64_t)p * C + c];
     sb[0] += pb[(int64_t)p * C + c];
   }
@@ -136,16 +143,16 @@ __device__ __forceinline__ void combine_partials(const float* __restrict__ pa, c
   b = ((sb[0] + sb[1]) + (sb[2] + sb[3])) + ((sb[4] + sb[5]) + (sb[6] + sb[7]));
 }
 
-// grid: ceil(C/64); block (64, 16)
-__global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restrict__ psum, const float* __restrict__ psq,
+// grid: ceil(C/8); block (8, 32)
+__global__ __launch_bounds__(256) void bn_stats_finalize_k(const float* __restrict__ psum, const float* __restrict__ psq,
                                                             int P, int C, int64_t M, const float* __restrict__ weight,
                                                             const float* __restrict__ bias, float* running_mean,
                                                             float* running_var, float momentum, float eps,
                                                             float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                                             float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ float red_s[16][64];
-  __shared__ float red_q[16][64];
-  const int c = blockIdx.x * 64 + threadIdx.x;
+  __shared__ float red_s[kFinGr][kFinCh];
+  __shared__ float red_q[kFinGr][kFinCh];
+  const int c = blockIdx.x * kFinCh + threadIdx.x;
   float a = 0.f, b = 0.f;
   if (c < C) combine_partials(psum, psq, P, C, c, a, b);
   red_s[threadIdx.y][threadIdx.x] = a;
@@ -153,7 +160,7 @@ __global__ __launch_bounds__(1024) void bn_stats_finalize_k(const float* __restr
   __syncthreads();
   if (threadIdx.y == 0 && c < C) {
     double da = a, db = b;
-    for (int i = 1; i < 16; ++i) {
+    for (int i = 1; i < kFinGr; ++i) {
       da += red_s[i][threadIdx.x];
       db += red_q[i][threadIdx.x];
     }
@@ -327,16 +334,16 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ pdz, const float* __restrict__ pdzx,
+__global__ __launch_bounds__(256) void bn_bwd_finalize_k(const float* __restrict__ pdz, const float* __restrict__ pdzx,
                                                           int P, int C, int64_t M, const float* __restrict__ weight,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, int training,
                                                           float* __restrict__ dweight, float* __restrict__ dbias,
                                                           float* __restrict__ kA, float* __restrict__ kB,
                                                           float* __restrict__ kC) {
-  __shared__ float red_s[16][64];
-  __shared__ float red_q[16][64];
-  const int c = blockIdx.x * 64 + threadIdx.x;
+  __shared__ float red_s[kFinGr][kFinCh];
+  __shared__ float red_q[kFinGr][kFinCh];
+  const int c = blockIdx.x * kFinCh + threadIdx.x;
   float a = 0.f, b = 0.f;
   if (c < C) combine_partials(pdz, pdzx, P, C, c, a, b);
   red_s[threadIdx.y][threadIdx.x] = a;
@@ -344,7 +351,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restric
   __syncthreads();
   if (threadIdx.y == 0 && c < C) {
     double da = a, db = b;
-    for (int i = 1; i < 16; ++i) {
+    for (int i = 1; i < kFinGr; ++i) {
       da += red_s[i][threadIdx.x];
       db += red_q[i][threadIdx.x];
     }
@@ -427,7 +434,7 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
     if (training) {
       hipLaunchKernelGGL(bn_stats_partial_k<T>, dim3(gs.P, gs.gy), dim3(kBlock), 0, stream, xt, M, C, gs.tpr, gs.rpi,
                          gs.rows_per_block, psum, psq);
-      hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + 63) / 64), dim3(64, 16), 0, stream, psum, psq, gs.P, C, M,
+      hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum, psq, gs.P, C, M,
                          weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
     } else {
       hipLaunchKernelGGL(bn_eval_consts_k, dim3((C + 255) / 256), dim3(256), 0, stream, C, weight, bias, running_mean,
@@ -469,7 +476,7 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
     else
       hipLaunchKernelGGL((bn_bwd_reduce_k<T, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr, gs.rpi,
                          gs.rows_per_block, pdz, pdzx);
-    hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(64, 16), 0, stream, pdz, pdzx, gs.P, C, M, weight,
+    hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, pdz, pdzx, gs.P, C, M, weight,
                        save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
     const dim3 gra(ga.P, ga.gy);
     T* dxt = static_cast<T*>(dx);

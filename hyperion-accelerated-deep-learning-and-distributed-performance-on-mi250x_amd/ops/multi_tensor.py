@@ -12,6 +12,18 @@ import torch
 
 CHUNK = 8192  # elements per block (multiple of 4 for the float4 body)
 
+_PENDING: List = []  # tables created during hipGraph capture, waiting for their contents
+
+
+def flush_pending() -> int:
+    """Fill the device tables created during a capture (call after capture, before replay)."""
+    n = len(_PENDING)
+    while _PENDING:
+        dev_t, host = _PENDING.pop()
+        for d, h in zip(dev_t, host):
+            d.copy_(h)
+    return n
+
 
 class MultiTensorTable:
     def __init__(self, groups: Sequence[Sequence[torch.Tensor]], chunk: int = CHUNK):
@@ -39,12 +51,11 @@ class MultiTensorTable:
             torch.tensor(blocks, dtype=torch.int32).view(-1, 2),
         ]
         if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-            # inside hipGraph capture: copy from pinned host memory (a memcpy node that replays the
-            # same bytes); keep the pinned tensors alive as long as the table
-            self._pinned = [h.pin_memory() for h in host]
+            # inside hipGraph capture no host->device copy may be recorded (pinned allocation is
+            # refused too): allocate the device tables now and fill them right after capture ends
+            # (flush_pending); the captured kernels read the tables at replay time.
             dev_t = [torch.empty_like(h, device=dev) for h in host]
-            for d, h in zip(dev_t, self._pinned):
-                d.copy_(h, non_blocking=True)
+            _PENDING.append((dev_t, host))
         else:
             dev_t = [h.to(dev) for h in host]
         self.ptrs, self.sizes, self.blocks = dev_t

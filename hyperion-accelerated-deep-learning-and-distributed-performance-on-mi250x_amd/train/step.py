@@ -16,6 +16,8 @@ from typing import Callable, Optional
 import torch
 import torch.nn as nn
 
+from ..ops.multi_tensor import flush_pending
+
 
 def autocast_ctx(device: torch.device, dtype: Optional[torch.dtype]):
     if dtype is None or dtype == torch.float32:
@@ -81,6 +83,7 @@ class TrainStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.static_loss = self._body(self.static_x, self.static_y)
+        flush_pending()  # multi-tensor pointer tables built during capture
         torch.cuda.synchronize()
         self.graph = g
 

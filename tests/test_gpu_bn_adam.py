@@ -120,22 +120,22 @@ def test_resnet50_native_step_runs_and_matches_torch_path():
     torch.manual_seed(0)
     m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
     m2 = copy.deepcopy(m)
-    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        out = m(x)
-    out.float().sum().backward()
+    x = torch.randn(8, 3, 96, 96, device="cuda").contiguous(memory_format=torch.channels_last)
+    out = m(x)  # fp32 end to end: fused BN kernels vs torch BN/add/relu
+    out.sum().backward()
     os.environ["HYPERION_KERNELS"] = "torch"
     try:
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            out2 = m2(x)
-        out2.float().sum().backward()
+        out2 = m2(x)
+        out2.sum().backward()
     finally:
         os.environ.pop("HYPERION_KERNELS", None)
-    torch.testing.assert_close(out.float(), out2.float(), atol=0.15, rtol=0.1)
-    g1 = m.conv1.weight.grad.float()
-    g2 = m2.conv1.weight.grad.float()
-    cos = F.cosine_similarity(g1.flatten(), g2.flatten(), dim=0)
-    assert cos > 0.98, cos
+    torch.testing.assert_close(out, out2, atol=2e-3, rtol=2e-3)
+    for (n1, p1), (_, p2) in zip(m.named_parameters(), m2.named_parameters()):
+        cos = F.cosine_similarity(p1.grad.flatten().double(), p2.grad.flatten().double(), dim=0)
+        assert cos > 0.999, (n1, float(cos))
+    for (n1, b1), (_, b2) in zip(m.named_buffers(), m2.named_buffers()):
+        if b1.is_floating_point():
+            torch.testing.assert_close(b1, b2, atol=1e-4, rtol=1e-3)
 
 
 def test_fused_adam_master_weights_bf16():
