@@ -1,0 +1,40 @@
+// Torch bindings: fused softmax cross-entropy (forward + in-place backward).
+#include "bindings/common.h"
+#include "bindings/registry.h"
+
+namespace hypbind {
+namespace {
+
+// logits [N, V] (row stride ld >= V, unit column stride) is overwritten with dlogits when
+// write_grad.  Returns (loss_rows [N] fp32, lse [N] fp32).
+std::vector<at::Tensor> ce_fwd_bwd(at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& scale,
+                                   double scale_mul, int64_t ignore_index, bool write_grad) {
+  HYP_CHECK_CUDA_TENSOR(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "ce_fwd_bwd: logits must be [N, V] with unit column stride");
+  TORCH_CHECK(target.dim() == 1 && target.size(0) == logits.size(0) && target.scalar_type() == at::kLong &&
+                  target.is_contiguous() && target.device() == logits.device(),
+              "ce_fwd_bwd: target must be a contiguous int64 [N] on the logits device");
+  if (scale.has_value() && scale->defined())
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->device() == logits.device(),
+                "ce_fwd_bwd: scale must be a 1-element fp32 device tensor");
+  TORCH_CHECK(logits.size(1) < (int64_t)INT32_MAX, "ce_fwd_bwd: V too large");
+  const at::DeviceGuard guard(logits.device());
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({logits.size(0)}, fopt);
+  auto lse = at::empty({logits.size(0)}, fopt);
+  HYP_CHECK_HIP(hyp::cross_entropy_fwd_bwd(dtype_code(logits), logits.data_ptr(), logits.size(0), (int)logits.size(1),
+                                           logits.stride(0), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                           lse.data_ptr<float>(), ptr_or_null<float>(scale), (float)scale_mul,
+                                           ignore_index, write_grad ? 1 : 0, cur_stream()));
+  return {loss, lse};
+}
+
+}  // namespace
+
+void register_loss_ops(pybind11::module& m) {
+  m.def("ce_fwd_bwd", &ce_fwd_bwd, "in-place softmax cross-entropy forward+backward", pybind11::arg("logits"),
+        pybind11::arg("target"), pybind11::arg("scale"), pybind11::arg("scale_mul"), pybind11::arg("ignore_index"),
+        pybind11::arg("write_grad"));
+}
+
+}  // namespace hypbind

@@ -8,4 +8,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("arch") = "gfx950";
   hypbind::register_norm_ops(m);
   hypbind::register_attn_ops(m);
+  hypbind::register_loss_ops(m);
+  hypbind::register_llama_ops(m);
 }

@@ -78,3 +78,25 @@ bool attention_supported(int dtype, int D);
 hipError_t attention_forward(int dtype, const AttnParams& p, hipStream_t st);
 hipError_t attention_backward(int dtype, const AttnBwdParams& p, hipStream_t st);
 }  // namespace hyp
+
+namespace hyp {
+// ---- cross_entropy.hip -----------------------------------------------------------------------
+// In-place softmax-CE fwd+bwd over [rows, V] logits with leading dimension ld (elements).
+// loss_rows[r] = lse - z[target] (0 for ignored rows); if write_grad, z <- (softmax - onehot) *
+// (*scale_ptr) * scale_mul (rows with an ignored target get 0).
+hipError_t cross_entropy_fwd_bwd(int dtype, void* logits, int64_t rows, int V, int64_t ld, const int64_t* target,
+                                 float* loss_rows, float* lse, const float* scale_ptr, float scale_mul,
+                                 int64_t ignore_index, int write_grad, hipStream_t st);
+}  // namespace hyp
+
+namespace hyp {
+// ---- rope_swiglu.hip -------------------------------------------------------------------------
+// q [tokens, Hq, D], k [tokens, Hk, D] with token / head strides in elements (unit stride in D);
+// pos: int64 [tokens] or null (position = token % S).  inverse=1 rotates by -angle (backward).
+hipError_t rope_apply(int dtype, const void* q, const void* k, void* qo, void* ko, int64_t tokens, int S, int Hq,
+                      int Hk, int D, int64_t q_tok, int64_t k_tok, int64_t q_head, int64_t k_head, const int64_t* pos,
+                      float theta, int inverse, hipStream_t st);
+hipError_t swiglu_forward(int dtype, const void* g, const void* u, void* h, int64_t n, hipStream_t st);
+hipError_t swiglu_backward(int dtype, const void* dh, const void* g, const void* u, void* dg, void* du, int64_t n,
+                           hipStream_t st);
+}  // namespace hyp

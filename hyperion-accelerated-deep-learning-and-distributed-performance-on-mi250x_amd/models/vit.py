@@ -1,0 +1,189 @@
+"""ViT-B/16 (torchvision-key compatible) and the reference's fallback CNN.
+
+Reference: ``create_vit_model()`` tried torchvision ``vit_b_16(pretrained=False)`` and, because
+torchvision lacked it on that install, fell back to a 5-layer CNN — the "Vision Transformer"
+row of the README (5.44 ms, batch 32) is that CNN (``Phase 1/baseline_performance.ipynb:207-236``,
+fallback proof :28-29).  Hyperion provides both, so one comparison is
+like-for-like (``fallback_cnn``) and the other is the real model (``vit_b_16``).
+
+ViT design for MI355X: pre-norm blocks whose residual adds are fused into the next LayerNorm
+(``layer_norm(..., residual=r, return_sum=True)`` returns both ``LN(x + r)`` and ``x + r`` in one
+pass), packed-QKV flash attention on ``[B, 197, 3, 12, 64]`` without permutes, GELU in the FC1
+GEMM epilogue.  ``use_checkpoint=True`` recomputes each encoder block in backward (the
+BASELINE.json "ViT-Base bf16 + activation checkpointing" config).  State-dict keys equal
+torchvision's (``conv_proj``, ``class_token``, ``encoder.pos_embedding``,
+``encoder.layers.encoder_layer_N.{ln_1,self_attention,ln_2,mlp.0,mlp.3}``, ``encoder.ln``,
+``heads.head``).
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+from torch.utils.checkpoint import checkpoint
+
+from ..ops.layernorm import LayerNorm, layer_norm
+from .transformer import MultiheadSelfAttention, _ffn_up
+
+
+class MLPBlock(nn.Sequential):
+    """torchvision ``MLPBlock`` layout: ``0`` Linear, ``1`` GELU, ``2`` Dropout, ``3`` Linear, ``4`` Dropout."""
+
+    def __init__(self, dim: int, hidden: int, dropout: float = 0.0):
+        super().__init__(nn.Linear(dim, hidden), nn.GELU(), nn.Dropout(dropout), nn.Linear(hidden, dim),
+                         nn.Dropout(dropout))
+        for m in (self[0], self[3]):
+            nn.init.xavier_uniform_(m.weight)
+            nn.init.normal_(m.bias, std=1e-6)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
+        h = _ffn_up(x, self[0].weight, self[0].bias, "gelu")
+        return self[4](self[3](self[2](h)))
+
+
+class EncoderBlock(nn.Module):
+    def __init__(self, num_heads: int, hidden_dim: int, mlp_dim: int, dropout: float = 0.0,
+                 attention_dropout: float = 0.0):
+        super().__init__()
+        self.num_heads = num_heads
+        self.ln_1 = LayerNorm(hidden_dim, eps=1e-6)
+        self.self_attention = MultiheadSelfAttention(hidden_dim, num_heads, dropout=attention_dropout)
+        self.dropout = nn.Dropout(dropout)
+        self.ln_2 = LayerNorm(hidden_dim, eps=1e-6)
+        self.mlp = MLPBlock(hidden_dim, mlp_dim, dropout)
+
+    def fused_forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One block on the residual stream.
+
+        Input ``stream + delta`` is the block input (``delta`` = previous block's MLP output, not yet
+        added).  Returns ``(mlp_out, new_stream)`` with ``new_stream + mlp_out`` = block output.
+        """
+        if delta is None:
+            h, s = self.ln_1(stream), stream
+        else:
+            h, s = layer_norm(delta, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps, residual=stream,
+                              return_sum=True)
+        a = self.dropout(self.self_attention(h))
+        h2, s2 = layer_norm(a, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps, residual=s, return_sum=True)
+        return self.mlp(h2), s2
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        d, s = self.fused_forward(None, x)
+        return s + d
+
+
+class Encoder(nn.Module):
+    def __init__(self, seq_length: int, num_layers: int, num_heads: int, hidden_dim: int, mlp_dim: int,
+                 dropout: float = 0.0, attention_dropout: float = 0.0, use_checkpoint: bool = False):
+        super().__init__()
+        self.pos_embedding = nn.Parameter(torch.empty(1, seq_length, hidden_dim).normal_(std=0.02))
+        self.dropout = nn.Dropout(dropout)
+        self.layers = nn.ModuleDict(
+            OrderedDict(
+                (f"encoder_layer_{i}", EncoderBlock(num_heads, hidden_dim, mlp_dim, dropout, attention_dropout))
+                for i in range(num_layers)
+            )
+        )
+        self.ln = LayerNorm(hidden_dim, eps=1e-6)
+        self.use_checkpoint = use_checkpoint
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        s = self.dropout(x + self.pos_embedding.to(x.dtype))
+        d: Optional[torch.Tensor] = None
+        ckpt = self.use_checkpoint and self.training and torch.is_grad_enabled()
+        for blk in self.layers.values():
+            if ckpt:
+                if d is None:
+                    d, s = checkpoint(blk.fused_forward, None, s, use_reentrant=False)
+                else:
+                    d, s = checkpoint(blk.fused_forward, d, s, use_reentrant=False)
+            else:
+                d, s = blk.fused_forward(d, s)
+        if d is None:
+            return self.ln(s)
+        return self.ln(d, residual=s)
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, image_size: int = 224, patch_size: int = 16, num_layers: int = 12, num_heads: int = 12,
+                 hidden_dim: int = 768, mlp_dim: int = 3072, dropout: float = 0.0, attention_dropout: float = 0.0,
+                 num_classes: int = 1000, use_checkpoint: bool = False):
+        super().__init__()
+        if image_size % patch_size:
+            raise ValueError("image size must be divisible by the patch size")
+        self.image_size = image_size
+        self.patch_size = patch_size
+        self.hidden_dim = hidden_dim
+        self.conv_proj = nn.Conv2d(3, hidden_dim, kernel_size=patch_size, stride=patch_size)
+        seq_length = (image_size // patch_size) ** 2 + 1
+        self.class_token = nn.Parameter(torch.zeros(1, 1, hidden_dim))
+        self.encoder = Encoder(seq_length, num_layers, num_heads, hidden_dim, mlp_dim, dropout, attention_dropout,
+                               use_checkpoint)
+        self.seq_length = seq_length
+        self.heads = nn.Sequential(OrderedDict(head=nn.Linear(hidden_dim, num_classes)))
+        fan_in = 3 * patch_size * patch_size
+        nn.init.trunc_normal_(self.conv_proj.weight, std=math.sqrt(1 / fan_in))
+        nn.init.zeros_(self.conv_proj.bias)
+        nn.init.zeros_(self.heads.head.weight)
+        nn.init.zeros_(self.heads.head.bias)
+
+    @property
+    def use_checkpoint(self) -> bool:
+        return self.encoder.use_checkpoint
+
+    @use_checkpoint.setter
+    def use_checkpoint(self, v: bool) -> None:
+        self.encoder.use_checkpoint = bool(v)
+
+    def _process_input(self, x: torch.Tensor) -> torch.Tensor:
+        n, c, h, w = x.shape
+        if h != self.image_size or w != self.image_size:
+            raise ValueError(f"expected {self.image_size}x{self.image_size} input, got {h}x{w}")
+        x = self.conv_proj(x)  # [n, hidden, h/p, w/p]
+        # channels-last conv output is already [n, h/p, w/p, hidden] in memory: flatten is free
+        return x.permute(0, 2, 3, 1).reshape(n, -1, self.hidden_dim)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self._process_input(x)
+        cls = self.class_token.to(x.dtype).expand(x.shape[0], -1, -1)
+        x = torch.cat([cls, x], dim=1)
+        x = self.encoder(x)
+        return self.heads(x[:, 0])
+
+
+def vit_b_16(num_classes: int = 1000, image_size: int = 224, use_checkpoint: bool = False, **kw) -> VisionTransformer:
+    """ViT-B/16: 86.6M parameters at 1000 classes."""
+    return VisionTransformer(image_size, 16, 12, 12, 768, 3072, num_classes=num_classes,
+                             use_checkpoint=use_checkpoint, **kw)
+
+
+def vit_tiny(num_classes: int = 10, image_size: int = 32, patch_size: int = 4, **kw) -> VisionTransformer:
+    """Small ViT for CPU tests."""
+    return VisionTransformer(image_size, patch_size, 2, 4, 64, 128, num_classes=num_classes, **kw)
+
+
+def fallback_cnn(num_classes: int = 1000) -> nn.Sequential:
+    """The CNN the reference actually benchmarked as "ViT" (212,328 params; keys 0/3/7)."""
+    return nn.Sequential(
+        nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3),
+        nn.ReLU(inplace=True),
+        nn.MaxPool2d(kernel_size=3, stride=2, padding=1),
+        nn.Conv2d(64, 128, kernel_size=3, padding=1),
+        nn.ReLU(inplace=True),
+        nn.MaxPool2d(kernel_size=3, stride=2, padding=1),
+        nn.AdaptiveAvgPool2d((1, 1)),
+        nn.Flatten(),
+        nn.Linear(128, num_classes),
+    )
+
+
+def create_vit_model(real: bool = False) -> nn.Module:
+    """Reference factory (``baseline_performance.ipynb:207``).
+
+    ``real=False`` (default) reproduces what the reference measured — the fallback CNN;
+    ``real=True`` returns ViT-B/16.
+    """
+    return vit_b_16() if real else fallback_cnn()

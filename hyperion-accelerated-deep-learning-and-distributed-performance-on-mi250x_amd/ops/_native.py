@@ -56,13 +56,19 @@ def native():
     return m
 
 
-def use_native(*tensors: torch.Tensor) -> bool:
+def torch_ops() -> set:
+    """Ops forced onto the PyTorch path via ``HYPERION_TORCH_OPS=bn,adam,...`` (A/B and bisection)."""
+    return {o.strip() for o in os.environ.get("HYPERION_TORCH_OPS", "").split(",") if o.strip()}
+
+
+def use_native(*tensors: torch.Tensor, op: Optional[str] = None) -> bool:
     """True when the native kernels should run for these tensors.
 
     GPU tensors + backend 'hyperion' -> native (raises if the extension is missing, unless
-    HYPERION_ALLOW_TORCH_FALLBACK=1).  CPU tensors or backend 'torch' -> reference path.
+    HYPERION_ALLOW_TORCH_FALLBACK=1).  CPU tensors, backend 'torch', or ``op`` listed in
+    ``HYPERION_TORCH_OPS`` -> reference path.
     """
-    if backend() == "torch":
+    if backend() == "torch" or (op is not None and op in torch_ops()):
         return False
     if not tensors or not all(t.is_cuda for t in tensors if t is not None):
         return False

@@ -103,7 +103,7 @@ def attention(
 ) -> torch.Tensor:
     """Self-attention on [B, S, H, D]; ``key_padding_mask`` [B, S] True = ignore that key."""
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
-    if _native.use_native(q) and q.shape == k.shape == v.shape and _native_ok(q, k, v):
+    if _native.use_native(q, op="attn") and q.shape == k.shape == v.shape and _native_ok(q, k, v):
         kpm = key_padding_mask.to(torch.uint8) if key_padding_mask is not None else None
         return _AttnFn.apply(q, k, v, causal, float(dropout_p), kpm, scale)
     return attention_reference(q, k, v, causal, dropout_p, key_padding_mask, scale)
@@ -119,7 +119,7 @@ def attention_packed(
     """Self-attention from a packed ``[B, S, 3, H, D]`` projection output; returns [B, S, H, D]."""
     scale = 1.0 / math.sqrt(qkv.shape[-1]) if scale is None else scale
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-    if _native.use_native(qkv) and _native_ok(q, k, v):
+    if _native.use_native(qkv, op="attn") and _native_ok(q, k, v):
         kpm = key_padding_mask.to(torch.uint8) if key_padding_mask is not None else None
         return _AttnPackedFn.apply(qkv, causal, float(dropout_p), kpm, scale)
     return attention_reference(q, k, v, causal, dropout_p, key_padding_mask, scale)

@@ -103,7 +103,7 @@ def bn_act(
 ) -> torch.Tensor:
     """Functional fused BN(+res)(+ReLU); dispatches to HIP when possible."""
     if (
-        _native.use_native(x)
+        _native.use_native(x, op="bn")
         and _native_ok(x)
         and (weight is None or weight.dtype == torch.float32)
         and (running_mean is None or running_mean.dtype == torch.float32)

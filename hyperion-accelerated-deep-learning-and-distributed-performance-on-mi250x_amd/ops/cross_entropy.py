@@ -1,0 +1,130 @@
+"""Fused linear + softmax cross-entropy (the LM head and its loss as one op).
+
+Reference: ``logits = fc(x)`` then ``nn.CrossEntropyLoss(ignore_index=pad)`` over V = 50257 in
+every LM trainer (``02_development/distributed_utils.py:161,175-177``, ``core_framework.ipynb:
+243-262``, ``mixed_precision.ipynb:121-145``) — the logits GEMM dominates LM compute (≈105 GFLOP
+forward at 4064 tokens) and PyTorch materialises fp32 log-softmax and its gradient.
+
+Hyperion computes the loss AND all three gradients inside the forward:
+
+1. ``z = x @ Wᵀ + b`` (one hipBLASLt GEMM; bf16 under AMP);
+2. ``ce_fwd_bwd`` (``csrc/kernels/cross_entropy.hip``) turns ``z`` into ``dz = (softmax(z) −
+   onehot) / n_valid`` in place and emits per-row losses — two passes over the logits, the
+   second served from L2;
+3. ``dx = dz @ W``, ``dW = dzᵀ @ x``, ``db = Σ dz``.
+
+Backward then only scales the saved gradients by the incoming scalar.  ``n_valid`` (non-ignored
+tokens) stays on the device, so the op has no host sync and is hipGraph-capturable.  With 288 GB
+of HBM per GPU the whole [N, V] logits block is processed at once unless it exceeds
+``max_logits_bytes`` (default 4 GiB), in which case rows are chunked and dW accumulates in fp32.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+DEFAULT_MAX_LOGITS_BYTES = 4 << 30
+
+
+def _compute_dtype(x: torch.Tensor, w: torch.Tensor) -> torch.dtype:
+    if torch.is_autocast_enabled(x.device.type):
+        return torch.get_autocast_dtype(x.device.type)
+    return x.dtype if x.dtype == w.dtype else torch.promote_types(x.dtype, w.dtype)
+
+
+def _ce_chunk_reference(z: torch.Tensor, t: torch.Tensor, scale: torch.Tensor, ignore_index: int):
+    """PyTorch oracle of the in-place kernel: returns (loss_rows, dz)."""
+    zf = z.float()
+    lse = torch.logsumexp(zf, dim=-1)
+    valid = t != ignore_index
+    tc = torch.where(valid, t, torch.zeros_like(t))
+    zt = zf.gather(1, tc[:, None]).squeeze(1)
+    loss = torch.where(valid, lse - zt, torch.zeros_like(lse))
+    p = torch.exp(zf - lse[:, None])
+    p.scatter_add_(1, tc[:, None], -torch.ones_like(zt)[:, None])
+    dz = p * (scale * valid.float())[:, None]
+    return loss, dz.to(z.dtype)
+
+
+class _FusedLinearCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, target, ignore_index, max_bytes):
+        cdt = _compute_dtype(x, weight)
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).to(cdt)
+        t = target.reshape(-1)
+        N, V = x2.shape[0], weight.shape[0]
+        w = weight.to(cdt)
+        b = bias.to(cdt) if bias is not None else None
+        n_valid = (t != ignore_index).sum().to(torch.float32).clamp_min(1.0)
+        scale = (1.0 / n_valid).reshape(1)
+        native = _native.use_native(x2, op="ce") and cdt in _native.DTYPE_CODE
+        rows = max(1, min(N, max_bytes // max(1, V * x2.element_size())))
+        dx = torch.empty_like(x2)
+        need_w = ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        dw = None
+        db = None
+        loss_sum = torch.zeros((), dtype=torch.float32, device=x.device)
+        chunked = rows < N
+        for r0 in range(0, N, rows):
+            xc, tc = x2[r0 : r0 + rows], t[r0 : r0 + rows].contiguous()
+            z = F.linear(xc, w, b)
+            if native:
+                loss_rows, _ = _native.native().ce_fwd_bwd(z, tc, scale, 1.0, int(ignore_index), True)
+                dz = z
+            else:
+                loss_rows, dz = _ce_chunk_reference(z, tc, scale, ignore_index)
+            loss_sum = loss_sum + loss_rows.sum()
+            torch.mm(dz, w, out=dx[r0 : r0 + rows])
+            if need_w:
+                g = dz.t().mm(xc)
+                if not chunked:
+                    dw = g
+                else:
+                    dw = g.float() if dw is None else dw.add_(g.float())
+            if need_b:
+                s = dz.sum(0, dtype=torch.float32)
+                db = s if db is None else db.add_(s)
+        loss = loss_sum * scale.reshape(())
+        ctx.save_for_backward(dx.view(shape), dw if dw is not None else torch.empty(0),
+                              db if db is not None else torch.empty(0))
+        ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype, need_w, need_b)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        dx, dw, db = ctx.saved_tensors
+        xdt, wdt, bdt, need_w, need_b = ctx.meta
+        gx = (dx * g.to(dx.dtype)).to(xdt) if ctx.needs_input_grad[0] else None
+        gw = (dw * g.to(dw.dtype)).to(wdt) if need_w else None
+        gb = (db * g.to(db.dtype)).to(bdt) if need_b else None
+        return gx, gw, gb, None, None, None
+
+
+def fused_linear_cross_entropy(
+    x: torch.Tensor,
+    weight: torch.Tensor,
+    bias: Optional[torch.Tensor],
+    target: torch.Tensor,
+    ignore_index: int = -100,
+    max_logits_bytes: int = DEFAULT_MAX_LOGITS_BYTES,
+) -> torch.Tensor:
+    """Mean cross-entropy of ``x @ weight.T + bias`` against ``target`` over non-ignored rows.
+
+    Equivalent to ``F.cross_entropy(F.linear(x, weight, bias).view(-1, V), target.view(-1),
+    ignore_index=ignore_index)`` without materialising fp32 log-probabilities.
+    """
+    if not torch.is_grad_enabled() or not (x.requires_grad or weight.requires_grad):
+        z = F.linear(x, weight, bias)
+        return F.cross_entropy(z.reshape(-1, z.shape[-1]).float(), target.reshape(-1), ignore_index=ignore_index)
+    return _FusedLinearCE.apply(x, weight, bias, target, int(ignore_index), int(max_logits_bytes))
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """Plain CE on materialised logits (small class counts, e.g. CIFAR's 10)."""
+    return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), target.reshape(-1), ignore_index=ignore_index)

@@ -76,7 +76,7 @@ def layer_norm(
 ) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
     d = x.shape[-1]
     native = (
-        _native.use_native(x)
+        _native.use_native(x, op="ln")
         and x.dtype in _native.DTYPE_CODE
         and _SUPPORTED_D(d)
         and (weight is None or weight.dtype == torch.float32)

@@ -1,7 +1,7 @@
 """Multi-tensor launch tables for the gfx950 multi-tensor kernels (``csrc/kernels/adam.hip``).
 
 A table is built once per set of tensor pointers and reused while the pointers stay the same
-(always, inside a captured hipGraph).  Each row of the block table is (tensor id, chunk id); one
+(always, inside a captured hipGraph — tables are built during warm-up, never during capture).  Each row of the block table is (tensor id, chunk id); one
 256-thread block processes ``chunk`` elements.
 """
 from __future__ import annotations
@@ -12,17 +12,11 @@ import torch
 
 CHUNK = 8192  # elements per block (multiple of 4 for the float4 body)
 
-_PENDING: List = []  # tables created during hipGraph capture, waiting for their contents
 
 
 def flush_pending() -> int:
-    """Fill the device tables created during a capture (call after capture, before replay)."""
-    n = len(_PENDING)
-    while _PENDING:
-        dev_t, host = _PENDING.pop()
-        for d, h in zip(dev_t, host):
-            d.copy_(h)
-    return n
+    """Kept for API compatibility: tables are never built during capture (see below)."""
+    return 0
 
 
 class MultiTensorTable:
@@ -51,13 +45,16 @@ class MultiTensorTable:
             torch.tensor(blocks, dtype=torch.int32).view(-1, 2),
         ]
         if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
-            # inside hipGraph capture no host->device copy may be recorded (pinned allocation is
-            # refused too): allocate the device tables now and fill them right after capture ends
-            # (flush_pending); the captured kernels read the tables at replay time.
-            dev_t = [torch.empty_like(h, device=dev) for h in host]
-            _PENDING.append((dev_t, host))
-        else:
-            dev_t = [h.to(dev) for h in host]
+            # A table allocated inside a hipGraph capture lives in the graph's private pool, and
+            # that pool recycles blocks freed EARLIER in the capture: on every replay the kernels
+            # that used the block before would overwrite the pointer table (illegal address).
+            # Tables must therefore exist before capture, over tensors whose addresses the
+            # captured step keeps (TrainStep keeps .grad allocated and zeroes it in place).
+            raise RuntimeError(
+                "hyperion: multi-tensor table built during hipGraph capture; tensor addresses changed "
+                "since warm-up (keep .grad allocated: zero_grad(set_to_none=False) inside the captured step)"
+            )
+        dev_t = [h.to(dev) for h in host]
         self.ptrs, self.sizes, self.blocks = dev_t
         if self.nblocks == 0:
             self.blocks = self.blocks[:0]

@@ -70,7 +70,7 @@ class FusedAdam(torch.optim.Optimizer):
         first = next((p for g in self.param_groups for p in g["params"] if p.grad is not None), None)
         if first is None:
             return loss
-        native = _native.use_native(first)
+        native = _native.use_native(first, op="adam")
         if native:
             if self._step_t is None or self._step_t.device != first.device:
                 self._step_t = torch.full((), float(self._host_step - 1), dtype=torch.float32, device=first.device)
@@ -172,7 +172,7 @@ def clip_grad_norm_(
     if not grads:
         return torch.zeros(())
     dev = grads[0].device
-    native = _native.use_native(grads[0]) and all(_dense(g) and g.dtype == grads[0].dtype for g in grads)
+    native = _native.use_native(grads[0], op="clip") and all(_dense(g) and g.dtype == grads[0].dtype for g in grads)
     if native:
         try:
             tab = _clip_tables.get("clip", [grads])

@@ -81,7 +81,7 @@ class LossScaler:
         for g in grads:
             by_dtype.setdefault(g.dtype, []).append(g)
         for dt, gs in by_dtype.items():
-            if _native.use_native(gs[0]) and all(g.is_contiguous() or g.dim() == 4 for g in gs):
+            if _native.use_native(gs[0], op="unscale") and all(g.is_contiguous() or g.dim() == 4 for g in gs):
                 try:
                     tab = self._tables.get(f"unscale_{dt}", [gs])
                     _native.native().unscale_mt(tab.ptrs, tab.sizes, tab.blocks, tab.chunk, self.inv_scale_t,

@@ -16,7 +16,6 @@ from typing import Callable, Optional
 import torch
 import torch.nn as nn
 
-from ..ops.multi_tensor import flush_pending
 
 
 def autocast_ctx(device: torch.device, dtype: Optional[torch.dtype]):
@@ -50,7 +49,9 @@ class TrainStep:
         self.static_y: Optional[torch.Tensor] = None
         self.static_loss: Optional[torch.Tensor] = None
 
-    def _body(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def _body(self, x: torch.Tensor, y: torch.Tensor, zero_in_place: bool = False) -> torch.Tensor:
+        if zero_in_place:  # graph mode: gradients keep their addresses, zeroed by a captured memset
+            self.opt.zero_grad(set_to_none=False)
         dev = x.device
         with autocast_ctx(dev, self.amp_dtype):
             out = self.model(x)
@@ -69,21 +70,25 @@ class TrainStep:
         return self._body(x, y)
 
     def _capture(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        """Warm up on a side stream, then capture one step.
+
+        Gradients allocated by the warm-up steps are KEPT (zeroed in place inside the captured
+        step): their addresses are baked into the fused optimizer's multi-tensor tables, which
+        are built during warm-up.  Nothing inside the capture allocates a table.
+        """
         self.static_x = x.clone()
         self.static_y = y.clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
+            self.opt.zero_grad(set_to_none=True)
             for _ in range(self.warmup_iters):
-                self.opt.zero_grad(set_to_none=True)
-                self._body(self.static_x, self.static_y)
+                self._body(self.static_x, self.static_y, zero_in_place=True)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self.opt.zero_grad(set_to_none=True)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.static_loss = self._body(self.static_x, self.static_y)
-        flush_pending()  # multi-tensor pointer tables built during capture
+            self.static_loss = self._body(self.static_x, self.static_y, zero_in_place=True)
         torch.cuda.synchronize()
         self.graph = g
 

@@ -157,7 +157,9 @@ def test_fused_adam_master_weights_bf16():
         ropt.step()
     for p, r in zip(lowp, ref):
         torch.testing.assert_close(opt.state[p]["master"], r.detach(), atol=1e-5, rtol=1e-4)
-        torch.testing.assert_close(p.detach(), r.detach().bfloat16(), atol=0, rtol=0)
+        # the compute copy is exactly the rounded master (the master itself may differ from the
+        # torch fp32 trajectory by an ulp, which can flip a bf16 rounding: compare to the master)
+        torch.testing.assert_close(p.detach(), opt.state[p]["master"].bfloat16(), atol=0, rtol=0)
 
 
 def test_fused_adam_channels_last_params_take_native_path():

@@ -1,0 +1,125 @@
+"""GPU numerics of the LM kernels against plain PyTorch fp32 references.
+
+fused linear+CE (cross_entropy.hip), RoPE + SwiGLU (rope_swiglu.hip).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("V", [50257, 1000, 32000])
+def test_fused_linear_ce_matches_fp32_reference(dtype, V):
+    from hyperion.ops.cross_entropy import fused_linear_cross_entropy
+
+    torch.manual_seed(0)
+    N, E, pad = 300, 256, V - 1
+    x = (torch.randn(N, E, device="cuda") * 0.5).to(dtype).requires_grad_(True)
+    w = (torch.randn(V, E, device="cuda") * 0.05).to(dtype).requires_grad_(True)
+    b = (torch.randn(V, device="cuda") * 0.1).to(dtype).requires_grad_(True)
+    t = torch.randint(0, V, (N,), device="cuda")
+    t[::7] = pad  # ignored rows
+    loss = fused_linear_cross_entropy(x, w, b, t, ignore_index=pad)
+    loss.backward()
+    xr, wr, br = (a.detach().float().requires_grad_(True) for a in (x, w, b))
+    ref = F.cross_entropy(F.linear(xr, wr, br), t, ignore_index=pad)
+    ref.backward()
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(loss.float(), ref, **tol)
+    gt = dict(rtol=1e-3, atol=1e-5) if dtype == torch.float32 else dict(rtol=5e-2, atol=3e-3)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **gt)
+    torch.testing.assert_close(w.grad.float(), wr.grad, **gt)
+    torch.testing.assert_close(b.grad.float(), br.grad, **gt)
+
+
+def test_fused_linear_ce_chunked_equals_unchunked():
+    from hyperion.ops.cross_entropy import fused_linear_cross_entropy
+
+    torch.manual_seed(1)
+    x = torch.randn(257, 64, device="cuda", requires_grad=True)
+    w = torch.randn(999, 64, device="cuda", requires_grad=True)
+    t = torch.randint(0, 999, (257,), device="cuda")
+    l1 = fused_linear_cross_entropy(x, w, None, t)
+    g1 = torch.autograd.grad(l1, (x, w))
+    l2 = fused_linear_cross_entropy(x, w, None, t, max_logits_bytes=999 * 4 * 50)  # 50-row chunks
+    g2 = torch.autograd.grad(l2, (x, w))
+    torch.testing.assert_close(l1, l2)
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("D", [64, 128])
+def test_rope_matches_reference(dtype, D):
+    from hyperion.ops.rope import apply_rope, rope_reference
+
+    torch.manual_seed(0)
+    B, S, H = 2, 77, 4
+    q = torch.randn(B, S, H, D, device="cuda", dtype=dtype, requires_grad=True)
+    k = torch.randn(B, S, H, D, device="cuda", dtype=dtype, requires_grad=True)
+    qo, ko = apply_rope(q, k, None, 10000.0)
+    qr, kr = (a.detach().float().requires_grad_(True) for a in (q, k))
+    qro, kro = rope_reference(qr, kr, None, 10000.0)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(qo.float(), qro, **tol)
+    torch.testing.assert_close(ko.float(), kro, **tol)
+    gq, gk = torch.randn_like(qo), torch.randn_like(ko)
+    (qo * gq).sum().add((ko * gk).sum()).backward()
+    (qro * gq.float()).sum().add((kro * gk.float()).sum()).backward()
+    torch.testing.assert_close(q.grad.float(), qr.grad, **tol)
+    torch.testing.assert_close(k.grad.float(), kr.grad, **tol)
+
+
+def test_rope_positions_argument():
+    from hyperion.ops.rope import apply_rope, rope_reference
+
+    q = torch.randn(1, 8, 2, 64, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(1, 8, 2, 64, device="cuda", dtype=torch.bfloat16)
+    pos = torch.tensor([[5, 6, 7, 8, 100, 200, 300, 4000]], device="cuda")
+    qo, ko = apply_rope(q, k, pos)
+    qr, kr = rope_reference(q.float(), k.float(), pos)
+    torch.testing.assert_close(qo.float(), qr, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_swiglu_matches_reference(dtype):
+    from hyperion.ops.swiglu import swiglu
+
+    torch.manual_seed(0)
+    g = torch.randn(33, 344, device="cuda", dtype=dtype, requires_grad=True)
+    u = torch.randn(33, 344, device="cuda", dtype=dtype, requires_grad=True)
+    h = swiglu(g, u)
+    gr, ur = (a.detach().float().requires_grad_(True) for a in (g, u))
+    hr = F.silu(gr) * ur
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(h.float(), hr, **tol)
+    dh = torch.randn_like(h)
+    h.backward(dh)
+    hr.backward(dh.float())
+    torch.testing.assert_close(g.grad.float(), gr.grad, **tol)
+    torch.testing.assert_close(u.grad.float(), ur.grad, **tol)
+
+
+def test_llama_tiny_native_matches_torch_path(monkeypatch):
+    from hyperion.models.llama import LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    cfg = LlamaConfig.tiny(hidden_size=256, num_attention_heads=2, intermediate_size=512)
+    m = LlamaForCausalLM(cfg).cuda().to(torch.bfloat16)
+    ids = torch.randint(0, cfg.vocab_size, (2, 64), device="cuda")
+    mask = torch.ones_like(ids)
+    mask[1, 50:] = 0
+    labels = ids.masked_fill(mask == 0, -100)
+    out = m(ids, attention_mask=mask, labels=labels)
+    out.loss.backward()
+    g_native = [p.grad.float().clone() for p in m.parameters()]
+    m.zero_grad(set_to_none=True)
+    monkeypatch.setenv("HYPERION_KERNELS", "torch")
+    ref = m(ids, attention_mask=mask, labels=labels)
+    ref.loss.backward()
+    torch.testing.assert_close(out.loss.float(), ref.loss.float(), rtol=2e-2, atol=2e-2)
+    for a, p in zip(g_native, m.parameters()):
+        b = p.grad.float()
+        assert (a - b).norm() <= 0.1 * b.norm() + 1e-3
