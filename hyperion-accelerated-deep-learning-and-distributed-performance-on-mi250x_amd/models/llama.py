@@ -27,7 +27,7 @@ import torch.nn as nn
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.attention import attention
-from ..ops.cross_entropy import fused_linear_cross_entropy
+from ..ops.cross_entropy import LinearCrossEntropy
 from ..ops.layernorm import RMSNorm
 from ..ops.rope import apply_rope
 from ..ops.swiglu import swiglu
@@ -162,7 +162,7 @@ class LlamaForCausalLM(nn.Module):
         super().__init__()
         self.config = cfg or LlamaConfig()
         self.model = LlamaModel(self.config)
-        self.lm_head = nn.Linear(self.config.hidden_size, self.config.vocab_size, bias=False)
+        self.lm_head = LinearCrossEntropy(self.config.hidden_size, self.config.vocab_size, bias=False)
         self.apply(self._init_weights)
 
     def _init_weights(self, m: nn.Module) -> None:
@@ -183,7 +183,7 @@ class LlamaForCausalLM(nn.Module):
             # HF semantics: predict labels[:, 1:] from positions [:, :-1]; -100 is ignored
             hs = h[:, :-1]
             tgt = labels[:, 1:].contiguous()
-            out["loss"] = fused_linear_cross_entropy(hs, self.lm_head.weight, None, tgt, ignore_index=-100)
+            out["loss"] = self.lm_head(hs, target=tgt, ignore_index=-100)
         if return_logits or (return_logits is None and labels is None):
             out["logits"] = self.lm_head(h)
         return out

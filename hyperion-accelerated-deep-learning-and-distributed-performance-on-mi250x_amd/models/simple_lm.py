@@ -26,7 +26,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from ..ops.cross_entropy import fused_linear_cross_entropy
+from ..ops.cross_entropy import LinearCrossEntropy
 from .transformer import encoder
 
 GPT2_VOCAB = 50257
@@ -59,7 +59,7 @@ class SimpleTransformerLM(nn.Module):
         setattr(self, self._emb_name, nn.Embedding(vocab_size, emb_dim))
         setattr(self, self._enc_name, encoder(emb_dim, n_heads, n_layers, ff_dim, dropout, activation,
                                               use_checkpoint=use_checkpoint))
-        self.fc = nn.Linear(emb_dim, vocab_size)
+        self.fc = LinearCrossEntropy(emb_dim, vocab_size)
         self.vocab_size = vocab_size
         self.max_len = max_len
         self.causal = causal
@@ -88,7 +88,7 @@ class SimpleTransformerLM(nn.Module):
                      attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Mean next-token CE (ignore pads) with the LM head fused into the loss."""
         h = self.hidden(ids, attention_mask)
-        return fused_linear_cross_entropy(h, self.fc.weight, self.fc.bias, targets, ignore_index=ignore_index)
+        return self.fc(h, target=targets, ignore_index=ignore_index)
 
 
 def simple_lm_256(vocab_size: int = GPT2_VOCAB, **kw) -> SimpleTransformerLM:

@@ -128,3 +128,17 @@ def fused_linear_cross_entropy(
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
     """Plain CE on materialised logits (small class counts, e.g. CIFAR's 10)."""
     return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), target.reshape(-1), ignore_index=ignore_index)
+
+
+class LinearCrossEntropy(torch.nn.Linear):
+    """``nn.Linear`` (same keys) whose call with ``target=`` returns the fused mean CE loss.
+
+    Running the head through ``__call__`` (instead of reading ``.weight`` from outside) keeps
+    module hooks — FSDP's parameter gather, activation checkpointing — working on the LM head.
+    """
+
+    def forward(self, x: torch.Tensor, target: Optional[torch.Tensor] = None,  # type: ignore[override]
+                ignore_index: int = -100) -> torch.Tensor:
+        if target is None:
+            return F.linear(x, self.weight, self.bias)
+        return fused_linear_cross_entropy(x, self.weight, self.bias, target, ignore_index=ignore_index)

@@ -1,0 +1,129 @@
+"""FSDP (flat-param FULL_SHARD) on gloo: parity with single-process training, state dicts, LoRA-frozen."""
+import copy
+
+import pytest
+import torch
+
+from dist_utils import run_world
+
+
+def _make_model(seed=0):
+    from hyperion.models.simple_lm import simple_lm_256
+
+    torch.manual_seed(seed)
+    return simple_lm_256(vocab_size=64, emb_dim=32, n_heads=2, n_layers=2, ff_dim=48, dropout=0.0)
+
+
+def _batch(step, n=8):
+    g = torch.Generator().manual_seed(100 + step)
+    ids = torch.randint(0, 64, (n, 9), generator=g)
+    return ids[:, :-1], ids[:, 1:]
+
+
+def _reference_train(steps, lr=1e-2, clip=None):
+    m = _make_model()
+    # SGD keeps the comparison strict: Adam would turn the (exactly zero in exact arithmetic) key-bias
+    # gradient's rounding noise into +-lr steps that depend on the summation order across ranks
+    opt = torch.optim.SGD(m.parameters(), lr=lr * 10, momentum=0.9, weight_decay=0.01)
+    for s in range(steps):
+        x, y = _batch(s)
+        loss = m.forward_loss(x, y, ignore_index=-100)
+        loss.backward()
+        if clip is not None:
+            torch.nn.utils.clip_grad_norm_(m.parameters(), clip)
+        opt.step()
+        opt.zero_grad()
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def _fsdp_train(rank, world, steps, policy_kind, clip, strategy):
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.parallel.fsdp import FSDP, size_based_auto_wrap_policy, transformer_auto_wrap_policy
+
+    policy = {"layer": transformer_auto_wrap_policy({TransformerEncoderLayer}),
+              "size": size_based_auto_wrap_policy(2000), "none": None}[policy_kind]
+    m = FSDP(_make_model(), auto_wrap_policy=policy, device_id=torch.device("cpu"), sharding_strategy=strategy)
+    opt = torch.optim.SGD(m.parameters(), lr=1e-1, momentum=0.9, weight_decay=0.01)
+    per = 8 // world
+    for s in range(steps):
+        x, y = _batch(s)
+        x, y = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
+        loss = m.forward_loss(x, y, ignore_index=-100)
+        loss.backward()
+        if clip is not None:
+            m.clip_grad_norm_(clip)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    sd = m.full_state_dict(rank0_only=True)
+    return {"sd": sd, "units": m.unit_sizes()}
+
+
+@pytest.mark.parametrize("policy", ["layer", "size", "none"])
+@pytest.mark.parametrize("strategy", ["FULL_SHARD", "SHARD_GRAD_OP"])
+def test_fsdp_matches_single_process(policy, strategy):
+    ref = _reference_train(3)
+    res = run_world(_fsdp_train, 2, (3, policy, None, strategy))
+    sd = res[0]["sd"]
+    assert res[1]["sd"] == {}
+    assert set(sd) == set(ref)
+    for k in ref:
+        torch.testing.assert_close(sd[k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
+    if policy == "layer":
+        assert len(res[0]["units"]) == 3  # 2 encoder layers + root (embed, fc)
+
+
+def test_fsdp_global_grad_clip_matches_single_process():
+    ref = _reference_train(3, clip=0.05)
+    res = run_world(_fsdp_train, 2, (3, "layer", 0.05, "FULL_SHARD"))
+    for k in ref:
+        torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def _sharded_roundtrip(rank, world, tmp):
+    from hyperion.parallel.fsdp import FSDP, size_based_auto_wrap_policy
+
+    m = FSDP(_make_model(), auto_wrap_policy=size_based_auto_wrap_policy(2000), device_id=torch.device("cpu"))
+    sd = m.sharded_state_dict()
+    torch.save(sd, f"{tmp}/shard{rank}.pt")
+    m2 = FSDP(_make_model(seed=5), auto_wrap_policy=size_based_auto_wrap_policy(2000), device_id=torch.device("cpu"))
+    m2.load_sharded_state_dict(torch.load(f"{tmp}/shard{rank}.pt", weights_only=True))
+    a = m.full_state_dict(rank0_only=False)
+    b = m2.full_state_dict(rank0_only=False)
+    # full -> load_full round trip as well
+    m3 = FSDP(_make_model(seed=9), device_id=torch.device("cpu"))
+    m3.load_full_state_dict(a)
+    c = m3.full_state_dict(rank0_only=False)
+    return all(torch.equal(a[k], b[k]) and torch.equal(a[k], c[k]) for k in a)
+
+
+def test_fsdp_sharded_and_full_state_dict_roundtrip(tmp_path):
+    res = run_world(_sharded_roundtrip, 2, (str(tmp_path),))
+    assert res[0] and res[1]
+
+
+def _frozen_train(rank, world):
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.parallel.fsdp import FSDP, transformer_auto_wrap_policy
+
+    m0 = _make_model()
+    for n, p in m0.named_parameters():
+        if "linear1" not in n:
+            p.requires_grad_(False)
+    before = {k: v.clone() for k, v in m0.state_dict().items()}
+    m = FSDP(m0, auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}), device_id=torch.device("cpu"))
+    n_opt = sum(p.numel() for p in m.parameters())
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-2)
+    x, y = _batch(0)
+    m.forward_loss(x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4], ignore_index=-100).backward()
+    opt.step()
+    sd = m.full_state_dict(rank0_only=False)
+    changed = {k for k in sd if not torch.equal(sd[k], before[k])}
+    return n_opt, changed
+
+
+def test_fsdp_frozen_params_not_sharded_into_optimizer():
+    res = run_world(_frozen_train, 2)
+    n_opt, changed = res[0]
+    # only linear1 (2 layers x (32*48 + 48)) is trainable; padded to a multiple of 2 per unit, sharded
+    assert n_opt == (32 * 48 + 48)
+    assert changed and all("linear1" in k for k in changed)

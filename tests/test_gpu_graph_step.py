@@ -32,5 +32,7 @@ def test_graph_step_matches_eager():
     lg, pg = _run(True, steps=4)  # 2 warm-up + 4 replays = 6 updates
     assert all(torch.isfinite(torch.tensor(lg)))
     torch.testing.assert_close(torch.tensor(lg[-1]), torch.tensor(le[-1]), rtol=2e-2, atol=2e-3)
+    # MIOpen's wgrad is not bitwise deterministic and Adam turns sign flips of near-zero grads into
+    # +-lr steps, so compare parameters by relative norm, not elementwise
     for a, b in zip(pe, pg):
-        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-3)
+        assert (a - b).norm() <= 0.05 * a.norm() + 1e-3
