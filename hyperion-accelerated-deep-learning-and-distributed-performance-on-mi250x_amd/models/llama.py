@@ -109,7 +109,7 @@ class LlamaDecoderLayer(nn.Module):
         self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
 
-    def fused_forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor, positions, kpm):
+    def forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor, positions=None, kpm=None):
         """Residual-stream form: block input = ``stream + delta``; returns ``(mlp_out, new_stream)``."""
         ln1 = self.input_layernorm
         if delta is None:
@@ -120,8 +120,9 @@ class LlamaDecoderLayer(nn.Module):
         h2, s2 = self.post_attention_layernorm(a, residual=s, return_sum=True)
         return self.mlp(h2), s2
 
-    def forward(self, x: torch.Tensor, positions=None, key_padding_mask=None) -> torch.Tensor:
-        d, s = self.fused_forward(None, x, positions, key_padding_mask)
+    def block(self, x: torch.Tensor, positions=None, key_padding_mask=None) -> torch.Tensor:
+        """Plain form: x -> layer output."""
+        d, s = self(None, x, positions, key_padding_mask)
         return s + d
 
 
@@ -145,9 +146,9 @@ class LlamaModel(nn.Module):
         ckpt = self.gradient_checkpointing and self.training and torch.is_grad_enabled()
         for layer in self.layers:
             if ckpt:
-                d, s = checkpoint(layer.fused_forward, d, s, positions, kpm, use_reentrant=False)
+                d, s = checkpoint(layer, d, s, positions, kpm, use_reentrant=False)
             else:
-                d, s = layer.fused_forward(d, s, positions, kpm)
+                d, s = layer(d, s, positions, kpm)
         return self.norm(d, residual=s) if d is not None else self.norm(s)
 
 

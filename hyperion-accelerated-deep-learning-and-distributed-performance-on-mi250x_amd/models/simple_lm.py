@@ -79,7 +79,12 @@ class SimpleTransformerLM(nn.Module):
         x = getattr(self, self._emb_name)(ids)
         return getattr(self, self._enc_name)(x, causal=self.causal)
 
-    def forward(self, ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None, **_) -> torch.Tensor:
+    def forward(self, ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                targets: Optional[torch.Tensor] = None, ignore_index: int = GPT2_PAD, **_) -> torch.Tensor:
+        """Logits like the reference; with ``targets`` the fused-head mean CE loss (so wrappers that
+        only intercept ``forward`` — DDP, FSDP — see the training path too)."""
+        if targets is not None:
+            return self.forward_loss(ids, targets, ignore_index, attention_mask)
         if self.seq_first_input:
             return self.fc(self.hidden(ids.t(), attention_mask)).transpose(0, 1)
         return self.fc(self.hidden(ids, attention_mask))

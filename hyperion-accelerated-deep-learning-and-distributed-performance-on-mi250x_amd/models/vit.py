@@ -55,7 +55,7 @@ class EncoderBlock(nn.Module):
         self.ln_2 = LayerNorm(hidden_dim, eps=1e-6)
         self.mlp = MLPBlock(hidden_dim, mlp_dim, dropout)
 
-    def fused_forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    def forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:  # type: ignore[override]
         """One block on the residual stream.
 
         Input ``stream + delta`` is the block input (``delta`` = previous block's MLP output, not yet
@@ -70,8 +70,9 @@ class EncoderBlock(nn.Module):
         h2, s2 = layer_norm(a, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps, residual=s, return_sum=True)
         return self.mlp(h2), s2
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        d, s = self.fused_forward(None, x)
+    def block(self, x: torch.Tensor) -> torch.Tensor:
+        """Plain form: x -> block output."""
+        d, s = self(None, x)
         return s + d
 
 
@@ -97,11 +98,11 @@ class Encoder(nn.Module):
         for blk in self.layers.values():
             if ckpt:
                 if d is None:
-                    d, s = checkpoint(blk.fused_forward, None, s, use_reentrant=False)
+                    d, s = checkpoint(blk, None, s, use_reentrant=False)
                 else:
-                    d, s = checkpoint(blk.fused_forward, d, s, use_reentrant=False)
+                    d, s = checkpoint(blk, d, s, use_reentrant=False)
             else:
-                d, s = blk.fused_forward(d, s)
+                d, s = blk(d, s)
         if d is None:
             return self.ln(s)
         return self.ln(d, residual=s)

@@ -63,6 +63,7 @@ class LossScaler:
         self.found_inf_t = torch.zeros((), dtype=torch.float32, device=dev)
         self.growth_tracker = torch.zeros((), dtype=torch.int32, device=dev)
         self._tables = TableCache()
+        self._unscaled = False
 
     def scale(self, loss: torch.Tensor) -> torch.Tensor:
         if not self.enabled:
@@ -71,8 +72,9 @@ class LossScaler:
 
     @torch.no_grad()
     def unscale_(self, optimizer: torch.optim.Optimizer) -> None:
-        if not self.enabled:
+        if not self.enabled or self._unscaled:
             return
+        self._unscaled = True  # GradScaler semantics: one unscale per step (clip may call it early)
         self.found_inf_t.zero_()
         grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
         if not grads:
@@ -108,6 +110,7 @@ class LossScaler:
     def update(self) -> None:
         if not self.enabled:
             return
+        self._unscaled = False
         torch._amp_update_scale_(self.scale_t, self.growth_tracker, self.found_inf_t, self.growth_factor,
                                  self.backoff_factor, self.growth_interval)
         torch.reciprocal(self.scale_t, out=self.inv_scale_t)

@@ -1,0 +1,466 @@
+"""Distributed trainers with the reference's names, signatures, CSV schemas and checkpoint layout.
+
+Reference (``02_development/distributed_utils.py``):
+
+* ``train_language_model_ddp(rank, world, epochs, base_dir)`` — SimpleTransformerLM-256, per-rank
+  batch 32, AdamW 2e-4, CE(ignore pad), fp16 autocast + GradScaler, DDP (:132-200);
+* ``train_cifar_model_ddp(rank, world, epochs, base_dir)`` — ResNet-18 (10 classes), batch 64,
+  AdamW 1e-3, fp16 AMP, DDP, accuracy (:208-278);
+* ``train_language_model_fsdp(rank, world, epochs, base_dir)`` — the LM under FSDP FULL_SHARD,
+  size-based wrap (100k), bf16 mixed precision, clip 1.0, AdamW 1e-4 (:290-406);
+* ``train_llama_fsdp(rank, world, *, epochs, base_dir, hf_token, model_id, lora, batch_size,
+  progress_every)`` — Llama-2-7B, LoRA r16 (DDP) or full FSDP, AdamW 1e-5 wd .01, clip 1.0
+  (:415-554).
+
+Hyperion differences (each documented where it happens): synthetic data of the real shapes by
+default (no network); seeded; device-side loss/accuracy accumulation (the reference synced with
+``loss.item()`` every step, K15); global-norm clipping under FSDP; collective-safe checkpoints on
+every rank; resume support; LoRA can also run under FSDP (the BASELINE config) with layer-class
+wrapping (the reference's policy never recursed, K8); fault injection (``HYPERION_FAULT``).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.data import DataLoader
+
+from ..data import DistributedSampler, SyntheticCIFAR10, SyntheticWikiText2, WikiText2TorchDataset, load_wikitext2
+from ..data.loader import DevicePrefetcher
+from ..models.simple_lm import GPT2_PAD, GPT2_VOCAB, simple_lm_256
+from ..ops.optim import FusedAdam, clip_grad_norm_
+from ..parallel.launch import cleanup, setup
+from ..utils.fault import maybe_inject
+from ..utils.seed import seed_everything
+from .amp import LossScaler
+from .checkpoint import load_checkpoint, save_checkpoint
+from .metrics import SCHEMAS, MetricsCSV, make_run_id, write_manifest
+
+DEFAULT_BASE_DIR = os.environ.get("HYPERION_BASE_DIR", os.getcwd())
+
+
+@dataclass
+class RunOptions:
+    """Knobs the reference hard-coded; defaults reproduce its settings."""
+
+    synthetic: bool = True
+    dataset_size: Optional[int] = None      # None = the real dataset's size
+    max_steps_per_epoch: Optional[int] = None
+    precision: Optional[str] = None         # override: fp32 | fp16 | bf16
+    seed: int = 0
+    save: bool = True
+    ckpt_mode: str = "full"                 # full | sharded (FSDP)
+    resume: Optional[str] = None
+    num_workers: int = 2
+    causal: bool = False                    # reference LM had no causal mask
+    timeout_s: float = 600.0
+    log: Callable[[str], None] = field(default=print)
+
+
+def _out_dir(base_dir: str) -> str:
+    d = os.path.join(base_dir, "data", "distributed")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def _loader(ds, world, rank, batch, opts: RunOptions, device, drop_last=False):
+    sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=opts.seed)
+    dl = DataLoader(ds, batch_size=batch, sampler=sampler, num_workers=opts.num_workers if device.type == "cuda" else 0,
+                    pin_memory=device.type == "cuda", drop_last=drop_last, persistent_workers=False)
+    return sampler, DevicePrefetcher(dl, device)
+
+
+def _wikitext(opts: RunOptions, base_dir: str):
+    if not opts.synthetic:
+        path = os.path.join(base_dir, "data", "processed", "wikitext2_tokenized")
+        return WikiText2TorchDataset(load_wikitext2(path, "train"), split="train")
+    kw = {} if opts.dataset_size is None else {"n": opts.dataset_size}
+    return SyntheticWikiText2(seed=opts.seed, **kw)
+
+
+def _reduce_mean(t: torch.Tensor, world: int) -> torch.Tensor:
+    if world > 1:
+        dist.all_reduce(t)
+        t = t / world
+    return t
+
+
+def _amp(precision: str):
+    return {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[precision]
+
+
+class _EpochRunner:
+    """Shared hot loop: device-side loss accumulation, fault hook, timing."""
+
+    def __init__(self, rank, world, device, model, opt, scaler, amp_dtype, clip, sharded_clip, opts: RunOptions):
+        self.rank, self.world, self.device = rank, world, device
+        self.model, self.opt, self.scaler = model, opt, scaler
+        self.amp_dtype = amp_dtype
+        self.clip, self.sharded_clip = clip, sharded_clip
+        self.opts = opts
+        self.global_step = 0
+
+    def step(self, loss_fn) -> torch.Tensor:
+        self.opt.zero_grad(set_to_none=True)
+        with torch.autocast(self.device.type, dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None
+                            and not (self.device.type == "cpu" and self.amp_dtype == torch.float16)):
+            loss, extra = loss_fn()
+        if maybe_inject(self.rank, self.global_step):
+            loss = loss * float("nan")
+        if self.scaler is not None and self.scaler.enabled:
+            self.scaler.scale(loss).backward()
+            if self.clip is not None:
+                self.scaler.unscale_(self.opt)
+                self._clip()
+            self.scaler.step(self.opt)
+            self.scaler.update()
+        else:
+            loss.backward()
+            if self.clip is not None:
+                self._clip()
+            self.opt.step()
+        self.global_step += 1
+        return loss.detach().float(), extra
+
+    def _clip(self) -> None:
+        if hasattr(self.model, "clip_grad_norm_"):
+            self.model.clip_grad_norm_(self.clip)
+        else:
+            clip_grad_norm_(self.model.parameters(), self.clip, sharded=self.sharded_clip)
+
+
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+# ---------------------------------------------------------------------------------------- LM DDP
+def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
+                             opts: Optional[RunOptions] = None, batch_size: int = 32) -> Dict:
+    """C23: SimpleTransformerLM-256 + DDP + fp16 AMP; CSV ``epoch,loss,duration,gpus``."""
+    from ..parallel.ddp import DDP
+
+    opts = opts or RunOptions()
+    device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
+    seed_everything(opts.seed, 0)  # identical init on every rank (DDP also broadcasts)
+    run_id = make_run_id("language_ddp", world)
+    out = _out_dir(base_dir)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["language_ddp"], enabled=rank == 0)
+    ds = _wikitext(opts, base_dir)
+    sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
+    model = simple_lm_256(GPT2_VOCAB, causal=opts.causal).to(device)
+    model = DDP(model) if world > 1 else model
+    precision = opts.precision or ("fp16" if device.type == "cuda" else "fp32")
+    opt = FusedAdam(model.parameters(), lr=2e-4, weight_decay=0.01, adamw=True)
+    scaler = LossScaler(enabled=precision == "fp16", device=device)
+    runner = _EpochRunner(rank, world, device, model, opt, scaler, _amp(precision), None, False, opts)
+    inner = model.module if hasattr(model, "module") else model
+    start_epoch = _maybe_resume(opts, model, opt, scaler)
+    history = []
+    for ep in range(start_epoch, epochs):
+        sampler.set_epoch(ep)
+        _sync(device)
+        t0 = time.time()
+        loss_sum = torch.zeros((), device=device)
+        n = 0
+        for i, (ids, _mask) in enumerate(loader):
+            if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
+                break
+            x, y = ids[:, :-1], ids[:, 1:]
+            ddp_fwd = model if world > 1 else None
+
+            def lm_loss():
+                if ddp_fwd is not None:  # DDP hooks need the wrapper's forward: run through it
+                    return ddp_fwd(x, targets=y, ignore_index=GPT2_PAD), None
+                return inner.forward_loss(x, y, ignore_index=GPT2_PAD), None
+
+            loss, _ = runner.step(lm_loss)
+            loss_sum += loss
+            n += 1
+        avg = _reduce_mean(loss_sum / max(n, 1), world).item()
+        _sync(device)
+        dur = time.time() - t0
+        csv.append(epoch=ep + 1, loss=round(avg, 6), duration=round(dur, 4), gpus=world)
+        history.append({"epoch": ep + 1, "loss": avg, "duration": dur, "steps": n})
+        if rank == 0:
+            opts.log(f"[language_ddp] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s ({n} steps)")
+    ck = _finish(opts, out, run_id, model, opt, scaler, epochs, runner.global_step)
+    _manifest(rank, out, run_id, history, batch_size, world, precision)
+    if world > 1:
+        cleanup()
+    return {"run_id": run_id, "history": history, "checkpoint": ck}
+
+
+# ---------------------------------------------------------------------------------------- CIFAR DDP
+def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
+                          opts: Optional[RunOptions] = None, batch_size: int = 64) -> Dict:
+    """C24: ResNet-18 (10 classes, ImageNet stem on 32x32) + DDP + fp16 AMP; CSV with accuracy."""
+    from ..data.datasets import CIFAR10TorchDataset, load_cifar10_pt
+    from ..models.resnet import resnet18
+    from ..parallel.ddp import DDP
+
+    opts = opts or RunOptions()
+    device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
+    seed_everything(opts.seed, 0)
+    run_id = make_run_id("cifar_ddp", world)
+    out = _out_dir(base_dir)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["cifar"], enabled=rank == 0)
+    if opts.synthetic:
+        ds = SyntheticCIFAR10(seed=opts.seed, **({} if opts.dataset_size is None else {"n": opts.dataset_size}))
+    else:
+        ds = CIFAR10TorchDataset(load_cifar10_pt(os.path.join(base_dir, "data", "processed", "cifar10_train.pt")))
+    sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
+    model = resnet18(num_classes=10).to(device)
+    if device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    model = DDP(model, broadcast_buffers=True) if world > 1 else model
+    precision = opts.precision or ("fp16" if device.type == "cuda" else "fp32")
+    opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01, adamw=True)
+    scaler = LossScaler(enabled=precision == "fp16", device=device)
+    runner = _EpochRunner(rank, world, device, model, opt, scaler, _amp(precision), None, False, opts)
+    start_epoch = _maybe_resume(opts, model, opt, scaler)
+    history = []
+    for ep in range(start_epoch, epochs):
+        sampler.set_epoch(ep)
+        _sync(device)
+        t0 = time.time()
+        stats = torch.zeros(3, device=device, dtype=torch.float64)  # loss_sum, correct, total
+        n = 0
+        model.train()
+        for i, (img, lbl) in enumerate(loader):
+            if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
+                break
+            if device.type == "cuda":
+                img = img.contiguous(memory_format=torch.channels_last)
+
+            def cifar_loss():
+                logits = model(img)
+                return F.cross_entropy(logits.float(), lbl), logits.detach()
+
+            loss, logits = runner.step(cifar_loss)
+            stats[0] += loss
+            stats[1] += (logits.argmax(1) == lbl).sum()
+            stats[2] += lbl.numel()
+            n += 1
+        if world > 1:
+            dist.all_reduce(stats)
+        loss_avg = (stats[0] / max(n, 1) / world).item()
+        acc = (stats[1] / stats[2].clamp_min(1)).item() * 100.0
+        _sync(device)
+        dur = time.time() - t0
+        csv.append(epoch=ep + 1, loss=round(loss_avg, 6), accuracy=round(acc, 4), duration=round(dur, 4), gpus=world)
+        history.append({"epoch": ep + 1, "loss": loss_avg, "accuracy": acc, "duration": dur, "steps": n})
+        if rank == 0:
+            opts.log(f"[cifar] epoch {ep + 1}/{epochs} loss {loss_avg:.4f} acc {acc:.2f}% {dur:.2f}s")
+    ck = _finish(opts, out, run_id, model, opt, scaler, epochs, runner.global_step)
+    _manifest(rank, out, run_id, history, batch_size, world, precision)
+    if world > 1:
+        cleanup()
+    return {"run_id": run_id, "history": history, "checkpoint": ck}
+
+
+# ---------------------------------------------------------------------------------------- LM FSDP
+def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
+                              opts: Optional[RunOptions] = None, batch_size: int = 32,
+                              model_fn: Optional[Callable[[], nn.Module]] = None, min_num_params: int = 100_000) -> Dict:
+    """C25: the LM under FSDP FULL_SHARD, size-based wrap, bf16 mixed precision, global clip 1.0."""
+    from ..parallel.fsdp import FSDP, MixedPrecision, size_based_auto_wrap_policy
+
+    opts = opts or RunOptions()
+    device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
+    seed_everything(opts.seed, 0)
+    run_id = make_run_id("language_fsdp", world)
+    out = _out_dir(base_dir)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["language_fsdp"], enabled=rank == 0)
+    ds = _wikitext(opts, base_dir)
+    sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
+    base = (model_fn or (lambda: simple_lm_256(GPT2_VOCAB, causal=opts.causal)))()
+    precision = opts.precision or ("bf16" if device.type == "cuda" else "fp32")
+    pdt = _amp(precision)
+    model = FSDP(base, auto_wrap_policy=size_based_auto_wrap_policy(min_num_params), device_id=device,
+                 mixed_precision=MixedPrecision(pdt, pdt, pdt))
+    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01, adamw=True)
+    runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, True, opts)
+    start_epoch = _maybe_resume(opts, model, opt, None)
+    history = []
+    for ep in range(start_epoch, epochs):
+        sampler.set_epoch(ep)
+        _sync(device)
+        t0 = time.time()
+        loss_sum = torch.zeros((), device=device)
+        n = 0
+        for i, (ids, _mask) in enumerate(loader):
+            if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
+                break
+            x, y = ids[:, :-1], ids[:, 1:]
+            loss, _ = runner.step(lambda: (model.forward_loss(x, y, ignore_index=GPT2_PAD), None))
+            loss_sum += loss
+            n += 1
+        avg = _reduce_mean(loss_sum / max(n, 1), world).item()
+        _sync(device)
+        dur = time.time() - t0
+        csv.append(epoch=ep + 1, loss=round(avg, 6), duration=round(dur, 4), gpus=world)
+        history.append({"epoch": ep + 1, "loss": avg, "duration": dur, "steps": n})
+        if rank == 0:
+            opts.log(f"[language_fsdp] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s")
+    if world > 1:
+        dist.barrier()
+    ck = _finish(opts, out, run_id, model, opt, None, epochs, runner.global_step)
+    _manifest(rank, out, run_id, history, batch_size, world, precision)
+    if world > 1:
+        cleanup()
+    return {"run_id": run_id, "history": history, "checkpoint": ck}
+
+
+# ---------------------------------------------------------------------------------------- Llama
+def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = DEFAULT_BASE_DIR,
+                     hf_token: Optional[str] = None, model_id: str = "NousResearch/Llama-2-7b-hf", lora: bool = False,
+                     batch_size: int = 1, progress_every: int = 50, opts: Optional[RunOptions] = None,
+                     config=None, lora_parallel: str = "fsdp", mask_pad_labels: bool = False) -> Dict:
+    """C26: Llama fine-tune.  ``lora=True``: frozen bf16 base + r16 adapters on q/k/v/o.
+
+    ``lora_parallel='fsdp'`` (default; the BASELINE.json config) shards the frozen base and
+    reduce-scatters only the adapters; ``'ddp'`` reproduces the reference (DDP over a replicated
+    model).  ``lora=False``: full bf16 FSDP with ``LlamaDecoderLayer`` units.  ``hf_token`` /
+    ``model_id`` are accepted for CLI compatibility; weights are random-init (no network).
+    ``mask_pad_labels`` fixes the reference's unmasked pad labels (:517) when set.
+    """
+    from ..models.llama import LlamaConfig, LlamaDecoderLayer, LlamaForCausalLM
+    from ..models.lora import apply_lora, save_adapter
+    from ..parallel.ddp import DDP
+    from ..parallel.fsdp import FSDP, MixedPrecision, transformer_auto_wrap_policy
+
+    del hf_token
+    opts = opts or RunOptions()
+    device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
+    seed_everything(opts.seed, 0)
+    run_id = make_run_id("llama", world)
+    out = _out_dir(base_dir)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["llama"], enabled=rank == 0)
+    cfg = config or LlamaConfig.llama2_7b()
+    ds = _wikitext(opts, base_dir)
+    sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
+    precision = opts.precision or ("bf16" if device.type == "cuda" else "fp32")
+    pdt = _amp(precision) or torch.float32
+    with torch.device(device):
+        base = LlamaForCausalLM(cfg)
+    if lora:
+        base = apply_lora(base, r=16, alpha=32, dropout=0.05)
+        mode = f"lora_{precision}"
+    else:
+        mode = f"fsdp_{precision}"
+    policy = transformer_auto_wrap_policy({LlamaDecoderLayer})
+    if lora and (lora_parallel == "ddp" or world == 1):
+        model = base.to(pdt)
+        model = DDP(model) if world > 1 else model
+    else:
+        model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt))
+    opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, adamw=True)
+    runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, isinstance(model, FSDP), opts)
+    start_epoch = _maybe_resume(opts, model, opt, None)
+    history = []
+    for ep in range(start_epoch, epochs):
+        sampler.set_epoch(ep)
+        _sync(device)
+        t0 = time.time()
+        loss_sum = torch.zeros((), device=device)
+        n = 0
+        for i, (ids, msk) in enumerate(loader):
+            if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
+                break
+            ids = ids % cfg.vocab_size  # GPT-2-tokenized synthetic ids folded into the Llama vocab
+            labels = ids.masked_fill(msk == 0, -100) if mask_pad_labels else ids.clone()
+
+            def llama_loss():
+                return model(ids, attention_mask=msk, labels=labels).loss, None
+
+            loss, _ = runner.step(llama_loss)
+            loss_sum += loss
+            n += 1
+            if rank == 0 and progress_every and n % progress_every == 0:
+                opts.log(f"[llama] epoch {ep + 1} step {n} loss {loss.item():.4f}")
+        avg = _reduce_mean(loss_sum / max(n, 1), world).item()
+        _sync(device)
+        dur = time.time() - t0
+        csv.append(epoch=ep + 1, loss=round(avg, 6), duration_s=round(dur, 4), gpus=world, mode=mode)
+        history.append({"epoch": ep + 1, "loss": avg, "duration_s": dur, "steps": n, "mode": mode})
+        if rank == 0:
+            opts.log(f"[llama] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s mode {mode}")
+    ck = None
+    if opts.save:
+        if lora:
+            # adapters only (PEFT save_pretrained layout); FSDP gathers them collectively first
+            if isinstance(model, FSDP):
+                sd = model.full_state_dict(rank0_only=True)
+                if rank == 0:
+                    ck = _save_adapter_from_sd(sd, os.path.join(out, f"{run_id}_{mode}"))
+            elif rank == 0:
+                inner = model.module if hasattr(model, "module") else model
+                ck = save_adapter(inner, os.path.join(out, f"{run_id}_{mode}"))
+        else:
+            ck = save_checkpoint(os.path.join(out, f"{run_id}_{mode}.pt"), model, None, None, epochs,
+                                 runner.global_step, mode=opts.ckpt_mode)
+    _manifest(rank, out, run_id, history, batch_size, world, precision)
+    if world > 1:
+        cleanup()
+    return {"run_id": run_id, "history": history, "checkpoint": ck, "mode": mode}
+
+
+def _save_adapter_from_sd(sd: Dict[str, torch.Tensor], out_dir: str) -> str:
+    import json
+
+    from safetensors.torch import save_file
+
+    from ..models.lora import lora_config_dict
+
+    os.makedirs(out_dir, exist_ok=True)
+    ad = {"base_model.model." + k.replace(".default.", "."): v.contiguous() for k, v in sd.items()
+          if ".lora_A." in k or ".lora_B." in k}
+    save_file(ad, os.path.join(out_dir, "adapter_model.safetensors"))
+    with open(os.path.join(out_dir, "adapter_config.json"), "w") as f:
+        json.dump(lora_config_dict(16, 32, 0.05, ["k_proj", "o_proj", "q_proj", "v_proj"]), f, indent=2)
+    return out_dir
+
+
+# ---------------------------------------------------------------------------------------- helpers
+def _single_device() -> torch.device:
+    from ..utils.device import get_device
+
+    d = get_device()
+    if d.type == "cuda":
+        torch.cuda.set_device(d)
+    return d
+
+
+def _maybe_resume(opts: RunOptions, model, opt, scaler) -> int:
+    if not opts.resume:
+        return 0
+    meta = load_checkpoint(opts.resume, model, opt, scaler)
+    return int(meta.get("epoch", 0))
+
+
+def _finish(opts: RunOptions, out: str, run_id: str, model, opt, scaler, epoch: int, step: int):
+    if not opts.save:
+        return None
+    return save_checkpoint(os.path.join(out, f"{run_id}_model.pt"), model, opt, scaler, epoch, step, mode=opts.ckpt_mode)
+
+
+def _manifest(rank: int, out: str, run_id: str, history, batch: int, world: int, precision: str) -> None:
+    if rank != 0 or not history:
+        return
+    steady = history[len(history) // 3:] or history
+    dur_key = "duration" if "duration" in steady[0] else "duration_s"
+    steps = sum(h["steps"] for h in steady)
+    secs = sum(h[dur_key] for h in steady)
+    write_manifest(os.path.join(out, f"{run_id}_run.json"), {
+        "run_id": run_id, "world": world, "per_rank_batch": batch, "precision": precision, "history": history,
+        "samples_per_s": (steps * batch * world / secs) if secs > 0 else None,
+        "ms_per_step": (secs / steps * 1e3) if steps else None,
+        "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20 if torch.cuda.is_available() else None,
+    })

@@ -1,0 +1,46 @@
+"""Fault injection for failure-detection tests (SURVEY §5.3 MI355X plan).
+
+``HYPERION_FAULT=rank:step:kind`` makes the given rank misbehave at the given training step:
+``exit`` (process dies with status 17), ``raise`` (Python exception), ``hang`` (sleeps far past
+the process-group timeout), ``nan`` (returns True so the caller poisons its loss).  Trainers call
+:func:`maybe_inject` once per step; tests assert that the surviving ranks fail within the
+configured timeout instead of hanging (the reference disabled the watchdog:
+``TORCH_NCCL_ASYNC_ERROR_HANDLING=0``, ``run_language_fsdp.sh:10``).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+from typing import Optional, Tuple
+
+
+def parse(spec: Optional[str] = None) -> Optional[Tuple[int, int, str]]:
+    spec = spec if spec is not None else os.environ.get("HYPERION_FAULT", "")
+    if not spec:
+        return None
+    r, s, k = spec.split(":")
+    if k not in ("exit", "raise", "hang", "nan"):
+        raise ValueError(f"unknown fault kind {k!r}")
+    return int(r), int(s), k
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+def maybe_inject(rank: int, step: int, spec: Optional[str] = None) -> bool:
+    f = parse(spec)
+    if f is None or f[0] != rank or f[1] != step:
+        return False
+    kind = f[2]
+    if kind == "exit":
+        sys.stderr.write(f"[hyperion] injected fault: rank {rank} exits at step {step}\n")
+        sys.stderr.flush()
+        os._exit(17)
+    if kind == "raise":
+        raise InjectedFault(f"injected fault at rank {rank} step {step}")
+    if kind == "hang":
+        time.sleep(float(os.environ.get("HYPERION_FAULT_HANG_S", "3600")))
+        return False
+    return True  # nan
