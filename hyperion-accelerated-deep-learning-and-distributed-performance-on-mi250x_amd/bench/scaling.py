@@ -1,0 +1,139 @@
+"""Scaling report and scaling-experiment orchestration.
+
+Reference: ``create_scaling_report(dist_dir)`` globs ``*_metrics.csv``, classifies runs by file
+name, averages epoch duration after skipping the first ⌊n/3⌋ epochs (min 1), and reports
+speedup = t₁ / t_g and efficiency = speedup / g (``distributed_utils.py:563-773``); it needed a
+``duration`` column, so Llama runs (``duration_s``) were always skipped, and with no CSVs it wrote
+hard-coded sample curves.  ``run_scaling_experiment`` launched nested ``torchrun`` jobs from inside
+a running worker group (:780-831).
+
+Here: the same formula and output schema (``scaling_analysis.csv``: ``gpus,ideal,{model}_speedup…,
+{model}_efficiency…`` + PNG), ``duration`` OR ``duration_s`` accepted (fix), no fake sample data
+(an empty report is an empty report), and the orchestrator is a plain top-level launcher that
+starts one ``torch.distributed.run`` per GPU count sequentially.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import re
+import subprocess
+import sys
+import time
+from collections import defaultdict
+from typing import Dict, List, Optional, Sequence
+
+KINDS = ("language_ddp", "language_fsdp", "cifar", "llama")
+
+
+def classify(filename: str) -> Optional[str]:
+    base = os.path.basename(filename)
+    for k in KINDS:
+        if base.startswith(k):
+            return k
+    return None
+
+
+def gpus_of(filename: str) -> Optional[int]:
+    m = re.search(r"_(\d+)gpus_", os.path.basename(filename))
+    return int(m.group(1)) if m else None
+
+
+def steady_mean(durations: Sequence[float]) -> float:
+    """Reference warm-up rule: drop the first max(1, ⌊n/3⌋) epochs when n > 1."""
+    d = list(durations)
+    if len(d) > 1:
+        d = d[max(1, len(d) // 3):]
+    return sum(d) / len(d)
+
+
+def collect(dist_dir: str) -> Dict[str, Dict[int, float]]:
+    import pandas as pd
+
+    out: Dict[str, Dict[int, List[float]]] = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(dist_dir, "*_metrics.csv"))):
+        kind, g = classify(f), gpus_of(f)
+        if kind is None or g is None:
+            continue
+        try:
+            df = pd.read_csv(f)
+        except Exception:
+            continue
+        col = "duration" if "duration" in df.columns else ("duration_s" if "duration_s" in df.columns else None)
+        if col is None or df.empty:
+            continue
+        out[kind][g].append(steady_mean(df[col].astype(float).tolist()))
+    # several runs at the same GPU count: keep the fastest (best-of)
+    return {k: {g: min(v) for g, v in d.items()} for k, d in out.items()}
+
+
+def create_scaling_report(dist_dir: str, make_plot: bool = True) -> Optional[str]:
+    import pandas as pd
+
+    times = collect(dist_dir)
+    if not times:
+        print(f"create_scaling_report: no *_metrics.csv with duration columns under {dist_dir}")
+        return None
+    gpus = sorted({g for d in times.values() for g in d})
+    rows = []
+    for g in gpus:
+        row = {"gpus": g, "ideal": float(g)}
+        for k, d in times.items():
+            if 1 in d and g in d:
+                sp = d[1] / d[g]
+                row[f"{k}_speedup"] = round(sp, 4)
+                row[f"{k}_efficiency"] = round(sp / g, 4)
+        rows.append(row)
+    df = pd.DataFrame(rows)
+    path = os.path.join(dist_dir, "scaling_analysis.csv")
+    df.to_csv(path, index=False)
+    if make_plot:
+        try:
+            import matplotlib
+
+            matplotlib.use("Agg")
+            import matplotlib.pyplot as plt
+
+            fig, ax = plt.subplots(1, 2, figsize=(12, 5))
+            ax[0].plot(df["gpus"], df["ideal"], "k--", label="ideal")
+            for c in df.columns:
+                if c.endswith("_speedup"):
+                    ax[0].plot(df["gpus"], df[c], "o-", label=c[:-8])
+                if c.endswith("_efficiency"):
+                    ax[1].plot(df["gpus"], df[c], "o-", label=c[:-11])
+            ax[0].set(xlabel="GPUs", ylabel="speedup", title="Speedup")
+            ax[1].set(xlabel="GPUs", ylabel="efficiency", title="Scaling efficiency", ylim=(0, 1.1))
+            for a in ax:
+                a.legend()
+                a.grid(alpha=0.3)
+            fig.tight_layout()
+            fig.savefig(os.path.join(dist_dir, "scaling_analysis.png"), dpi=120)
+            plt.close(fig)
+        except Exception as e:  # matplotlib missing is not fatal
+            print(f"(plot skipped: {e})")
+    print(df.to_string(index=False))
+    return path
+
+
+def run_scaling_experiment(model_type: str, gpu_counts: Sequence[int] = (1, 2, 4, 8), epochs: int = 5,
+                           base_dir: str = ".", hf_token: Optional[str] = None, extra_args: Sequence[str] = (),
+                           dry_run: bool = False) -> List[List[str]]:
+    """Launch one ``torch.distributed.run`` job per GPU count (sequentially), then report."""
+    cmds = []
+    for g in gpu_counts:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", f"--nproc-per-node={g}",
+               "--master-addr", "127.0.0.1", "-m", "hyperion.cli.run_distributed", "--model", model_type,
+               "--epochs", str(epochs), "--base_dir", base_dir] + list(extra_args)
+        if hf_token:
+            cmd += ["--hf_token", hf_token]
+        cmds.append(cmd)
+        if dry_run:
+            continue
+        try:
+            subprocess.run(cmd, check=True)
+        except subprocess.CalledProcessError as e:  # keep going, like the reference (:826-827)
+            print(f"scaling run with {g} GPUs failed: {e}")
+        time.sleep(2)
+    if not dry_run:
+        create_scaling_report(os.path.join(base_dir, "data", "distributed"))
+    return cmds
