@@ -1,0 +1,130 @@
+"""Training-step throughput of the LM / ViT / Llama configs on one GPU (BASELINE.json configs 3-5).
+
+Each function builds the model exactly as the matching trainer does, runs ``warmup`` steps, then
+times ``steps`` full steps (forward, backward, optimizer) between device syncs, and returns
+samples/s, tokens/s, ms/step and peak memory.  Used by ``cli/bench_models`` and the profiling runs.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict
+
+import torch
+
+
+def _timeit(step, steps: int, warmup: int) -> float:
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", steps: int = 20, warmup: int = 5,
+                  model: str = "lm256", causal: bool = False) -> Dict:
+    """SimpleTransformerLM (C14) training step as in train_language_model_ddp (single GPU)."""
+    from ..data.synthetic import SyntheticWikiText2
+    from ..models.simple_lm import GPT2_PAD, gpt2_small_lm, simple_lm_256
+    from ..ops.optim import FusedAdam
+    from ..train.amp import LossScaler
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    m = (simple_lm_256(causal=causal) if model == "lm256" else gpt2_small_lm()).to(dev)
+    opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True)
+    dt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[precision]
+    scaler = LossScaler(enabled=precision == "fp16", device=dev)
+    ids = SyntheticWikiText2(n=batch, seq_len=seq, seed=0).input_ids.to(dev)
+    x, y = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=dt or torch.float32, enabled=dt is not None):
+            loss = m.forward_loss(x, y, ignore_index=GPT2_PAD)
+        if scaler.enabled:
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+        else:
+            loss.backward()
+            opt.step()
+
+    torch.cuda.reset_peak_memory_stats()
+    t = _timeit(step, steps, warmup)
+    return {"model": model, "batch": batch, "seq": seq, "precision": precision, "ms_per_step": t * 1e3,
+            "samples_per_s": batch / t, "tokens_per_s": batch * (seq - 1) / t,
+            "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
+
+
+def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool = True, steps: int = 20,
+                   warmup: int = 5) -> Dict:
+    """ViT-B/16 bf16 + activation checkpointing (BASELINE.json config 3), MSE/Adam like C6."""
+    from ..models.vit import vit_b_16
+    from ..ops.optim import FusedAdam
+    from ..train.amp import cast_for_compute
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    m = vit_b_16(use_checkpoint=checkpointing).to(dev).to(memory_format=torch.channels_last)
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(precision)
+    if dt is not None:
+        cast_for_compute(m, dt)
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    x = torch.rand(batch, 3, 224, 224, device=dev).contiguous(memory_format=torch.channels_last)
+    x = x.to(dt) if dt is not None else x
+    y = torch.rand(batch, 1000, device=dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.mse_loss(m(x).float(), y)
+        loss.backward()
+        opt.step()
+
+    torch.cuda.reset_peak_memory_stats()
+    t = _timeit(step, steps, warmup)
+    return {"model": "vit_b_16", "batch": batch, "precision": precision, "checkpointing": checkpointing,
+            "ms_per_step": t * 1e3, "samples_per_s": batch / t, "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
+
+
+def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmup: int = 3, lora: bool = True,
+                          config=None, grad_ckpt: bool = False) -> Dict:
+    """Llama-2-7B (random init) LoRA r16 bf16 step, batch 1 x 128 tokens (the reference's Llama run)."""
+    from ..data.synthetic import SyntheticWikiText2
+    from ..models.llama import LlamaConfig, LlamaForCausalLM
+    from ..models.lora import apply_lora, trainable_parameters
+    from ..ops.optim import FusedAdam
+
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    cfg = config or LlamaConfig.llama2_7b()
+    with torch.device(dev):
+        m = LlamaForCausalLM(cfg).to(torch.bfloat16)
+    if lora:
+        apply_lora(m)
+    if grad_ckpt:
+        m.gradient_checkpointing_enable()
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = FusedAdam(params, lr=1e-5, weight_decay=0.01, adamw=True)
+    ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=0)
+    ids = (ds.input_ids % cfg.vocab_size).to(dev)
+    mask = ds.attention_mask.to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = m(ids, attention_mask=mask, labels=ids).loss
+        loss.backward()
+        from ..ops.optim import clip_grad_norm_
+
+        clip_grad_norm_(params, 1.0)
+        opt.step()
+
+    torch.cuda.reset_peak_memory_stats()
+    t = _timeit(step, steps, warmup)
+    return {"model": "llama2_7b" if config is None else "llama_custom", "lora": lora, "batch": batch, "seq": seq,
+            "ms_per_step": t * 1e3, "samples_per_s": batch / t, "tokens_per_s": batch * seq / t,
+            "trainable_params": trainable_parameters(m), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
+
+

@@ -10,4 +10,5 @@ PYBIND11_MODULE(_C, m) {
   hypbind::register_attn_ops(m);
   hypbind::register_loss_ops(m);
   hypbind::register_llama_ops(m);
+  hypbind::register_gemm_ops(m);
 }

@@ -100,3 +100,11 @@ hipError_t swiglu_forward(int dtype, const void* g, const void* u, void* h, int6
 hipError_t swiglu_backward(int dtype, const void* dh, const void* g, const void* u, void* dg, void* du, int64_t n,
                            hipStream_t st);
 }  // namespace hyp
+
+namespace hyp {
+// ---- gemm_mfma.hip ---------------------------------------------------------------------------
+// C[M,N] = alpha * A[M,K] · B[N,K]^T ; in bf16/f16, out f32/bf16/f16; 128x128 tiles, BK 32 or 64.
+bool gemm_nt_supported(int M, int N, int K, int lda, int ldb, int bk);
+hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                   int ldb, int ldc, float alpha, int bk, hipStream_t st);
+}  // namespace hyp

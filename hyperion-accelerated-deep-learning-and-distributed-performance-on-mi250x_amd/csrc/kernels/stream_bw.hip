@@ -13,31 +13,48 @@ namespace hyp {
 namespace {
 
 template <int OP, bool NT>
+__device__ __forceinline__ float4 stream_apply(float4 x, float4 y, float s) {
+  if (OP == 0) return x;                                                             // copy
+  if (OP == 1) return make_float4(s * x.x, s * x.y, s * x.z, s * x.w);               // scale
+  if (OP == 2) return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);       // add
+  return make_float4(fmaf(s, y.x, x.x), fmaf(s, y.y, x.y), fmaf(s, y.z, x.z), fmaf(s, y.w, x.w));  // triad
+}
+
+template <bool NT>
+__device__ __forceinline__ void stream_store(float4* p, float4 r) {
+  if (NT) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v rv = {r.x, r.y, r.z, r.w};
+    __builtin_nontemporal_store(rv, reinterpret_cast<f4v*>(p));
+  } else {
+    *p = r;
+  }
+}
+
+// Each thread moves kUnroll float4 per trip with all loads issued before any store (≥ 4 × 16 B per
+// operand in flight per lane: HBM latency is hidden by memory-level parallelism, not occupancy).
+constexpr int kUnroll = 4;
+
+template <int OP, bool NT>
 __global__ __launch_bounds__(256) void stream_k(const float4* __restrict__ a, const float4* __restrict__ b,
                                                 float4* __restrict__ c, float s, int64_t n4) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 r;
-    const float4 x = a[i];
-    if (OP == 0) {  // copy
-      r = x;
-    } else if (OP == 1) {  // scale
-      r = make_float4(s * x.x, s * x.y, s * x.z, s * x.w);
-    } else {
-      const float4 y = b[i];
-      if (OP == 2)  // add
-        r = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
-      else  // triad
-        r = make_float4(fmaf(s, y.x, x.x), fmaf(s, y.y, x.y), fmaf(s, y.z, x.z), fmaf(s, y.w, x.w));
+  const int64_t tile = (int64_t)blockDim.x * kUnroll;
+  const int64_t stride = (int64_t)gridDim.x * tile;
+  int64_t base = (int64_t)blockIdx.x * tile + threadIdx.x;
+  for (; base + (kUnroll - 1) * blockDim.x < n4; base += stride) {
+    float4 x[kUnroll], y[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) x[u] = a[base + u * blockDim.x];
+    if (OP >= 2) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) y[u] = b[base + u * blockDim.x];
     }
-    if (NT) {
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      f4v rv = {r.x, r.y, r.z, r.w};
-      __builtin_nontemporal_store(rv, reinterpret_cast<f4v*>(c + i));
-    } else {
-      c[i] = r;
-    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      stream_store<NT>(c + base + u * blockDim.x, stream_apply<OP, NT>(x[u], OP >= 2 ? y[u] : x[u], s));
   }
+  for (int64_t i = base; i < n4; i += blockDim.x)  // ragged end of this thread's last tile
+    stream_store<NT>(c + i, stream_apply<OP, NT>(a[i], OP >= 2 ? b[i] : a[i], s));
 }
 
 }  // namespace
@@ -46,8 +63,8 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
                      int blocks, hipStream_t stream) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
-  int grid = blocks > 0 ? blocks : 2048;
-  const int64_t need = (n4 + 255) / 256;
+  int grid = blocks > 0 ? blocks : 2048;  // 8 x 256-thread WGs per CU
+  const int64_t need = (n4 + 256 * kUnroll - 1) / (256 * kUnroll);
   if (need < grid) grid = (int)need;
   if (grid < 1) grid = 1;
   auto A = reinterpret_cast<const float4*>(a);
