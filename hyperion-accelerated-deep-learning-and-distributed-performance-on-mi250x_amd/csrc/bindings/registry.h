@@ -8,4 +8,5 @@ void register_attn_ops(pybind11::module& m);
 void register_loss_ops(pybind11::module& m);
 void register_llama_ops(pybind11::module& m);
 void register_gemm_ops(pybind11::module& m);
+void register_comm(pybind11::module& m);
 }  // namespace hypbind

@@ -122,13 +122,18 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
         need_link = any(os.path.getmtime(o) > out_m for o in objs)
     if need_link:
         tmp = OUT + ".tmp"
+        # Link with plain clang++ (hipcc would append /opt/rocm's libamdhip64.so.7) and do NOT name
+        # the HIP runtime or RCCL at all: their symbols resolve at load time through libtorch_hip's
+        # own dependencies (torch/lib/libamdhip64.so, torch/lib/librccl.so).  The process then holds
+        # ONE HIP runtime and ONE RCCL — our kernels launch on torch's streams and our communicator
+        # shares torch's RCCL.  (Naming them here would add NEEDED libamdhip64.so.7 / librccl.so.1,
+        # which resolve to /opt/rocm's copies: a second runtime in the process.)
         cmd = (
-            [_hipcc(), "-shared", "-o", tmp]
+            [os.path.join(os.path.dirname(os.path.realpath(_hipcc())), "..", "lib", "llvm", "bin", "clang++"),
+             "-shared", "-o", tmp]
             + objs
-            + [f"--offload-arch={ARCH}", "-fPIC"]
-            + [f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}", "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"]
-            + ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
-            + [os.path.join(torch_lib, "librccl.so")]
+            + ["-fPIC", f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}"]
+            + ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python"]
         )
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -18,7 +18,7 @@ the view at the boundary — the reference's two ``permute`` copies per forward 
 packed QKV projection output is viewed as ``[B, S, 3, H, Dh]`` and handed straight to the
 flash-attention kernel (``ops.attention.attention_packed``: no split/permute/contiguous), the
 residual add is fused into the LayerNorm kernel (``ops.layernorm``), and the FFN's bias+activation
-rides the GEMM epilogue (``torch._addmm_activation`` → hipBLASLt epilogue) when available.
+rides the GEMM epilogue (``ops.linear_act``: ``torch._addmm_activation`` → hipBLASLt epilogue).
 Parameter names match ``nn.TransformerEncoderLayer`` / ``nn.TransformerEncoder`` exactly
 (``self_attn.in_proj_weight`` …, ``layers.N.…``) so reference checkpoints load unchanged.
 """
@@ -33,6 +33,7 @@ from torch.utils.checkpoint import checkpoint
 
 from ..ops.attention import attention_packed
 from ..ops.layernorm import LayerNorm
+from ..ops.linear_act import linear_act
 
 
 class MultiheadSelfAttention(nn.Module):
@@ -71,16 +72,8 @@ class MultiheadSelfAttention(nn.Module):
 
 
 def _ffn_up(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
-    """``act(x @ w.T + b)``; bias + activation fused into the GEMM epilogue on GPU."""
-    if x.is_cuda and b is not None and x.dim() >= 2:
-        x2 = x.reshape(-1, x.shape[-1])
-        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled() else x.dtype
-        if dt in (torch.bfloat16, torch.float16, torch.float32):
-            xc, wc, bc = x2.to(dt), w.to(dt), b.to(dt)
-            y = torch._addmm_activation(bc, xc, wc.t(), use_gelu=(activation == "gelu"))
-            return y.view(*x.shape[:-1], w.shape[0])
-    y = F.linear(x, w, b)
-    return F.gelu(y) if activation == "gelu" else F.relu(y)
+    """``act(x @ w.T + b)``; bias + ReLU ride the hipBLASLt epilogue on GPU (``ops.linear_act``)."""
+    return linear_act(x, w, b, activation)
 
 
 class TransformerEncoderLayer(nn.Module):

@@ -1,0 +1,52 @@
+"""Linear + bias + activation with the activation in the GEMM epilogue (hipBLASLt).
+
+Reference: every ``nn.TransformerEncoderLayer`` FFN runs ``linear1`` then ReLU/GELU as separate
+kernels (C14/C15/C5), and the ViT MLP likewise.  ``torch._addmm_activation`` asks hipBLASLt for the
+bias+ReLU (or bias+GELU) epilogue, so the activation costs no extra pass over the [tokens, ff]
+tensor — but it has no autograd formula.  ``linear_act`` wraps it:
+
+* ReLU: forward = one epilogue GEMM; backward masks with the saved OUTPUT (``h > 0`` ⇔ ``y > 0``),
+  so the pre-activation is never stored;
+* GELU: backward needs the pre-activation, so the forward keeps ``y = x Wᵀ + b`` (bias epilogue)
+  and applies GELU once (the fused epilogue would force a GEMM recompute in backward).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+
+def _cdt(x: torch.Tensor) -> torch.dtype:
+    return torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else x.dtype
+
+
+class _LinearReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        dt = _cdt(x)
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).to(dt)
+        wc, bc = w.to(dt), b.to(dt)
+        h = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
+        ctx.save_for_backward(x2, wc, h)
+        ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
+        return h.view(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, wc, h = ctx.saved_tensors
+        xdt, wdt, bdt, shape = ctx.meta
+        dy = torch.ops.aten.threshold_backward(dh.reshape(h.shape).to(h.dtype), h, 0)
+        dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
+        dw = (dy.t() @ x2).to(wdt) if ctx.needs_input_grad[1] else None
+        db = dy.sum(0, dtype=torch.float32).to(bdt) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
+    if activation == "relu" and x.is_cuda and b is not None:
+        return _LinearReLU.apply(x, w, b)
+    y = F.linear(x, w, b)
+    return F.gelu(y) if activation == "gelu" else F.relu(y)

@@ -27,6 +27,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..utils.nvtx import range_push, range_pop
+from .comm import get_comm
 
 
 def _flat_broadcast(tensors: List[torch.Tensor], src: int, group) -> None:
@@ -74,10 +75,16 @@ class DistributedDataParallel(nn.Module):
         comm_dtype: Optional[torch.dtype] = None,
         device_ids=None,  # accepted for API compatibility with torch DDP
         find_unused_parameters: bool = False,
+        comm=None,
     ):
         super().__init__()
         self.module = module
         self.process_group = process_group
+        # bucket all-reduces go through the comm layer: Hyperion's native RCCL communicator (own
+        # high-priority stream) on GPU, torch.distributed elsewhere (parallel/comm.py)
+        dev = next((p.device for p in module.parameters()), torch.device("cpu"))
+        self.comm = comm if comm is not None else (get_comm(dev, process_group) if dist.is_available()
+                                                   and dist.is_initialized() else None)
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
@@ -154,7 +161,7 @@ class DistributedDataParallel(nn.Module):
             if b.ready < len(b.params):
                 break
             range_push(f"ddp_allreduce_b{b.index}")
-            b.work = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.process_group, async_op=True)
+            b.work = self.comm.all_reduce(b.buf, "sum")
             range_pop()
             b.launched = True
             self._next_launch += 1

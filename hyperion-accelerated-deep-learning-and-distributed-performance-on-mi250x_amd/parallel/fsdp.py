@@ -47,6 +47,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.optim import clip_grad_norm_
+from .comm import get_comm
 
 
 # ------------------------------------------------------------------------------------ policies
@@ -162,7 +163,7 @@ class _FlatGroup:
             self.gathered = True
             return
         self._send = send
-        self.gather_work = dist.all_gather_into_tensor(out, send, group=self.fsdp.group, async_op=True)
+        self.gather_work = self.fsdp.comm.all_gather(out, send)
         if not async_op:
             self.wait_gather()
 
@@ -211,7 +212,7 @@ class _FlatGroup:
             self.rs_out, self.rs_work = buf, None
         else:
             self.rs_out = torch.empty(self.shard_numel, dtype=self.rdtype, device=buf.device)
-            self.rs_work = dist.reduce_scatter_tensor(self.rs_out, buf, group=self.fsdp.group, async_op=True)
+            self.rs_work = self.fsdp.comm.reduce_scatter(self.rs_out, buf, "sum")
 
     def finish_reduce(self) -> None:
         if not self.reduced:
@@ -304,12 +305,14 @@ class FullyShardedDataParallel(nn.Module):
         forward_prefetch: bool = True,
         backward_prefetch: bool = True,
         sync_module_states: bool = True,
+        comm=None,
     ):
         super().__init__()
         if sharding_strategy not in ("FULL_SHARD", "SHARD_GRAD_OP"):
             raise ValueError("sharding_strategy must be FULL_SHARD or SHARD_GRAD_OP (NO_SHARD = use DDP)")
         self.module = module
         self.group = process_group
+        self._comm = comm
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
         if device_id is None:
@@ -354,6 +357,13 @@ class FullyShardedDataParallel(nn.Module):
             for p in u.params:
                 if p.requires_grad:
                     self._handles.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
+
+    @property
+    def comm(self):
+        """AG / RS transport: native RCCL communicator on GPU, torch.distributed elsewhere."""
+        if self._comm is None:
+            self._comm = get_comm(self.device, self.group)
+        return self._comm
 
     # -- parameters the optimizer sees ------------------------------------------------------
     def parameters(self, recurse: bool = True) -> Iterator[nn.Parameter]:  # type: ignore[override]

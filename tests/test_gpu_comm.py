@@ -1,0 +1,66 @@
+"""Native RCCL communicator (csrc/comm/rccl_comm.cpp) on one GPU (world 1: every collective is an
+identity, which still exercises the bootstrap, the comm stream, event fencing and recordStream)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def pg():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+def test_native_comm_collectives_world1(pg):
+    from hyperion.ops import _native
+    from hyperion.parallel.comm import NativeComm
+
+    assert _native.native().rccl_version() > 0
+    c = NativeComm(torch.device("cuda", 0))
+    x = torch.arange(1024, device="cuda", dtype=torch.float32)
+    w = c.all_reduce(x, "sum")
+    w.wait()
+    torch.testing.assert_close(x, torch.arange(1024, device="cuda", dtype=torch.float32))
+    out = torch.empty(1024, device="cuda", dtype=torch.bfloat16)
+    c.all_gather(out, x.to(torch.bfloat16)).wait()
+    torch.testing.assert_close(out.float(), x)
+    rs = torch.empty(1024, device="cuda")
+    c.reduce_scatter(rs, x, "sum").wait()
+    torch.testing.assert_close(rs, x)
+    a2a = torch.empty_like(x)
+    c.all_to_all(a2a, x).wait()
+    torch.testing.assert_close(a2a, x)
+    ts = [torch.ones(10, device="cuda"), torch.full((7,), 2.0, device="cuda")]
+    c.all_reduce_coalesced(ts, "sum").synchronize()
+    assert ts[1].sum().item() == 14.0
+    c.barrier()
+    assert c.async_error() == ""
+    c.destroy()
+
+
+def test_native_comm_orders_against_compute_stream(pg):
+    # a producer kernel on the current stream, then the collective on the comm stream, then a
+    # consumer: the result must see the producer's data and the consumer must see the collective
+    from hyperion.parallel.comm import NativeComm
+
+    c = NativeComm(torch.device("cuda", 0))
+    x = torch.zeros(1 << 22, device="cuda")
+    for _ in range(20):
+        x.add_(1.0)  # queue work on the compute stream
+    w = c.all_reduce(x, "sum")
+    w.wait()
+    y = x * 2
+    torch.cuda.synchronize()
+    assert float(y[0]) == 40.0 and float(y[-1]) == 40.0
+    c.destroy()

@@ -16,7 +16,9 @@ def _run(graph: bool, steps: int):
     model = resnet18(num_classes=10).to(dev).to(memory_format=torch.channels_last)
     cast_for_compute(model, torch.bfloat16)
     init = [p.detach().float().clone() for p in model.parameters()]
-    opt = FusedAdam(model.parameters(), lr=1e-3)
+    # eps=1: update ~ lr*m (linear in the gradient), so MIOpen wgrad nondeterminism is not amplified
+    # into +-lr sign steps the way Adam does it for near-zero gradients
+    opt = FusedAdam(model.parameters(), lr=1e-2, eps=1.0)
     step = TrainStep(model, opt, torch.nn.MSELoss(), amp_dtype=None, graph=graph, warmup_iters=2)
     g = torch.Generator(device="cuda").manual_seed(1)
     x = torch.rand(8, 3, 64, 64, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -37,4 +39,4 @@ def test_graph_step_matches_eager():
     # +-lr steps, so compare the parameter UPDATES by norm: the replays must apply the same updates
     num = sum(float((a - b).norm() ** 2) for a, b in zip(de, dg)) ** 0.5
     den = sum(float(a.norm() ** 2) for a in de) ** 0.5
-    assert den > 0 and num <= 0.35 * den, (num, den)
+    assert den > 0 and num <= 0.1 * den, (num, den)
