@@ -108,3 +108,19 @@ bool gemm_nt_supported(int M, int N, int K, int lda, int ldb, int bk);
 hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, void* C, int M, int N, int K, int lda,
                    int ldb, int ldc, float alpha, int bk, hipStream_t st);
 }  // namespace hyp
+
+namespace hyp {
+// ---- conv_igemm.hip --------------------------------------------------------------------------
+// NHWC implicit-GEMM conv (bf16/f16), optional BN-statistics epilogue (psum/psq: [ceil(M/bm), K]).
+bool conv_fwd_supported(int C, int K);
+void conv_fwd_tile(int M, int K, int* bm, int* bn);
+hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
+                    int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
+                    int bm, int bn, hipStream_t st);
+// ---- bn_act.hip (conv-epilogue statistics) ---------------------------------------------------
+hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                                    const float* weight, const float* bias, float* running_mean, float* running_var,
+                                    float momentum, float eps, int act, const float* psum, const float* psq, int P,
+                                    float* save_mean, float* save_invstd, float* scale, float* shift,
+                                    hipStream_t stream);
+}  // namespace hyp

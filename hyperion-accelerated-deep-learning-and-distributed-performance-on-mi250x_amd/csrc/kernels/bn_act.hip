@@ -498,3 +498,39 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
 }
 
 }  // namespace hyp
+
+namespace hyp {
+// Training-mode BN forward whose per-channel partial sums were produced elsewhere (the conv
+// epilogue of conv_igemm.hip: one partial row per M-tile) — finalize + apply only, no statistics
+// pass over x.
+hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                                    const float* weight, const float* bias, float* running_mean, float* running_var,
+                                    float momentum, float eps, int act, const float* psum, const float* psq, int P,
+                                    float* save_mean, float* save_invstd, float* scale, float* shift,
+                                    hipStream_t stream) {
+  BnGeom ga;
+  if (!bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum, psq,
+                     P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale,
+                     shift);
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    const T* xt = static_cast<const T*>(x);
+    const T* rt = static_cast<const T*>(res);
+    T* yt = static_cast<T*>(y);
+    const dim3 grid(ga.P, ga.gy);
+    if (act && res)
+      hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+    else if (act)
+      hipLaunchKernelGGL((bn_apply_k<T, true, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+    else if (res)
+      hipLaunchKernelGGL((bn_apply_k<T, false, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+    else
+      hipLaunchKernelGGL((bn_apply_k<T, false, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
+                         ga.tpr, ga.rpi, ga.rows_per_block);
+  });
+  return hipGetLastError();
+}
+}  // namespace hyp

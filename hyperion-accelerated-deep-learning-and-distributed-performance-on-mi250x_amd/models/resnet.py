@@ -19,6 +19,12 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import conv_bn_act
+
+
+def _downsample(ds: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """``downsample = Sequential(conv1x1, BatchNormAct2d)`` (torchvision keys ``downsample.0/1``)."""
+    return conv_bn_act(ds[0], ds[1], x)
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -42,9 +48,9 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), residual=identity)
+        identity = x if self.downsample is None else _downsample(self.downsample, x)
+        out = conv_bn_act(self.conv1, self.bn1, x)
+        return conv_bn_act(self.conv2, self.bn2, out, residual=identity)
 
 
 class Bottleneck(nn.Module):
@@ -63,10 +69,10 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=identity)
+        identity = x if self.downsample is None else _downsample(self.downsample, x)
+        out = conv_bn_act(self.conv1, self.bn1, x)
+        out = conv_bn_act(self.conv2, self.bn2, out)
+        return conv_bn_act(self.conv3, self.bn3, out, residual=identity)
 
 
 class ResNet(nn.Module):
@@ -113,7 +119,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(conv_bn_act(self.conv1, self.bn1, x))
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

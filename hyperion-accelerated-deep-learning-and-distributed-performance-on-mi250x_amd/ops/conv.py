@@ -1,0 +1,112 @@
+"""Convolution + BatchNorm (+ residual) (+ ReLU) on the gfx950 implicit-GEMM kernel.
+
+Reference: every ResNet ``conv → bn → relu`` (and ``conv → bn → += identity → relu``) ran as a
+MIOpen convolution plus a MIOpen BN (statistics pass, normalize pass) plus separate ReLU / add
+kernels (``baseline_performance.ipynb:203-205``, torchvision ResNet-18 in ``distributed_utils.py:229``;
+SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
+
+``conv_bn_act(conv, bn, x, residual)`` (training mode, bf16/f16 channels-last):
+
+* forward  — ``csrc/kernels/conv_igemm.hip`` computes the convolution on MFMA AND the per-channel
+  Σy, Σy² of its (rounded) outputs in the epilogue; BN then only finalizes the statistics and runs
+  one apply pass with the residual add and ReLU folded in (``bn_act.hip``).  The separate BN
+  statistics read of the conv output is gone.
+* backward — the fused BN/ReLU/residual backward (``bn_act.hip``) produces dconv; the data
+  gradient of a stride-1 convolution is the same implicit-GEMM kernel run on dconv with the
+  flipped, channel-transposed filter; a 1x1 stride-1 weight gradient is one GEMM
+  (``dW = dYᵀ X``); strided data gradients and k x k weight gradients use the vendor kernels
+  (``aten.convolution_backward``).
+
+Anything outside the kernel's envelope (fp32, C % 64 != 0 such as the RGB stem, groups, dilation,
+eval mode) falls back to ``bn(conv(x), residual)`` — the same math.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import _native
+
+
+def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    w = conv.weight
+    return (
+        x.is_cuda
+        and x.dim() == 4
+        and x.dtype in (torch.bfloat16, torch.float16)
+        and w.dtype == x.dtype
+        and conv.groups == 1
+        and tuple(conv.dilation) == (1, 1)
+        and conv.bias is None
+        and isinstance(conv.padding, tuple)
+        and x.shape[1] % 64 == 0
+        and w.shape[0] % 8 == 0
+        and x.is_contiguous(memory_format=torch.channels_last)
+        and w.is_contiguous(memory_format=torch.channels_last)
+    )
+
+
+def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+    R, S = w.shape[2], w.shape[3]
+    if tuple(stride) == (1, 1) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0:
+        # dX = conv(dY, flip(W) with C <-> K), stride 1, padding R-1-p
+        wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        dx, _, _ = _native.native().conv_fwd(dyc, wt, 1, 1, R - 1 - padding[0], S - 1 - padding[1], False)
+        return dx
+    return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                                               [True, False, False])[0]
+
+
+def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+    K, C, R, S = w.shape
+    if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(padding) == (0, 0):
+        dy2 = dy.permute(0, 2, 3, 1).reshape(-1, K)  # channels-last: a free view
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+        return (dy2.t() @ x2).view(K, C, 1, 1).contiguous(memory_format=torch.channels_last)
+    return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
+
+
+class _ConvBNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act):
+        C = _native.native()
+        yc, psum, psq = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True)
+        if residual is not None:
+            residual = residual.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        out, mean, invstd = C.bn_fwd_partials(yc, residual, psum, psq, bn_w, bn_b, rm, rv, momentum, eps, act)
+        ctx.save_for_backward(x, w, yc, out if act else None, bn_w, mean, invstd)
+        ctx.cfg = (stride, padding, act, residual is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, yc, out, bn_w, mean, invstd = ctx.saved_tensors
+        stride, padding, act, has_res = ctx.cfg
+        need_res = has_res and ctx.needs_input_grad[6]
+        dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, mean, invstd, True, act, need_res)
+        dx = _dgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[0] else None
+        dw = _wgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[1] else None
+        return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
+                dres if need_res else None, None, None, None, None, None)
+
+
+def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``bn(conv(x), residual)`` for a ``BatchNormAct2d`` ``bn``; fused on gfx950 when possible."""
+    use = (
+        bn.training
+        and bn.track_running_stats
+        and bn.momentum is not None
+        and bn.affine
+        and _native.use_native(x, op="conv")
+        and _native.use_native(x, op="bn")
+        and _native_conv_ok(x, conv)
+    )
+    if not use:
+        return bn(conv(x), residual=residual)
+    bn._host_batches += 1  # BatchNormAct2d's host-side num_batches_tracked mirror
+    return _ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
+                              tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act))
