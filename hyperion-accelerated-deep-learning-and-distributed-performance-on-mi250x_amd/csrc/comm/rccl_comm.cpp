@@ -7,7 +7,7 @@
 //  * the communicator is a raw ncclComm_t (RCCL — the same librccl.so torch loads, so one RCCL
 //    per process), bootstrapped from an ncclUniqueId that Python shares through the torchrun
 //    TCPStore (env:// rendezvous);
-//  * every collective runs on the communicator's own stream, created at the highest priority so
+//  * every collective runs on a highest-priority stream from torch's stream pool, so
 //    bucket all-reduces / FSDP all-gathers are not starved by compute kernels; the comm stream
 //    waits on an event recorded on the caller's current stream (inputs ready), and `wait()` makes
 //    the caller's current stream wait on the completion event — the host never blocks;
@@ -85,9 +85,11 @@ class RcclComm {
     ncclUniqueId id;
     memcpy(&id, uid_bytes.data(), sizeof(id));
     const at::DeviceGuard g(at::Device(at::kCUDA, device_));
-    int lo = 0, hi = 0;
-    HYP_CHECK_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HYP_CHECK_HIP(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));  // hi = greatest priority
+    // a HIGH-priority stream from torch's own pool: it outlives this communicator, so the caching
+    // allocator's recordStream bookkeeping (events recorded on this stream when a tensor used by a
+    // collective is freed) can never touch a destroyed stream
+    stream_obj_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_);
+    stream_ = stream_obj_.stream();
     HYP_CHECK_NCCL(ncclCommInitRank(&comm_, world_, id, rank_));
   }
   ~RcclComm() { destroy(); }
@@ -98,7 +100,7 @@ class RcclComm {
       comm_ = nullptr;
     }
     if (stream_) {
-      (void)hipStreamDestroy(stream_);
+      (void)hipStreamSynchronize(stream_);  // pooled stream: drained, never destroyed
       stream_ = nullptr;
     }
   }
@@ -201,8 +203,7 @@ class RcclComm {
     HYP_CHECK_HIP(hipEventRecord(ready, cur.stream()));
     HYP_CHECK_HIP(hipStreamWaitEvent(stream_, ready, 0));
     HYP_CHECK_HIP(hipEventDestroy(ready));  // destruction is deferred until the wait is satisfied
-    auto hs = c10::hip::getStreamFromExternal(stream_, device_);
-    for (auto& t : ts) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), hs);
+    for (auto& t : ts) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_obj_);
   }
 
   std::shared_ptr<Work> end() {
@@ -213,6 +214,7 @@ class RcclComm {
   }
 
   ncclComm_t comm_ = nullptr;
+  c10::hip::HIPStream stream_obj_ = c10::hip::getDefaultHIPStream();
   hipStream_t stream_ = nullptr;
   int rank_, world_, device_;
 };

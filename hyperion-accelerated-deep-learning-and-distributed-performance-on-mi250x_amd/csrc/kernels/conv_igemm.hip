@@ -170,7 +170,13 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue: acc[i][j][e] -> out[m0 + wm*BM/2 + i*16 + c4*4 + e][n0 + wn*BN/2 + j*16 + r16]
+  // ---- epilogue.  acc[i][j][e] is out[m0 + wm*BM/2 + i*16 + c4*4 + e][n0 + wn*BN/2 + j*16 + r16].
+  // Values are rounded to T once; the BN statistics use the rounded values (what BN will read),
+  // and the tile is transposed through LDS so the global stores are whole 16-byte row chunks
+  // (a raw accumulator store would be 2-byte scattered writes).
+  constexpr int kLd = BN + 8;  // padded LDS row (elements)
+  uint16_t* tile = smem;       // [BM][kLd] of T (the K loop ended with a barrier: smem is free)
+  float* red = reinterpret_cast<float*>(smem + BM * kLd);  // [2 (wm)][2 (sum, sq)][BN]
   float csum[FN], csq[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) csum[j] = csq[j] = 0.f;
@@ -178,19 +184,16 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int m = m0 + wm * (BM / 2) + i * 16 + c4 * 4 + e;
-      if (m >= a.M) continue;
-      T* orow = reinterpret_cast<T*>(a.out) + (int64_t)m * a.K;
+      const int lr = wm * (BM / 2) + i * 16 + c4 * 4 + e;
+      const bool row_ok = m0 + lr < a.M;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int k = n0 + wn * (BN / 2) + j * 16 + r16;
-        if (k < a.K) {
-          const float v = rnd<T>(acc[i][j][e]);
-          st1<T>(orow + k, v);
-          if (STATS) {
-            csum[j] += v;
-            csq[j] += v * v;
-          }
+        const int lc = wn * (BN / 2) + j * 16 + r16;
+        const float v = rnd<T>(acc[i][j][e]);
+        st1<T>(reinterpret_cast<T*>(tile) + lr * kLd + lc, v);
+        if (STATS && row_ok) {
+          csum[j] += v;
+          csq[j] += v * v;
         }
       }
     }
@@ -204,8 +207,6 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       csq[j] += __shfl_xor(csq[j], 16, 64);
       csq[j] += __shfl_xor(csq[j], 32, 64);
     }
-    // combine the two M-waves through LDS (the K loop ended with a barrier: smem is free)
-    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2 (sum, sq)][BN]
     if (c4 == 0) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -214,13 +215,24 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
         red[(wm * 2 + 1) * BN + col] = csq[j];
       }
     }
-    __syncthreads();
-    if (tid < BN) {
-      const int k = n0 + tid;
-      if (k < a.K) {
-        a.psum[(int64_t)tm * a.K + k] = red[0 * BN + tid] + red[2 * BN + tid];
-        a.psq[(int64_t)tm * a.K + k] = red[1 * BN + tid] + red[3 * BN + tid];
-      }
+  }
+  __syncthreads();
+  constexpr int kChunksPerRow = BN / 8;
+#pragma unroll
+  for (int it = 0; it < BM * kChunksPerRow / kThreads; ++it) {
+    const int idx = it * kThreads + tid;
+    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
+    const int m = m0 + lr, k = n0 + ch * 8;
+    if (m < a.M && k < a.K) {
+      const uint4 v = *reinterpret_cast<const uint4*>(tile + lr * kLd + ch * 8);
+      *reinterpret_cast<uint4*>(a.out + (int64_t)m * a.K + k) = v;
+    }
+  }
+  if (STATS && tid < BN) {
+    const int k = n0 + tid;
+    if (k < a.K) {
+      a.psum[(int64_t)tm * a.K + k] = red[0 * BN + tid] + red[2 * BN + tid];
+      a.psq[(int64_t)tm * a.K + k] = red[1 * BN + tid] + red[3 * BN + tid];
     }
   }
 }
