@@ -41,15 +41,20 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, const c10::optional<at::Tens
 }
 
 // returns (dx, dres or undefined, dweight, dbias)
+// y may be None with act (training, no residual): the ReLU mask is recomputed from x, weight, bias
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& y,
-                               const c10::optional<at::Tensor>& weight, const at::Tensor& save_mean,
-                               const at::Tensor& save_invstd, bool training, bool act, bool has_res) {
+                               const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
+                               const at::Tensor& save_mean, const at::Tensor& save_invstd, bool training, bool act,
+                               bool has_res) {
   HYP_CHECK_CUDA_TENSOR(x);
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd: dy shape mismatch");
   at::Tensor dyc = is_rows_by_channels(dy) ? dy : (dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous());
-  if (act) TORCH_CHECK(y.has_value() && is_rows_by_channels(*y), "bn_bwd: act needs the forward output");
+  const bool have_y = y.has_value() && y->defined();
+  if (act && have_y) TORCH_CHECK(is_rows_by_channels(*y), "bn_bwd: y must be channels-last");
+  if (act && !have_y)
+    TORCH_CHECK(training && !has_res, "bn_bwd: the mask-from-x backward (y=None) is training-mode, non-residual");
   const at::DeviceGuard guard(x.device());
   auto dx = at::empty_like(x);
   at::Tensor dres;
@@ -60,9 +65,10 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const 
   auto ws = at::empty({2 * (int64_t)P * C + 3 * C}, fopt);
   float* base = ws.data_ptr<float>();
   auto dwb = at::empty({2, C}, fopt);
-  HYP_CHECK_HIP(hyp::bn_backward(dtype_code(x), dyc.data_ptr(), x.data_ptr(), act ? y->data_ptr() : nullptr,
+  HYP_CHECK_HIP(hyp::bn_backward(dtype_code(x), dyc.data_ptr(), x.data_ptr(), (act && have_y) ? y->data_ptr() : nullptr,
                                  dx.data_ptr(), has_res ? dres.data_ptr() : nullptr, M, (int)C,
-                                 ptr_or_null<float>(weight), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                                 ptr_or_null<float>(weight), ptr_or_null<float>(bias), save_mean.data_ptr<float>(),
+                                 save_invstd.data_ptr<float>(),
                                  training ? 1 : 0, act ? 1 : 0, base + 3 * C, base + 3 * C + (int64_t)P * C,
                                  dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, base, base + C, base + 2 * C,
                                  cur_stream()));

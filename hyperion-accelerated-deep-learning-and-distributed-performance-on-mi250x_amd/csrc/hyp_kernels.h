@@ -12,10 +12,11 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
                       const float* bias, float* running_mean, float* running_var, float momentum, float eps,
                       int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
                       float* scale, float* shift, hipStream_t stream);
+// y == nullptr with act: the ReLU mask is recomputed from x (training, no residual gradient only)
 hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
-                       const float* weight, const float* save_mean, const float* save_invstd, int training, int act,
-                       float* pdz, float* pdzx, float* dweight, float* dbias, float* kA, float* kB, float* kC,
-                       hipStream_t stream);
+                       const float* weight, const float* bias, const float* save_mean, const float* save_invstd,
+                       int training, int act, float* pdz, float* pdzx, float* dweight, float* dbias, float* kA,
+                       float* kB, float* kC, hipStream_t stream);
 
 // ---- adam.hip ------------------------------------------------------------------------------
 // param_dtype kF32: ptrs = [param, grad, m, v]; kBF16/kF16: ptrs = [lowp param, grad, m, v, fp32 master]

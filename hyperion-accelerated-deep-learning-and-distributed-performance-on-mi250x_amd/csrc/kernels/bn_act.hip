@@ -266,11 +266,36 @@ __global__ __launch_bounds__(kBlock) void bn_apply_k(const T* __restrict__ x, co
 }
 
 // ---------------------------------------------------------------- backward
-template <typename T, bool ACT>
+// ReLU mask of the forward output.  MASKX: recomputed from x as x*scale + shift > 0 with the
+// forward's exact float scale/shift (scale = w*invstd, shift = b - mean*scale, the finalize
+// kernel's arithmetic), so the non-residual backward never reads y (one stream less).
+template <typename T, bool ACT, bool MASKX>
+struct ReluMask {
+  float sc[8], sh[8];
+  __device__ __forceinline__ void init(const float* w, const float* b, const float* mean, const float* invstd, int c0) {
+    if (MASKX) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float s = (w ? w[c0 + j] : 1.f) * invstd[c0 + j];
+        sc[j] = s;
+        sh[j] = (b ? b[c0 + j] : 0.f) - mean[c0 + j] * s;
+      }
+    }
+  }
+  __device__ __forceinline__ bool keep(const float (&xv)[8], const float (&yv)[8], int j) const {
+    if (!ACT) return true;
+    if (MASKX) return fmaf(xv[j], sc[j], sh[j]) > 0.f;
+    return yv[j] > 0.f;
+  }
+};
+
+template <typename T, bool ACT, bool MASKX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ y, int64_t M, int C, int tpr, int rpi,
                                                           int64_t rpb, float* __restrict__ pdz,
-                                                          float* __restrict__ pdzx) {
+                                                          float* __restrict__ pdzx, const float* __restrict__ w,
+                                                          const float* __restrict__ b, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd) {
   __shared__ float ls[kBlock * 8];
   __shared__ float lq[kBlock * 8];
   const int tid = threadIdx.x;
@@ -281,6 +306,8 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ 
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  ReluMask<T, ACT, MASKX> mk;
+  if (r < rpi) mk.init(w, b, mean, invstd, cbase + c8 * 8);
   if (r < rpi) {
     const int64_t step = (int64_t)rpi * C;
     int64_t off = (row0 + r) * C + cbase + c8 * 8;
@@ -291,14 +318,14 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ 
       Vec8<T>::load(dy + off + step, g1);
       Vec8<T>::load(x + off, x0);
       Vec8<T>::load(x + off + step, x1);
-      if (ACT) {
+      if (ACT && !MASKX) {
         Vec8<T>::load(y + off, y0);
         Vec8<T>::load(y + off + step, y1);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d0 = (!ACT || y0[j] > 0.f) ? g0[j] : 0.f;
-        const float d1 = (!ACT || y1[j] > 0.f) ? g1[j] : 0.f;
+        const float d0 = mk.keep(x0, y0, j) ? g0[j] : 0.f;
+        const float d1 = mk.keep(x1, y1, j) ? g1[j] : 0.f;
         s[j] += d0 + d1;
         q[j] += d0 * x0[j] + d1 * x1[j];
       }
@@ -307,10 +334,10 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ 
       float g[8], xv[8], yv[8];
       Vec8<T>::load(dy + off, g);
       Vec8<T>::load(x + off, xv);
-      if (ACT) Vec8<T>::load(y + off, yv);
+      if (ACT && !MASKX) Vec8<T>::load(y + off, yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = (!ACT || yv[j] > 0.f) ? g[j] : 0.f;
+        const float d = mk.keep(xv, yv, j) ? g[j] : 0.f;
         s[j] += d;
         q[j] += d * xv[j];
       }
@@ -376,16 +403,21 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(const float* __restrict
   }
 }
 
-template <typename T, bool ACT, bool RES>
+template <typename T, bool ACT, bool RES, bool MASKX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const T* __restrict__ y, T* __restrict__ dx,
                                                       T* __restrict__ dres, const float* __restrict__ kA,
                                                       const float* __restrict__ kB, const float* __restrict__ kC,
-                                                      int64_t M, int C, int tpr, int rpi, int64_t rpb) {
+                                                      int64_t M, int C, int tpr, int rpi, int64_t rpb,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd) {
   const int tid = threadIdx.x;
   const int r = tid / tpr, c8 = tid - r * tpr;
   if (r >= rpi) return;
   const int c0 = blockIdx.y * tpr * 8 + c8 * 8;
+  ReluMask<T, ACT, MASKX> mk;
+  mk.init(w, b, mean, invstd, c0);
   float A[8], B[8], Cc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -401,10 +433,10 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, 
     float g[8], xv[8], yv[8];
     Vec8<T>::load(dy + off, g);
     Vec8<T>::load(x + off, xv);
-    if (ACT) Vec8<T>::load(y + off, yv);
+    if (ACT && !MASKX) Vec8<T>::load(y + off, yv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d = (!ACT || yv[j] > 0.f) ? g[j] : 0.f;
+      const float d = mk.keep(xv, yv, j) ? g[j] : 0.f;
       g[j] = d;
       xv[j] = fmaf(A[j], d, fmaf(B[j], xv[j], Cc[j]));
     }
@@ -459,40 +491,54 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
   return hipGetLastError();
 }
 
+template <typename T>
+void launch_bn_dx(bool maskx, bool act, bool res, dim3 grid, hipStream_t stream, const T* dy, const T* x, const T* y,
+                  T* dx, T* dres, const float* kA, const float* kB, const float* kC, int64_t M, int C,
+                  const BnGeom& ga, const float* w, const float* b, const float* mean, const float* invstd) {
+#define HYP_BN_DX(ACTV, RESV, MX)                                                                                 \
+  hipLaunchKernelGGL((bn_bwd_dx_k<T, ACTV, RESV, MX>), grid, dim3(kBlock), 0, stream, dy, x, y, dx, dres, kA, kB, \
+                     kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block, w, b, mean, invstd)
+  if (maskx)
+    HYP_BN_DX(true, false, true);
+  else if (act && res)
+    HYP_BN_DX(true, true, false);
+  else if (act)
+    HYP_BN_DX(true, false, false);
+  else if (res)
+    HYP_BN_DX(false, true, false);
+  else
+    HYP_BN_DX(false, false, false);
+#undef HYP_BN_DX
+}
+
 hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
-                       const float* weight, const float* save_mean, const float* save_invstd, int training, int act,
-                       float* pdz, float* pdzx, float* dweight, float* dbias, float* kA, float* kB, float* kC,
-                       hipStream_t stream) {
+                       const float* weight, const float* bias, const float* save_mean, const float* save_invstd,
+                       int training, int act, float* pdz, float* pdzx, float* dweight, float* dbias, float* kA,
+                       float* kB, float* kC, hipStream_t stream) {
   BnGeom gs, ga;
   if (!bn_geom(M, C, kStatsBlocks, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  // act with no forward output given: recompute the ReLU mask from x (training stats only: the
+  // eval-mode constants are running stats, which the mask recomputation below does not model)
+  const bool maskx = act && y == nullptr;
+  if (maskx && (!training || dres != nullptr)) return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     const T* dyt = static_cast<const T*>(dy);
     const T* xt = static_cast<const T*>(x);
     const T* yt = static_cast<const T*>(y);
     const dim3 grs(gs.P, gs.gy);
-    if (act)
-      hipLaunchKernelGGL((bn_bwd_reduce_k<T, true>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr, gs.rpi,
-                         gs.rows_per_block, pdz, pdzx);
-    else
-      hipLaunchKernelGGL((bn_bwd_reduce_k<T, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr, gs.rpi,
-                         gs.rows_per_block, pdz, pdzx);
-    hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, pdz, pdzx, gs.P, C, M, weight,
-                       save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
-    const dim3 gra(ga.P, ga.gy);
-    T* dxt = static_cast<T*>(dx);
-    T* drt = static_cast<T*>(dres);
-    if (act && dres)
-      hipLaunchKernelGGL((bn_bwd_dx_k<T, true, true>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB, kC,
-                         M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+    if (maskx)
+      hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, true>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
+                         gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
     else if (act)
-      hipLaunchKernelGGL((bn_bwd_dx_k<T, true, false>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB,
-                         kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block);
-    else if (dres)
-      hipLaunchKernelGGL((bn_bwd_dx_k<T, false, true>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB,
-                         kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+      hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
+                         gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
     else
-      hipLaunchKernelGGL((bn_bwd_dx_k<T, false, false>), gra, dim3(kBlock), 0, stream, dyt, xt, yt, dxt, drt, kA, kB,
-                         kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block);
+      hipLaunchKernelGGL((bn_bwd_reduce_k<T, false, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
+                         gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
+    hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, pdz, pdzx,
+                       gs.P, C, M, weight, save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
+    launch_bn_dx<T>(maskx, act, dres != nullptr, dim3(ga.P, ga.gy), stream, dyt, xt, yt, static_cast<T*>(dx),
+                    static_cast<T*>(dres), kA, kB, kC, M, C, ga, weight, bias, save_mean, save_invstd);
   });
   return hipGetLastError();
 }

@@ -252,7 +252,9 @@ hipError_t launch(const ConvArgs& a, bool stats, hipStream_t st) {
 // Tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), else 64 x 64.
 void conv_fwd_tile(int M, int K, int* bm, int* bn) {
   auto tiles = [&](int m, int n) { return (int64_t)((M + m - 1) / m) * ((K + n - 1) / n); };
-  if (tiles(128, 128) >= 512) {
+  if (K <= 64) {  // a 128-wide tile would compute half zeros
+    *bm = tiles(128, 64) >= 256 ? 128 : 64, *bn = 64;
+  } else if (tiles(128, 128) >= 512) {
     *bm = 128, *bn = 128;
   } else if (K <= 64 || tiles(128, 64) >= 512) {
     *bm = 128, *bn = 64;

@@ -70,15 +70,18 @@ class _BNActFn(torch.autograd.Function):
         ctx.act = act
         ctx.training = training
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if act else None, weight, mean, invstd)
+        # training without a residual: the backward recomputes the ReLU mask from x (one stream
+        # fewer to read); otherwise it needs the forward output
+        keep_y = act and (residual is not None or not training)
+        ctx.save_for_backward(x, y if keep_y else None, weight, bias, mean, invstd)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, y, weight, bias, mean, invstd = ctx.saved_tensors
         need_res = ctx.has_res and ctx.needs_input_grad[1]
         dx, dres, dw, db = _native.native().bn_bwd(
-            dy, x, y, weight, mean, invstd, ctx.training, ctx.act, need_res
+            dy, x, y, weight, bias, mean, invstd, ctx.training, ctx.act, need_res
         )
         return (
             dx if ctx.needs_input_grad[0] else None,

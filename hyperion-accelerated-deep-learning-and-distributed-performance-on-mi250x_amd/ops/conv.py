@@ -61,11 +61,8 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) 
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
-    K, C, R, S = w.shape
-    if R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(padding) == (0, 0):
-        dy2 = dy.permute(0, 2, 3, 1).reshape(-1, K)  # channels-last: a free view
-        x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
-        return (dy2.t() @ x2).view(K, C, 1, 1).contiguous(memory_format=torch.channels_last)
+    # (A 1x1 weight gradient is the GEMM dYᵀ·X with a 10⁵-long reduction; hipBLASLt runs it on a
+    # handful of workgroups without split-K — 10x slower than the vendor conv path, measured.)
     return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
 
@@ -78,16 +75,17 @@ class _ConvBNActFn(torch.autograd.Function):
         if residual is not None:
             residual = residual.to(x.dtype).contiguous(memory_format=torch.channels_last)
         out, mean, invstd = C.bn_fwd_partials(yc, residual, psum, psq, bn_w, bn_b, rm, rv, momentum, eps, act)
-        ctx.save_for_backward(x, w, yc, out if act else None, bn_w, mean, invstd)
+        # without a residual the backward recomputes the ReLU mask from yc (no need to keep `out`)
+        ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, w, yc, out, bn_w, mean, invstd = ctx.saved_tensors
+        x, w, yc, out, bn_w, bn_b, mean, invstd = ctx.saved_tensors
         stride, padding, act, has_res = ctx.cfg
         need_res = has_res and ctx.needs_input_grad[6]
-        dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, mean, invstd, True, act, need_res)
+        dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res)
         dx = _dgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[1] else None
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,

@@ -32,6 +32,12 @@ def _dense(t: torch.Tensor) -> bool:
     return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 
 
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same element order in memory (strides of size-1 dims are irrelevant: a [K, C, 1, 1] weight is
+    'contiguous' and 'channels-last' at once, and autograd may hand back either stride set)."""
+    return a.shape == b.shape and all(sa == sb for sa, sb, n in zip(a.stride(), b.stride(), a.shape) if n > 1)
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(
         self,
@@ -88,7 +94,7 @@ class FusedAdam(torch.optim.Optimizer):
                 vs = [s["exp_avg_sq"] for s in sts]
                 masters = [s["master"] for s in sts] if pdt != torch.float32 else None
                 ok = native and pdt in _native.DTYPE_CODE and gdt in _native.DTYPE_CODE and all(
-                    _dense(p) and p.stride() == g.stride() == m.stride() for p, g, m in zip(ps, gs, ms)
+                    _dense(p) and _dense(g) and _same_layout(p, g) and _same_layout(p, m) for p, g, m in zip(ps, gs, ms)
                 )
                 if ok:
                     groups = [ps, gs, ms, vs] + ([masters] if masters is not None else [])

@@ -140,6 +140,6 @@ def test_linear_act_matches_reference(act):
     yr = F.linear(xr, wr, br)
     yr = F.relu(yr) if act == "relu" else F.gelu(yr)
     yr.square().sum().backward()
-    torch.testing.assert_close(y.float(), yr, rtol=3e-2, atol=3e-2)
+    assert (y.float() - yr).norm() <= 2e-2 * yr.norm()
     for a, r in ((x, xr), (w, wr), (b, br)):
         assert (a.grad.float() - r.grad).norm() <= 0.03 * r.grad.norm()
