@@ -24,7 +24,7 @@ def _timeit(step, steps: int, warmup: int) -> float:
 
 
 def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", steps: int = 20, warmup: int = 5,
-                  model: str = "lm256", causal: bool = False) -> Dict:
+                  model: str = "lm256", causal: bool = False, graph: bool = False) -> Dict:
     """SimpleTransformerLM (C14) training step as in train_language_model_ddp (single GPU)."""
     from ..data.synthetic import SyntheticWikiText2
     from ..models.simple_lm import GPT2_PAD, gpt2_small_lm, simple_lm_256
@@ -40,8 +40,8 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
     ids = SyntheticWikiText2(n=batch, seq_len=seq, seed=0).input_ids.to(dev)
     x, y = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
 
-    def step():
-        opt.zero_grad(set_to_none=True)
+    def body():
+        opt.zero_grad(set_to_none=not graph)
         with torch.autocast("cuda", dtype=dt or torch.float32, enabled=dt is not None):
             loss = m.forward_loss(x, y, ignore_index=GPT2_PAD)
         if scaler.enabled:
@@ -51,10 +51,14 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
         else:
             loss.backward()
             opt.step()
+        return loss.detach()
 
+    from ..train.step import GraphedClosure
+
+    step = GraphedClosure(body, warmup=2) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
-    return {"model": model, "batch": batch, "seq": seq, "precision": precision, "ms_per_step": t * 1e3,
+    return {"model": model, "batch": batch, "seq": seq, "precision": precision, "graph": graph, "ms_per_step": t * 1e3,
             "samples_per_s": batch / t, "tokens_per_s": batch * (seq - 1) / t,
             "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
@@ -90,7 +94,7 @@ def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool
 
 
 def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmup: int = 3, lora: bool = True,
-                          config=None, grad_ckpt: bool = False) -> Dict:
+                          config=None, grad_ckpt: bool = False, graph: bool = True) -> Dict:
     """Llama-2-7B (random init) LoRA r16 bf16 step, batch 1 x 128 tokens (the reference's Llama run)."""
     from ..data.synthetic import SyntheticWikiText2
     from ..models.llama import LlamaConfig, LlamaForCausalLM
@@ -112,18 +116,22 @@ def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmu
     ids = (ds.input_ids % cfg.vocab_size).to(dev)
     mask = ds.attention_mask.to(dev)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
+    from ..ops.optim import clip_grad_norm_
+    from ..train.step import GraphedClosure
+
+    def body():
+        opt.zero_grad(set_to_none=not graph)
         loss = m(ids, attention_mask=mask, labels=ids).loss
         loss.backward()
-        from ..ops.optim import clip_grad_norm_
-
         clip_grad_norm_(params, 1.0)
         opt.step()
+        return loss.detach()
 
+    step = GraphedClosure(body, warmup=2) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
-    return {"model": "llama2_7b" if config is None else "llama_custom", "lora": lora, "batch": batch, "seq": seq,
+    return {"model": "llama2_7b" if config is None else "llama_custom", "lora": lora, "graph": graph, "batch": batch,
+            "seq": seq,
             "ms_per_step": t * 1e3, "samples_per_s": batch / t, "tokens_per_s": batch * seq / t,
             "trainable_params": trainable_parameters(m), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 

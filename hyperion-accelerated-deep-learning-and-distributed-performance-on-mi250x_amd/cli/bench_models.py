@@ -49,7 +49,10 @@ def main(argv=None) -> int:
 
         summary["lm256_fp16"] = bench_lm_step(precision="fp16")
         summary["lm256_bf16"] = bench_lm_step(precision="bf16")
-        print(summary["lm256_fp16"], summary["lm256_bf16"], flush=True)
+        summary["lm256_bf16_graph"] = bench_lm_step(precision="bf16", graph=True)
+        summary["gpt2_small_bf16_graph"] = bench_lm_step(precision="bf16", graph=True, model="gpt2_small", batch=16)
+        print(summary["lm256_fp16"], summary["lm256_bf16"], summary["lm256_bf16_graph"],
+              summary["gpt2_small_bf16_graph"], flush=True)
         dump()
     if "vit" in parts:
         from hyperion.bench.models import bench_vit_step
@@ -61,8 +64,9 @@ def main(argv=None) -> int:
     if "llama" in parts:
         from hyperion.bench.models import bench_llama_lora_step
 
-        summary["llama7b_lora_bf16"] = bench_llama_lora_step()
-        print(summary["llama7b_lora_bf16"], flush=True)
+        summary["llama7b_lora_bf16_graph"] = bench_llama_lora_step(graph=True)
+        summary["llama7b_lora_bf16_eager"] = bench_llama_lora_step(graph=False)
+        print(summary["llama7b_lora_bf16_graph"], summary["llama7b_lora_bf16_eager"], flush=True)
         dump()
     if "fusion" in parts:
         from hyperion.bench.fusion import run_fusion_benchmark

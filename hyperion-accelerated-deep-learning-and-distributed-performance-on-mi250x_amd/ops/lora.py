@@ -8,25 +8,24 @@ add) as 4-5 separate kernels with the dropped activations stored for backward (S
 
 * forward: base GEMM (hipBLASLt), ``t = s·drop(x)Aᵀ`` ([N, r] — tiny), then ``y += t Bᵀ`` as an
   in-place rank-r update (``addmm_`` with beta=1: no second [N, out] tensor);
-* backward: ``dx = dy W + (dy B · s) A∘mask``, ``dA = (s·dy B)ᵀ drop(x)``, ``dB = dyᵀ t``; the
-  dropout mask is regenerated from the saved seed (never stored), W never gets a gradient buffer.
+* backward: ``dx = dy W + (dy B · s) A∘mask``, ``dA = (s·dy B)ᵀ drop(x)``, ``dB = dyᵀ t``; W never
+  gets a gradient buffer.  The dropout keep-mask is drawn from the default device generator (so the
+  whole step stays hipGraph-capturable) and kept as uint8 for backward — at fine-tune shapes
+  (hundreds of tokens) that is a few hundred KB per projection.
 """
 from __future__ import annotations
 
-import itertools
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 
-_seed = itertools.count(1)
+def _keep_mask(x: torch.Tensor, p: float) -> torch.Tensor:
+    return torch.empty(x.shape, device=x.device, dtype=torch.float32).bernoulli_(1.0 - p).to(torch.uint8)
 
 
-def _mask(x: torch.Tensor, p: float, seed: int) -> torch.Tensor:
-    g = torch.Generator(device=x.device)
-    g.manual_seed(seed)
-    keep = torch.empty(x.shape, device=x.device, dtype=torch.float32).bernoulli_(1.0 - p, generator=g)
-    return (keep / (1.0 - p)).to(x.dtype)
+def _apply(x: torch.Tensor, keep: torch.Tensor, p: float) -> torch.Tensor:
+    return x * keep.to(x.dtype) * (1.0 / (1.0 - p))
 
 
 class _LoRAFn(torch.autograd.Function):
@@ -35,30 +34,30 @@ class _LoRAFn(torch.autograd.Function):
         cdt = torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else x.dtype
         xc, wc = x.to(cdt), w.to(cdt)
         ac, bc = a.to(cdt), bm.to(cdt)
-        seed = next(_seed) if p > 0 else 0
-        xd = xc * _mask(xc, p, seed) if p > 0 else xc
+        keep = _keep_mask(xc, p) if p > 0 else None
+        xd = _apply(xc, keep, p) if p > 0 else xc
         x2 = xc.reshape(-1, xc.shape[-1])
         t = (xd.reshape(-1, xd.shape[-1]) @ ac.t()) * scaling  # [N, r]
         y = F.linear(x2, wc, b.to(cdt) if b is not None else None)
         y.addmm_(t, bc.t())  # rank-r update in place
-        ctx.save_for_backward(xc, wc, ac, bc, t)
-        ctx.cfg = (scaling, p, seed, x.dtype, a.dtype, bm.dtype)
+        ctx.save_for_backward(xc, wc, ac, bc, t, keep)
+        ctx.cfg = (scaling, p, x.dtype, a.dtype, bm.dtype)
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        xc, wc, ac, bc, t = ctx.saved_tensors
-        scaling, p, seed, xdt, adt, bdt = ctx.cfg
+        xc, wc, ac, bc, t, keep = ctx.saved_tensors
+        scaling, p, xdt, adt, bdt = ctx.cfg
         dy2 = dy.reshape(-1, dy.shape[-1]).to(wc.dtype)
         dx = dA = dB = None
         dt = (dy2 @ bc) * scaling  # [N, r]
         if ctx.needs_input_grad[0]:
             dxd = dt @ ac  # grad wrt drop(x)
             if p > 0:
-                dxd = dxd * _mask(xc, p, seed).reshape(dxd.shape)
+                dxd = _apply(dxd, keep.reshape(dxd.shape), p)
             dx = torch.addmm(dxd, dy2, wc).view(xc.shape).to(xdt)
         if ctx.needs_input_grad[3]:
-            xd = xc * _mask(xc, p, seed) if p > 0 else xc
+            xd = _apply(xc, keep, p) if p > 0 else xc
             dA = (dt.t() @ xd.reshape(-1, xd.shape[-1])).to(adt)
         if ctx.needs_input_grad[4]:
             dB = (dy2.t() @ t).to(bdt)

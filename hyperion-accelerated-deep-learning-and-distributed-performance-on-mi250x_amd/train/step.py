@@ -103,3 +103,36 @@ class TrainStep:
             self.static_y.copy_(y, non_blocking=True)
         self.graph.replay()
         return self.static_loss
+
+
+class GraphedClosure:
+    """Capture an arbitrary training-step closure into a hipGraph after ``warmup`` eager calls.
+
+    ``fn`` must zero gradients IN PLACE (``zero_grad(set_to_none=False)``), read its inputs from
+    persistent tensors and return a tensor (e.g. the loss); replays then re-run the whole step —
+    forward, backward, clipping, optimizer — as one graph launch.  Used where the model call is not
+    ``loss_fn(model(x), y)`` (Llama with masks and labels, the LM with its fused head).
+    """
+
+    def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3):
+        self.fn = fn
+        self.warmup = warmup
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.out: Optional[torch.Tensor] = None
+
+    def __call__(self) -> torch.Tensor:
+        if self.graph is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):
+                    self.fn()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.out = self.fn()
+            torch.cuda.synchronize()
+            self.graph = g
+        self.graph.replay()
+        return self.out
