@@ -27,7 +27,7 @@ run_step() {
 for s in $STEPS; do
   case $s in
     smoke) run_step smoke 300 python3 __graft_entry__.py smoke ;;
-    tests) run_step pytest_gpu 900 python3 -m pytest tests -m gpu -q ;;
+    tests) run_step pytest_gpu 600 python3 -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     bench) run_step bench_graph 400 python3 bench.py --steps 50 --warmup 10 --json-out gpurun_out/bench_graph.json ;;
     eager) run_step bench_eager 400 python3 bench.py --steps 30 --warmup 10 --graph 0 --json-out gpurun_out/bench_eager.json ;;
     torch)
