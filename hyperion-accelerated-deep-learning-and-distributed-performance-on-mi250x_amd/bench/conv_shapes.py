@@ -55,7 +55,7 @@ def _med(fn, repeat=20, warmup=5) -> float:
     return statistics.median(ts)
 
 
-def run(batch: int = 32) -> List[Dict]:
+def run(batch: int = 32, sweep: bool = False) -> List[Dict]:
     from ..ops import _native
 
     torch.backends.cudnn.benchmark = True
@@ -77,9 +77,19 @@ def run(batch: int = 32) -> List[Dict]:
         r["miopen_wgrad_us"] = _med(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False]))
         if s == 1 and K % 64 == 0:
-            wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-            r["hyp_dgrad_us"] = _med(lambda: C_.conv_fwd(dy, wt, 1, 1, R - 1 - p, R - 1 - p, False))
-        for k in ("hyp_fwd_us", "miopen_fwd_us"):
+            r["hyp_dgrad_us"] = _med(lambda: C_.conv_dgrad(dy, w, p, p))
+        if C % 64 == 0:
+            r["hyp_wgrad_us"] = _med(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p))
+        if sweep:  # LDS pipeline depth of each kernel (conv_set_stages), automatic plans otherwise
+            for nb in (2, 3, 4):
+                C_.conv_set_stages(nb, nb)
+                if C % 64 == 0:
+                    r[f"hyp_fwd_nb{nb}_us"] = _med(lambda: C_.conv_fwd(x, w, s, s, p, p, True), repeat=10)
+                    r[f"hyp_wgrad_nb{nb}_us"] = _med(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p), repeat=10)
+                if s == 1 and K % 64 == 0:
+                    r[f"hyp_dgrad_nb{nb}_us"] = _med(lambda: C_.conv_dgrad(dy, w, p, p), repeat=10)
+            C_.conv_set_stages(0, 0)
+        for k in ("hyp_fwd_us", "miopen_fwd_us", "hyp_dgrad_us", "miopen_dgrad_us", "hyp_wgrad_us", "miopen_wgrad_us"):
             if k in r:
                 r[k.replace("_us", "_tflops")] = flop / (r[k] * 1e-6) / 1e12
         rows.append(r)

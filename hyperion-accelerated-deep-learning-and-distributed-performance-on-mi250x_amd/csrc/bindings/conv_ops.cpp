@@ -1,4 +1,6 @@
 // Torch bindings: implicit-GEMM convolution (+ BN-statistics epilogue) and BN from partials.
+#include <algorithm>
+
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
@@ -41,8 +43,127 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   }
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
                               stats ? psum.data_ptr<float>() : nullptr, stats ? psq.data_ptr<float>() : nullptr, N, H, W,
-                              C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, cur_stream()));
+                              C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, 1, nullptr, cur_stream()));
   return {y, psum, psq};
+}
+
+// Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
+// filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw) {
+  HYP_CHECK_CUDA_TENSOR(dy);
+  TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad: channels-last dy and weight required");
+  TORCH_CHECK(dy.scalar_type() == w.scalar_type() &&
+                  (dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf),
+              "conv_dgrad: bf16/f16 dy and weight of one dtype");
+  const int N = dy.size(0), K = dy.size(1), P = dy.size(2), Q = dy.size(3);
+  const int C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(0) == K, "conv_dgrad: channel mismatch");
+  TORCH_CHECK(hyp::conv_fwd_supported(K, C), "conv_dgrad: needs K % 64 == 0 and C % 8 == 0");
+  const int dph = R - 1 - (int)ph, dpw = S - 1 - (int)pw;
+  TORCH_CHECK(dph >= 0 && dpw >= 0, "conv_dgrad: padding larger than the filter");
+  const int H = P + R - 1 - 2 * (int)ph, W = Q + S - 1 - 2 * (int)pw;
+  TORCH_CHECK(H > 0 && W > 0, "conv_dgrad: empty output");
+  const at::DeviceGuard guard(dy.device());
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  int bm = 128, bn = 128;
+  hyp::conv_fwd_tile(N * H * W, C, &bm, &bn);
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
+                              zero_page(dy.device()).data_ptr(), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
+                              dph, dpw, bm, bn, 1, 1, nullptr, cur_stream()));
+  return dx;
+}
+
+// ---- skinny GEMMs (weight-streaming regime: few hundred tokens x large frozen weights) ----------
+// The same implicit-GEMM kernel with R = S = 1 and split-K over the reduction: at M = 128 tokens a
+// 4096 x 4096 projection is only 64 output tiles, so the reduction is split until ~320 workgroups
+// stream disjoint weight slices (the vendor GEMM launched 64 workgroups: 0.6 TB/s of weight reads).
+namespace {
+int skinny_splits(int M, int N, int Kred, int bm, int bn, int64_t splits_req) {
+  if (splits_req > 0) return (int)splits_req;
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const int nk = Kred / 64;
+  int sp = (320 + tiles / 2) / tiles;
+  return std::max(1, std::min(sp, nk / 4));
+}
+}  // namespace
+
+// y[M, N] = x[M, K] · w[N, K]ᵀ  (nn.Linear layout; K % 64 == 0, N % 8 == 0)
+at::Tensor linear_nt(const at::Tensor& x, const at::Tensor& w, int64_t splits_req) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), "linear_nt: contiguous 2D");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "linear_nt: bf16/f16 of one dtype");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && hyp::conv_fwd_supported(K, N), "linear_nt: needs K % 64 == 0, N % 8 == 0");
+  const at::DeviceGuard guard(x.device());
+  auto y = at::empty({M, N}, x.options());
+  const int bm = M <= 64 ? 64 : 128, bn = 64;
+  const int sp = skinny_splits(M, N, K, bm, bn, splits_req);
+  at::Tensor part;
+  if (sp > 1) part = at::empty({(int64_t)sp * M * N}, x.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
+                              nullptr, nullptr, M, 1, 1, K, N, 1, 1, 1, 1, 1, 1, 0, 0, bm, bn, 0, sp,
+                              sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+  return y;
+}
+
+// dx[M, K] = dy[M, N] · w[N, K]  (the data gradient of linear_nt; N % 64 == 0, K % 8 == 0)
+at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_req) {
+  HYP_CHECK_CUDA_TENSOR(dy);
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.is_contiguous() && w.is_contiguous(), "linear_nn: contiguous 2D");
+  TORCH_CHECK(dy.scalar_type() == w.scalar_type() &&
+                  (dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf),
+              "linear_nn: bf16/f16 of one dtype");
+  const int M = dy.size(0), N = dy.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == N && hyp::conv_fwd_supported(N, K), "linear_nn: needs N % 64 == 0, K % 8 == 0");
+  const at::DeviceGuard guard(dy.device());
+  auto dx = at::empty({M, K}, dy.options());
+  const int bm = M <= 64 ? 64 : 128, bn = 64;
+  const int sp = skinny_splits(M, K, N, bm, bn, splits_req);
+  at::Tensor part;
+  if (sp > 1) part = at::empty({(int64_t)sp * M * K}, dy.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
+                              zero_page(dy.device()).data_ptr(), nullptr, nullptr, M, 1, 1, N, K, 1, 1, 1, 1, 1, 1, 0,
+                              0, bm, bn, 1, sp, sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+  return dx;
+}
+
+// dy [N,K,P,Q] channels-last, x [N,C,H,W] channels-last -> dW [K,C,R,S] channels-last (x's dtype)
+// bm / bn / splits < 0: automatic plan (conv_wgrad_plan); explicit values are for tuning sweeps.
+at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int64_t S, int64_t sh, int64_t sw,
+                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  HYP_CHECK_CUDA_TENSOR(dy);
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4D tensors");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_wgrad: channels-last x and dy required");
+  TORCH_CHECK(x.scalar_type() == dy.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "conv_wgrad: bf16/f16 x and dy of one dtype");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int K = dy.size(1), P = dy.size(2), Q = dy.size(3);
+  TORCH_CHECK(dy.size(0) == N, "conv_wgrad: batch mismatch");
+  TORCH_CHECK(P == (H + 2 * ph - R) / sh + 1 && Q == (W + 2 * pw - S) / sw + 1, "conv_wgrad: dy spatial shape");
+  TORCH_CHECK(hyp::conv_wgrad_supported(C, K), "conv_wgrad: needs C % 64 == 0 and K % 8 == 0");
+  const at::DeviceGuard guard(x.device());
+  auto dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  int bm, bn, splits, per;
+  hyp::conv_wgrad_plan(N * P * Q, K, C, (int)R, (int)S, &bm, &bn, &splits, &per);
+  if (bm_ > 0) bm = (int)bm_;
+  if (bn_ > 0) bn = (int)bn_;
+  if (splits_ > 0) {
+    const int steps = (N * P * Q + 63) / 64;
+    per = (steps + (int)splits_ - 1) / (int)splits_;
+    splits = (steps + per - 1) / per;
+  }
+  at::Tensor part;
+  if (splits > 1) part = at::empty({(int64_t)splits * K * R * S * C}, x.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::conv_wgrad(dtype_code(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                splits > 1 ? part.data_ptr<float>() : nullptr, zero_page(x.device()).data_ptr(), N, H,
+                                W, C, K, P, Q, (int)R, (int)S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, splits, per,
+                                cur_stream()));
+  return dw;
 }
 
 // BN forward (training) given conv-epilogue partials: returns (y, save_mean, save_invstd)
@@ -77,6 +198,19 @@ std::vector<at::Tensor> bn_fwd_partials(const at::Tensor& x, const c10::optional
 
 void register_conv_ops(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)");
+  m.def("conv_set_stages", [](int64_t fwd, int64_t wgrad) {
+    hyp::conv_set_stages((int)fwd);
+    hyp::conv_wgrad_set_stages((int)wgrad);
+  }, "LDS pipeline depth of the conv kernels (2..4; 0 = automatic) — tuning sweeps only");
+  m.def("linear_nt", &linear_nt, "skinny y = x wᵀ (split-K MFMA, weight streaming)", pybind11::arg("x"),
+        pybind11::arg("w"), pybind11::arg("splits") = -1);
+  m.def("linear_nn", &linear_nn, "skinny dx = dy w (split-K MFMA, weight read transposed in-kernel)",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("splits") = -1);
+  m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)");
+  m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
+        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
+        pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1);
   m.def("bn_fwd_partials", &bn_fwd_partials, "BN finalize + apply from conv-epilogue partials");
 }
 

@@ -114,10 +114,24 @@ namespace hyp {
 // ---- conv_igemm.hip --------------------------------------------------------------------------
 // NHWC implicit-GEMM conv (bf16/f16), optional BN-statistics epilogue (psum/psq: [ceil(M/bm), K]).
 bool conv_fwd_supported(int C, int K);
+void conv_set_stages(int nb);        // LDS pipeline depth 2..4 (0 = automatic); tuning only
+void conv_wgrad_set_stages(int nb);
 void conv_fwd_tile(int M, int K, int* bm, int* bn);
+// dgrad != 0: stride-1 data gradient; "in" is dY [N,H,W,C], "w" the ORIGINAL filter [C][R][S][K]
+// (read flipped and transposed in-kernel), (ph, pw) the dgrad padding R-1-p.
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
-                    int bm, int bn, hipStream_t st);
+                    int bm, int bn, int dgrad, int splits, float* part, hipStream_t st);
+// out (T) = sum over `splits` fp32 partial slabs of n elements (fixed order; n % 4 == 0)
+hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st);
+// ---- conv_wgrad.hip --------------------------------------------------------------------------
+// NHWC conv weight gradient on MFMA (split-K over pixels; fp32 partials [splits, K, R*S*C] when
+// splits > 1, reduced + cast into dw by a second kernel).
+bool conv_wgrad_supported(int C, int K);
+void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* splits, int* steps_per_split);
+hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
+                      int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
+                      int bn, int splits, int steps_per_split, hipStream_t st);
 // ---- bn_act.hip (conv-epilogue statistics) ---------------------------------------------------
 hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                                     const float* weight, const float* bias, float* running_mean, float* running_var,

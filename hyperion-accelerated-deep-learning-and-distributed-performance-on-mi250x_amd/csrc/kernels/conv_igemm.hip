@@ -22,6 +22,7 @@
 // Requirements: C % 64 == 0 (every ResNet conv but the 3-channel stem), 16-byte aligned tensors.
 #include "hyp_common.h"
 #include "hyp_kernels.h"
+#include "mfma_lds.h"
 
 namespace hyp {
 namespace {
@@ -66,24 +67,31 @@ struct ConvArgs {
   float* psq;
   int N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw;
   int M;                 // N*P*Q
+  int group;             // M-tiles per tile-order group (see conv_fwd_group)
+  int splits, steps_per_split;  // split-K over the reduction (splits > 1: fp32 partials, no STATS)
+  float* part;                  // [splits, M, K] fp32 when splits > 1
 };
 
-template <typename T, int BM, int BN, bool STATS>
+// DGRAD = false: W is [K, R, S, C] (reduction contiguous; B tiles are row slices, read row-wise).
+// DGRAD = true:  the stride-1 data gradient dX = conv(dY, flip(W) with C <-> K, pad R-1-p), run on
+//   the ORIGINAL filter [C_dgrad_in = a.C][R][S][K_dgrad_out = a.K]: a B tile is 64 reduction rows
+//   of W[c, R-1-r, S-1-s, n0 : n0+BN] (output channels contiguous), staged row-permuted
+//   (tr_row_to_k) and read transposed with ds_read_b64_tr_b16 — no flipped/transposed filter copy.
+template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB>
 __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (wave tile BM/2 x BN/2)
   constexpr int IA = BM / 32, IB = BN / 32;  // glds instructions per wave per slice
   constexpr int kBuf = (BM + BN) * kBK;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * kBuf];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NB * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.K + BN - 1) / BN, nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {  // XCD-aware remap (bijective for any nwg)
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  }
-  constexpr int kGroup = 8;
+  // split-major logical order: an XCD's contiguous range is tiles of ONE reduction split
+  int bid = mfl::xcd_remap(blockIdx.x, nwg * a.splits);
+  const int split = bid / nwg;
+  bid -= split * nwg;
+  const int kGroup = a.group;
   const int group = kGroup * tiles_n;
   const int first_m = (bid / group) * kGroup;
   const int gsize = min(tiles_m - first_m, kGroup);
@@ -113,17 +121,26 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   const uint16_t* b_src[IB];
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
-    const int row = (i * 4 + wave) * 8 + (lane >> 3);
-    const int k = n0 + row;
-    const int chunk = slot ^ swz(row);
-    b_src[i] = k < a.K ? a.w + (int64_t)k * ldw + chunk * 8 : nullptr;
+    if (!DGRAD) {
+      const int row = (i * 4 + wave) * 8 + (lane >> 3);
+      const int k = n0 + row;
+      const int chunk = slot ^ swz(row);
+      b_src[i] = k < a.K ? a.w + (int64_t)k * ldw + chunk * 8 : nullptr;
+    } else {  // image [64 reduction rows][BN]: a wave instruction fills 1024 / (2 BN) rows
+      constexpr int RB = 1024 / (2 * BN), CB = BN / 8;
+      const int row = (i * 4 + wave) * RB + lane / CB;
+      const int col = n0 + (((lane % CB) ^ mfl::swz_tr<BN>(row)) << 3);
+      b_src[i] = col < a.K ? a.w + (int64_t)mfl::tr_row_to_k(row) * a.R * a.S * a.K + col : nullptr;
+    }
   }
   const uint16_t* zero = a.zero + slot * 8;
 
   const int cpb = a.C / kBK;  // 64-channel slices per filter tap
-  const int nk = a.R * a.S * cpb;
+  const int kt0 = split * a.steps_per_split;  // this split's reduction steps [kt0, kt0 + nk)
+  const int nk = max(0, min(a.R * a.S * cpb - kt0, a.steps_per_split));
 
-  auto stage = [&](int t, uint16_t* buf) {
+  auto stage = [&](int tl, uint16_t* buf) {
+    const int t = kt0 + tl;
     const int rs = t / cpb, c0 = (t - rs * cpb) * kBK;
     const int r = rs / a.S, s = rs - r * a.S;
     const int64_t tap = ((int64_t)r * a.W + s) * a.C + c0;
@@ -133,10 +150,12 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       const bool ok = a_ok[i] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       glds16(ok ? a.in + a_off[i] + tap : zero, buf + (i * 4 + wave) * 8 * kBK);
     }
-    const int64_t kofs = (int64_t)t * kBK;
+    // DGRAD: filter tap (R-1-r, S-1-s) of reduction channels c0 .. c0+63
+    const int64_t kofs = DGRAD ? ((int64_t)c0 * a.R * a.S + (a.R - 1 - r) * a.S + (a.S - 1 - s)) * a.K
+                               : (int64_t)t * kBK;
 #pragma unroll
     for (int i = 0; i < IB; ++i)
-      glds16(b_src[i] ? b_src[i] + kofs : zero, buf + BM * kBK + (i * 4 + wave) * 8 * kBK);
+      glds16(b_src[i] ? b_src[i] + kofs : zero, buf + BM * kBK + (i * 4 + wave) * 512);
   };
 
   f32x4 acc[FM][FN];
@@ -145,14 +164,16 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, smem);
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
+  // NB-deep ring: stage t+NB-1 is issued right after the barrier that retires stage t-1's buffer
+#pragma unroll
+  for (int i = 0; i < NB - 1; ++i)
+    if (i < nk) stage(i, smem + i * kBuf);
   const int r16 = lane & 15, c4 = lane >> 4;
   for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) stage(t + 1, smem + (cur ^ 1) * kBuf);
-    const uint16_t* as = smem + cur * kBuf;
+    mfl::wait_stage<IA + IB, NB>(min(NB - 2, nk - 1 - t));
+    mfl::barrier_keep_vm();  // stage t visible to all waves; every wave is done with buffer (t-1) % NB
+    if (t + NB - 1 < nk) stage(t + NB - 1, smem + ((t + NB - 1) % NB) * kBuf);
+    const uint16_t* as = smem + (t % NB) * kBuf;
     const uint16_t* bs = as + BM * kBK;
 #pragma unroll
     for (int ks = 0; ks < kBK / 32; ++ks) {
@@ -160,14 +181,33 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) fa[i] = frag(as, wm * (BM / 2) + i * 16 + r16, ks * 4 + c4);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = frag(bs, wn * (BN / 2) + j * 16 + r16, ks * 4 + c4);
+      for (int j = 0; j < FN; ++j)
+        fb[j] = DGRAD ? mfl::frag_tr<BN>(bs, ks * 32, wn * (BN / 2) + j * 16, lane)
+                      : frag(bs, wn * (BN / 2) + j * 16 + r16, ks * 4 + c4);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mma<T>(fa[i], fb[j], acc[i][j]);
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+  }
+  __syncthreads();  // the epilogue reuses the ring
+
+  if (a.splits > 1) {  // split-K: raw fp32 partials (16 lanes = one 64-byte row segment per store)
+    float* part = a.part + (int64_t)split * a.M * a.K;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * (BM / 2) + i * 16 + c4 * 4 + e;
+        if (m < a.M) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int n = n0 + wn * (BN / 2) + j * 16 + r16;
+            if (n < a.K) part[(int64_t)m * a.K + n] = acc[i][j][e];
+          }
+        }
+      }
+    return;
   }
 
   // ---- epilogue.  acc[i][j][e] is out[m0 + wm*BM/2 + i*16 + c4*4 + e][n0 + wn*BN/2 + j*16 + r16].
@@ -237,14 +277,28 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   }
 }
 
-template <typename T, int BM, int BN>
-hipError_t launch(const ConvArgs& a, bool stats, hipStream_t st) {
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.K + BN - 1) / BN);
-  if (stats)
-    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true>), dim3(tiles), dim3(kThreads), 0, st, a);
+template <typename T, int BM, int BN, int NB>
+hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.K + BN - 1) / BN) * a.splits;
+  if (dgrad)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
+  else if (stats)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, false, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false>), dim3(tiles), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, false, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   return hipGetLastError();
+}
+
+int g_stages = 0;  // 0 = automatic (conv_set_stages, for tuning sweeps)
+
+template <typename T, int BM, int BN>
+hipError_t launch(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
+  // LDS per workgroup = NB * (BM + BN) * 128 B: 64x64 -> 4 stages (64 KiB, 2 workgroups / CU);
+  // larger tiles -> 3 stages (72 / 96 KiB)
+  const int nb = g_stages > 0 ? g_stages : (BM == 64 && BN == 64 ? 4 : 3);
+  if (nb == 2) return launch_nb<T, BM, BN, 2>(a, stats, dgrad, st);
+  if (nb == 3) return launch_nb<T, BM, BN, 3>(a, stats, dgrad, st);
+  return launch_nb<T, BM, BN, 4>(a, stats, dgrad, st);
 }
 
 }  // namespace
@@ -265,23 +319,58 @@ void conv_fwd_tile(int M, int K, int* bm, int* bn) {
 
 bool conv_fwd_supported(int C, int K) { return C % 64 == 0 && K % 8 == 0; }
 
+// Tile order: ids run M-fastest inside groups of `group` M-tiles, and each XCD takes a contiguous
+// 1/8 of the ids, so an XCD's L2 holds ~group A-slices and ~(tiles/8)/group filter slices.  A
+// filter slice is R*S*BN/BM times an activation slice; the footprint group*a + (T/8/group)*b is
+// smallest at group = sqrt(T*b / (8a)).  (ResNet layer4 3x3: 200 tiles -> group 15; the old fixed
+// 8 made every XCD stream all 4.7 MB of filter through a 4 MB L2.)
+int conv_fwd_group(int M, int K, int RS, int bm, int bn) {
+  const int tm = (M + bm - 1) / bm, tn = (K + bn - 1) / bn;
+  const double g = sqrt((double)tm * tn * RS * bn / (8.0 * bm));
+  return max(1, min(tm, (int)(g + 0.5)));
+}
+
+void conv_set_stages(int nb) { g_stages = (nb >= 2 && nb <= 4) ? nb : 0; }
+
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
-                    int bm, int bn, hipStream_t st) {
+                    int bm, int bn, int dgrad, int splits, float* part, hipStream_t st) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
+  if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
+  if (splits > 1 && (psum != nullptr || part == nullptr)) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
   if (M64 <= 0 || M64 > INT32_MAX) return hipErrorInvalidValue;
   ConvArgs a{static_cast<const uint16_t*>(in), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out),
              static_cast<const uint16_t*>(zero), psum, psq, N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw, (int)M64};
+  a.group = conv_fwd_group(a.M, K, R * S, bm, bn);
+  const int nk = R * S * (C / kBK);
+  splits = max(1, min(splits, nk));
+  a.steps_per_split = (nk + splits - 1) / splits;
+  a.splits = (nk + a.steps_per_split - 1) / a.steps_per_split;  // no empty splits
+  a.part = part;
+  if (a.splits > 1) {
+    hipError_t e;
+    if (dtype == kBF16) {
+      if (bm == 128 && bn == 128) e = launch<bf16_t, 128, 128>(a, false, dgrad, st);
+      else if (bm == 128 && bn == 64) e = launch<bf16_t, 128, 64>(a, false, dgrad, st);
+      else e = launch<bf16_t, 64, 64>(a, false, dgrad, st);
+    } else {
+      if (bm == 128 && bn == 128) e = launch<f16_t, 128, 128>(a, false, dgrad, st);
+      else if (bm == 128 && bn == 64) e = launch<f16_t, 128, 64>(a, false, dgrad, st);
+      else e = launch<f16_t, 64, 64>(a, false, dgrad, st);
+    }
+    if (e != hipSuccess) return e;
+    return splitk_reduce(dtype, part, out, (int64_t)a.M * K, a.splits, st);
+  }
   const bool stats = psum != nullptr && psq != nullptr;
   if (dtype == kBF16) {
-    if (bm == 128 && bn == 128) return launch<bf16_t, 128, 128>(a, stats, st);
-    if (bm == 128 && bn == 64) return launch<bf16_t, 128, 64>(a, stats, st);
-    return launch<bf16_t, 64, 64>(a, stats, st);
+    if (bm == 128 && bn == 128) return launch<bf16_t, 128, 128>(a, stats, dgrad, st);
+    if (bm == 128 && bn == 64) return launch<bf16_t, 128, 64>(a, stats, dgrad, st);
+    return launch<bf16_t, 64, 64>(a, stats, dgrad, st);
   }
-  if (bm == 128 && bn == 128) return launch<f16_t, 128, 128>(a, stats, st);
-  if (bm == 128 && bn == 64) return launch<f16_t, 128, 64>(a, stats, st);
-  return launch<f16_t, 64, 64>(a, stats, st);
+  if (bm == 128 && bn == 128) return launch<f16_t, 128, 128>(a, stats, dgrad, st);
+  if (bm == 128 && bn == 64) return launch<f16_t, 128, 64>(a, stats, dgrad, st);
+  return launch<f16_t, 64, 64>(a, stats, dgrad, st);
 }
 
 }  // namespace hyp

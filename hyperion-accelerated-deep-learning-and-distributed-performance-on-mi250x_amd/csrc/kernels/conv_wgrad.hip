@@ -1,0 +1,272 @@
+// NHWC convolution WEIGHT gradient on gfx950 MFMA (split-K implicit GEMM).
+//
+// Reference: ResNet-50/18 weight gradients ran through MIOpen's `igemm_wrw` / CK batched-GEMM
+// solvers plus their zero-fill and cast kernels (3-4 launches per conv; SURVEY §2.4
+// "Convolution + BatchNorm + ReLU" backward, §2.5 ResNet rows).  Here
+//
+//   dW[k, r, s, c] = Σ_{m = (n,p,q)} dY[m, k] · X[n, p*sh + r - ph, q*sw + s - pw, c]
+//
+// is a GEMM with rows = output channels k, columns = (r, s, c) in the channels-last filter's own
+// order, and a reduction over the N·P·Q output pixels.  BOTH operands have the reduction (pixel)
+// dimension strided in memory — dY rows and input pixels are channel-contiguous — so tiles are
+// staged pixel-major straight from HBM with 16-byte global_load_lds (a pixel's BM/BN-channel run
+// is one contiguous row), and the MFMA operands are read back TRANSPOSED with gfx950's
+// ds_read_b64_tr_b16 (guide T10): no register transpose, no ds_permute.
+//
+// LDS image per operand: [64 pixels][W channels] with W*2-byte rows and an XOR swizzle of the
+// 16-byte chunks chosen so every 32-lane half of a transposed read touches 64 distinct banks
+// (rows 0..7 of a read half land on disjoint chunk pairs).  The pixel <-> MFMA k-slot mapping is
+// free (both operands sum over the same pixels), so each 16-lane group reads 4 consecutive rows.
+//
+// Work split: tiles BM x BN (k x c) of one filter tap, 4 waves as 2 x 2, 16x16x32 bf16/f16 MFMA;
+// the pixel reduction is split over `splits` workgroups (the outputs of a ResNet wgrad are small —
+// 64 x 576 for a layer1 3x3 — while the reduction is up to 10^5 pixels long).  splits == 1 stores
+// the result in the parameter dtype; otherwise fp32 partials [splits][K][R·S·C] are summed (in a
+// fixed order: deterministic) and cast by conv_wgrad_reduce_k.
+#include "hyp_common.h"
+#include "hyp_kernels.h"
+#include "mfma_lds.h"
+
+namespace hyp {
+namespace {
+
+using namespace mfl;
+
+constexpr int kBP = 64;  // pixels (reduction) per LDS stage
+constexpr int kThreads = 256;
+
+struct WgradArgs {
+  const uint16_t* dy;    // [M, K]   (M = N*P*Q output pixels, channels-last)
+  const uint16_t* x;     // [N, H, W, C]
+  void* out;             // splits == 1: dW [K, R, S, C] in T; else fp32 partials [splits, K, R*S*C]
+  const uint16_t* zero;  // >= 1 KiB of zeros
+  int N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw;
+  int M, splits, steps_per_split;
+  uint64_t mq, mpq;  // magic multipliers: floor(m / Q) = (m * mq) >> 36 (same for P*Q)
+};
+
+// floor(x / d) with magic = ceil(2^36 / d): exact while x * d < 2^36 (host: M < 2^22, P*Q < 2^14)
+__device__ __forceinline__ int fdiv(int x, uint64_t magic) { return (int)(((uint64_t)(uint32_t)x * magic) >> 36); }
+
+template <typename T, int BM, int BN, int NB>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
+  constexpr int FM = BM / 32, FN = BN / 32;          // 16x16 fragments per wave (wave tile BM/2 x BN/2)
+  constexpr int IA = BM / 32, IB = BN / 32;          // glds per wave per stage (8-row blocks)
+  constexpr int CA = BM / 8, CB = BN / 8;            // 16-byte chunks per image row
+  constexpr int kBuf = (BM + BN) * kBP;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NB * kBuf];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int RSC = a.R * a.S * a.C;
+  const int tiles_k = (a.K + BM - 1) / BM, tiles_c = RSC / BN, ntiles = tiles_k * tiles_c;
+  const int nwg = ntiles * a.splits;
+  int bid = blockIdx.x;
+  bid = xcd_remap(bid, nwg);  // consecutive logical tiles (same pixel split) share an XCD's L2
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int tk = tile % tiles_k, tc = tile / tiles_k;
+  const int k0 = tk * BM;
+  const int col0 = tc * BN;               // column in (r, s, c) order; BN | C so one tap per tile
+  const int rs = col0 / a.C, c0 = col0 - rs * a.C;
+  const int r = rs / a.S, s = rs - r * a.S;
+  const int mbeg = split * a.steps_per_split * kBP;
+  const int nsteps = min(a.steps_per_split, (a.M - mbeg + kBP - 1) / kBP);
+
+  // ---- per-lane staging bookkeeping: lane covers image row (i*4 + wave)*8 + lane/CA ... for the
+  // A (dY) image, a wave instruction writes 1024 B = 1024 / (2*BM) rows.
+  constexpr int RA = 1024 / (2 * BM), RB = 1024 / (2 * BN);  // rows per wave instruction
+  int a_row[IA], a_col[IA], b_row[IB], b_col[IB];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int row = (i * 4 + wave) * RA + lane / CA;
+    const int slot = lane % CA;
+    a_row[i] = row;
+    a_col[i] = k0 + ((slot ^ swz_tr<BM>(row)) << 3);
+  }
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int row = (i * 4 + wave) * RB + lane / CB;
+    const int slot = lane % CB;
+    b_row[i] = row;
+    b_col[i] = c0 + ((slot ^ swz_tr<BN>(row)) << 3);
+  }
+  const uint16_t* zero = a.zero;
+
+  auto stage = [&](int t, uint16_t* buf) {
+    const int mb = mbeg + t * kBP;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int m = mb + a_row[i];
+      const bool ok = m < a.M && a_col[i] < a.K;
+      glds16(ok ? a.dy + (int64_t)m * a.K + a_col[i] : zero, buf + (i * 4 + wave) * 512);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int m = mb + b_row[i];
+      const int n = fdiv(m, a.mpq), pq = m - n * a.P * a.Q;
+      const int p = fdiv(pq, a.mq), q = pq - p * a.Q;
+      const int h = p * a.sh + r - a.ph, w = q * a.sw + s - a.pw;
+      const bool ok = m < a.M && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      glds16(ok ? a.x + (((int64_t)n * a.H + h) * a.W + w) * a.C + b_col[i] : zero,
+             buf + BM * kBP + (i * 4 + wave) * 512);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // NB-deep ring (see mfma_lds.h wait_stage): stage t+NB-1 is issued after the barrier that
+  // retires stage t-1's buffer
+#pragma unroll
+  for (int i = 0; i < NB - 1; ++i)
+    if (i < nsteps) stage(i, smem + i * kBuf);
+  for (int t = 0; t < nsteps; ++t) {
+    wait_stage<IA + IB, NB>(min(NB - 2, nsteps - 1 - t));
+    barrier_keep_vm();
+    if (t + NB - 1 < nsteps) stage(t + NB - 1, smem + ((t + NB - 1) % NB) * kBuf);
+    const uint16_t* as = smem + (t % NB) * kBuf;
+    const uint16_t* bs = as + BM * kBP;
+#pragma unroll
+    for (int ks = 0; ks < kBP / 32; ++ks) {
+      u16x8 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = frag_tr<BM>(as, ks * 32, wm * (BM / 2) + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = frag_tr<BN>(bs, ks * 32, wn * (BN / 2) + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mma16<T>(fa[i], fb[j], acc[i][j]);
+    }
+  }
+
+  // ---- epilogue: acc[i][j][e] = dW[k0 + wm*BM/2 + i*16 + (lane>>4)*4 + e][col0 + wn*BN/2 + j*16 + (lane&15)]
+  const int r16 = lane & 15, c4 = lane >> 4;
+  if (a.splits == 1) {
+    T* out = reinterpret_cast<T*>(a.out);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm * (BM / 2) + i * 16 + c4 * 4 + e;
+        if (k < a.K) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) st1<T>(out + (int64_t)k * RSC + col0 + wn * (BN / 2) + j * 16 + r16, acc[i][j][e]);
+        }
+      }
+  } else {
+    float* out = reinterpret_cast<float*>(a.out) + (int64_t)split * a.K * RSC;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm * (BM / 2) + i * 16 + c4 * 4 + e;
+        if (k < a.K) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) out[(int64_t)k * RSC + col0 + wn * (BN / 2) + j * 16 + r16] = acc[i][j][e];
+        }
+      }
+  }
+}
+
+// dW = Σ_s part[s] in a fixed order, cast to T.  4 elements per thread (16-byte loads).
+template <typename T>
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_k(const float* __restrict__ part, T* __restrict__ out,
+                                                           int64_t n, int splits) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  f32x4 acc = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + i4));
+  for (int s = 1; s < splits; ++s) acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i4));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) st1<T>(out + i4 + e, acc[e]);
+}
+
+}  // namespace
+
+hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st) {
+  if (n % 4 != 0 || splits < 1) return hipErrorInvalidValue;
+  const int blocks = (int)((n / 4 + 255) / 256);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(conv_wgrad_reduce_k<bf16_t>, dim3(blocks), dim3(256), 0, st, part, static_cast<bf16_t*>(out), n,
+                       splits);
+  else if (dtype == kF16)
+    hipLaunchKernelGGL(conv_wgrad_reduce_k<f16_t>, dim3(blocks), dim3(256), 0, st, part, static_cast<f16_t*>(out), n,
+                       splits);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+namespace {
+
+uint64_t magic36(int d) { return ((1ull << 36) + (uint64_t)d - 1) / (uint64_t)d; }
+
+int g_wgrad_stages = 0;  // 0 = automatic (conv_wgrad_set_stages, for tuning sweeps)
+
+template <typename T, int BM, int BN>
+hipError_t launch(const WgradArgs& a, hipStream_t st) {
+  const int tiles = ((a.K + BM - 1) / BM) * (a.R * a.S * a.C / BN);
+  const int nb = g_wgrad_stages > 0 ? g_wgrad_stages : (BM == 64 && BN == 64 ? 4 : 3);
+  if (nb == 2)
+    hipLaunchKernelGGL((conv_wgrad_k<T, BM, BN, 2>), dim3(tiles * a.splits), dim3(kThreads), 0, st, a);
+  else if (nb == 3)
+    hipLaunchKernelGGL((conv_wgrad_k<T, BM, BN, 3>), dim3(tiles * a.splits), dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_k<T, BM, BN, 4>), dim3(tiles * a.splits), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv_wgrad_supported(int C, int K) { return C % 64 == 0 && K % 8 == 0; }
+
+void conv_wgrad_set_stages(int nb) { g_wgrad_stages = (nb >= 2 && nb <= 4) ? nb : 0; }
+
+// Plan (from the per-layer sweep of bench/conv_shapes.py over ResNet-50 at batch 32 on MI355X,
+// profiles/conv_r01/conv_shapes_wgrad_sweep.json): 64 x 64 tiles win at every layer (more workgroups in flight;
+// the kernel is latency- not MFMA-bound at these sizes), and the best pixel split keeps each
+// workgroup at ~16-25 stages of 64 pixels — enough to amortize the prologue/epilogue, short enough
+// that the grid fills the chip.  Fewer splits also bound the fp32 partial traffic (splits*K*RSC*8 B).
+void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* splits, int* steps_per_split) {
+  (void)K, (void)C, (void)R, (void)S;
+  *bm = 64;
+  *bn = 64;
+  const int total_steps = (M + kBP - 1) / kBP;
+  const int per = max(16, (total_steps + 63) / 64);
+  *steps_per_split = per;
+  *splits = (total_steps + per - 1) / per;
+}
+
+hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
+                      int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
+                      int bn, int splits, int steps_per_split, hipStream_t st) {
+  if (!conv_wgrad_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
+  if (C % bn != 0 || (bm != 64 && bm != 128) || (bn != 64 && bn != 128) || splits < 1) return hipErrorInvalidValue;
+  const int64_t M64 = (int64_t)N * P * Q;
+  // fdiv's 36-bit magic is exact for numerators < 2^22 and divisors < 2^14
+  if (M64 <= 0 || M64 >= (1ll << 22) || (int64_t)P * Q >= (1 << 14)) return hipErrorInvalidValue;
+  if ((int64_t)splits * steps_per_split * kBP < M64) return hipErrorInvalidValue;
+  if (splits > 1 && partials == nullptr) return hipErrorInvalidValue;
+  WgradArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x),
+              splits > 1 ? static_cast<void*>(partials) : dw, static_cast<const uint16_t*>(zero), N, H, W, C, K, P, Q,
+              R, S, sh, sw, ph, pw, (int)M64, splits, steps_per_split, magic36(Q), magic36(P * Q)};
+  hipError_t e;
+  if (dtype == kBF16) {
+    if (bm == 128 && bn == 128) e = launch<bf16_t, 128, 128>(a, st);
+    else if (bm == 128) e = launch<bf16_t, 128, 64>(a, st);
+    else if (bn == 128) e = launch<bf16_t, 64, 128>(a, st);
+    else e = launch<bf16_t, 64, 64>(a, st);
+  } else {
+    if (bm == 128 && bn == 128) e = launch<f16_t, 128, 128>(a, st);
+    else if (bm == 128) e = launch<f16_t, 128, 64>(a, st);
+    else if (bn == 128) e = launch<f16_t, 64, 128>(a, st);
+    else e = launch<f16_t, 64, 64>(a, st);
+  }
+  if (e != hipSuccess || splits == 1) return e;
+  return splitk_reduce(dtype, partials, dw, (int64_t)K * R * S * C, splits, st);  // C % 64 == 0: n % 4 == 0
+}
+
+}  // namespace hyp

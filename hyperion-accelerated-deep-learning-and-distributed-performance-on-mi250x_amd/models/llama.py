@@ -29,6 +29,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops.attention import attention
 from ..ops.cross_entropy import LinearCrossEntropy
 from ..ops.layernorm import RMSNorm
+from ..ops.linear import Linear as HypLinear
 from ..ops.rope import apply_rope
 from ..ops.swiglu import swiglu
 
@@ -71,10 +72,10 @@ class LlamaAttention(nn.Module):
         self.cfg = cfg
         h, nh, nkv, hd = cfg.hidden_size, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         self.num_heads, self.num_kv, self.head_dim = nh, nkv, hd
-        self.q_proj = nn.Linear(h, nh * hd, bias=False)
-        self.k_proj = nn.Linear(h, nkv * hd, bias=False)
-        self.v_proj = nn.Linear(h, nkv * hd, bias=False)
-        self.o_proj = nn.Linear(nh * hd, h, bias=False)
+        self.q_proj = HypLinear(h, nh * hd, bias=False)
+        self.k_proj = HypLinear(h, nkv * hd, bias=False)
+        self.v_proj = HypLinear(h, nkv * hd, bias=False)
+        self.o_proj = HypLinear(nh * hd, h, bias=False)
 
     def forward(self, x: torch.Tensor, positions: Optional[torch.Tensor], key_padding_mask: Optional[torch.Tensor]):
         B, S, _ = x.shape
@@ -93,9 +94,9 @@ class LlamaAttention(nn.Module):
 class LlamaMLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.gate_proj = nn.Linear(cfg.hidden_size, cfg.intermediate_size, bias=False)
-        self.up_proj = nn.Linear(cfg.hidden_size, cfg.intermediate_size, bias=False)
-        self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+        self.gate_proj = HypLinear(cfg.hidden_size, cfg.intermediate_size, bias=False)
+        self.up_proj = HypLinear(cfg.hidden_size, cfg.intermediate_size, bias=False)
+        self.down_proj = HypLinear(cfg.intermediate_size, cfg.hidden_size, bias=False)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.down_proj(swiglu(self.gate_proj(x), self.up_proj(x)))

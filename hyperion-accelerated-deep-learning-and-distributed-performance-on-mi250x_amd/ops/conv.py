@@ -12,10 +12,10 @@ SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
   one apply pass with the residual add and ReLU folded in (``bn_act.hip``).  The separate BN
   statistics read of the conv output is gone.
 * backward — the fused BN/ReLU/residual backward (``bn_act.hip``) produces dconv; the data
-  gradient of a stride-1 convolution is the same implicit-GEMM kernel run on dconv with the
-  flipped, channel-transposed filter; a 1x1 stride-1 weight gradient is one GEMM
-  (``dW = dYᵀ X``); strided data gradients and k x k weight gradients use the vendor kernels
-  (``aten.convolution_backward``).
+  gradient of a stride-1 convolution is the same implicit-GEMM kernel in DGRAD mode (the forward
+  filter read flipped and channel-transposed through ds_read_b64_tr_b16, no filter copy); weight
+  gradients run on ``conv_wgrad.hip`` (split-K MFMA over the output pixels); strided data
+  gradients use the vendor kernels (``aten.convolution_backward``).
 
 Anything outside the kernel's envelope (fp32, C % 64 != 0 such as the RGB stem, groups, dilation,
 eval mode) falls back to ``bn(conv(x), residual)`` — the same math.
@@ -50,19 +50,26 @@ def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 
 def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
     R, S = w.shape[2], w.shape[3]
-    if tuple(stride) == (1, 1) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0:
-        # dX = conv(dY, flip(W) with C <-> K), stride 1, padding R-1-p
-        wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+    if (tuple(stride) == (1, 1) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0 and padding[0] <= R - 1
+            and padding[1] <= S - 1 and _native.use_native(dy, op="dgrad")):
+        # dX = conv(dY, flip(W) with C <-> K), stride 1, padding R-1-p: conv_igemm.hip's DGRAD mode
+        # reads the forward filter flipped and transposed in-kernel (no filter copy)
         dyc = dy.contiguous(memory_format=torch.channels_last)
-        dx, _, _ = _native.native().conv_fwd(dyc, wt, 1, 1, R - 1 - padding[0], S - 1 - padding[1], False)
-        return dx
+        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1])
     return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                                [True, False, False])[0]
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
-    # (A 1x1 weight gradient is the GEMM dYᵀ·X with a 10⁵-long reduction; hipBLASLt runs it on a
-    # handful of workgroups without split-K — 10x slower than the vendor conv path, measured.)
+    # csrc/kernels/conv_wgrad.hip: split-K MFMA GEMM over the output pixels with transposed LDS
+    # reads (one kernel + one deterministic partial-sum/cast kernel; MIOpen used 3-4 launches).
+    # (hipBLASLt on the 1x1 case dYᵀ·X runs a 10⁵-long reduction without split-K: 10x slower.)
+    R, S = w.shape[2], w.shape[3]
+    P, Q = dy.shape[2], dy.shape[3]
+    if (x.shape[1] % 64 == 0 and dy.shape[1] % 8 == 0 and P * Q < (1 << 14) and dy.shape[0] * P * Q < (1 << 22)
+            and _native.use_native(x, op="wgrad")):
+        dyc = dy.contiguous(memory_format=torch.channels_last)
+        return _native.native().conv_wgrad(dyc, x, R, S, stride[0], stride[1], padding[0], padding[1])
     return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
 

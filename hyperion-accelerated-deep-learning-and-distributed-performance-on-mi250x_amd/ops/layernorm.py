@@ -75,6 +75,12 @@ def layer_norm(
     return_sum: bool = False,
 ) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
     d = x.shape[-1]
+    # the kernels take fp32 affine parameters; a model cast wholesale to bf16 (HF-style Llama) hands
+    # us bf16 ones — upcast them (d elements, differentiable) rather than leave the fused path
+    if weight is not None and weight.dtype in (torch.bfloat16, torch.float16):
+        weight = weight.float()
+    if bias is not None and bias.dtype in (torch.bfloat16, torch.float16):
+        bias = bias.float()
     native = (
         _native.use_native(x, op="ln")
         and x.dtype in _native.DTYPE_CODE

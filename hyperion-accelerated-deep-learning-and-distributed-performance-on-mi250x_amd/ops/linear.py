@@ -1,0 +1,88 @@
+"""Linear layers in the weight-streaming regime (a few hundred tokens x large weights).
+
+Reference: the Llama-2-7B LoRA fine-tune (``distributed_utils.py:415-554``, batch 1 x 128 tokens)
+runs every projection as ``torch.nn.functional.linear`` → hipBLASLt.  At M = 128 tokens a
+4096 x 4096 projection is a 64-workgroup launch that streams its 32 MiB weight at ~0.6 TB/s on
+MI355X (profiles/llama_r01).  ``linear_nt`` / ``linear_nn`` (``csrc/kernels/conv_igemm.hip`` with
+R = S = 1) split the reduction until ~320 workgroups stream disjoint weight slices with a
+multi-stage global_load_lds ring, and the data gradient reads the SAME row-major weight
+transposed in-kernel (ds_read_b64_tr_b16) — no ``w.t().contiguous()`` copy.
+
+``linear(x, w, b)``: native forward when M <= ``SKINNY_MAX_M`` tokens and the shapes fit the
+kernel (in % 64, out % 8); native data gradient when out % 64 and in % 8.  Weight / bias grads
+(only for trainable weights) use the vendor GEMM / reduction.  Everything else is ``F.linear``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+SKINNY_MAX_M = int(os.environ.get("HYPERION_SKINNY_MAX_M", "1024"))
+
+
+def _fwd_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x2.dtype in (torch.bfloat16, torch.float16) and w.dtype == x2.dtype and x2.shape[0] <= SKINNY_MAX_M
+            and x2.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 and w.is_contiguous()
+            and _native.use_native(x2, w, op="linear"))
+
+
+def _bwd_ok(dy2: torch.Tensor, w: torch.Tensor) -> bool:
+    return (dy2.dtype == w.dtype and dy2.dtype in (torch.bfloat16, torch.float16) and dy2.shape[0] <= SKINNY_MAX_M
+            and w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0 and w.is_contiguous()
+            and _native.use_native(dy2, w, op="linear"))
+
+
+def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``x2 @ w.T`` for 2D ``x2`` (native when the shape fits, else the vendor GEMM)."""
+    if x2.is_cuda and _fwd_ok(x2, w):
+        return _native.native().linear_nt(x2.contiguous(), w)
+    return F.linear(x2, w)
+
+
+def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``dy2 @ w`` (the data gradient of ``linear_fwd``)."""
+    if dy2.is_cuda and _bwd_ok(dy2, w):
+        return _native.native().linear_nn(dy2.contiguous(), w)
+    return dy2 @ w
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = linear_fwd(x2, w)
+        if b is not None:
+            y = y + b.to(y.dtype)
+        ctx.save_for_backward(x2 if ctx.needs_input_grad[1] else None, w)
+        ctx.has_b = b is not None
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(w.dtype)
+        dx = linear_dgrad(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = (dy2.t() @ x2).to(w.dtype) if ctx.needs_input_grad[1] else None
+        db = dy2.sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear`` with the weight-streaming kernels on gfx950 (same math, same grads)."""
+    if not (x.is_cuda and _native.use_native(x, op="linear")) or torch.is_autocast_enabled(x.device.type):
+        return F.linear(x, w, b)
+    return _LinearFn.apply(x, w, b)
+
+
+class Linear(nn.Linear):
+    """``nn.Linear`` (same parameters and state-dict keys) routed through :func:`linear`."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return linear(x, self.weight, self.bias)

@@ -1,0 +1,23 @@
+"""Run one model step benchmark (for rocprofv3 kernel traces): python scripts/run_model_step.py {vit,llama,lm,gpt2}"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from hyperion.bench import models as M  # noqa: E402
+
+which = sys.argv[1]
+if which == "vit":
+    r = M.bench_vit_step(checkpointing=False, steps=5, warmup=3)
+elif which == "vitckpt":
+    r = M.bench_vit_step(checkpointing=True, steps=5, warmup=3)
+elif which == "llama":
+    r = M.bench_llama_lora_step(steps=3, warmup=2, graph=False)
+elif which == "llamagraph":
+    r = M.bench_llama_lora_step(steps=5, warmup=3, graph=True)
+elif which == "lm":
+    r = M.bench_lm_step(precision="bf16", steps=5, warmup=3)
+else:
+    r = M.bench_lm_step(precision="bf16", graph=True, model="gpt2_small", batch=16, steps=5, warmup=3)
+print(json.dumps(r), flush=True)

@@ -89,3 +89,46 @@ def test_conv_bn_running_stats_updated():
     y = F.conv2d(x.float(), conv.weight.float())
     torch.testing.assert_close(bn.running_mean, 0.1 * y.mean((0, 2, 3)), rtol=2e-2, atol=2e-3)
     assert bn.num_batches_tracked.item() + bn._host_batches == 1
+
+
+WGRAD_SHAPES = SHAPES + [  # N, C, H, W, K, R, stride, pad
+    (4, 64, 56, 56, 256, 1, 1, 0),   # layer1 expand (splits, 128x64 tiles)
+    (4, 256, 56, 56, 128, 1, 2, 0),  # layer2 downsample 1x1 / 2
+    (2, 128, 28, 28, 128, 3, 2, 1),  # stride-2 3x3, 128x128 tiles
+    (3, 192, 10, 10, 24, 3, 1, 1),   # K not a multiple of the tile (64x64, masked rows)
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_SHAPES)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_wgrad_matches_fp32(shape, dtype):
+    from hyperion.ops import _native
+
+    N, C, H, W, K, R, s, p = shape
+    torch.manual_seed(0)
+    P = (H + 2 * p - R) // s + 1
+    x = torch.randn(N, C, H, W, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, P, P, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    dw = _native.native().conv_wgrad(dy, x, R, R, s, s, p, p)
+    assert dw.shape == (K, C, R, R) and dw.dtype == dtype and dw.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float().cpu(), (K, C, R, R), dy.float().cpu(), stride=s, padding=p)
+    err = (dw.float().cpu() - ref).norm() / ref.norm()
+    assert err < 1e-2, f"rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("shape", [s for s in WGRAD_SHAPES if s[6] == 1 and s[4] % 64 == 0])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_conv_dgrad_matches_fp32(shape, dtype):
+    from hyperion.ops import _native
+
+    N, C, H, W, K, R, s, p = shape
+    torch.manual_seed(0)
+    P = (H + 2 * p - R) // s + 1
+    w = (torch.randn(K, C, R, R, device="cuda") / (K * R * R) ** 0.5).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    dy = torch.randn(N, K, P, P, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    dx = _native.native().conv_dgrad(dy, w, p, p)
+    assert dx.shape == (N, C, H, W) and dx.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float().cpu(), dy.float().cpu(), stride=s, padding=p)
+    err = (dx.float().cpu() - ref).norm() / ref.norm()
+    assert err < 1e-2, f"rel err {err:.3e}"

@@ -99,3 +99,26 @@ def test_adapter_save_load_roundtrip_and_merge(tmp_path):
     torch.testing.assert_close(m(ids).logits, m2(ids).logits)
     merged = merge_lora(m2)
     torch.testing.assert_close(merged(ids).logits, m(ids).logits, rtol=1e-4, atol=1e-4)
+
+
+def test_lora_linear_dropout_grads_match_reference():
+    """Dropout path: same draws (seeded), reference = base + s * ((x * keep / (1-p)) A^T) B^T."""
+    from hyperion.ops.lora import lora_linear, lora_linear_reference
+
+    torch.manual_seed(1)
+    x = torch.randn(2, 5, 32, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(24, 32, dtype=torch.float64)
+    a = torch.randn(4, 32, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(24, 4, dtype=torch.float64, requires_grad=True)
+    p, s = 0.3, 2.0
+    torch.manual_seed(7)
+    y = lora_linear(x, w, None, a, b, s, p)
+    torch.manual_seed(7)
+    keep = torch.empty(10, 32, dtype=torch.float64).bernoulli_(1 - p).view(2, 5, 32)
+    xr, ar, br = (t.detach().clone().requires_grad_(True) for t in (x, a, b))
+    yr = lora_linear_reference(xr, w, None, ar, br, s, mask=keep / (1 - p))
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for u, v in ((y, yr), (x.grad, xr.grad), (a.grad, ar.grad), (b.grad, br.grad)):
+        torch.testing.assert_close(u, v)
