@@ -77,20 +77,56 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
 
 // ---- skinny GEMMs (weight-streaming regime: few hundred tokens x large frozen weights) ----------
 // The same implicit-GEMM kernel with R = S = 1 and split-K over the reduction: at M = 128 tokens a
-// 4096 x 4096 projection is only 64 output tiles, so the reduction is split until ~320 workgroups
+// 4096 x 4096 projection is only 64 output tiles, so the reduction is split until ~600 workgroups
 // stream disjoint weight slices (the vendor GEMM launched 64 workgroups: 0.6 TB/s of weight reads).
+// Plan from scripts/skinny_sweep.py on MI355X (profiles/llama_r01/skinny_sweep.json): 64-wide
+// tiles, 2 LDS stages, splits = ceil(600 / tiles) — 512-700 workgroups won at every Llama-2-7B
+// projection shape, forward and data gradient.
 namespace {
 int skinny_splits(int M, int N, int Kred, int bm, int bn, int64_t splits_req) {
   if (splits_req > 0) return (int)splits_req;
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nk = Kred / 64;
-  int sp = (320 + tiles / 2) / tiles;
+  int sp = (600 + tiles - 1) / tiles;
   return std::max(1, std::min(sp, nk / 4));
 }
 }  // namespace
 
+// Rank-r epilogue arguments: U [M, r]; V [r, N] (v_nr = false) or [N, r] (v_nr = true); mask [M, N].
+hyp::SplitkEpilogue make_epilogue(const c10::optional<at::Tensor>& U, const c10::optional<at::Tensor>& V, bool v_nr,
+                                  const c10::optional<at::Tensor>& mask, double beta, int64_t M, int64_t N,
+                                  const at::Tensor& like) {
+  hyp::SplitkEpilogue ep;
+  if (!(U.has_value() && U->defined())) return ep;
+  TORCH_CHECK(V.has_value() && V->defined(), "low-rank epilogue: V required with U");
+  const int64_t r = U->size(1);
+  TORCH_CHECK(U->dim() == 2 && U->size(0) == M && U->is_contiguous() && U->scalar_type() == like.scalar_type(),
+              "low-rank epilogue: U must be a contiguous [M, r] tensor of the output dtype");
+  TORCH_CHECK(V->dim() == 2 && V->is_contiguous() && V->scalar_type() == like.scalar_type(),
+              "low-rank epilogue: V must be contiguous, output dtype");
+  TORCH_CHECK(v_nr ? (V->size(0) == N && V->size(1) == r) : (V->size(0) == r && V->size(1) == N),
+              "low-rank epilogue: V must be [N, r] (v_nr) or [r, N]");
+  TORCH_CHECK(N % 4 == 0, "low-rank epilogue: N % 4 == 0");
+  ep.U = U->data_ptr();
+  ep.V = V->data_ptr();
+  ep.sv_j = v_nr ? 1 : N;
+  ep.sv_n = v_nr ? r : 1;
+  ep.N = (int)N;
+  ep.r = (int)r;
+  ep.beta = (float)beta;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->numel() == M * N && mask->is_contiguous() && mask->scalar_type() == like.scalar_type(),
+                "low-rank epilogue: mask must be a contiguous [M, N] tensor of the output dtype");
+    ep.mask = mask->data_ptr();
+  }
+  return ep;
+}
+
 // y[M, N] = x[M, K] · w[N, K]ᵀ  (nn.Linear layout; K % 64 == 0, N % 8 == 0)
-at::Tensor linear_nt(const at::Tensor& x, const at::Tensor& w, int64_t splits_req) {
+// alpha scales x·wᵀ; U/V/mask/beta add the rank-r epilogue (forces a split-K launch: it runs in the reduce).
+at::Tensor linear_nt(const at::Tensor& x, const at::Tensor& w, int64_t splits_req, int64_t bn_req, double alpha,
+                     const c10::optional<at::Tensor>& U, const c10::optional<at::Tensor>& V, bool v_nr,
+                     const c10::optional<at::Tensor>& mask, double beta) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous(), "linear_nt: contiguous 2D");
   TORCH_CHECK(x.scalar_type() == w.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
@@ -99,18 +135,23 @@ at::Tensor linear_nt(const at::Tensor& x, const at::Tensor& w, int64_t splits_re
   TORCH_CHECK(w.size(1) == K && hyp::conv_fwd_supported(K, N), "linear_nt: needs K % 64 == 0, N % 8 == 0");
   const at::DeviceGuard guard(x.device());
   auto y = at::empty({M, N}, x.options());
-  const int bm = M <= 64 ? 64 : 128, bn = 64;
-  const int sp = skinny_splits(M, N, K, bm, bn, splits_req);
+  const int bm = M <= 64 ? 64 : 128, bn = bn_req == 128 && bm == 128 ? 128 : 64;
+  const hyp::SplitkEpilogue ep = make_epilogue(U, V, v_nr, mask, beta, M, N, x);
+  int sp = skinny_splits(M, N, K, bm, bn, splits_req);
+  if ((ep.U != nullptr || alpha != 1.0) && sp < 2) sp = std::min(2, K / 64);
+  TORCH_CHECK(sp >= 2 || (ep.U == nullptr && alpha == 1.0), "linear_nt: epilogue needs K >= 128");
   at::Tensor part;
   if (sp > 1) part = at::empty({(int64_t)sp * M * N}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
                               nullptr, nullptr, M, 1, 1, K, N, 1, 1, 1, 1, 1, 1, 0, 0, bm, bn, 0, sp,
-                              sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+                              sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream(), (float)alpha, &ep));
   return y;
 }
 
 // dx[M, K] = dy[M, N] · w[N, K]  (the data gradient of linear_nt; N % 64 == 0, K % 8 == 0)
-at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_req) {
+at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_req, int64_t bn_req, double alpha,
+                     const c10::optional<at::Tensor>& U, const c10::optional<at::Tensor>& V, bool v_nr,
+                     const c10::optional<at::Tensor>& mask, double beta) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && dy.is_contiguous() && w.is_contiguous(), "linear_nn: contiguous 2D");
   TORCH_CHECK(dy.scalar_type() == w.scalar_type() &&
@@ -120,20 +161,24 @@ at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_r
   TORCH_CHECK(w.size(0) == N && hyp::conv_fwd_supported(N, K), "linear_nn: needs N % 64 == 0, K % 8 == 0");
   const at::DeviceGuard guard(dy.device());
   auto dx = at::empty({M, K}, dy.options());
-  const int bm = M <= 64 ? 64 : 128, bn = 64;
-  const int sp = skinny_splits(M, K, N, bm, bn, splits_req);
+  const int bm = M <= 64 ? 64 : 128, bn = bn_req == 128 && bm == 128 ? 128 : 64;
+  const hyp::SplitkEpilogue ep = make_epilogue(U, V, v_nr, mask, beta, M, K, dy);
+  int sp = skinny_splits(M, K, N, bm, bn, splits_req);
+  if ((ep.U != nullptr || alpha != 1.0) && sp < 2) sp = std::min(2, N / 64);
+  TORCH_CHECK(sp >= 2 || (ep.U == nullptr && alpha == 1.0), "linear_nn: epilogue needs N >= 128");
   at::Tensor part;
   if (sp > 1) part = at::empty({(int64_t)sp * M * K}, dy.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                               zero_page(dy.device()).data_ptr(), nullptr, nullptr, M, 1, 1, N, K, 1, 1, 1, 1, 1, 1, 0,
-                              0, bm, bn, 1, sp, sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream()));
+                              0, bm, bn, 1, sp, sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream(), (float)alpha,
+                              &ep));
   return dx;
 }
 
 // dy [N,K,P,Q] channels-last, x [N,C,H,W] channels-last -> dW [K,C,R,S] channels-last (x's dtype)
 // bm / bn / splits < 0: automatic plan (conv_wgrad_plan); explicit values are for tuning sweeps.
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int64_t S, int64_t sh, int64_t sw,
-                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_) {
+                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_, double alpha) {
   HYP_CHECK_CUDA_TENSOR(x);
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4D tensors");
@@ -162,7 +207,7 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int6
   HYP_CHECK_HIP(hyp::conv_wgrad(dtype_code(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                                 splits > 1 ? part.data_ptr<float>() : nullptr, zero_page(x.device()).data_ptr(), N, H,
                                 W, C, K, P, Q, (int)R, (int)S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, splits, per,
-                                cur_stream()));
+                                cur_stream(), (float)alpha));
   return dw;
 }
 
@@ -202,15 +247,19 @@ void register_conv_ops(pybind11::module& m) {
     hyp::conv_set_stages((int)fwd);
     hyp::conv_wgrad_set_stages((int)wgrad);
   }, "LDS pipeline depth of the conv kernels (2..4; 0 = automatic) — tuning sweeps only");
-  m.def("linear_nt", &linear_nt, "skinny y = x wᵀ (split-K MFMA, weight streaming)", pybind11::arg("x"),
-        pybind11::arg("w"), pybind11::arg("splits") = -1);
-  m.def("linear_nn", &linear_nn, "skinny dx = dy w (split-K MFMA, weight read transposed in-kernel)",
-        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("splits") = -1);
+  m.def("linear_nt", &linear_nt, "skinny y = alpha x wᵀ [+ beta mask∘(U V)] (split-K MFMA, weight streaming)",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("splits") = -1, pybind11::arg("bn") = -1,
+        pybind11::arg("alpha") = 1.0, pybind11::arg("U") = pybind11::none(), pybind11::arg("V") = pybind11::none(),
+        pybind11::arg("v_nr") = false, pybind11::arg("mask") = pybind11::none(), pybind11::arg("beta") = 1.0);
+  m.def("linear_nn", &linear_nn, "skinny dx = alpha dy w [+ beta mask∘(U V)] (split-K MFMA, w read transposed)",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("splits") = -1, pybind11::arg("bn") = -1,
+        pybind11::arg("alpha") = 1.0, pybind11::arg("U") = pybind11::none(), pybind11::arg("V") = pybind11::none(),
+        pybind11::arg("v_nr") = false, pybind11::arg("mask") = pybind11::none(), pybind11::arg("beta") = 1.0);
   m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
-        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1);
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("alpha") = 1.0);
   m.def("bn_fwd_partials", &bn_fwd_partials, "BN finalize + apply from conv-epilogue partials");
 }
 

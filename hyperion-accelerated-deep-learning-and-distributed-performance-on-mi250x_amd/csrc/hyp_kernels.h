@@ -121,9 +121,23 @@ void conv_fwd_tile(int M, int K, int* bm, int* bn);
 // (read flipped and transposed in-kernel), (ph, pw) the dgrad padding R-1-p.
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
-                    int bm, int bn, int dgrad, int splits, float* part, hipStream_t st);
-// out (T) = sum over `splits` fp32 partial slabs of n elements (fixed order; n % 4 == 0)
-hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st);
+                    int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
+                    const struct SplitkEpilogue* ep = nullptr);
+// Optional rank-r epilogue of a split-K reduce over an [M, N] output:
+//   out[m, n] += beta * (mask ? mask[m, n] : 1) * sum_j U[m, j] * V[j * sv_j + n * sv_n]
+// (U, V, mask in the output dtype).  U == nullptr: no epilogue.
+struct SplitkEpilogue {
+  const void* U = nullptr;
+  const void* V = nullptr;
+  const void* mask = nullptr;
+  int64_t sv_j = 0, sv_n = 0;
+  int N = 0, r = 0;
+  float beta = 1.f;
+};
+// out (T) = alpha * sum over `splits` fp32 partial slabs of n elements (fixed order; n % 4 == 0)
+// [+ the rank-r epilogue]
+hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st,
+                         float alpha = 1.f, const SplitkEpilogue* ep = nullptr);
 // ---- conv_wgrad.hip --------------------------------------------------------------------------
 // NHWC conv weight gradient on MFMA (split-K over pixels; fp32 partials [splits, K, R*S*C] when
 // splits > 1, reduced + cast into dw by a second kernel).
@@ -131,7 +145,7 @@ bool conv_wgrad_supported(int C, int K);
 void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* splits, int* steps_per_split);
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
-                      int bn, int splits, int steps_per_split, hipStream_t st);
+                      int bn, int splits, int steps_per_split, hipStream_t st, float alpha = 1.f);
 // ---- bn_act.hip (conv-epilogue statistics) ---------------------------------------------------
 hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                                     const float* weight, const float* bias, float* running_mean, float* running_var,

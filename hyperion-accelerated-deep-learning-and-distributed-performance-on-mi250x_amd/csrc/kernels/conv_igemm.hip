@@ -293,9 +293,10 @@ int g_stages = 0;  // 0 = automatic (conv_set_stages, for tuning sweeps)
 
 template <typename T, int BM, int BN>
 hipError_t launch(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
-  // LDS per workgroup = NB * (BM + BN) * 128 B: 64x64 -> 4 stages (64 KiB, 2 workgroups / CU);
-  // larger tiles -> 3 stages (72 / 96 KiB)
-  const int nb = g_stages > 0 ? g_stages : (BM == 64 && BN == 64 ? 4 : 3);
+  // 2 stages: the deeper rings (3/4, counted vmcnt across raw barriers) measured no better on any
+  // ResNet-50 layer or Llama projection (profiles/conv_r01, profiles/llama_r01) — at 2-5
+  // workgroups per CU the other workgroups already hide the glds latency (guide: "regime-gated")
+  const int nb = g_stages > 0 ? g_stages : 2;
   if (nb == 2) return launch_nb<T, BM, BN, 2>(a, stats, dgrad, st);
   if (nb == 3) return launch_nb<T, BM, BN, 3>(a, stats, dgrad, st);
   return launch_nb<T, BM, BN, 4>(a, stats, dgrad, st);
@@ -334,10 +335,13 @@ void conv_set_stages(int nb) { g_stages = (nb >= 2 && nb <= 4) ? nb : 0; }
 
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
-                    int bm, int bn, int dgrad, int splits, float* part, hipStream_t st) {
+                    int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
+                    const SplitkEpilogue* ep) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
   if (splits > 1 && (psum != nullptr || part == nullptr)) return hipErrorInvalidValue;
+  // alpha / the rank-r epilogue live in the split-K reduce
+  if ((alpha != 1.f || (ep != nullptr && ep->U != nullptr)) && splits < 2) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
   if (M64 <= 0 || M64 > INT32_MAX) return hipErrorInvalidValue;
   ConvArgs a{static_cast<const uint16_t*>(in), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out),
@@ -360,7 +364,7 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
       else e = launch<f16_t, 64, 64>(a, false, dgrad, st);
     }
     if (e != hipSuccess) return e;
-    return splitk_reduce(dtype, part, out, (int64_t)a.M * K, a.splits, st);
+    return splitk_reduce(dtype, part, out, (int64_t)a.M * K, a.splits, st, alpha, ep);
   }
   const bool stats = psum != nullptr && psq != nullptr;
   if (dtype == kBF16) {

@@ -43,6 +43,7 @@ struct WgradArgs {
   int N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw;
   int M, splits, steps_per_split;
   uint64_t mq, mpq;  // magic multipliers: floor(m / Q) = (m * mq) >> 36 (same for P*Q)
+  float alpha;       // output scale (splits == 1: applied in the store; else in the reduce)
 };
 
 // floor(x / d) with magic = ceil(2^36 / d): exact while x * d < 2^36 (host: M < 2^22, P*Q < 2^14)
@@ -154,7 +155,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
         const int k = k0 + wm * (BM / 2) + i * 16 + c4 * 4 + e;
         if (k < a.K) {
 #pragma unroll
-          for (int j = 0; j < FN; ++j) st1<T>(out + (int64_t)k * RSC + col0 + wn * (BN / 2) + j * 16 + r16, acc[i][j][e]);
+          for (int j = 0; j < FN; ++j)
+            st1<T>(out + (int64_t)k * RSC + col0 + wn * (BN / 2) + j * 16 + r16, a.alpha * acc[i][j][e]);
         }
       }
   } else {
@@ -172,32 +174,60 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
   }
 }
 
-// dW = Σ_s part[s] in a fixed order, cast to T.  4 elements per thread (16-byte loads).
-template <typename T>
-__global__ __launch_bounds__(256) void conv_wgrad_reduce_k(const float* __restrict__ part, T* __restrict__ out,
-                                                           int64_t n, int splits) {
+// out = alpha * Σ_s part[s] (fixed order: deterministic), cast to T; 4 elements per thread
+// (16-byte loads).  Optional rank-r epilogue (the LoRA update fused into the base GEMM's reduce):
+//   out[m, n] += beta * (mask ? mask[m, n] : 1) * Σ_j U[m, j] · V[j * sv_j + n * sv_n]
+// with U [M, r] and V any 2D view (B of y += t·Bᵀ is V = Bᵀ: sv_j = 1, sv_n = r).
+template <typename T, bool LOWRANK>
+__global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__ part, T* __restrict__ out, int64_t n,
+                                                       int splits, float alpha, SplitkEpilogue ep) {
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 >= n) return;
   f32x4 acc = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + i4));
   for (int s = 1; s < splits; ++s) acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i4));
+  acc *= alpha;
+  if (LOWRANK) {
+    const int64_t m = i4 / ep.N, n0 = i4 - m * ep.N;  // N % 4 == 0: the 4 elements share a row
+    const T* u = reinterpret_cast<const T*>(ep.U) + m * ep.r;
+    const T* v = reinterpret_cast<const T*>(ep.V);
+    f32x4 lr = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < ep.r; ++j) {
+      const float uj = ld1<T>(u + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lr[e] += uj * ld1<T>(v + (int64_t)j * ep.sv_j + (n0 + e) * ep.sv_n);
+    }
+    if (ep.mask != nullptr) {
+      const T* mk = reinterpret_cast<const T*>(ep.mask) + i4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lr[e] *= ld1<T>(mk + e);
+    }
+    acc += ep.beta * lr;
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) st1<T>(out + i4 + e, acc[e]);
 }
 
+template <typename T>
+hipError_t reduce_launch(const float* part, T* out, int64_t n, int splits, float alpha, const SplitkEpilogue* ep,
+                         hipStream_t st) {
+  const int blocks = (int)((n / 4 + 255) / 256);
+  if (ep != nullptr && ep->U != nullptr)
+    hipLaunchKernelGGL((splitk_reduce_k<T, true>), dim3(blocks), dim3(256), 0, st, part, out, n, splits, alpha, *ep);
+  else
+    hipLaunchKernelGGL((splitk_reduce_k<T, false>), dim3(blocks), dim3(256), 0, st, part, out, n, splits, alpha,
+                       SplitkEpilogue{});
+  return hipGetLastError();
+}
+
 }  // namespace
 
-hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st) {
+hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st, float alpha,
+                         const SplitkEpilogue* ep) {
   if (n % 4 != 0 || splits < 1) return hipErrorInvalidValue;
-  const int blocks = (int)((n / 4 + 255) / 256);
-  if (dtype == kBF16)
-    hipLaunchKernelGGL(conv_wgrad_reduce_k<bf16_t>, dim3(blocks), dim3(256), 0, st, part, static_cast<bf16_t*>(out), n,
-                       splits);
-  else if (dtype == kF16)
-    hipLaunchKernelGGL(conv_wgrad_reduce_k<f16_t>, dim3(blocks), dim3(256), 0, st, part, static_cast<f16_t*>(out), n,
-                       splits);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (ep != nullptr && ep->U != nullptr && (ep->N % 4 != 0 || ep->r < 1 || n % ep->N != 0)) return hipErrorInvalidValue;
+  if (dtype == kBF16) return reduce_launch<bf16_t>(part, static_cast<bf16_t*>(out), n, splits, alpha, ep, st);
+  if (dtype == kF16) return reduce_launch<f16_t>(part, static_cast<f16_t*>(out), n, splits, alpha, ep, st);
+  return hipErrorInvalidValue;
 }
 
 namespace {
@@ -209,7 +239,7 @@ int g_wgrad_stages = 0;  // 0 = automatic (conv_wgrad_set_stages, for tuning swe
 template <typename T, int BM, int BN>
 hipError_t launch(const WgradArgs& a, hipStream_t st) {
   const int tiles = ((a.K + BM - 1) / BM) * (a.R * a.S * a.C / BN);
-  const int nb = g_wgrad_stages > 0 ? g_wgrad_stages : (BM == 64 && BN == 64 ? 4 : 3);
+  const int nb = g_wgrad_stages > 0 ? g_wgrad_stages : 2;  // deeper rings measured no better (conv_r01)
   if (nb == 2)
     hipLaunchKernelGGL((conv_wgrad_k<T, BM, BN, 2>), dim3(tiles * a.splits), dim3(kThreads), 0, st, a);
   else if (nb == 3)
@@ -242,7 +272,7 @@ void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* s
 
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
-                      int bn, int splits, int steps_per_split, hipStream_t st) {
+                      int bn, int splits, int steps_per_split, hipStream_t st, float alpha) {
   if (!conv_wgrad_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (C % bn != 0 || (bm != 64 && bm != 128) || (bn != 64 && bn != 128) || splits < 1) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
@@ -252,7 +282,7 @@ hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float*
   if (splits > 1 && partials == nullptr) return hipErrorInvalidValue;
   WgradArgs a{static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(x),
               splits > 1 ? static_cast<void*>(partials) : dw, static_cast<const uint16_t*>(zero), N, H, W, C, K, P, Q,
-              R, S, sh, sw, ph, pw, (int)M64, splits, steps_per_split, magic36(Q), magic36(P * Q)};
+              R, S, sh, sw, ph, pw, (int)M64, splits, steps_per_split, magic36(Q), magic36(P * Q), alpha};
   hipError_t e;
   if (dtype == kBF16) {
     if (bm == 128 && bn == 128) e = launch<bf16_t, 128, 128>(a, st);
@@ -266,7 +296,7 @@ hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float*
     else e = launch<f16_t, 64, 64>(a, st);
   }
   if (e != hipSuccess || splits == 1) return e;
-  return splitk_reduce(dtype, partials, dw, (int64_t)K * R * S * C, splits, st);  // C % 64 == 0: n % 4 == 0
+  return splitk_reduce(dtype, partials, dw, (int64_t)K * R * S * C, splits, st, alpha);  // C % 64 == 0: n % 4 == 0
 }
 
 }  // namespace hyp

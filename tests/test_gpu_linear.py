@@ -69,3 +69,42 @@ def test_lora_linear_uses_native_base_and_matches():
     yr.backward(g.float())
     for u, v in ((y, yr), (x.grad, xr.grad), (a.grad, ar.grad), (bm.grad, br.grad)):
         assert (u.float() - v).norm() <= 2e-2 * v.norm() + 1e-3
+
+
+@pytest.mark.parametrize("v_nr", [True, False])
+def test_linear_lowrank_epilogue_and_alpha(v_nr):
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    M, K, N, r = 96, 1024, 512, 16
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    U = torch.randn(M, r, device="cuda").to(torch.bfloat16)
+    V = torch.randn(N, r, device="cuda").to(torch.bfloat16) if v_nr else torch.randn(r, N, device="cuda").to(torch.bfloat16)
+    mask = (torch.rand(M, N, device="cuda") > 0.3).to(torch.bfloat16)
+    y = _native.native().linear_nt(x, w, alpha=0.5, U=U, V=V, v_nr=v_nr, mask=mask, beta=3.0)
+    lr = U.float() @ (V.float().t() if v_nr else V.float())
+    ref = 0.5 * (x.float() @ w.float().t()) + 3.0 * mask.float() * lr
+    assert (y.float() - ref).norm() <= 1e-2 * ref.norm()
+
+
+def test_lora_dropout_native_matches_reference():
+    from hyperion.ops.lora import lora_linear, lora_linear_reference
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 64, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(1024, 512, device="cuda") / 512 ** 0.5).to(torch.bfloat16)
+    a = (torch.randn(16, 512, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_(True)
+    bm = (torch.randn(1024, 16, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_(True)
+    p, s = 0.1, 2.0
+    torch.cuda.manual_seed(11)
+    y = lora_linear(x, w, None, a, bm, s, p)
+    torch.cuda.manual_seed(11)
+    keep = torch.empty(128, 512, device="cuda", dtype=torch.bfloat16).bernoulli_(1 - p).view(2, 64, 512)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, ar, br = (t.detach().float().requires_grad_(True) for t in (x, a, bm))
+    yr = lora_linear_reference(xr, w.float(), None, ar, br, s, mask=keep.float() / (1 - p))
+    yr.backward(g.float())
+    for u, v in ((y, yr), (x.grad, xr.grad), (a.grad, ar.grad), (bm.grad, br.grad)):
+        assert (u.float() - v).norm() <= 2e-2 * v.norm() + 1e-3
