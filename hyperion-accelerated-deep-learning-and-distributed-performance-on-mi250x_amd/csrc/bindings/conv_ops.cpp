@@ -106,7 +106,7 @@ hyp::SplitkEpilogue make_epilogue(const c10::optional<at::Tensor>& U, const c10:
               "low-rank epilogue: V must be contiguous, output dtype");
   TORCH_CHECK(v_nr ? (V->size(0) == N && V->size(1) == r) : (V->size(0) == r && V->size(1) == N),
               "low-rank epilogue: V must be [N, r] (v_nr) or [r, N]");
-  TORCH_CHECK(N % 4 == 0, "low-rank epilogue: N % 4 == 0");
+  TORCH_CHECK(N % 4 == 0 && r % 8 == 0 && r <= 64, "low-rank epilogue: N % 4 == 0, r % 8 == 0, r <= 64");
   ep.U = U->data_ptr();
   ep.V = V->data_ptr();
   ep.sv_j = v_nr ? 1 : N;

@@ -187,17 +187,35 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
   for (int s = 1; s < splits; ++s) acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i4));
   acc *= alpha;
   if (LOWRANK) {
+    // r % 8 == 0, r <= 64: U's row and V's rows / columns are read as 16- / 8-byte vectors
     const int64_t m = i4 / ep.N, n0 = i4 - m * ep.N;  // N % 4 == 0: the 4 elements share a row
     const T* u = reinterpret_cast<const T*>(ep.U) + m * ep.r;
     const T* v = reinterpret_cast<const T*>(ep.V);
     f32x4 lr = {0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < ep.r; ++j) {
-      const float uj = ld1<T>(u + j);
+    for (int j0 = 0; j0 < ep.r; j0 += 8) {
+      float uj[8];
+      Vec8<T>::load(u + j0, uj);
+      if (ep.sv_n != 1) {  // V = [N, r] (row n holds the r coefficients of output column n)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) lr[e] += uj * ld1<T>(v + (int64_t)j * ep.sv_j + (n0 + e) * ep.sv_n);
+        for (int e = 0; e < 4; ++e) {
+          float vv[8];
+          Vec8<T>::load(v + (n0 + e) * ep.sv_n + j0, vv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) lr[e] += uj[q] * vv[q];
+        }
+      } else {  // V = [r, N]: 4 consecutive outputs = one 8-byte run per coefficient row
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint2 raw = *reinterpret_cast<const uint2*>(v + (int64_t)(j0 + q) * ep.sv_j + n0);
+          const T* h = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) lr[e] += uj[q] * ld1<T>(h + e);
+        }
+      }
     }
     if (ep.mask != nullptr) {
-      const T* mk = reinterpret_cast<const T*>(ep.mask) + i4;
+      const uint2 raw = *reinterpret_cast<const uint2*>(reinterpret_cast<const T*>(ep.mask) + i4);
+      const T* mk = reinterpret_cast<const T*>(&raw);
 #pragma unroll
       for (int e = 0; e < 4; ++e) lr[e] *= ld1<T>(mk + e);
     }
@@ -224,7 +242,8 @@ hipError_t reduce_launch(const float* part, T* out, int64_t n, int splits, float
 hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st, float alpha,
                          const SplitkEpilogue* ep) {
   if (n % 4 != 0 || splits < 1) return hipErrorInvalidValue;
-  if (ep != nullptr && ep->U != nullptr && (ep->N % 4 != 0 || ep->r < 1 || n % ep->N != 0)) return hipErrorInvalidValue;
+  if (ep != nullptr && ep->U != nullptr && (ep->N % 4 != 0 || ep->r < 8 || ep->r % 8 != 0 || n % ep->N != 0))
+    return hipErrorInvalidValue;
   if (dtype == kBF16) return reduce_launch<bf16_t>(part, static_cast<bf16_t*>(out), n, splits, alpha, ep, st);
   if (dtype == kF16) return reduce_launch<f16_t>(part, static_cast<f16_t*>(out), n, splits, alpha, ep, st);
   return hipErrorInvalidValue;

@@ -259,8 +259,12 @@ bool layernorm_supported(int d) {
 }
 
 void layernorm_bwd_geom(int64_t rows, int* P, int* rows_per_wave) {
-  // enough waves to fill 256 CUs, but few partial rows for the column reduction
-  int64_t waves = (rows + 7) / 8;  // >= 8 rows per wave
+  // enough waves to fill 256 CUs (>= min(rows, 1024) waves: a 128-token Llama step has only 128
+  // rows of 4096 — at 8 rows per wave that was 4 workgroups, 136 us per RMSNorm backward), but
+  // few partial rows for the column reduction (<= 2048 waves, >= 8 rows per wave when possible)
+  int64_t waves = (rows + 7) / 8;
+  const int64_t floor_waves = rows < 1024 ? rows : 1024;
+  if (waves < floor_waves) waves = floor_waves;
   if (waves > 2048) waves = 2048;
   if (waves < 1) waves = 1;
   int rpw = (int)((rows + waves - 1) / waves);
