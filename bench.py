@@ -86,7 +86,7 @@ def main(argv=None) -> int:
     if n_gpus > 1:
         model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                     comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None)
-    opt = FusedAdam(model.parameters(), lr=1e-3)
+    opt = FusedAdam(model.parameters(), lr=1e-3, zero_grad_in_step=True)
     loss_fn = nn.MSELoss()
 
     B = args.batch

@@ -34,7 +34,7 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
     dev = torch.device("cuda")
     torch.manual_seed(0)
     m = (simple_lm_256(causal=causal) if model == "lm256" else gpt2_small_lm()).to(dev)
-    opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True)
+    opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True, zero_grad_in_step=graph)
     dt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[precision]
     scaler = LossScaler(enabled=precision == "fp16", device=dev)
     ids = SyntheticWikiText2(n=batch, seq_len=seq, seed=0).input_ids.to(dev)
@@ -111,7 +111,7 @@ def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmu
     if grad_ckpt:
         m.gradient_checkpointing_enable()
     params = [p for p in m.parameters() if p.requires_grad]
-    opt = FusedAdam(params, lr=1e-5, weight_decay=0.01, adamw=True)
+    opt = FusedAdam(params, lr=1e-5, weight_decay=0.01, adamw=True, zero_grad_in_step=graph)
     ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=0)
     ids = (ds.input_ids % cfg.vocab_size).to(dev)
     mask = ds.attention_mask.to(dev)

@@ -79,13 +79,14 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const 
 void adam_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t T, int64_t chunk,
              double lr, double b1, double b2, double eps, double wd, bool adamw, const c10::optional<at::Tensor>& lr_t,
              const at::Tensor& step_t, const c10::optional<at::Tensor>& inv_scale,
-             const c10::optional<at::Tensor>& found_inf, int64_t grad_dtype, int64_t param_dtype) {
+             const c10::optional<at::Tensor>& found_inf, int64_t grad_dtype, int64_t param_dtype, bool zero_grad) {
   const at::DeviceGuard guard(ptrs.device());
   HYP_CHECK_HIP(hyp::adam_multi_tensor((int)grad_dtype, (int)param_dtype, ptrs.data_ptr<int64_t>(), sizes.data_ptr<int64_t>(),
                                        blocks.data_ptr<int>(), (int)blocks.size(0), (int)T, (int)chunk, (float)lr,
                                        (float)b1, (float)b2, (float)eps, (float)wd, adamw ? 1 : 0,
                                        ptr_or_null<float>(lr_t), step_t.data_ptr<float>(),
-                                       ptr_or_null<float>(inv_scale), ptr_or_null<float>(found_inf), cur_stream()));
+                                       ptr_or_null<float>(inv_scale), ptr_or_null<float>(found_inf), cur_stream(),
+                                       zero_grad ? 1 : 0));
 }
 
 void unscale_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t chunk,

@@ -23,7 +23,7 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
 hipError_t adam_multi_tensor(int grad_dtype, int param_dtype, const int64_t* ptrs, const int64_t* sizes,
                              const int* blocks, int nblocks, int T, int chunk, float lr, float b1, float b2, float eps,
                              float wd, int adamw, const float* lr_t, const float* step_t, const float* inv_scale,
-                             const float* found_inf, hipStream_t stream);
+                             const float* found_inf, hipStream_t stream, int zero_grad = 0);
 hipError_t unscale_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks,
                                 int nblocks, int chunk, const float* inv_scale, float* found_inf, hipStream_t stream);
 hipError_t sumsq_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,

@@ -39,7 +39,7 @@ __device__ __forceinline__ void load4<f16_t>(const f16_t* p, float (&v)[4]) {
 struct AdamArgs {
   float lr, b1, b2, eps, wd;
   int adamw;
-  int amsgrad_unused;
+  int zero_grad;  // write zeros over the gradient once read (replaces a separate zero_grad pass)
 };
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a, float lr,
@@ -66,6 +66,12 @@ __device__ __forceinline__ void store4<f16_t>(f16_t* p, const float4& v) {
   *reinterpret_cast<uint2*>(p) = make_uint2(pack_f16x2(v.x, v.y), pack_f16x2(v.z, v.w));
 }
 
+template <typename G>
+__device__ __forceinline__ void store4z(G* p) {
+  if (sizeof(G) == 4) *reinterpret_cast<float4*>(p) = make_float4(0.f, 0.f, 0.f, 0.f);
+  else *reinterpret_cast<uint2*>(p) = make_uint2(0u, 0u);
+}
+
 // ptrs: [4][T] int64 addresses (param f32, grad G, exp_avg f32, exp_avg_sq f32)
 // MASTER: [5][T] (param PL (bf16/f16 compute copy), grad G, exp_avg, exp_avg_sq, fp32 master);
 // the fp32 master is updated and the low-precision compute copy rewritten in the same pass.
@@ -75,12 +81,19 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
                                                       const float* __restrict__ lr_t, const float* __restrict__ step_t,
                                                       const float* __restrict__ inv_scale,
                                                       const float* __restrict__ found_inf) {
-  if (found_inf != nullptr && *found_inf != 0.f) return;  // GradScaler: skip the step on inf/nan
   const int t = blocks[2 * blockIdx.x];
   const int ck = blocks[2 * blockIdx.x + 1];
+  if (found_inf != nullptr && *found_inf != 0.f) {  // GradScaler: skip the step on inf/nan
+    if (a.zero_grad) {
+      G* gz = reinterpret_cast<G*>(ptrs[T + t]);
+      const int64_t n = sizes[t], s0 = (int64_t)ck * chunk, s1 = min(n, s0 + chunk);
+      for (int64_t i = s0 + threadIdx.x; i < s1; i += kThreads) st1<G>(gz + i, 0.f);
+    }
+    return;
+  }
   float* __restrict__ p = reinterpret_cast<float*>(MASTER ? ptrs[4 * T + t] : ptrs[t]);
   PL* __restrict__ pl = reinterpret_cast<PL*>(ptrs[t]);
-  const G* __restrict__ g = reinterpret_cast<const G*>(ptrs[T + t]);
+  G* __restrict__ g = reinterpret_cast<G*>(ptrs[T + t]);
   float* __restrict__ m = reinterpret_cast<float*>(ptrs[2 * T + t]);
   float* __restrict__ v = reinterpret_cast<float*>(ptrs[3 * T + t]);
   const int64_t n = sizes[t];
@@ -99,6 +112,7 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
     float4 vv = *reinterpret_cast<float4*>(v + i);
     float gv[4];
     load4<G>(g + i, gv);
+    if (a.zero_grad) store4z<G>(g + i);
     adam_elem(pv.x, gv[0] * gs, mv.x, vv.x, a, lr, bc1, bc2_sqrt);
     adam_elem(pv.y, gv[1] * gs, mv.y, vv.y, a, lr, bc1, bc2_sqrt);
     adam_elem(pv.z, gv[2] * gs, mv.z, vv.z, a, lr, bc1, bc2_sqrt);
@@ -111,6 +125,7 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
   for (int64_t i = nvec_end + threadIdx.x; i < end; i += kThreads) {
     float pp = p[i], mm = m[i], vv = v[i];
     adam_elem(pp, ld1<G>(g + i) * gs, mm, vv, a, lr, bc1, bc2_sqrt);
+    if (a.zero_grad) st1<G>(g + i, 0.f);
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
@@ -189,9 +204,9 @@ __global__ void sum_partials_k(const float* __restrict__ part, int n, float* __r
 hipError_t adam_multi_tensor(int grad_dtype, int param_dtype, const int64_t* ptrs, const int64_t* sizes,
                              const int* blocks, int nblocks, int T, int chunk, float lr, float b1, float b2, float eps,
                              float wd, int adamw, const float* lr_t, const float* step_t, const float* inv_scale,
-                             const float* found_inf, hipStream_t stream) {
+                             const float* found_inf, hipStream_t stream, int zero_grad) {
   if (nblocks == 0) return hipSuccess;
-  AdamArgs a{lr, b1, b2, eps, wd, adamw, 0};
+  AdamArgs a{lr, b1, b2, eps, wd, adamw, zero_grad};
   HYP_DISPATCH_FLOAT(grad_dtype, G, {
     if (param_dtype == kF32)
       hipLaunchKernelGGL((adam_mt_k<G, float, false>), dim3(nblocks), dim3(kThreads), 0, stream, ptrs, sizes, blocks,

@@ -172,3 +172,25 @@ def test_fused_adam_channels_last_params_take_native_path():
     m(x).sum().backward()
     opt.step()
     assert opt._tables._tables, "channels-last params must use the multi-tensor kernel"
+
+
+def test_fused_adam_zero_grad_in_step():
+    from hyperion.ops.optim import FusedAdam
+
+    torch.manual_seed(0)
+    ps = [torch.randn(1000, device="cuda", requires_grad=True), torch.randn(33, 7, device="cuda", requires_grad=True)]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    o1 = FusedAdam(ps, lr=1e-2, zero_grad_in_step=True)
+    o2 = torch.optim.Adam(ref, lr=1e-2)
+    for _ in range(3):
+        for p, r in zip(ps, ref):
+            g = torch.randn_like(p)
+            p.grad = g.clone() if p.grad is None else p.grad.add_(g)  # accumulate into the zeroed grad
+            r.grad = g.clone()
+        o1.step()
+        o2.step()
+        for p in ps:
+            assert torch.count_nonzero(p.grad) == 0
+        o1.zero_grad(set_to_none=False)  # no-op: already zero
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
