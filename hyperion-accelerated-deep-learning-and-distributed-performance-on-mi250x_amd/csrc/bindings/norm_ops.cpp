@@ -75,6 +75,24 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const 
   return {dx, dres, dwb[0], dwb[1]};
 }
 
+// ---- column sums (bias gradients) ---------------------------------------------------------------
+// x: [..., N] contiguous -> Σ over all leading dims, [N] in out_dtype (default x's dtype)
+at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dtype) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.is_contiguous() && x.dim() >= 1, "column_sum: contiguous input");
+  const int64_t N = x.size(-1), M = N > 0 ? x.numel() / N : 0;
+  TORCH_CHECK(N % 8 == 0 && M >= 1, "column_sum: N % 8 == 0 and at least one row");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "column_sum: 16-byte aligned input");
+  const at::DeviceGuard guard(x.device());
+  const auto odt = out_dtype.value_or(x.scalar_type());
+  auto out = at::empty({N}, x.options().dtype(odt));
+  const int P = hyp::colsum_partials(M, (int)N);
+  auto part = at::empty({(int64_t)P * N}, x.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::column_sum(dtype_code(x), x.data_ptr(), M, (int)N, out.data_ptr(), dtype_code(out),
+                                part.data_ptr<float>(), P, cur_stream()));
+  return out;
+}
+
 // ---- multi-tensor optimizer ------------------------------------------------------------------
 void adam_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t T, int64_t chunk,
              double lr, double b1, double b2, double eps, double wd, bool adamw, const c10::optional<at::Tensor>& lr_t,
@@ -132,6 +150,8 @@ void register_norm_ops(pybind11::module& m) {
   m.def("bn_fwd", &bn_fwd, "fused NHWC batch-norm (+residual)(+relu) forward");
   m.def("bn_bwd", &bn_bwd, "fused NHWC batch-norm (+residual)(+relu) backward");
   m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
+  m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
+        pybind11::arg("out_dtype") = pybind11::none());
   m.def("unscale_mt", &unscale_mt, "multi-tensor unscale + non-finite check");
   m.def("sumsq_mt", &sumsq_mt, "multi-tensor sum of squares");
   m.def("clip_mt", &clip_mt, "multi-tensor clip by global norm (device scalar)");

@@ -153,3 +153,13 @@ hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, v
                                     float* save_mean, float* save_invstd, float* scale, float* shift,
                                     hipStream_t stream);
 }  // namespace hyp
+
+namespace hyp {
+// ---- reduce.hip ------------------------------------------------------------------------------
+// Column sums of a row-major [M, N] matrix (bias gradients): P partial rows (colsum_partials) in
+// `part` [P, N] fp32, then combined into out[N] (out_dtype).  N % 8 == 0, 16-byte aligned x.
+int colsum_partials(int64_t M, int N);
+hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,
+                      hipStream_t st);
+hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);
+}  // namespace hyp

@@ -179,19 +179,6 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
   }
 }
 
-// column sums of [P, d] partials -> out[d]
-__global__ __launch_bounds__(256) void col_sum_k(const float* __restrict__ part, int P, int d, float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
-  float a = 0.f;
-  if (c < d)
-    for (int p = g; p < P; p += 4) a += part[(int64_t)p * d + c];
-  red[g][threadIdx.x & 63] = a;
-  __syncthreads();
-  if (g == 0 && c < d) out[c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-
 template <typename T, bool RMS>
 hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, const float* b, float* mean,
                            float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
@@ -245,9 +232,10 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
       return hipErrorInvalidValue;
   }
 #undef HYP_LN_B
-  if (dw) hipLaunchKernelGGL(col_sum_k, dim3((d + 63) / 64), dim3(256), 0, st, pdw, P, d, dw);
-  if (db && pdb) hipLaunchKernelGGL(col_sum_k, dim3((d + 63) / 64), dim3(256), 0, st, pdb, P, d, db);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, kF32, st);
+  if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, kF32, st);
+  return e;
 }
 
 }  // namespace

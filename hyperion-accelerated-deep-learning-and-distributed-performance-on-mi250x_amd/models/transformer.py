@@ -33,6 +33,7 @@ from torch.utils.checkpoint import checkpoint
 
 from ..ops.attention import attention_packed
 from ..ops.layernorm import LayerNorm
+from ..ops.linear import linear
 from ..ops.linear_act import linear_act
 
 
@@ -65,10 +66,10 @@ class MultiheadSelfAttention(nn.Module):
         key_padding_mask: Optional[torch.Tensor] = None,
     ) -> torch.Tensor:
         B, S, E = x.shape
-        qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias).view(B, S, 3, self.num_heads, self.head_dim)
+        qkv = linear(x, self.in_proj_weight, self.in_proj_bias).view(B, S, 3, self.num_heads, self.head_dim)
         p = self.dropout if self.training else 0.0
         o = attention_packed(qkv, causal=causal, dropout_p=p, key_padding_mask=key_padding_mask)
-        return self.out_proj(o.reshape(B, S, E))
+        return linear(o.reshape(B, S, E), self.out_proj.weight, self.out_proj.bias)
 
 
 def _ffn_up(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
@@ -106,7 +107,7 @@ class TransformerEncoderLayer(nn.Module):
 
     def _ff(self, x: torch.Tensor) -> torch.Tensor:
         h = _ffn_up(x, self.linear1.weight, self.linear1.bias, self.activation)
-        return self.linear2(self.dropout(h))
+        return linear(self.dropout(h), self.linear2.weight, self.linear2.bias)
 
     def forward(self, x: torch.Tensor, causal: bool = False,
                 key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -26,6 +26,7 @@ import torch.nn as nn
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.layernorm import LayerNorm, layer_norm
+from ..ops.linear import linear
 from .transformer import MultiheadSelfAttention, _ffn_up
 
 
@@ -41,7 +42,7 @@ class MLPBlock(nn.Sequential):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
         h = _ffn_up(x, self[0].weight, self[0].bias, "gelu")
-        return self[4](self[3](self[2](h)))
+        return self[4](linear(self[2](h), self[3].weight, self[3].bias))
 
 
 class EncoderBlock(nn.Module):

@@ -9,8 +9,9 @@ multi-stage global_load_lds ring, and the data gradient reads the SAME row-major
 transposed in-kernel (ds_read_b64_tr_b16) — no ``w.t().contiguous()`` copy.
 
 ``linear(x, w, b)``: native forward when M <= ``SKINNY_MAX_M`` tokens and the shapes fit the
-kernel (in % 64, out % 8); native data gradient when out % 64 and in % 8.  Weight / bias grads
-(only for trainable weights) use the vendor GEMM / reduction.  Everything else is ``F.linear``.
+kernel (in % 64, out % 8); native data gradient when out % 64 and in % 8; otherwise the vendor
+GEMM (bias in its epilogue).  The bias gradient is ``csrc/kernels/reduce.hip``'s column sum at
+any size; the weight gradient (only for trainable weights) is the vendor GEMM.
 """
 from __future__ import annotations
 
@@ -52,15 +53,29 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dy2 @ w
 
 
+def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """``dy2.sum(0)`` (a bias gradient) — ``csrc/kernels/reduce.hip`` column sums on gfx950 (autograd's
+    generic reduction ran [6304, 768] bf16 at 0.4 TB/s in the ViT step)."""
+    if (dy2.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16, torch.float32) and dy2.shape[-1] % 8 == 0
+            and dy2.is_contiguous() and dy2.data_ptr() % 16 == 0 and dy2.numel() > 0
+            and _native.use_native(dy2, op="bias_grad")):
+        return _native.native().column_sum(dy2, dtype)
+    return dy2.sum(0, dtype=torch.float32).to(dtype)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        y = linear_fwd(x2, w)
-        if b is not None:
-            y = y + b.to(y.dtype)
+        if b is not None and not _fwd_ok(x2, w):
+            y = F.linear(x2, w, b.to(x2.dtype))  # bias in the vendor GEMM's epilogue
+        else:
+            y = linear_fwd(x2, w)
+            if b is not None:
+                y = y + b.to(y.dtype)
         ctx.save_for_backward(x2 if ctx.needs_input_grad[1] else None, w)
         ctx.has_b = b is not None
+        ctx.bdt = b.dtype if b is not None else None
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
 
@@ -70,7 +85,7 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).to(w.dtype)
         dx = linear_dgrad(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = (dy2.t() @ x2).to(w.dtype) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        db = bias_grad(dy2.contiguous(), ctx.bdt) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db
 
 

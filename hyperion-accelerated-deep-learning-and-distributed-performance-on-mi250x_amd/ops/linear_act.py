@@ -17,6 +17,8 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from .linear import bias_grad
+
 
 def _cdt(x: torch.Tensor) -> torch.dtype:
     return torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else x.dtype
@@ -41,12 +43,39 @@ class _LinearReLU(torch.autograd.Function):
         dy = torch.ops.aten.threshold_backward(dh.reshape(h.shape).to(h.dtype), h, 0)
         dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = (dy.t() @ x2).to(wdt) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0, dtype=torch.float32).to(bdt) if ctx.needs_input_grad[2] else None
+        db = bias_grad(dy, bdt) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+class _LinearGELU(torch.autograd.Function):
+    """``gelu(x Wᵀ + b)``: bias in the GEMM epilogue, the pre-activation kept for backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        dt = _cdt(x)
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).to(dt)
+        wc, bc = w.to(dt), b.to(dt)
+        y = torch.addmm(bc, x2, wc.t())
+        ctx.save_for_backward(x2, wc, y)
+        ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
+        return F.gelu(y).view(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, wc, y = ctx.saved_tensors
+        xdt, wdt, bdt, shape = ctx.meta
+        dy = torch.ops.aten.gelu_backward(dh.reshape(y.shape).to(y.dtype), y)
+        dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
+        dw = (dy.t() @ x2).to(wdt) if ctx.needs_input_grad[1] else None
+        db = bias_grad(dy, bdt) if ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
     if activation == "relu" and x.is_cuda and b is not None:
         return _LinearReLU.apply(x, w, b)
+    if activation == "gelu" and x.is_cuda and b is not None:
+        return _LinearGELU.apply(x, w, b)
     y = F.linear(x, w, b)
     return F.gelu(y) if activation == "gelu" else F.relu(y)

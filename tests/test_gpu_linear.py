@@ -108,3 +108,32 @@ def test_lora_dropout_native_matches_reference():
     yr.backward(g.float())
     for u, v in ((y, yr), (x.grad, xr.grad), (a.grad, ar.grad), (bm.grad, br.grad)):
         assert (u.float() - v).norm() <= 2e-2 * v.norm() + 1e-3
+
+
+@pytest.mark.parametrize("shape", [(6304, 768), (6304, 3072), (3, 8), (4064, 2304), (128, 11008)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_column_sum_matches_fp64(shape, dtype):
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device="cuda").to(dtype)
+    out = _native.native().column_sum(x, torch.float32)
+    ref = x.double().sum(0)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gelu_linear_act_grads_match_reference():
+    from hyperion.ops.linear_act import linear_act
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 197, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(512, 256, device="cuda") / 16).to(torch.bfloat16).requires_grad_(True)
+    b = (torch.randn(512, device="cuda") * 0.1).to(torch.bfloat16).requires_grad_(True)
+    y = linear_act(x, w, b, "gelu")
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.gelu(torch.nn.functional.linear(xr, wr, br))
+    yr.backward(g.float())
+    for u, v in ((y, yr), (x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert (u.float() - v).norm() <= 2e-2 * v.norm() + 1e-3
