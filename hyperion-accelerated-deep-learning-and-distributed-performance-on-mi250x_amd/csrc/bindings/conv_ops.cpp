@@ -239,6 +239,59 @@ std::vector<at::Tensor> bn_fwd_partials(const at::Tensor& x, const c10::optional
   return {y, stats[0], stats[1]};
 }
 
+// ---- pooling (NHWC) -------------------------------------------------------------------------
+std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
+              "maxpool2d_fwd: channels-last [N, C, H, W] with C % 8 == 0");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(P > 0 && Q > 0 && k * k <= 256 && pad < k, "maxpool2d_fwd: bad geometry");
+  const at::DeviceGuard guard(x.device());
+  auto y = at::empty({N, C, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  HYP_CHECK_HIP(hyp::maxpool2d_forward(dtype_code(x), x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C,
+                                       (int)k, (int)s, (int)pad, cur_stream()));
+  return {y, idx};
+}
+
+at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s,
+                         int64_t pad) {
+  HYP_CHECK_CUDA_TENSOR(dy);
+  TORCH_CHECK(dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool2d_bwd: channels-last dy");
+  const int N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(dy.size(2) == (H + 2 * pad - k) / s + 1 && dy.size(3) == (W + 2 * pad - k) / s + 1 &&
+                  idx.numel() == dy.numel() && idx.scalar_type() == at::kByte,
+              "maxpool2d_bwd: shape mismatch");
+  const at::DeviceGuard guard(dy.device());
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  HYP_CHECK_HIP(hyp::maxpool2d_backward(dtype_code(dy), dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), N,
+                                        (int)H, (int)W, C, (int)k, (int)s, (int)pad, cur_stream()));
+  return dx;
+}
+
+// x [N, C, H, W] channels-last -> [N, C]
+at::Tensor global_avgpool_fwd(const at::Tensor& x) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
+              "global_avgpool_fwd: channels-last [N, C, H, W] with C % 8 == 0");
+  const at::DeviceGuard guard(x.device());
+  auto y = at::empty({x.size(0), x.size(1)}, x.options());
+  HYP_CHECK_HIP(hyp::global_avgpool_forward(dtype_code(x), x.data_ptr(), y.data_ptr(), x.size(0),
+                                            x.size(2) * x.size(3), x.size(1), cur_stream()));
+  return y;
+}
+
+at::Tensor global_avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
+  HYP_CHECK_CUDA_TENSOR(dy);
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous() && dy.size(1) % 8 == 0, "global_avgpool_bwd: [N, C] dy");
+  const at::DeviceGuard guard(dy.device());
+  auto dx = at::empty({dy.size(0), dy.size(1), H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  HYP_CHECK_HIP(hyp::global_avgpool_backward(dtype_code(dy), dy.data_ptr(), dx.data_ptr(), dy.size(0), H * W,
+                                             dy.size(1), cur_stream()));
+  return dx;
+}
+
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
@@ -255,6 +308,10 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("splits") = -1, pybind11::arg("bn") = -1,
         pybind11::arg("alpha") = 1.0, pybind11::arg("U") = pybind11::none(), pybind11::arg("V") = pybind11::none(),
         pybind11::arg("v_nr") = false, pybind11::arg("mask") = pybind11::none(), pybind11::arg("beta") = 1.0);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd, "NHWC max pool (+ window-tap index)");
+  m.def("maxpool2d_bwd", &maxpool2d_bwd, "NHWC max pool backward (gather, deterministic)");
+  m.def("global_avgpool_fwd", &global_avgpool_fwd, "NHWC global average pool");
+  m.def("global_avgpool_bwd", &global_avgpool_bwd, "NHWC global average pool backward");
   m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),

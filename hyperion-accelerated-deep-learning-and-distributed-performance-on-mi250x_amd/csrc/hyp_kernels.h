@@ -163,3 +163,14 @@ hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int
                       hipStream_t st);
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);
 }  // namespace hyp
+
+namespace hyp {
+// ---- pool.hip --------------------------------------------------------------------------------
+// NHWC max pool (idx: per-element window tap, uint8) and global average pool; C % 8 == 0.
+hipError_t maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int k,
+                             int s, int pad, hipStream_t st);
+hipError_t maxpool2d_backward(int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C,
+                              int k, int s, int pad, hipStream_t st);
+hipError_t global_avgpool_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t st);
+hipError_t global_avgpool_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+}  // namespace hyp

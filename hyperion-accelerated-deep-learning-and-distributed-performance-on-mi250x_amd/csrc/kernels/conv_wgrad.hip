@@ -178,13 +178,27 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
 // (16-byte loads).  Optional rank-r epilogue (the LoRA update fused into the base GEMM's reduce):
 //   out[m, n] += beta * (mask ? mask[m, n] : 1) * Σ_j U[m, j] · V[j * sv_j + n * sv_n]
 // with U [M, r] and V any 2D view (B of y += t·Bᵀ is V = Bᵀ: sv_j = 1, sv_n = r).
+// 64-thread blocks (a wgrad output can be only 37K floats: 256-thread blocks left ~36 workgroups
+// on 256 CUs) and 4 independent accumulators, so 4 slab loads are in flight per thread.
+constexpr int kRedThreads = 64;
+
 template <typename T, bool LOWRANK>
-__global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__ part, T* __restrict__ out, int64_t n,
-                                                       int splits, float alpha, SplitkEpilogue ep) {
-  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+__global__ __launch_bounds__(kRedThreads) void splitk_reduce_k(const float* __restrict__ part, T* __restrict__ out,
+                                                               int64_t n, int splits, float alpha, SplitkEpilogue ep) {
+  const int64_t i4 = ((int64_t)blockIdx.x * kRedThreads + threadIdx.x) * 4;
   if (i4 >= n) return;
-  f32x4 acc = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + i4));
-  for (int s = 1; s < splits; ++s) acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i4));
+  const f32x4* src = reinterpret_cast<const f32x4*>(part + i4);
+  const int64_t sn = n / 4;  // slab stride in f32x4
+  f32x4 a0 = __builtin_nontemporal_load(src), a1 = {0.f, 0.f, 0.f, 0.f}, a2 = a1, a3 = a1;
+  int s = 1;
+  for (; s + 3 < splits; s += 4) {
+    a0 += __builtin_nontemporal_load(src + (int64_t)s * sn);
+    a1 += __builtin_nontemporal_load(src + (int64_t)(s + 1) * sn);
+    a2 += __builtin_nontemporal_load(src + (int64_t)(s + 2) * sn);
+    a3 += __builtin_nontemporal_load(src + (int64_t)(s + 3) * sn);
+  }
+  for (; s < splits; ++s) a0 += __builtin_nontemporal_load(src + (int64_t)s * sn);
+  f32x4 acc = (a0 + a1) + (a2 + a3);
   acc *= alpha;
   if (LOWRANK) {
     // r % 8 == 0, r <= 64: U's row and V's rows / columns are read as 16- / 8-byte vectors
@@ -228,12 +242,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__
 template <typename T>
 hipError_t reduce_launch(const float* part, T* out, int64_t n, int splits, float alpha, const SplitkEpilogue* ep,
                          hipStream_t st) {
-  const int blocks = (int)((n / 4 + 255) / 256);
+  const int blocks = (int)((n / 4 + kRedThreads - 1) / kRedThreads);
   if (ep != nullptr && ep->U != nullptr)
-    hipLaunchKernelGGL((splitk_reduce_k<T, true>), dim3(blocks), dim3(256), 0, st, part, out, n, splits, alpha, *ep);
+    hipLaunchKernelGGL((splitk_reduce_k<T, true>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n, splits, alpha,
+                       *ep);
   else
-    hipLaunchKernelGGL((splitk_reduce_k<T, false>), dim3(blocks), dim3(256), 0, st, part, out, n, splits, alpha,
-                       SplitkEpilogue{});
+    hipLaunchKernelGGL((splitk_reduce_k<T, false>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n, splits,
+                       alpha, SplitkEpilogue{});
   return hipGetLastError();
 }
 

@@ -23,6 +23,8 @@ from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
+
+from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.layernorm import LayerNorm, layer_norm
@@ -172,11 +174,11 @@ def fallback_cnn(num_classes: int = 1000) -> nn.Sequential:
     return nn.Sequential(
         nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3),
         nn.ReLU(inplace=True),
-        nn.MaxPool2d(kernel_size=3, stride=2, padding=1),
+        MaxPool2d(kernel_size=3, stride=2, padding=1),
         nn.Conv2d(64, 128, kernel_size=3, padding=1),
         nn.ReLU(inplace=True),
-        nn.MaxPool2d(kernel_size=3, stride=2, padding=1),
-        nn.AdaptiveAvgPool2d((1, 1)),
+        MaxPool2d(kernel_size=3, stride=2, padding=1),
+        AdaptiveAvgPool2d((1, 1)),
         nn.Flatten(),
         nn.Linear(128, num_classes),
     )
