@@ -29,9 +29,43 @@ std::vector<at::Tensor> ce_fwd_bwd(at::Tensor& logits, const at::Tensor& target,
   return {loss, lse};
 }
 
+// ---- embedding ---------------------------------------------------------------------------------
+at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& w) {
+  HYP_CHECK_CUDA_TENSOR(w);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.device() == w.device(),
+              "embedding_fwd: contiguous int64 ids on the weight's device");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) % 8 == 0, "embedding_fwd: contiguous [V, E], E % 8 == 0");
+  const at::DeviceGuard guard(w.device());
+  std::vector<int64_t> shape(ids.sizes().begin(), ids.sizes().end());
+  shape.push_back(w.size(1));
+  auto out = at::empty(shape, w.options());
+  HYP_CHECK_HIP(hyp::embedding_forward(dtype_code(w), ids.data_ptr<int64_t>(), w.data_ptr(), out.data_ptr(),
+                                       ids.numel(), (int)w.size(1), w.size(0), cur_stream()));
+  return out;
+}
+
+// dy [..., E] (contiguous), ids [...] -> dense dW [V, E] (rows of absent ids and of pad_idx are zero)
+at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V, int64_t pad_idx) {
+  HYP_CHECK_CUDA_TENSOR(dy);
+  const int64_t E = dy.size(-1), n = ids.numel();
+  TORCH_CHECK(dy.is_contiguous() && dy.numel() == n * E && E % 8 == 0, "embedding_bwd: contiguous dy [..., E]");
+  const at::DeviceGuard guard(dy.device());
+  auto flat = ids.reshape({-1});
+  auto sorted = at::sort(flat, /*stable=*/true, 0, false);
+  auto sid = std::get<0>(sorted).contiguous(), order = std::get<1>(sorted).contiguous();
+  auto dw = at::empty({V, E}, dy.options());
+  auto present = at::zeros({V}, dy.options().dtype(at::kByte));
+  HYP_CHECK_HIP(hyp::embedding_backward(dtype_code(dy), sid.data_ptr<int64_t>(), order.data_ptr<int64_t>(),
+                                        dy.data_ptr(), dw.data_ptr(), present.data_ptr<uint8_t>(), n, (int)E, V,
+                                        pad_idx, cur_stream()));
+  return dw;
+}
+
 }  // namespace
 
 void register_loss_ops(pybind11::module& m) {
+  m.def("embedding_fwd", &embedding_fwd, "token embedding gather");
+  m.def("embedding_bwd", &embedding_bwd, "deterministic dense embedding gradient (sorted runs)");
   m.def("ce_fwd_bwd", &ce_fwd_bwd, "in-place softmax cross-entropy forward+backward", pybind11::arg("logits"),
         pybind11::arg("target"), pybind11::arg("scale"), pybind11::arg("scale_mul"), pybind11::arg("ignore_index"),
         pybind11::arg("write_grad"));

@@ -174,3 +174,12 @@ hipError_t maxpool2d_backward(int dtype, const void* dy, const uint8_t* idx, voi
 hipError_t global_avgpool_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t st);
 hipError_t global_avgpool_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
 }  // namespace hyp
+
+namespace hyp {
+// ---- embedding.hip ---------------------------------------------------------------------------
+hipError_t embedding_forward(int dtype, const int64_t* ids, const void* w, void* out, int64_t n, int E, int64_t V,
+                             hipStream_t st);
+// sorted_ids / order: the flattened ids sorted ascending and their positions; present: [V] zeroed
+hipError_t embedding_backward(int dtype, const int64_t* sorted_ids, const int64_t* order, const void* dy, void* dw,
+                              uint8_t* present, int64_t n, int E, int64_t V, int64_t pad_idx, hipStream_t st);
+}  // namespace hyp

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 from torch.utils.checkpoint import checkpoint
 
+from ..ops.embedding import Embedding
 from ..ops.attention import attention
 from ..ops.cross_entropy import LinearCrossEntropy
 from ..ops.layernorm import RMSNorm
@@ -130,7 +131,7 @@ class LlamaDecoderLayer(nn.Module):
 class LlamaModel(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size, padding_idx=cfg.pad_token_id)
+        self.embed_tokens = Embedding(cfg.vocab_size, cfg.hidden_size, padding_idx=cfg.pad_token_id)
         self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.gradient_checkpointing = False

@@ -26,6 +26,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
+from ..ops.embedding import Embedding
 from ..ops.cross_entropy import LinearCrossEntropy
 from .transformer import encoder
 
@@ -56,7 +57,7 @@ class SimpleTransformerLM(nn.Module):
             raise ValueError(f"key_style {key_style!r}")
         self.key_style = key_style
         self._emb_name, self._enc_name = ("embed", "tr") if key_style == "ddp" else ("embedding", "transformer")
-        setattr(self, self._emb_name, nn.Embedding(vocab_size, emb_dim))
+        setattr(self, self._emb_name, Embedding(vocab_size, emb_dim))
         setattr(self, self._enc_name, encoder(emb_dim, n_heads, n_layers, ff_dim, dropout, activation,
                                               use_checkpoint=use_checkpoint))
         self.fc = LinearCrossEntropy(emb_dim, vocab_size)
