@@ -49,15 +49,12 @@ at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V,
   HYP_CHECK_CUDA_TENSOR(dy);
   const int64_t E = dy.size(-1), n = ids.numel();
   TORCH_CHECK(dy.is_contiguous() && dy.numel() == n * E && E % 8 == 0, "embedding_bwd: contiguous dy [..., E]");
+  TORCH_CHECK(ids.is_contiguous() && ids.scalar_type() == at::kLong, "embedding_bwd: contiguous int64 ids");
   const at::DeviceGuard guard(dy.device());
-  auto flat = ids.reshape({-1});
-  auto sorted = at::sort(flat, /*stable=*/true, 0, false);
-  auto sid = std::get<0>(sorted).contiguous(), order = std::get<1>(sorted).contiguous();
-  auto dw = at::empty({V, E}, dy.options());
-  auto present = at::zeros({V}, dy.options().dtype(at::kByte));
-  HYP_CHECK_HIP(hyp::embedding_backward(dtype_code(dy), sid.data_ptr<int64_t>(), order.data_ptr<int64_t>(),
-                                        dy.data_ptr(), dw.data_ptr(), present.data_ptr<uint8_t>(), n, (int)E, V,
-                                        pad_idx, cur_stream()));
+  auto dw32 = at::zeros({V, E}, dy.options().dtype(at::kFloat));
+  at::Tensor dw = dy.scalar_type() == at::kFloat ? dw32 : at::empty({V, E}, dy.options());
+  HYP_CHECK_HIP(hyp::embedding_backward(dtype_code(dy), ids.data_ptr<int64_t>(), dy.data_ptr(),
+                                        dw32.data_ptr<float>(), dw.data_ptr(), n, (int)E, V, pad_idx, cur_stream()));
   return dw;
 }
 
@@ -65,7 +62,7 @@ at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V,
 
 void register_loss_ops(pybind11::module& m) {
   m.def("embedding_fwd", &embedding_fwd, "token embedding gather");
-  m.def("embedding_bwd", &embedding_bwd, "deterministic dense embedding gradient (sorted runs)");
+  m.def("embedding_bwd", &embedding_bwd, "dense embedding gradient (fp32 atomic accumulate + cast)");
   m.def("ce_fwd_bwd", &ce_fwd_bwd, "in-place softmax cross-entropy forward+backward", pybind11::arg("logits"),
         pybind11::arg("target"), pybind11::arg("scale"), pybind11::arg("scale_mul"), pybind11::arg("ignore_index"),
         pybind11::arg("write_grad"));

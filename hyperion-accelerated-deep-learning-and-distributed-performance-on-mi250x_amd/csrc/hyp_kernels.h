@@ -179,7 +179,7 @@ namespace hyp {
 // ---- embedding.hip ---------------------------------------------------------------------------
 hipError_t embedding_forward(int dtype, const int64_t* ids, const void* w, void* out, int64_t n, int E, int64_t V,
                              hipStream_t st);
-// sorted_ids / order: the flattened ids sorted ascending and their positions; present: [V] zeroed
-hipError_t embedding_backward(int dtype, const int64_t* sorted_ids, const int64_t* order, const void* dy, void* dw,
-                              uint8_t* present, int64_t n, int E, int64_t V, int64_t pad_idx, hipStream_t st);
+// dw32: zeroed [V, E] fp32 accumulator (the result for f32 weights); dw: output in the weight dtype
+hipError_t embedding_backward(int dtype, const int64_t* ids, const void* dy, float* dw32, void* dw, int64_t n, int E,
+                              int64_t V, int64_t pad_idx, hipStream_t st);
 }  // namespace hyp

@@ -1,15 +1,14 @@
-// Token embedding forward (row gather) and a deterministic backward (sorted-segment row sums).
+// Token embedding forward (row gather) and backward (fp32 atomic row accumulation).
 //
 // Reference: ``nn.Embedding`` in SimpleTransformerLM (V = 50257, E = 256 / 768; C14/C15) and HF
 // Llama's ``embed_tokens`` (V = 32000, E = 4096; C26) — PyTorch's index_select forward and
 // ``embedding_dense_backward`` (SURVEY §2.4 "Embedding fwd/bwd").
 //
 // Forward: one wave per token, 16-byte vectors along the row.
-// Backward: the token ids are sorted once (with their positions); one wave per sorted position,
-// and only the wave that starts a run of equal ids sums the run's gradient rows (fp32, in sorted
-// order: deterministic) and writes that id's row.  Rows of ids that never occur are zeroed by the
-// same launch (a second grid stripe walks the "absent" rows), so the dense [V, E] gradient is
-// written exactly once, with no atomics and no separate memset.
+// Backward: fp32 atomic accumulation into a zeroed [V, E] buffer, one wave per token (full-rate
+// 256-byte atomic runs), then one cast pass for bf16/f16 weights.  (A first, deterministic
+// sorted-run version serialized each id's run in one wave: the LM's pad token is ~1/3 of all
+// tokens, so one wave summed ~1300 rows — 1.35 ms per step; profiles/lm_r01.)
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -33,53 +32,30 @@ __global__ __launch_bounds__(256) void embed_fwd_k(const int64_t* __restrict__ i
   }
 }
 
-// blocks [0, nrun_blocks): one wave per sorted position (run heads write their row);
-// blocks [nrun_blocks, ...): one wave per row id, zeroing rows whose id is absent (present[id] == 0).
+// One wave per token: dW[id, :] += dY[token, :] with no-return fp32 atomics, one dword per lane so
+// each wave instruction adds a contiguous 256-byte run (the full-rate shape: MI355X_MICROARCH
+// "Global float atomics").  The pad id gets no gradient.
 template <typename T>
-__global__ __launch_bounds__(256) void embed_bwd_k(const int64_t* __restrict__ sorted_ids,
-                                                   const int64_t* __restrict__ order, const T* __restrict__ dy,
-                                                   T* __restrict__ dw, const uint8_t* __restrict__ present, int64_t n,
-                                                   int E, int64_t V, int nrun_blocks, int64_t pad_idx) {
+__global__ __launch_bounds__(256) void embed_bwd_atomic_k(const int64_t* __restrict__ ids, const T* __restrict__ dy,
+                                                          float* __restrict__ dw, int64_t n, int E, int64_t V,
+                                                          int64_t pad_idx) {
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= n) return;
+  const int64_t id = ids[tok];
+  if (id < 0 || id >= V || id == pad_idx) return;
   const int lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < nrun_blocks) {
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= n) return;
-    const int64_t id = sorted_ids[i];
-    if (i > 0 && sorted_ids[i - 1] == id) return;  // not a run head
-    if (id < 0 || id >= V) return;
-    int64_t j1 = i + 1;
-    while (j1 < n && sorted_ids[j1] == id) ++j1;
-    for (int c = lane * 8; c < E; c += 64 * 8) {
-      float acc[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-      if (id != pad_idx) {
-        for (int64_t j = i; j < j1; ++j) {
-          float v[8];
-          Vec8<T>::load(dy + order[j] * E + c, v);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc[q] += v[q];
-        }
-      }
-      Vec8<T>::store(dw + id * E + c, acc);
-    }
-    return;
-  }
-  const int64_t row = (int64_t)(blockIdx.x - nrun_blocks) * 4 + (threadIdx.x >> 6);
-  if (row >= V || present[row]) return;
-  float z[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) z[q] = 0.f;
-  for (int c = lane * 8; c < E; c += 64 * 8) Vec8<T>::store(dw + row * E + c, z);
+  const T* src = dy + tok * E;
+  float* dst = dw + id * E;
+  for (int c = lane; c < E; c += 64) atomicAdd(dst + c, ld1<T>(src + c));
 }
 
-__global__ __launch_bounds__(256) void mark_present_k(const int64_t* __restrict__ ids, uint8_t* __restrict__ present,
-                                                      int64_t n, int64_t V) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    const int64_t id = ids[i];
-    if (id >= 0 && id < V) present[id] = 1;
-  }
+template <typename T>
+__global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ src, T* __restrict__ dst, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= n) return;
+  float v[8];
+  Vec8<float>::load(src + i, v);
+  Vec8<T>::store(dst + i, v);
 }
 
 }  // namespace
@@ -95,17 +71,20 @@ hipError_t embedding_forward(int dtype, const int64_t* ids, const void* w, void*
   return hipGetLastError();
 }
 
-// present: [V] uint8 scratch, ZEROED by the caller
-hipError_t embedding_backward(int dtype, const int64_t* sorted_ids, const int64_t* order, const void* dy, void* dw,
-                              uint8_t* present, int64_t n, int E, int64_t V, int64_t pad_idx, hipStream_t st) {
+// dw32: [V, E] fp32 accumulator (ZEROED by the caller; it is the result itself when dtype is f32);
+// dw: the output in the weight dtype (ignored for f32)
+hipError_t embedding_backward(int dtype, const int64_t* ids, const void* dy, float* dw32, void* dw, int64_t n, int E,
+                              int64_t V, int64_t pad_idx, hipStream_t st) {
   if (E % 8 != 0) return hipErrorInvalidValue;
-  if (n > 0)
-    hipLaunchKernelGGL(mark_present_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sorted_ids, present, n, V);
-  const int nrun = (int)((n + 3) / 4);
-  const int nrow = (int)((V + 3) / 4);
   HYP_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL(embed_bwd_k<T>, dim3(nrun + nrow), dim3(256), 0, st, sorted_ids, order, (const T*)dy, (T*)dw,
-                       present, n, E, V, nrun, pad_idx);
+    if (n > 0)
+      hipLaunchKernelGGL(embed_bwd_atomic_k<T>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, ids, (const T*)dy,
+                         dw32, n, E, V, pad_idx);
+    if (dtype != kF32) {
+      const int64_t total = V * E;  // E % 8 == 0
+      hipLaunchKernelGGL(cast_f32_k<T>, dim3((unsigned)((total / 8 + 255) / 256)), dim3(256), 0, st, dw32, (T*)dw,
+                         total);
+    }
   });
   return hipGetLastError();
 }

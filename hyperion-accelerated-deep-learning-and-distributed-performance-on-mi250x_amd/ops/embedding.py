@@ -3,9 +3,9 @@
 Reference: ``nn.Embedding`` in SimpleTransformerLM (V = 50257) and HF Llama ``embed_tokens``
 (V = 32000) — index_select forward, ``embedding_dense_backward`` (SURVEY §2.4 "Embedding").
 ``Embedding`` keeps ``nn.Embedding``'s parameters, keys and ``padding_idx`` semantics (the pad row
-gets no gradient); on GPU the forward is a vectorized row gather and the backward a
-deterministic sorted-run reduction that writes the dense gradient exactly once (no atomics, no
-separate zero fill).  ``max_norm`` / ``scale_grad_by_freq`` / ``sparse`` fall back to PyTorch.
+gets no gradient); on GPU the forward is a vectorized row gather and the backward accumulates
+token rows with full-rate fp32 atomics (one 256-byte run per wave instruction) into a zeroed
+buffer, cast once to the weight dtype.  ``max_norm`` / ``scale_grad_by_freq`` / ``sparse`` fall back to PyTorch.
 """
 from __future__ import annotations
 

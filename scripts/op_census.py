@@ -42,10 +42,23 @@ elif which == "resnet50":
         opt.zero_grad(set_to_none=True)
         torch.nn.functional.mse_loss(m(x).float(), y).backward()
         opt.step()
-else:
-    from hyperion.bench import models as M
+elif which == "lm":
+    from hyperion.data.synthetic import SyntheticWikiText2
+    from hyperion.models.simple_lm import GPT2_PAD, simple_lm_256
 
-    raise SystemExit("use vit / resnet50")
+    m = simple_lm_256().to(dev)
+    opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True)
+    ids = SyntheticWikiText2(n=32, seq_len=128, seed=0).input_ids.to(dev)
+    x, yy = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
+
+    def body():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = m.forward_loss(x, yy, ignore_index=GPT2_PAD)
+        loss.backward()
+        opt.step()
+else:
+    raise SystemExit("use vit / resnet50 / lm")
 for _ in range(3):
     body()
 torch.cuda.synchronize()
