@@ -43,7 +43,8 @@ def parse(argv=None):
     ap.add_argument("--kernels", default=None, choices=["hyperion", "torch"],
                     help="hyperion = fused gfx950 kernels (default); torch = PyTorch eager ops (A/B)")
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (1-GPU; N>1 see --graph-multi)")
-    ap.add_argument("--graph-multi", type=int, default=0, help="also capture when N>1")
+    ap.add_argument("--graph-multi", type=int, default=1,
+                    help="N>1: capture fwd+bwd and the optimizer as two hipGraphs around eager bucket all-reduces")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--channels-last", type=int, default=1)

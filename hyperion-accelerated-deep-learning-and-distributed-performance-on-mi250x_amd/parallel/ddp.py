@@ -15,7 +15,11 @@ MI355X design:
 * after backward, ``param.grad`` is re-pointed at its bucket slice, so the fused optimizer reads
   the reduced gradient in place (no copy back) and its pointer table stays valid across steps;
 * ``comm_dtype=torch.bfloat16`` halves the bytes on the wire (the reduction runs in RCCL);
-* ``broadcast_buffers`` reproduces the reference's per-forward BN buffer broadcast (K5).
+* ``broadcast_buffers`` reproduces the reference's per-forward BN buffer broadcast (K5);
+* ``defer_allreduce`` (set by ``TrainStep`` for hipGraph replay): backward only packs the buckets
+  and ``allreduce_buckets()`` reduces them afterwards — the captured fwd+bwd graph and the
+  optimizer graph then hold no RCCL call, and the collectives run eagerly between the two
+  replays (one launch per bucket; no communication inside a captured graph).
 """
 from __future__ import annotations
 
@@ -76,7 +80,10 @@ class DistributedDataParallel(nn.Module):
         device_ids=None,  # accepted for API compatibility with torch DDP
         find_unused_parameters: bool = False,
         comm=None,
+        buckets_at_world_1: bool = False,
     ):
+        """``buckets_at_world_1``: build the bucket machinery even for a single rank (tests of the
+        bucket / deferred-all-reduce / graph paths on a one-GPU box)."""
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -89,13 +96,15 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
         self._sync = True
+        self.defer_allreduce = False
         self._buckets: List[_Bucket] = []
         self._where: Dict[nn.Parameter, Tuple[_Bucket, int]] = {}
         self._next_launch = 0
         self._callback_queued = False
         self._hooks = []
-        if self.world > 1:
-            _flat_broadcast([p.data for p in module.parameters()] + list(module.buffers()), 0, process_group)
+        if self.world > 1 or (buckets_at_world_1 and self.comm is not None):
+            if self.world > 1:
+                _flat_broadcast([p.data for p in module.parameters()] + list(module.buffers()), 0, process_group)
             self._build_buckets(bucket_cap_mb, first_bucket_mb, comm_dtype)
             for p in module.parameters():
                 if p.requires_grad:
@@ -152,7 +161,7 @@ class DistributedDataParallel(nn.Module):
                 slot.copy_(g * (1.0 / self.world))
         b.got[i] = True
         b.ready += 1
-        if b.ready == len(b.params):
+        if b.ready == len(b.params) and not self.defer_allreduce:
             self._launch_ready()
 
     def _launch_ready(self) -> None:
@@ -176,7 +185,8 @@ class DistributedDataParallel(nn.Module):
                             b.buf[off : off + p.numel()].zero_()
                             b.got[i] = True
                 b.ready = len(b.params)
-        self._launch_ready()
+        if not self.defer_allreduce:
+            self._launch_ready()
         for b in self._buckets:
             if b.work is not None:
                 b.work.wait()  # stream-ordered: the compute stream waits on RCCL, the host does not
@@ -194,6 +204,26 @@ class DistributedDataParallel(nn.Module):
             b.launched = False
         self._next_launch = 0
         self._callback_queued = False
+
+    def allreduce_buckets(self) -> None:
+        """Reduce every bucket now (``defer_allreduce`` mode; call between backward and step).
+
+        The gradients already point at their bucket slices (pre-scaled by 1/world), so after this
+        the optimizer reads the averaged gradients in place."""
+        if not self._buckets or not self._sync:
+            return
+        works = []
+        for b in self._buckets:
+            range_push(f"ddp_allreduce_b{b.index}")
+            works.append(self.comm.all_reduce(b.buf, "sum"))
+            range_pop()
+        for w in works:
+            if w is not None:
+                w.wait()
+
+    @property
+    def bucketed(self) -> bool:
+        return bool(self._buckets)
 
     # ------------------------------------------------------------------ module API
     @contextlib.contextmanager

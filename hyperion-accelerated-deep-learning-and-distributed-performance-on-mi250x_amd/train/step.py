@@ -7,6 +7,12 @@ kernels: convs, fused BN, fused optimizer) costs one graph launch on the host.
 
 Requirements for capture (all satisfied by Hyperion ops): no host syncs inside the step, no
 pageable H2D copies, device-side optimizer scalars (``FusedAdam`` keeps step count on device).
+
+Data-parallel steps (Hyperion ``DDP`` over more than one rank, ``broadcast_buffers=False``) are
+captured as TWO graphs — forward+backward (the gradient hooks pack the buckets) and the optimizer
+— with the bucket all-reduces issued eagerly between the replays (``DDP.defer_allreduce``): no
+RCCL call is ever recorded into a graph, and the ~500 per-step kernel launches still cost two
+graph launches.
 """
 from __future__ import annotations
 
@@ -48,22 +54,44 @@ class TrainStep:
         self.static_x: Optional[torch.Tensor] = None
         self.static_y: Optional[torch.Tensor] = None
         self.static_loss: Optional[torch.Tensor] = None
+        self.graph2: Optional[torch.cuda.CUDAGraph] = None
 
-    def _body(self, x: torch.Tensor, y: torch.Tensor, zero_in_place: bool = False) -> torch.Tensor:
-        if zero_in_place:  # graph mode: gradients keep their addresses, zeroed by a captured memset
+    def _ddp(self):
+        """The model if it is a bucketed Hyperion DDP whose step can be split around its collectives."""
+        from ..parallel.ddp import DistributedDataParallel
+
+        m = self.model
+        if isinstance(m, DistributedDataParallel) and m.bucketed and not m.broadcast_buffers and self.scaler is None:
+            return m
+        return None
+
+    def _fwd_bwd(self, x: torch.Tensor, y: torch.Tensor, zero_in_place: bool = False) -> torch.Tensor:
+        if zero_in_place:  # graph mode: gradients keep their addresses, zeroed in place
             self.opt.zero_grad(set_to_none=False)
         dev = x.device
         with autocast_ctx(dev, self.amp_dtype):
             out = self.model(x)
             loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
+        loss.backward()
+        return loss.detach()
+
+    def _body(self, x: torch.Tensor, y: torch.Tensor, zero_in_place: bool = False) -> torch.Tensor:
         if self.scaler is not None:
+            if zero_in_place:
+                self.opt.zero_grad(set_to_none=False)
+            with autocast_ctx(x.device, self.amp_dtype):
+                out = self.model(x)
+                loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
             self.scaler.scale(loss).backward()
             self.scaler.step(self.opt)
             self.scaler.update()
-        else:
-            loss.backward()
-            self.opt.step()
-        return loss.detach()
+            return loss.detach()
+        loss = self._fwd_bwd(x, y, zero_in_place)
+        ddp = self._ddp()
+        if ddp is not None and ddp.defer_allreduce:
+            ddp.allreduce_buckets()
+        self.opt.step()
+        return loss
 
     def eager_step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         self.opt.zero_grad(set_to_none=True)
@@ -86,6 +114,16 @@ class TrainStep:
                 self._body(self.static_x, self.static_y, zero_in_place=True)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        ddp = self._ddp()
+        if ddp is not None:  # two graphs around the (eager) bucket all-reduces
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self.static_loss = self._fwd_bwd(self.static_x, self.static_y, zero_in_place=True)
+            with torch.cuda.graph(g2, pool=g1.pool()):
+                self.opt.step()
+            torch.cuda.synchronize()
+            self.graph, self.graph2 = g1, g2
+            return
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.static_loss = self._body(self.static_x, self.static_y, zero_in_place=True)
@@ -96,12 +134,18 @@ class TrainStep:
         if not self.use_graph:
             return self.eager_step(x, y)
         if self.graph is None:
+            ddp = self._ddp()
+            if ddp is not None:
+                ddp.defer_allreduce = True  # warm-up and replays: all-reduce between the graphs
             self._capture(x, y)
         if x.data_ptr() != self.static_x.data_ptr():
             self.static_x.copy_(x, non_blocking=True)
         if y.data_ptr() != self.static_y.data_ptr():
             self.static_y.copy_(y, non_blocking=True)
         self.graph.replay()
+        if self.graph2 is not None:
+            self.model.allreduce_buckets()
+            self.graph2.replay()
         return self.static_loss
 
 

@@ -68,3 +68,28 @@ def _ddp_no_sync(rank, world):
 def test_ddp_no_sync_keeps_local_grads():
     res = run_world(_ddp_no_sync, 2)
     assert res[0] != res[1]
+
+
+def _ddp_deferred(rank, world, steps):
+    """defer_allreduce: backward packs buckets only; allreduce_buckets() between backward and step."""
+    from hyperion.parallel import DDP
+
+    m = DDP(_model(seed=rank), bucket_cap_mb=1.0, first_bucket_mb=0.1, broadcast_buffers=False)
+    m.defer_allreduce = True
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    for s in range(steps):
+        x, y = _data(s)
+        x, y = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        m.allreduce_buckets()
+        opt.step()
+        opt.zero_grad(set_to_none=False)  # graph-style: gradients keep their bucket addresses
+    return {k: v for k, v in m.state_dict().items() if "running" not in k and "num_batches" not in k}
+
+
+def test_ddp_deferred_allreduce_matches_single_process():
+    ref = _ref(3)
+    res = run_world(_ddp_deferred, 2, (3,))
+    for k in ref:
+        torch.testing.assert_close(res[0][k], res[1][k], rtol=0, atol=0, msg=k)
+        torch.testing.assert_close(res[0][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
