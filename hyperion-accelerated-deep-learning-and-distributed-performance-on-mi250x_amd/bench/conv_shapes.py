@@ -80,15 +80,12 @@ def run(batch: int = 32, sweep: bool = False) -> List[Dict]:
             r["hyp_dgrad_us"] = _med(lambda: C_.conv_dgrad(dy, w, p, p))
         if C % 64 == 0:
             r["hyp_wgrad_us"] = _med(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p))
-        if sweep:  # LDS pipeline depth of each kernel (conv_set_stages), automatic plans otherwise
-            for nb in (2, 3, 4):
-                C_.conv_set_stages(nb, nb)
+        if sweep:  # tile shapes of the fwd / dgrad kernels (automatic plan otherwise)
+            for bm, bn in ((64, 64), (128, 64), (128, 128)):
                 if C % 64 == 0:
-                    r[f"hyp_fwd_nb{nb}_us"] = _med(lambda: C_.conv_fwd(x, w, s, s, p, p, True), repeat=10)
-                    r[f"hyp_wgrad_nb{nb}_us"] = _med(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p), repeat=10)
+                    r[f"hyp_fwd_{bm}x{bn}_us"] = _med(lambda: C_.conv_fwd(x, w, s, s, p, p, True, bm, bn), repeat=10)
                 if s == 1 and K % 64 == 0:
-                    r[f"hyp_dgrad_nb{nb}_us"] = _med(lambda: C_.conv_dgrad(dy, w, p, p), repeat=10)
-            C_.conv_set_stages(0, 0)
+                    r[f"hyp_dgrad_{bm}x{bn}_us"] = _med(lambda: C_.conv_dgrad(dy, w, p, p, bm, bn), repeat=10)
         for k in ("hyp_fwd_us", "miopen_fwd_us", "hyp_dgrad_us", "miopen_dgrad_us", "hyp_wgrad_us", "miopen_wgrad_us"):
             if k in r:
                 r[k.replace("_us", "_tflops")] = flop / (r[k] * 1e-6) / 1e12

@@ -16,7 +16,7 @@ at::Tensor& zero_page(const at::Device& dev) {
 
 // x [N,C,H,W] channels-last, w [K,C,R,S] channels-last -> (y [N,K,P,Q] channels-last, psum, psq)
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t sh, int64_t sw, int64_t ph,
-                                 int64_t pw, bool stats) {
+                                 int64_t pw, bool stats, int64_t bm_req, int64_t bn_req) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: 4D tensors");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -34,6 +34,10 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   const int M = N * P * Q;
   int bm = 128, bn = 128;
   hyp::conv_fwd_tile(M, K, &bm, &bn);
+  if (bm_req > 0) bm = (int)bm_req;  // tuning sweeps
+  if (bn_req > 0) bn = (int)bn_req;
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
+              "conv_fwd: tiles 64x64, 128x64 or 128x128");
   at::Tensor psum, psq;
   if (stats) {
     const int mt = (M + bm - 1) / bm;
@@ -49,7 +53,8 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
 
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
 // filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
-at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw) {
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
+                      int64_t bn_req) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -69,6 +74,10 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   int bm = 128, bn = 128;
   hyp::conv_fwd_tile(N * H * W, C, &bm, &bn);
+  if (bm_req > 0) bm = (int)bm_req;
+  if (bn_req > 0) bn = (int)bn_req;
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
+              "conv_dgrad: tiles 64x64, 128x64 or 128x128");
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                               zero_page(dy.device()).data_ptr(), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
                               dph, dpw, bm, bn, 1, 1, nullptr, cur_stream()));
@@ -295,7 +304,9 @@ at::Tensor global_avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
-  m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)");
+  m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)", pybind11::arg("x"),
+        pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
+        pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1);
   m.def("conv_set_stages", [](int64_t fwd, int64_t wgrad) {
     hyp::conv_set_stages((int)fwd);
     hyp::conv_wgrad_set_stages((int)wgrad);
@@ -312,7 +323,9 @@ void register_conv_ops(pybind11::module& m) {
   m.def("maxpool2d_bwd", &maxpool2d_bwd, "NHWC max pool backward (gather, deterministic)");
   m.def("global_avgpool_fwd", &global_avgpool_fwd, "NHWC global average pool");
   m.def("global_avgpool_bwd", &global_avgpool_bwd, "NHWC global average pool backward");
-  m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)");
+  m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)",
+        pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
+        pybind11::arg("bn") = -1);
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

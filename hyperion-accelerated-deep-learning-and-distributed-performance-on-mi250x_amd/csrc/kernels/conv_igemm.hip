@@ -139,23 +139,40 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   const int kt0 = split * a.steps_per_split;  // this split's reduction steps [kt0, kt0 + nk)
   const int nk = max(0, min(a.R * a.S * cpb - kt0, a.steps_per_split));
 
-  auto stage = [&](int tl, uint16_t* buf) {
-    const int t = kt0 + tl;
-    const int rs = t / cpb, c0 = (t - rs * cpb) * kBK;
-    const int r = rs / a.S, s = rs - r * a.S;
+  // reduction position of the NEXT stage to issue, advanced incrementally (stages are issued in
+  // order): filter tap (r, s) and channel slice c0 — no per-stage integer divisions
+  int st_r, st_s, st_c0;
+  {
+    const int rs = kt0 / cpb;
+    st_c0 = (kt0 - rs * cpb) * kBK;
+    st_r = rs / a.S;
+    st_s = rs - st_r * a.S;
+  }
+  int64_t st_t = kt0;
+  auto stage = [&](uint16_t* buf) {
+    const int r = st_r, s = st_s, c0 = st_c0;
     const int64_t tap = ((int64_t)r * a.W + s) * a.C + c0;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       const int h = a_h0[i] + r, w = a_w0[i] + s;
-      const bool ok = a_ok[i] && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const bool ok = a_ok[i] & ((unsigned)h < (unsigned)a.H) & ((unsigned)w < (unsigned)a.W);
       glds16(ok ? a.in + a_off[i] + tap : zero, buf + (i * 4 + wave) * 8 * kBK);
     }
     // DGRAD: filter tap (R-1-r, S-1-s) of reduction channels c0 .. c0+63
     const int64_t kofs = DGRAD ? ((int64_t)c0 * a.R * a.S + (a.R - 1 - r) * a.S + (a.S - 1 - s)) * a.K
-                               : (int64_t)t * kBK;
+                               : st_t * kBK;
 #pragma unroll
     for (int i = 0; i < IB; ++i)
       glds16(b_src[i] ? b_src[i] + kofs : zero, buf + BM * kBK + (i * 4 + wave) * 512);
+    ++st_t;
+    st_c0 += kBK;
+    if (st_c0 == a.C) {
+      st_c0 = 0;
+      if (++st_s == a.S) {
+        st_s = 0;
+        ++st_r;
+      }
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -167,12 +184,12 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   // NB-deep ring: stage t+NB-1 is issued right after the barrier that retires stage t-1's buffer
 #pragma unroll
   for (int i = 0; i < NB - 1; ++i)
-    if (i < nk) stage(i, smem + i * kBuf);
+    if (i < nk) stage(smem + i * kBuf);
   const int r16 = lane & 15, c4 = lane >> 4;
   for (int t = 0; t < nk; ++t) {
     mfl::wait_stage<IA + IB, NB>(min(NB - 2, nk - 1 - t));
     mfl::barrier_keep_vm();  // stage t visible to all waves; every wave is done with buffer (t-1) % NB
-    if (t + NB - 1 < nk) stage(t + NB - 1, smem + ((t + NB - 1) % NB) * kBuf);
+    if (t + NB - 1 < nk) stage(smem + ((t + NB - 1) % NB) * kBuf);
     const uint16_t* as = smem + (t % NB) * kBuf;
     const uint16_t* bs = as + BM * kBK;
 #pragma unroll
