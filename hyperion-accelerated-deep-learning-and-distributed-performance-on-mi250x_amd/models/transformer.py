@@ -33,8 +33,8 @@ from torch.utils.checkpoint import checkpoint
 
 from ..ops.attention import attention_packed
 from ..ops.layernorm import LayerNorm
-from ..ops.linear import linear
-from ..ops.linear_act import linear_act
+from ..ops.linear import Linear, linear
+from ..ops.linear_act import LinearAct, linear_act
 
 
 class MultiheadSelfAttention(nn.Module):
@@ -50,7 +50,7 @@ class MultiheadSelfAttention(nn.Module):
         self.dropout = dropout
         self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
         self.in_proj_bias = nn.Parameter(torch.empty(3 * embed_dim)) if bias else None
-        self.out_proj = nn.Linear(embed_dim, embed_dim, bias=bias)
+        self.out_proj = Linear(embed_dim, embed_dim, bias=bias)
         self._reset_parameters()
 
     def _reset_parameters(self) -> None:  # same init as nn.MultiheadAttention
@@ -69,7 +69,7 @@ class MultiheadSelfAttention(nn.Module):
         qkv = linear(x, self.in_proj_weight, self.in_proj_bias).view(B, S, 3, self.num_heads, self.head_dim)
         p = self.dropout if self.training else 0.0
         o = attention_packed(qkv, causal=causal, dropout_p=p, key_padding_mask=key_padding_mask)
-        return linear(o.reshape(B, S, E), self.out_proj.weight, self.out_proj.bias)
+        return self.out_proj(o.reshape(B, S, E))
 
 
 def _ffn_up(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
@@ -95,9 +95,10 @@ class TransformerEncoderLayer(nn.Module):
         if activation not in ("relu", "gelu"):
             raise ValueError(f"activation {activation!r}")
         self.self_attn = MultiheadSelfAttention(d_model, nhead, dropout=dropout, bias=bias)
-        self.linear1 = nn.Linear(d_model, dim_feedforward, bias=bias)
+        # modules called as modules (FSDP gathers a unit's shard in its forward pre-hook)
+        self.linear1 = LinearAct(d_model, dim_feedforward, bias=bias, activation=activation)
         self.dropout = nn.Dropout(dropout)
-        self.linear2 = nn.Linear(dim_feedforward, d_model, bias=bias)
+        self.linear2 = Linear(dim_feedforward, d_model, bias=bias)
         self.norm_first = norm_first
         self.norm1 = LayerNorm(d_model, eps=layer_norm_eps)
         self.norm2 = LayerNorm(d_model, eps=layer_norm_eps)
@@ -106,8 +107,7 @@ class TransformerEncoderLayer(nn.Module):
         self.activation = activation
 
     def _ff(self, x: torch.Tensor) -> torch.Tensor:
-        h = _ffn_up(x, self.linear1.weight, self.linear1.bias, self.activation)
-        return linear(self.dropout(h), self.linear2.weight, self.linear2.bias)
+        return self.linear2(self.dropout(self.linear1(x)))
 
     def forward(self, x: torch.Tensor, causal: bool = False,
                 key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:

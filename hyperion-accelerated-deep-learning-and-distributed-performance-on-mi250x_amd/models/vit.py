@@ -28,7 +28,8 @@ from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.layernorm import LayerNorm, layer_norm
-from ..ops.linear import linear
+from ..ops.linear import Linear
+from ..ops.linear_act import LinearAct
 from .transformer import MultiheadSelfAttention, _ffn_up
 
 
@@ -36,15 +37,15 @@ class MLPBlock(nn.Sequential):
     """torchvision ``MLPBlock`` layout: ``0`` Linear, ``1`` GELU, ``2`` Dropout, ``3`` Linear, ``4`` Dropout."""
 
     def __init__(self, dim: int, hidden: int, dropout: float = 0.0):
-        super().__init__(nn.Linear(dim, hidden), nn.GELU(), nn.Dropout(dropout), nn.Linear(hidden, dim),
-                         nn.Dropout(dropout))
+        # [0] applies the GELU itself (bias + GELU with the GEMM); [1] stays for the torchvision layout
+        super().__init__(LinearAct(dim, hidden, activation="gelu"), nn.GELU(), nn.Dropout(dropout),
+                         Linear(hidden, dim), nn.Dropout(dropout))
         for m in (self[0], self[3]):
             nn.init.xavier_uniform_(m.weight)
             nn.init.normal_(m.bias, std=1e-6)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
-        h = _ffn_up(x, self[0].weight, self[0].bias, "gelu")
-        return self[4](linear(self[2](h), self[3].weight, self[3].bias))
+        return self[4](self[3](self[2](self[0](x))))
 
 
 class EncoderBlock(nn.Module):

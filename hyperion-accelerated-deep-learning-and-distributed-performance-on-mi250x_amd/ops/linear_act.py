@@ -79,3 +79,17 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], acti
         return _LinearGELU.apply(x, w, b)
     y = F.linear(x, w, b)
     return F.gelu(y) if activation == "gelu" else F.relu(y)
+
+
+class LinearAct(torch.nn.Linear):
+    """``nn.Linear`` (same parameters / keys) whose forward is ``act(x Wᵀ + b)`` via :func:`linear_act`.
+
+    Calling it as a MODULE matters under FSDP: the unit's forward pre-hook gathers the sharded
+    weight; reaching into ``.weight`` from a parent module would read a freed shard."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, activation: str = "relu", **kw):
+        super().__init__(in_features, out_features, bias=bias, **kw)
+        self.activation = activation
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
+        return linear_act(x, self.weight, self.bias, self.activation)

@@ -41,7 +41,10 @@ def _fsdp_train(rank, world, steps, policy_kind, clip, strategy):
     from hyperion.parallel.fsdp import FSDP, size_based_auto_wrap_policy, transformer_auto_wrap_policy
 
     policy = {"layer": transformer_auto_wrap_policy({TransformerEncoderLayer}),
-              "size": size_based_auto_wrap_policy(2000), "none": None}[policy_kind]
+              "size": size_based_auto_wrap_policy(2000),
+              # every Linear its own unit (the reference's min_num_params=100_000 at full size):
+              # the FFN / attention projections must be CALLED as modules for the gather hooks
+              "leaf": size_based_auto_wrap_policy(500), "none": None}[policy_kind]
     m = FSDP(_make_model(), auto_wrap_policy=policy, device_id=torch.device("cpu"), sharding_strategy=strategy)
     opt = torch.optim.SGD(m.parameters(), lr=1e-1, momentum=0.9, weight_decay=0.01)
     per = 8 // world
@@ -58,7 +61,7 @@ def _fsdp_train(rank, world, steps, policy_kind, clip, strategy):
     return {"sd": sd, "units": m.unit_sizes()}
 
 
-@pytest.mark.parametrize("policy", ["layer", "size", "none"])
+@pytest.mark.parametrize("policy", ["layer", "size", "leaf", "none"])
 @pytest.mark.parametrize("strategy", ["FULL_SHARD", "SHARD_GRAD_OP"])
 def test_fsdp_matches_single_process(policy, strategy):
     ref = _reference_train(3)
