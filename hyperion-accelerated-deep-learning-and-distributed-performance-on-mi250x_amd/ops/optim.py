@@ -131,6 +131,10 @@ class FusedAdam(torch.optim.Optimizer):
 
     def _reference_step(self, group, ps, gs, ms, vs, masters=None):
         """PyTorch reference (CPU / fallback); identical math to the kernel."""
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # the host-side step count would be baked into the graph (frozen bias correction)
+            raise RuntimeError("FusedAdam: reference path reached during hipGraph capture (grad/param layouts "
+                               "or dtypes outside the fused kernel's envelope)")
         if self.found_inf is not None and float(self.found_inf) != 0.0:
             return
         b1, b2 = group["betas"]

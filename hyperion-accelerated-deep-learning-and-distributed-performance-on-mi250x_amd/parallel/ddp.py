@@ -50,6 +50,17 @@ def _flat_broadcast(tensors: List[torch.Tensor], src: int, group) -> None:
                 off += n
 
 
+def _param_view(flat: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """``flat`` (p.numel() elements) viewed with p's own strides when p is densely packed in some
+    dimension order (channels-last conv weights): the gradient then has the parameter's layout
+    (the fused optimizer needs grad and param element orders to match), else a plain view."""
+    if p.is_contiguous():
+        return flat.view(p.shape)
+    if p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last):
+        return flat.as_strided(p.shape, p.stride())
+    return flat.view(p.shape)
+
+
 class _Bucket:
     __slots__ = ("index", "params", "offsets", "buf", "ready", "got", "work", "launched")
 
@@ -57,10 +68,13 @@ class _Bucket:
         self.index = index
         self.params = params
         self.offsets: List[int] = []
+        # every slot starts on a 64-byte boundary: the fused optimizer's vector loads (and its
+        # table builder) need >= 16-byte aligned gradients; the padding stays zero
+        align = max(1, 64 // torch.empty((), dtype=dtype).element_size())
         off = 0
         for p in params:
             self.offsets.append(off)
-            off += p.numel()
+            off += (p.numel() + align - 1) // align * align
         self.buf = torch.zeros(off, dtype=dtype, device=device)
         self.ready = 0
         self.got = [False] * len(params)
@@ -152,9 +166,9 @@ class DistributedDataParallel(nn.Module):
         if b.got[i]:
             return
         off, n = b.offsets[i], p.numel()
-        slot = b.buf[off : off + n]
+        slot = _param_view(b.buf[off : off + n], p)
         with torch.no_grad():
-            g = p.grad.reshape(-1)
+            g = p.grad
             if g.dtype == slot.dtype:
                 torch.mul(g, 1.0 / self.world, out=slot)  # pack + pre-scale in one pass
             else:
@@ -192,7 +206,7 @@ class DistributedDataParallel(nn.Module):
                 b.work.wait()  # stream-ordered: the compute stream waits on RCCL, the host does not
                 b.work = None
             for p, off in zip(b.params, b.offsets):
-                view = b.buf[off : off + p.numel()].view_as(p)
+                view = _param_view(b.buf[off : off + p.numel()], p)
                 if view.dtype == p.dtype:
                     p.grad = view
                 elif p.grad is not None:
