@@ -111,7 +111,9 @@ class _FlatGroup:
             self.offsets.append(self.offsets[-1] + n)
         self.numel = sum(self.numels)
         W, r = fsdp.world, fsdp.rank
-        self.padded = int(math.ceil(max(self.numel, 1) / W) * W)
+        # shards of a multiple of 64 elements: every rank's slice of the gathered buffer (and every
+        # reduce-scatter output) starts 128-byte aligned for RCCL and the vector kernels
+        self.padded = int(math.ceil(max(self.numel, 1) / (W * 64)) * W * 64)
         self.shard_numel = self.padded // W
         dev = fsdp.device
         self.cdtype = fsdp.mp.param_dtype or torch.float32
