@@ -49,6 +49,7 @@ def parse(argv=None):
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--channels-last", type=int, default=1)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--smi", type=int, default=0, help="sample amd-smi power / clocks during the timed steps")
     return ap.parse_args(argv)
 
 
@@ -106,6 +107,11 @@ def main(argv=None) -> int:
         dist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    smi = None
+    if args.smi and env.rank == 0:
+        from hyperion.profiling.smi import SmiSampler
+
+        smi = SmiSampler(interval_s=0.5).__enter__()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step(x, y)
@@ -116,6 +122,8 @@ def main(argv=None) -> int:
     if dev.type == "cuda":
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if smi is not None:
+        smi.__exit__(None, None, None)
     if n_gpus > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -136,7 +144,7 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 3) if args.model == "resnet50" else None,
             "dtype": args.precision,
-            "data": "synthetic (torch.rand images 3x224x224, rand targets; random-init weights)",
+            "data": f"synthetic (torch.rand images 3x{args.image}x{args.image}, rand targets; random-init weights)",
             "config": {
                 "model": args.model,
                 "global_batch": B * n_gpus,
@@ -156,6 +164,8 @@ def main(argv=None) -> int:
             "baseline": {"value": BASELINE_SAMPLES_PER_S, "ms_per_step": 56.32, "hw": "1x MI250X GCD, fp32"},
             "final_loss": round(final_loss, 6),
         }
+        if smi is not None:
+            rec["smi"] = smi.summary()
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:

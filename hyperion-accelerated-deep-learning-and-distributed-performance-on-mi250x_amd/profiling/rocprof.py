@@ -25,10 +25,12 @@ FAMILIES = [
     ("layernorm", r"ln_(fwd|bwd)_k|layer_norm|col_sum_k"),
     ("attention", r"attn_|flash|fmha|attention"),
     ("conv_wgrad", r"wrw|bwd_weight|conv.*wgrad|BackwardWeight"),
-    ("conv_dgrad", r"igemm_bwd|bwd_data|conv.*dgrad|BackwardData"),
+    ("splitk_reduce", r"splitk_reduce|colsum_"),
+    ("conv_dgrad", r"igemm_bwd|bwd_data|conv.*dgrad|BackwardData|conv_fwd_k<[^,]+, \d+, \d+, (true|false), true"),
     ("conv_fwd", r"igemm_fwd|conv_fwd|grouped_conv_fwd|naive_conv.*fwd|ConvFwd|conv2d"),
     ("gemm", r"gemm|Cijk|gemm_mfma|xdl"),
-    ("pool", r"pool"),
+    ("pool", r"pool|gap_(fwd|bwd)"),
+    ("embedding", r"embed_"),
     ("softmax_ce", r"softmax|cross_entropy|nll_loss|ce_"),
     ("bn_torch", r"batch_norm|batchnorm|BatchNorm|MIOpenBatchNorm"),
     ("copy_cast", r"copy|Cast|fill"),

@@ -62,3 +62,22 @@ def test_scaling_report_reproduces_reference_numbers(tmp_path):
 def test_run_scaling_experiment_dry_run_commands():
     cmds = run_scaling_experiment("language_ddp", [1, 2], epochs=1, base_dir="/tmp/x", dry_run=True)
     assert len(cmds) == 2 and "--nproc-per-node=2" in cmds[1] and "127.0.0.1" in cmds[1]
+
+
+def test_amd_smi_json_parsing():
+    from hyperion.profiling.smi import parse_amd_smi
+
+    text = ('[{"gpu": 0, "power": {"socket_power": {"value": 812, "unit": "W"}}, '
+            '"clock": {"gfx_0": {"clk": {"value": 2400, "unit": "MHz"}}}, '
+            '"temperature": {"hotspot": {"value": 61, "unit": "C"}}}]')
+    recs = parse_amd_smi(text)
+    assert recs == [{"power_w": 812.0, "gfx_clock_mhz": 2400.0, "temp_c": 61.0}]
+    assert parse_amd_smi("not json") == []
+
+
+def test_rocprof_families_split_dgrad_from_fwd():
+    from hyperion.profiling.rocprof import family
+
+    assert family("void hyp::(anonymous namespace)::conv_fwd_k<unsigned short, 64, 64, false, true, 2>(x)") == "conv_dgrad"
+    assert family("void hyp::(anonymous namespace)::conv_fwd_k<unsigned short, 64, 64, true, false, 2>(x)") == "conv_fwd"
+    assert family("void hyp::(anonymous namespace)::conv_wgrad_k<unsigned short, 64, 64, 2>(x)") == "conv_wgrad"
