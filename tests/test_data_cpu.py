@@ -66,3 +66,39 @@ def test_reference_arrow_test_split_loads():
     ids, m = w[0]
     assert ids.shape == (128,) and m.shape == (128,)
     assert int(ids[m == 0][0]) == 50256 if (m == 0).any() else True
+
+
+def test_prepare_wikitext2_roundtrip(tmp_path):
+    """C11: filter empty lines, tokenize to 128 with pad = eos, save_to_disk, read back with the
+    reference wrapper."""
+    from hyperion.data.datasets import WikiText2TorchDataset, load_wikitext2
+    from hyperion.data.prepare import HashTokenizer, prepare_wikitext2
+
+    raw = {"train": ["", " = Title = ", "   ", "some words, more words .", ""] * 3, "test": ["", "x y"]}
+    counts = prepare_wikitext2(raw, str(tmp_path / "wt2"), tokenizer=HashTokenizer())
+    assert counts == {"train": 6, "test": 1}
+    ds = WikiText2TorchDataset(load_wikitext2(str(tmp_path / "wt2"), "train"))
+    assert len(ds) == 6
+    ids, mask = ds[0]
+    assert ids.shape == (128,) and ids.dtype == torch.long and mask.dtype == torch.long
+    assert int(mask.sum()) == 3 and int(ids[-1]) == 50256  # "= Title =" -> 3 tokens, then eos padding
+
+
+def test_prepare_cifar10_binary(tmp_path):
+    """C12: CIFAR-10 binary records -> normalized (Tensor[3,32,32], label) list, all-zero image dropped."""
+    import numpy as np
+
+    from hyperion.data.datasets import load_cifar10_pt
+    from hyperion.data.prepare import prepare_cifar10
+
+    rng = np.random.default_rng(0)
+    recs = rng.integers(0, 256, size=(5, 3073), dtype=np.uint8)
+    recs[:, 0] = [0, 3, 9, 1, 2]
+    recs[2, 1:] = 0  # all-zero image: filtered like the reference
+    recs.tofile(tmp_path / "data_batch_1.bin")
+    recs[:2].tofile(tmp_path / "test_batch.bin")
+    counts = prepare_cifar10(str(tmp_path), str(tmp_path / "out"))
+    assert counts == {"train": 4, "test": 2}
+    pairs = load_cifar10_pt(str(tmp_path / "out" / "cifar10_train.pt"))
+    x, y = pairs[0]
+    assert x.shape == (3, 32, 32) and y == 0 and float(x.min()) >= -1.0 and float(x.max()) <= 1.0
