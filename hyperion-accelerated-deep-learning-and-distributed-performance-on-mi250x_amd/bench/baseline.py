@@ -172,7 +172,17 @@ def run_baseline_benchmarks(results_dir: str = "results/benchmarks/baseline", pr
             print(f"{name:28s} total {r['Total Time (ms)']:.2f} ms  {r['Throughput (samples/s)']:.1f} samples/s")
     os.makedirs(results_dir, exist_ok=True)
     pd.DataFrame(rows).to_csv(os.path.join(results_dir, out_name), index=False)
+    _plot("visualize_baseline_results", os.path.join(results_dir, out_name))
     return rows
+
+
+def _plot(fn: str, csv_path: str) -> None:
+    try:
+        from . import plots
+
+        getattr(plots, fn)(csv_path)
+    except Exception as e:  # a missing plotting backend never fails a benchmark
+        print(f"[plot] {fn} skipped: {e}")
 
 
 def test_batch_size_scaling(model_fn: Callable[[], nn.Module], input_shape_fn: Callable[[int], Sequence[int]],
@@ -199,8 +209,9 @@ def test_batch_size_scaling(model_fn: Callable[[], nn.Module], input_shape_fn: C
         import pandas as pd
 
         os.makedirs(results_dir, exist_ok=True)
-        pd.DataFrame(rows).to_csv(os.path.join(results_dir, f"{getattr(model_fn, '__name__', 'model')}_batch_scaling.csv"),
-                                  index=False)
+        path = os.path.join(results_dir, f"{getattr(model_fn, '__name__', 'model')}_batch_scaling.csv")
+        pd.DataFrame(rows).to_csv(path, index=False)
+        _plot("visualize_batch_scaling", path)
     return rows
 
 

@@ -173,6 +173,14 @@ def _save(rows: List[Dict], results_dir: Optional[str], name: str) -> None:
 
     os.makedirs(results_dir, exist_ok=True)
     pd.DataFrame(rows).to_csv(os.path.join(results_dir, name), index=False)
+    fn = {"precision_results.csv": "plot_precision_performance", "bandwidth_results.csv": "plot_memory_bandwidth"}.get(name)
+    if fn:
+        try:
+            from . import plots
+
+            getattr(plots, fn)(os.path.join(results_dir, name))
+        except Exception as e:  # plotting is never fatal
+            print(f"[plot] {fn} skipped: {e}")
 
 
 test_precision_formats.__test__ = False  # reference names start with "test_"

@@ -81,3 +81,26 @@ def test_rocprof_families_split_dgrad_from_fwd():
     assert family("void hyp::(anonymous namespace)::conv_fwd_k<unsigned short, 64, 64, false, true, 2>(x)") == "conv_dgrad"
     assert family("void hyp::(anonymous namespace)::conv_fwd_k<unsigned short, 64, 64, true, false, 2>(x)") == "conv_fwd"
     assert family("void hyp::(anonymous namespace)::conv_wgrad_k<unsigned short, 64, 64, 2>(x)") == "conv_wgrad"
+
+
+def test_reference_plots_from_csvs(tmp_path):
+    import pandas as pd
+
+    from hyperion.bench.plots import (plot_memory_bandwidth, plot_precision_performance, visualize_baseline_results,
+                                      visualize_batch_scaling)
+
+    cols = ["Model", "Forward Time (ms)", "Backward Time (ms)", "Optimizer Time (ms)", "Total Time (ms)",
+            "Memory Usage (MB)", "Throughput (samples/s)"]
+    pd.DataFrame([["ResNet-50", 2, 4, 1, 7, 3000, 4500], ["ViT", 4, 8, 1, 13, 3600, 2400]], columns=cols).to_csv(
+        tmp_path / "model_benchmarks.csv", index=False)
+    pd.DataFrame([[b, 1, 1, 1, 5 + b / 8, 100 * b, b / (5 + b / 8) * 1000] for b in (1, 2, 4, 8)],
+                 columns=["Batch Size"] + cols[1:]).assign(Model="r50").to_csv(tmp_path / "bs.csv", index=False)
+    pd.DataFrame({"Size": [1024, 2048] * 2, "Precision": ["BF16"] * 2 + ["FP32"] * 2, "Time (s)": [1e-4] * 4,
+                  "TFLOPS": [100, 500, 50, 100]}).to_csv(tmp_path / "precision_results.csv", index=False)
+    pd.DataFrame({"Size (M elements)": [10, 500], "Bandwidth (GB/s)": [3000, 5500]}).to_csv(
+        tmp_path / "bandwidth_results.csv", index=False)
+    for out in (visualize_baseline_results(str(tmp_path / "model_benchmarks.csv")),
+                visualize_batch_scaling(str(tmp_path / "bs.csv")),
+                plot_precision_performance(str(tmp_path / "precision_results.csv")),
+                plot_memory_bandwidth(str(tmp_path / "bandwidth_results.csv"))):
+        assert os.path.getsize(out) > 1000
