@@ -15,8 +15,16 @@ at::Tensor& zero_page(const at::Device& dev) {
 }
 
 // x [N,C,H,W] channels-last, w [K,C,R,S] channels-last -> (y [N,K,P,Q] channels-last, psum, psq)
+// Effective split-K count for a conv of nk reduction steps (conv_fwd's own rounding: no empty splits).
+int plan_splits(int M, int K, int nk, int bm, int bn, int64_t splits_req) {
+  int sp = splits_req > 0 ? (int)splits_req : (splits_req == 0 ? 1 : hyp::conv_fwd_splits(M, K, nk, bm, bn));
+  sp = std::max(1, std::min(sp, nk));
+  const int steps = (nk + sp - 1) / sp;
+  return (nk + steps - 1) / steps;
+}
+
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t sh, int64_t sw, int64_t ph,
-                                 int64_t pw, bool stats, int64_t bm_req, int64_t bn_req) {
+                                 int64_t pw, bool stats, int64_t bm_req, int64_t bn_req, int64_t splits_req) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: 4D tensors");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -38,23 +46,27 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   if (bn_req > 0) bn = (int)bn_req;
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
               "conv_fwd: tiles 64x64, 128x64 or 128x128");
-  at::Tensor psum, psq;
+  // split-K below ~2 workgroups per CU (the stats then come from the reduce, kStatRows-row partials)
+  const int splits = plan_splits(M, K, R * S * (C / 64), bm, bn, splits_req);
+  at::Tensor psum, psq, slabs;
   if (stats) {
-    const int mt = (M + bm - 1) / bm;
+    const int mt = splits > 1 ? (M + hyp::kStatRows - 1) / hyp::kStatRows : (M + bm - 1) / bm;
     auto part = at::empty({2, mt, K}, x.options().dtype(at::kFloat));
     psum = part[0];
     psq = part[1];
   }
+  if (splits > 1) slabs = at::empty({splits, M, K}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
                               stats ? psum.data_ptr<float>() : nullptr, stats ? psq.data_ptr<float>() : nullptr, N, H, W,
-                              C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, 1, nullptr, cur_stream()));
+                              C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, splits,
+                              splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream()));
   return {y, psum, psq};
 }
 
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
 // filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
-                      int64_t bn_req) {
+                      int64_t bn_req, int64_t splits_req) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -78,9 +90,13 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
   if (bn_req > 0) bn = (int)bn_req;
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
               "conv_dgrad: tiles 64x64, 128x64 or 128x128");
+  const int splits = plan_splits(N * H * W, C, R * S * (K / 64), bm, bn, splits_req);
+  at::Tensor slabs;
+  if (splits > 1) slabs = at::empty({splits, (int64_t)N * H * W, C}, dy.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                               zero_page(dy.device()).data_ptr(), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
-                              dph, dpw, bm, bn, 1, 1, nullptr, cur_stream()));
+                              dph, dpw, bm, bn, 1, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr,
+                              cur_stream()));
   return dx;
 }
 
@@ -306,7 +322,7 @@ at::Tensor global_avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
 void register_conv_ops(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)", pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
-        pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1);
+        pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1, pybind11::arg("splits") = -1);
   m.def("conv_set_stages", [](int64_t fwd, int64_t wgrad) {
     hyp::conv_set_stages((int)fwd);
     hyp::conv_wgrad_set_stages((int)wgrad);
@@ -325,7 +341,7 @@ void register_conv_ops(pybind11::module& m) {
   m.def("global_avgpool_bwd", &global_avgpool_bwd, "NHWC global average pool backward");
   m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
-        pybind11::arg("bn") = -1);
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1);
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

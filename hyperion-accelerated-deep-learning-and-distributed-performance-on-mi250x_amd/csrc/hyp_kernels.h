@@ -112,7 +112,8 @@ hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, vo
 
 namespace hyp {
 // ---- conv_igemm.hip --------------------------------------------------------------------------
-// NHWC implicit-GEMM conv (bf16/f16), optional BN-statistics epilogue (psum/psq: [ceil(M/bm), K]).
+// NHWC implicit-GEMM conv (bf16/f16), optional BN-statistics epilogue (psum/psq: [ceil(M/bm), K];
+// with splits > 1 the stats come from the split-K reduce: [ceil(M/kStatRows), K]).
 bool conv_fwd_supported(int C, int K);
 void conv_set_stages(int nb);        // LDS pipeline depth 2..4 (0 = automatic); tuning only
 void conv_wgrad_set_stages(int nb);
@@ -138,6 +139,14 @@ struct SplitkEpilogue {
 // [+ the rank-r epilogue]
 hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st,
                          float alpha = 1.f, const SplitkEpilogue* ep = nullptr);
+// Split-K reduce of a conv forward's [splits, M, K] fp32 partials into out [M, K] (T) plus the BN
+// statistics of the rounded outputs: psum/psq [ceil(M / kStatRows), K].
+constexpr int kStatRows = 16;
+hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, float* psum,
+                               float* psq, hipStream_t st);
+// Split-K plan for a convolution (forward or stride-1 dgrad) whose bm x bn tiling leaves fewer than
+// ~2 workgroups per CU: returns splits >= 1 over the nk = R*S*C/64 reduction steps.
+int conv_fwd_splits(int M, int K, int nk, int bm, int bn);
 // ---- conv_wgrad.hip --------------------------------------------------------------------------
 // NHWC conv weight gradient on MFMA (split-K over pixels; fp32 partials [splits, K, R*S*C] when
 // splits > 1, reduced + cast into dw by a second kernel).

@@ -350,13 +350,26 @@ int conv_fwd_group(int M, int K, int RS, int bm, int bn) {
 
 void conv_set_stages(int nb) { g_stages = (nb >= 2 && nb <= 4) ? nb : 0; }
 
+// Below ~2 workgroups per CU a conv runs latency-bound on its long reduction (ResNet-50 layer4
+// 3x3: 200 tiles x 72 K-steps, 55 us).  Split the reduction until ~768 workgroups run, keeping
+// >= 6 K-steps per split.  The reduce launch costs ~5 us, so at 300-480 tiles only long
+// reductions split (MI355X, bench profile: layer3 3x3 (392 tiles, 36 steps) 31 -> 23 + 5 us;
+// layer3 1x1 (392 tiles, 16 steps) 18 -> 16 + 5 us, a loss).
+int conv_fwd_splits(int M, int K, int nk, int bm, int bn) {
+  const int tiles = ((M + bm - 1) / bm) * ((K + bn - 1) / bn);
+  if (tiles >= 480 || (tiles >= 300 && nk < 32)) return 1;
+  int sp = (768 + tiles - 1) / tiles;
+  sp = min(sp, nk / 6);
+  return max(1, sp);
+}
+
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
                     const SplitkEpilogue* ep) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
-  if (splits > 1 && (psum != nullptr || part == nullptr)) return hipErrorInvalidValue;
+  if (splits > 1 && part == nullptr) return hipErrorInvalidValue;
   // alpha / the rank-r epilogue live in the split-K reduce
   if ((alpha != 1.f || (ep != nullptr && ep->U != nullptr)) && splits < 2) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
@@ -381,6 +394,10 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
       else e = launch<f16_t, 64, 64>(a, false, dgrad, st);
     }
     if (e != hipSuccess) return e;
+    if (psum != nullptr) {  // BN statistics from the reduce (rows of kStatRows)
+      if (alpha != 1.f || (ep != nullptr && ep->U != nullptr)) return hipErrorInvalidValue;
+      return splitk_reduce_stats(dtype, part, out, a.M, K, a.splits, psum, psq, st);
+    }
     return splitk_reduce(dtype, part, out, (int64_t)a.M * K, a.splits, st, alpha, ep);
   }
   const bool stats = psum != nullptr && psq != nullptr;

@@ -254,6 +254,77 @@ hipError_t reduce_launch(const float* part, T* out, int64_t n, int splits, float
 
 }  // namespace
 
+namespace {
+// Split-K reduce of a convolution's [splits, M, K] fp32 partials with the BN-statistics epilogue
+// of conv_fwd_k: out = Σ_s part[s] rounded to T, and per-channel Σy, Σy² of the ROUNDED outputs
+// over kStatRows-row blocks -> psum/psq [ceil(M / kStatRows), K] (the partial layout the BN
+// finalize consumes).  Used when a forward conv has too few output tiles to fill 256 CUs
+// (ResNet-50 layer3/4: 200-392 tiles, 55 us at 0.8 workgroups per CU).  Block = 64 column quads
+// (256 channels, 16-byte loads) x 4 row lanes; fixed summation order (deterministic).
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_stats_k(const float* __restrict__ part, T* __restrict__ out,
+                                                             int M, int K, int splits, float* __restrict__ psum,
+                                                             float* __restrict__ psq) {
+  __shared__ float red[2][4][256];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.y * 256 + tx * 4;
+  const int r0 = blockIdx.x * kStatRows;
+  const int r1 = min(M, r0 + kStatRows);
+  const int64_t slab = (int64_t)M * K;
+  f32x4 cs = {0.f, 0.f, 0.f, 0.f}, cq = cs;
+  if (c < K) {
+    for (int r = r0 + ty; r < r1; r += 4) {
+      const float* src = part + (int64_t)r * K + c;
+      f32x4 a0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src)), a1 = {0.f, 0.f, 0.f, 0.f};
+      int s = 1;
+      for (; s + 1 < splits; s += 2) {
+        a0 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (int64_t)s * slab));
+        a1 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (int64_t)(s + 1) * slab));
+      }
+      if (s < splits) a0 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (int64_t)s * slab));
+      const f32x4 acc = a0 + a1;
+      T* o = out + (int64_t)r * K + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = rnd<T>(acc[e]);
+        st1<T>(o + e, v);
+        cs[e] += v;
+        cq[e] += v * v;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][ty][tx * 4 + e] = cs[e];
+    red[1][ty][tx * 4 + e] = cq[e];
+  }
+  __syncthreads();
+  if (ty == 0 && c < K) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = tx * 4 + e;
+      psum[(int64_t)blockIdx.x * K + c + e] = (red[0][0][j] + red[0][1][j]) + (red[0][2][j] + red[0][3][j]);
+      psq[(int64_t)blockIdx.x * K + c + e] = (red[1][0][j] + red[1][1][j]) + (red[1][2][j] + red[1][3][j]);
+    }
+  }
+}
+}  // namespace
+
+hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, float* psum,
+                               float* psq, hipStream_t st) {
+  if (K % 4 != 0 || splits < 1 || M < 1) return hipErrorInvalidValue;
+  const dim3 grid((M + kStatRows - 1) / kStatRows, (K + 255) / 256);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(splitk_reduce_stats_k<bf16_t>, grid, dim3(256), 0, st, part, static_cast<bf16_t*>(out), M, K,
+                       splits, psum, psq);
+  else if (dtype == kF16)
+    hipLaunchKernelGGL(splitk_reduce_stats_k<f16_t>, grid, dim3(256), 0, st, part, static_cast<f16_t*>(out), M, K,
+                       splits, psum, psq);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st, float alpha,
                          const SplitkEpilogue* ep) {
   if (n % 4 != 0 || splits < 1) return hipErrorInvalidValue;

@@ -194,3 +194,43 @@ def test_fused_adam_zero_grad_in_step():
         o1.zero_grad(set_to_none=False)  # no-op: already zero
     for p, r in zip(ps, ref):
         torch.testing.assert_close(p, r, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("C", [64, 256, 4096, 6144])
+def test_bn_combine_multichunk_matches_and_is_deterministic(C):
+    """Large M: the partial-row combine runs with many row chunks + last-arriver finalize
+    (C = 6144 exceeds the static ticket array and takes the one-chunk path)."""
+    from hyperion.ops.batchnorm import _BNActFn
+
+    torch.manual_seed(1)
+    N, H, W = (32, 28, 28) if C <= 256 else (8, 8, 8)
+    x = (torch.randn(N, C, H, W, device="cuda") * 1.5 + 0.25).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+    gy = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run():
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        xn = x.detach().requires_grad_(True)
+        wn, bn = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        yn = _BNActFn.apply(xn, None, wn, bn, rm, rv, 0.1, 1e-5, True, True)
+        yn.backward(gy)
+        return yn, xn.grad, wn.grad, bn.grad, rm, rv
+
+    outs = [run() for _ in range(3)]
+    for o in outs[1:]:
+        for a, b2 in zip(outs[0], o):
+            assert torch.equal(a, b2), "combine must be deterministic"
+    xr = x.detach().float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rm2, rv2 = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    yr = _ref_bn(xr, None, wr, br, rm2, rv2, True, 0.1, 1e-5, True)
+    yr.backward(gy.float())
+    yn, gx, gw, gb, rm, rv = outs[0]
+    torch.testing.assert_close(yn.float(), yr, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(rv, rv2, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(gx.float(), xr.grad, atol=6e-2, rtol=6e-2)
+    M = N * H * W
+    torch.testing.assert_close(gw, wr.grad, atol=1e-3 * M ** 0.5, rtol=2e-2)
+    torch.testing.assert_close(gb, br.grad, atol=1e-3 * M ** 0.5, rtol=2e-2)

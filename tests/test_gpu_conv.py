@@ -132,3 +132,29 @@ def test_conv_dgrad_matches_fp32(shape, dtype):
     ref = torch.nn.grad.conv2d_input((N, C, H, W), w.float().cpu(), dy.float().cpu(), stride=s, padding=p)
     err = (dx.float().cpu() - ref).norm() / ref.norm()
     assert err < 1e-2, f"rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("shape", [(32, 512, 7, 7, 512, 3, 1, 1), (32, 2048, 7, 7, 512, 1, 1, 0),
+                                   (32, 256, 14, 14, 256, 3, 1, 1), (5, 128, 9, 9, 72, 3, 1, 1)])
+@pytest.mark.parametrize("splits", [1, 2, 5, -1])
+def test_conv_splitk_fwd_stats_and_dgrad(shape, splits):
+    """Split-K forward (BN statistics from the split-K reduce) and split-K dgrad vs fp32."""
+    from hyperion.ops import _native
+
+    N, C, H, W, K, R, s, p = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") / (C * R * R) ** 0.5).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    y, psum, psq = _native.native().conv_fwd(x, w, s, s, p, p, True, splits=splits)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    yr = y.float()
+    torch.testing.assert_close(psum.sum(0), yr.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(psq.sum(0), (yr * yr).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    if K % 64 == 0:
+        dy = torch.randn(N, K, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        dx = _native.native().conv_dgrad(dy, w, p, p, splits=splits)
+        dref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=1, padding=p)
+        err = (dx.float() - dref).norm() / dref.norm()
+        assert err < 1e-2, f"rel err {err:.3e}"
