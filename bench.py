@@ -155,6 +155,11 @@ def main(argv=None) -> int:
                 "loss": "MSE vs rand(B,1000) (reference benchmark_model)",
                 "optimizer": "Adam lr=1e-3 (hyperion FusedAdam, multi-tensor)",
                 "hipgraph": use_graph,
+                "ddp_schedule": (None if n_gpus == 1 else
+                                 "3 graphs: top fwd+bwd | bottom bwd overlapping the top buckets' RCCL all-reduce | optimizer"
+                                 if step.graph3 is not None else
+                                 "2 graphs around eager bucket all-reduces" if step.graph2 is not None else
+                                 "eager, all-reduce overlapped with backward"),
                 "amp": ("bf16 compute copies + fp32 master weights" if copies else
                         ("torch.autocast " + args.precision if amp is not None else "none")),
                 "kernels": _native.backend(),

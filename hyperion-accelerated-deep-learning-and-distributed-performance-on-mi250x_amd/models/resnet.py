@@ -132,6 +132,20 @@ class ResNet(nn.Module):
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
+    def _bottom(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.maxpool(conv_bn_act(self.conv1, self.bn1, x))
+        return self.layer2(self.layer1(x))
+
+    def _top(self, h: torch.Tensor) -> torch.Tensor:
+        x = self.layer4(self.layer3(h))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def graph_stages(self):
+        """``forward(x) == top(bottom(x))``, split where ~85% of the parameters (layer3, layer4, fc)
+        are above the cut: the data-parallel hipGraph step (``train/step.py``) all-reduces those
+        gradients on the comm stream while the bottom half's backward replays."""
+        return [self._bottom, self._top]
+
 
 def resnet18(num_classes: int = 1000, **kw) -> ResNet:
     return ResNet(BasicBlock, [2, 2, 2, 2], num_classes=num_classes, **kw)

@@ -19,7 +19,10 @@ MI355X design:
 * ``defer_allreduce`` (set by ``TrainStep`` for hipGraph replay): backward only packs the buckets
   and ``allreduce_buckets()`` reduces them afterwards — the captured fwd+bwd graph and the
   optimizer graph then hold no RCCL call, and the collectives run eagerly between the two
-  replays (one launch per bucket; no communication inside a captured graph).
+  replays (one launch per bucket; no communication inside a captured graph);
+* ``partial_backward`` / ``complete_buckets`` / ``allreduce_buckets(indices, wait=False)`` let a
+  captured step split its backward in two graphs and reduce the buckets completed by the first
+  (the top layers: most of the bytes) on the comm stream while the second replays.
 """
 from __future__ import annotations
 
@@ -111,6 +114,9 @@ class DistributedDataParallel(nn.Module):
         self.find_unused_parameters = find_unused_parameters
         self._sync = True
         self.defer_allreduce = False
+        # set while the first of a two-part backward runs (top stages; see TrainStep's split
+        # graphs): the end-of-backward callback then keeps the bucket state for the second part
+        self.partial_backward = False
         self._buckets: List[_Bucket] = []
         self._where: Dict[nn.Parameter, Tuple[_Bucket, int]] = {}
         self._next_launch = 0
@@ -190,6 +196,9 @@ class DistributedDataParallel(nn.Module):
             self._next_launch += 1
 
     def _finalize(self) -> None:
+        if self.partial_backward:  # more of this step's backward follows: keep the bucket state
+            self._callback_queued = False
+            return
         # parameters that got no gradient this step contribute zeros (find_unused_parameters)
         for b in self._buckets[self._next_launch :]:
             if b.ready < len(b.params):
@@ -219,21 +228,31 @@ class DistributedDataParallel(nn.Module):
         self._next_launch = 0
         self._callback_queued = False
 
-    def allreduce_buckets(self) -> None:
-        """Reduce every bucket now (``defer_allreduce`` mode; call between backward and step).
+    def complete_buckets(self) -> List[int]:
+        """Indices of the buckets whose every gradient has been packed so far this step."""
+        return [b.index for b in self._buckets if b.ready == len(b.params)]
+
+    def allreduce_buckets(self, indices: Optional[List[int]] = None, wait: bool = True) -> list:
+        """Reduce the given buckets (default: all) now (``defer_allreduce`` mode).
 
         The gradients already point at their bucket slices (pre-scaled by 1/world), so after this
-        the optimizer reads the averaged gradients in place."""
+        the optimizer reads the averaged gradients in place.  ``wait=False`` returns the work
+        handles instead of ordering the current stream after them, so compute issued next (the
+        second half of a split backward) overlaps the collectives on the comm stream; every rank
+        must pass the same ``indices`` in the same order."""
         if not self._buckets or not self._sync:
-            return
+            return []
         works = []
-        for b in self._buckets:
+        for b in self._buckets if indices is None else [self._buckets[i] for i in indices]:
             range_push(f"ddp_allreduce_b{b.index}")
             works.append(self.comm.all_reduce(b.buf, "sum"))
             range_pop()
-        for w in works:
-            if w is not None:
-                w.wait()
+        if wait:
+            for w in works:
+                if w is not None:
+                    w.wait()
+            return []
+        return [w for w in works if w is not None]
 
     @property
     def bucketed(self) -> bool:

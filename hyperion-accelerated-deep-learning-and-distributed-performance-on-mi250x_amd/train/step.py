@@ -13,6 +13,15 @@ captured as TWO graphs — forward+backward (the gradient hooks pack the buckets
 — with the bucket all-reduces issued eagerly between the replays (``DDP.defer_allreduce``): no
 RCCL call is ever recorded into a graph, and the ~500 per-step kernel launches still cost two
 graph launches.
+
+When the model exposes ``graph_stages()`` (``[bottom, top]`` with ``forward == top∘bottom``;
+ResNet splits after layer2), the backward itself is cut in two graphs at that boundary: graph 1 =
+forward + backward of the top (its buckets — ~85% of ResNet-50's gradient bytes — are complete),
+then those buckets' all-reduces are issued on the comm stream WITHOUT ordering the compute
+stream after them, graph 2 = backward of the bottom (overlapping the collectives), the remaining
+buckets are reduced, and graph 3 = the optimizer after all collectives.  On point-to-point xGMI a
+2-GPU all-reduce of ResNet-50's 51 MB of bf16 gradients runs over ONE ≈64-77 GB/s link: hiding it
+behind the bottom half's backward is worth ~10% of a 7 ms step.
 """
 from __future__ import annotations
 
@@ -42,6 +51,7 @@ class TrainStep:
         graph: bool = False,
         warmup_iters: int = 3,
         scaler=None,
+        split_backward: bool = True,
     ):
         self.model = model
         self.opt = optimizer
@@ -55,6 +65,11 @@ class TrainStep:
         self.static_y: Optional[torch.Tensor] = None
         self.static_loss: Optional[torch.Tensor] = None
         self.graph2: Optional[torch.cuda.CUDAGraph] = None
+        self.graph3: Optional[torch.cuda.CUDAGraph] = None
+        self.split_backward = split_backward
+        self._phase1: list = []
+        self._phase2: list = []
+        self._keep = None
 
     def _ddp(self):
         """The model if it is a bucketed Hyperion DDP whose step can be split around its collectives."""
@@ -64,6 +79,49 @@ class TrainStep:
         if isinstance(m, DistributedDataParallel) and m.bucketed and not m.broadcast_buffers and self.scaler is None:
             return m
         return None
+
+    def _stages(self):
+        """``[bottom, top]`` of a DDP-wrapped model that can split its backward, else None."""
+        ddp = self._ddp()
+        if ddp is None or not self.split_backward:
+            return None
+        fn = getattr(ddp.module, "graph_stages", None)
+        st = fn() if callable(fn) else None
+        return st if st is not None and len(st) == 2 else None
+
+    def _fwd_bwd_top(self, x: torch.Tensor, y: torch.Tensor, stages, zero_in_place: bool = False):
+        """Forward through both stages, backward through the top one only."""
+        if zero_in_place:
+            self.opt.zero_grad(set_to_none=False)
+        ddp = self._ddp()
+        with autocast_ctx(x.device, self.amp_dtype):
+            h = stages[0](x)
+            h2 = h.detach().requires_grad_(True)
+            out = stages[1](h2)
+            loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
+        ddp.partial_backward = True
+        try:
+            loss.backward()
+        finally:
+            ddp.partial_backward = False
+        return loss.detach(), h, h2
+
+    def split_step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """Eager two-part backward with the top buckets' all-reduce overlapping the bottom
+        backward (the captured path's schedule without graphs; CPU-testable over gloo)."""
+        stages = self._stages()
+        ddp = self._ddp()
+        assert stages is not None and ddp is not None and ddp.defer_allreduce
+        self.opt.zero_grad(set_to_none=False)
+        loss, h, h2 = self._fwd_bwd_top(x, y, stages)
+        first = ddp.complete_buckets()
+        works = ddp.allreduce_buckets(first, wait=False)
+        h.backward(h2.grad)
+        works += ddp.allreduce_buckets([i for i in range(len(ddp.bucket_sizes())) if i not in first], wait=False)
+        for w in works:
+            w.wait()
+        self.opt.step()
+        return loss
 
     def _fwd_bwd(self, x: torch.Tensor, y: torch.Tensor, zero_in_place: bool = False) -> torch.Tensor:
         if zero_in_place:  # graph mode: gradients keep their addresses, zeroed in place
@@ -115,6 +173,21 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         ddp = self._ddp()
+        stages = self._stages()
+        if ddp is not None and stages is not None:  # three graphs: top fwd+bwd | bottom bwd | optimizer
+            g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self.static_loss, h, h2 = self._fwd_bwd_top(self.static_x, self.static_y, stages, zero_in_place=True)
+            self._phase1 = ddp.complete_buckets()
+            self._phase2 = [i for i in range(len(ddp.bucket_sizes())) if i not in self._phase1]
+            with torch.cuda.graph(g2, pool=g1.pool()):
+                h.backward(h2.grad)
+            with torch.cuda.graph(g3, pool=g1.pool()):
+                self.opt.step()
+            torch.cuda.synchronize()
+            self._keep = (h2,)
+            self.graph, self.graph2, self.graph3 = g1, g2, g3
+            return
         if ddp is not None:  # two graphs around the (eager) bucket all-reduces
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
@@ -143,7 +216,15 @@ class TrainStep:
         if y.data_ptr() != self.static_y.data_ptr():
             self.static_y.copy_(y, non_blocking=True)
         self.graph.replay()
-        if self.graph2 is not None:
+        if self.graph3 is not None:
+            # top buckets reduce on the comm stream while the bottom backward replays
+            works = self.model.allreduce_buckets(self._phase1, wait=False)
+            self.graph2.replay()
+            works += self.model.allreduce_buckets(self._phase2, wait=False)
+            for w in works:
+                w.wait()
+            self.graph3.replay()
+        elif self.graph2 is not None:
             self.model.allreduce_buckets()
             self.graph2.replay()
         return self.static_loss

@@ -93,3 +93,43 @@ def test_ddp_deferred_allreduce_matches_single_process():
     for k in ref:
         torch.testing.assert_close(res[0][k], res[1][k], rtol=0, atol=0, msg=k)
         torch.testing.assert_close(res[0][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def _ddp_split(rank, world, steps):
+    """TrainStep.split_step: top-stage backward, its complete buckets all-reduced without waiting
+    while the bottom-stage backward runs, then the rest (the captured 3-graph schedule, eager)."""
+    from hyperion.parallel import DDP
+    from hyperion.train.step import TrainStep
+
+    m = DDP(_model(seed=rank), bucket_cap_mb=1.0, first_bucket_mb=0.1, broadcast_buffers=False)
+    m.defer_allreduce = True
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    step = TrainStep(m, opt, torch.nn.functional.cross_entropy, amp_dtype=None, graph=False)
+    calls = []
+    orig = m.allreduce_buckets
+
+    def spy(indices=None, wait=True):
+        calls.append(list(indices))
+        return orig(indices, wait)
+
+    m.allreduce_buckets = spy
+    firsts = []
+    for s in range(steps):
+        x, y = _data(s)
+        x, y = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+        step.split_step(x, y)
+        firsts.append(m.complete_buckets())  # state reset after the full backward: []
+    sd = {k: v for k, v in m.state_dict().items() if "running" not in k and "num_batches" not in k}
+    return {"sd": sd, "firsts": firsts, "n": len(m.bucket_sizes()), "calls": calls}
+
+
+def test_ddp_split_backward_overlap_matches_single_process():
+    ref = _ref(3)
+    res = run_world(_ddp_split, 2, (3,))
+    assert res[0]["n"] > 3 and all(f == [] for f in res[0]["firsts"])
+    first, rest = res[0]["calls"][0], res[0]["calls"][1]
+    assert first and rest and sorted(first + rest) == list(range(res[0]["n"]))  # a real two-phase split
+    assert res[0]["calls"] == res[1]["calls"]
+    for k in ref:
+        torch.testing.assert_close(res[0]["sd"][k], res[1]["sd"][k], rtol=0, atol=0, msg=k)
+        torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)

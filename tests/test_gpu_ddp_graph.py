@@ -17,7 +17,11 @@ def _port():
     return p
 
 
-def test_ddp_two_graph_step_matches_eager():
+@pytest.mark.parametrize("split,native", [(False, False), (True, False), (True, True)])
+def test_ddp_two_graph_step_matches_eager(split, native):
+    """split: three graphs (top fwd+bwd | bottom bwd | optimizer) with the top buckets' all-reduce
+    issued between graphs 1 and 2 without a stream wait; native: Hyperion's RCCL communicator
+    (single rank) instead of the torch.distributed no-op comm."""
     import torch.distributed as dist
 
     from hyperion.models.resnet import resnet18
@@ -40,10 +44,17 @@ def test_ddp_two_graph_step_matches_eager():
         ref = make()
         ropt = FusedAdam(ref.parameters(), lr=1e-3, zero_grad_in_step=True)
         rstep = TrainStep(ref, ropt, torch.nn.MSELoss(), amp_dtype=None, graph=False)
-        ddp = DDP(make(), bucket_cap_mb=2.0, first_bucket_mb=0.5, broadcast_buffers=False, buckets_at_world_1=True)
+        comm = None
+        if native:
+            from hyperion.parallel.comm import NativeComm
+
+            comm = NativeComm(torch.device("cuda", 0))
+        ddp = DDP(make(), bucket_cap_mb=2.0, first_bucket_mb=0.5, broadcast_buffers=False, buckets_at_world_1=True,
+                  comm=comm)
         assert ddp.bucketed and len(ddp.bucket_sizes()) > 1
         dopt = FusedAdam(ddp.parameters(), lr=1e-3, zero_grad_in_step=True)
-        dstep = TrainStep(ddp, dopt, torch.nn.MSELoss(), amp_dtype=None, graph=True, warmup_iters=2)
+        dstep = TrainStep(ddp, dopt, torch.nn.MSELoss(), amp_dtype=None, graph=True, warmup_iters=2,
+                          split_backward=split)
         for _ in range(2):  # the graph path's warm-up steps are real updates: align the reference
             rstep(x, y)
         for _ in range(6):
@@ -51,6 +62,9 @@ def test_ddp_two_graph_step_matches_eager():
             dl = dstep(x, y)
         torch.cuda.synchronize()
         assert dstep.graph2 is not None  # the two-graph path ran
+        assert (dstep.graph3 is not None) == split
+        if split:
+            assert dstep._phase1 and dstep._phase2  # both halves own buckets
         torch.testing.assert_close(dl.float(), rl.float(), rtol=2e-2, atol=2e-3)
         for (n, a), b in zip(ref.named_parameters(), ddp.module.parameters()):
             assert (a.float() - b.float()).abs().max() <= 2e-2, n
