@@ -133,18 +133,22 @@ class ResNet(nn.Module):
         return self.fc(x)
 
     def _bottom(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(conv_bn_act(self.conv1, self.bn1, x))
-        return self.layer2(self.layer1(x))
+        return self.layer1(self.maxpool(conv_bn_act(self.conv1, self.bn1, x)))
 
     def _top(self, h: torch.Tensor) -> torch.Tensor:
-        x = self.layer4(self.layer3(h))
+        x = self.layer4(self.layer3(self.layer2(h)))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
     def graph_stages(self):
-        """``forward(x) == top(bottom(x))``, split where ~85% of the parameters (layer3, layer4, fc)
-        are above the cut: the data-parallel hipGraph step (``train/step.py``) all-reduces those
-        gradients on the comm stream while the bottom half's backward replays."""
+        """``forward(x) == top(bottom(x))``, cut after layer1: 99% of the gradient bytes (layer2-4,
+        fc) are above the cut, while the bottom's backward (stem + the 56x56 layer1, ~1/4 of the
+        backward time) is long enough to hide their all-reduce — the data-parallel hipGraph step
+        (``train/step.py``) reduces the top buckets on the comm stream while it replays."""
         return [self._bottom, self._top]
+
+    def graph_stage_modules(self):
+        """Modules of each ``graph_stages`` stage (DDP starts a new gradient bucket at the cut)."""
+        return [[self.conv1, self.bn1, self.layer1], [self.layer2, self.layer3, self.layer4, self.fc]]
 
 
 def resnet18(num_classes: int = 1000, **kw) -> ResNet:

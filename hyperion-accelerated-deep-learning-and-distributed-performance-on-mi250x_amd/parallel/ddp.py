@@ -134,6 +134,15 @@ class DistributedDataParallel(nn.Module):
     def _build_buckets(self, cap_mb: float, first_mb: float, comm_dtype: Optional[torch.dtype]) -> None:
         params = [p for p in self.module.parameters() if p.requires_grad]
         params.reverse()  # gradients become ready roughly in reverse registration order
+        # a bucket never straddles a graph-stage cut (models with graph_stage_modules(): the
+        # split hipGraph step reduces the top stage's buckets while the bottom's backward runs)
+        stage_of: Dict[int, int] = {}
+        fn = getattr(self.module, "graph_stage_modules", None)
+        if callable(fn):
+            for si, mods in enumerate(fn()):
+                for mod in mods:
+                    for p in mod.parameters():
+                        stage_of[id(p)] = si
         groups: List[Tuple[torch.dtype, torch.device, List[nn.Parameter]]] = []
         cur: List[nn.Parameter] = []
         cur_bytes = 0
@@ -141,7 +150,7 @@ class DistributedDataParallel(nn.Module):
         limit = first_mb * 2**20
         for p in params:
             dt = comm_dtype or p.dtype
-            key = (dt, p.device)
+            key = (dt, p.device, stage_of.get(id(p), -1))
             nbytes = p.numel() * torch.empty((), dtype=dt).element_size()
             if cur and (key != cur_key or cur_bytes + nbytes > limit):
                 groups.append((cur_key[0], cur_key[1], cur))

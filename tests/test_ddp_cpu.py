@@ -120,7 +120,10 @@ def _ddp_split(rank, world, steps):
         step.split_step(x, y)
         firsts.append(m.complete_buckets())  # state reset after the full backward: []
     sd = {k: v for k, v in m.state_dict().items() if "running" not in k and "num_batches" not in k}
-    return {"sd": sd, "firsts": firsts, "n": len(m.bucket_sizes()), "calls": calls}
+    stage = {id(p): i for i, mods in enumerate(m.module.graph_stage_modules()) for mod in mods
+             for p in mod.parameters()}
+    straddle = [b.index for b in m._buckets if len({stage[id(p)] for p in b.params}) != 1]
+    return {"sd": sd, "firsts": firsts, "n": len(m.bucket_sizes()), "calls": calls, "straddle": straddle}
 
 
 def test_ddp_split_backward_overlap_matches_single_process():
@@ -129,7 +132,7 @@ def test_ddp_split_backward_overlap_matches_single_process():
     assert res[0]["n"] > 3 and all(f == [] for f in res[0]["firsts"])
     first, rest = res[0]["calls"][0], res[0]["calls"][1]
     assert first and rest and sorted(first + rest) == list(range(res[0]["n"]))  # a real two-phase split
-    assert res[0]["calls"] == res[1]["calls"]
+    assert res[0]["calls"] == res[1]["calls"] and res[0]["straddle"] == []
     for k in ref:
         torch.testing.assert_close(res[0]["sd"][k], res[1]["sd"][k], rtol=0, atol=0, msg=k)
         torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
