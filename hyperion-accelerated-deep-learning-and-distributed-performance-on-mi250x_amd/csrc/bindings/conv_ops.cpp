@@ -66,7 +66,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
 // filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
-                      int64_t bn_req, int64_t splits_req) {
+                      int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -93,10 +93,16 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
   const int splits = plan_splits(N * H * W, C, R * S * (K / 64), bm, bn, splits_req);
   at::Tensor slabs;
   if (splits > 1) slabs = at::empty({splits, (int64_t)N * H * W, C}, dy.options().dtype(at::kFloat));
+  const bool add = addend.has_value() && addend->defined();
+  if (add)
+    TORCH_CHECK(addend->sizes() == dx.sizes() && addend->scalar_type() == dx.scalar_type() &&
+                    addend->is_contiguous(at::MemoryFormat::ChannelsLast) && addend->device() == dx.device(),
+                "conv_dgrad: addend must match dx (shape, dtype, channels-last)");
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                               zero_page(dy.device()).data_ptr(), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
                               dph, dpw, bm, bn, 1, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr,
-                              cur_stream()));
+                              cur_stream(), 1.f, nullptr, (add && splits == 1) ? addend->data_ptr() : nullptr));
+  if (add && splits > 1) dx.add_(*addend);  // the split-K reduce has no addend input
   return dx;
 }
 
@@ -341,7 +347,7 @@ void register_conv_ops(pybind11::module& m) {
   m.def("global_avgpool_bwd", &global_avgpool_bwd, "NHWC global average pool backward");
   m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
-        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1);
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("addend") = pybind11::none());
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

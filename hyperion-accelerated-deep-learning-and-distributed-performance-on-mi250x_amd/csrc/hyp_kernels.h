@@ -118,12 +118,13 @@ bool conv_fwd_supported(int C, int K);
 void conv_set_stages(int nb);        // LDS pipeline depth 2..4 (0 = automatic); tuning only
 void conv_wgrad_set_stages(int nb);
 void conv_fwd_tile(int M, int K, int* bm, int* bn);
+// addend (optional, splits == 1, no stats): out [M, K] += addend after rounding (fused residual grad).
 // dgrad != 0: stride-1 data gradient; "in" is dY [N,H,W,C], "w" the ORIGINAL filter [C][R][S][K]
 // (read flipped and transposed in-kernel), (ph, pw) the dgrad padding R-1-p.
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
-                    const struct SplitkEpilogue* ep = nullptr);
+                    const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr);
 // Optional rank-r epilogue of a split-K reduce over an [M, N] output:
 //   out[m, n] += beta * (mask ? mask[m, n] : 1) * sum_j U[m, j] * V[j * sv_j + n * sv_n]
 // (U, V, mask in the output dtype).  U == nullptr: no epilogue.

@@ -70,6 +70,7 @@ struct ConvArgs {
   int group;             // M-tiles per tile-order group (see conv_fwd_group)
   int splits, steps_per_split;  // split-K over the reduction (splits > 1: fp32 partials, no STATS)
   float* part;                  // [splits, M, K] fp32 when splits > 1
+  const uint16_t* addend;       // optional [M, K] tensor added to the rounded output (no STATS, no split)
 };
 
 // DGRAD = false: W is [K, R, S, C] (reduction contiguous; B tiles are row slices, read row-wise).
@@ -281,7 +282,16 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
     const int m = m0 + lr, k = n0 + ch * 8;
     if (m < a.M && k < a.K) {
-      const uint4 v = *reinterpret_cast<const uint4*>(tile + lr * kLd + ch * 8);
+      uint4 v = *reinterpret_cast<const uint4*>(tile + lr * kLd + ch * 8);
+      if (!STATS && a.addend != nullptr) {
+        // out = round(round(acc) + addend): the same two roundings as a separate T add kernel
+        float o[8], d[8];
+        Vec8<T>::load(reinterpret_cast<const T*>(&v), o);
+        Vec8<T>::load(reinterpret_cast<const T*>(a.addend + (int64_t)m * a.K + k), d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += d[e];
+        Vec8<T>::store(reinterpret_cast<T*>(&v), o);
+      }
       *reinterpret_cast<uint4*>(a.out + (int64_t)m * a.K + k) = v;
     }
   }
@@ -366,10 +376,11 @@ int conv_fwd_splits(int M, int K, int nk, int bm, int bn) {
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
-                    const SplitkEpilogue* ep) {
+                    const SplitkEpilogue* ep, const void* addend) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
   if (splits > 1 && part == nullptr) return hipErrorInvalidValue;
+  if (addend != nullptr && (splits > 1 || psum != nullptr)) return hipErrorInvalidValue;
   // alpha / the rank-r epilogue live in the split-K reduce
   if ((alpha != 1.f || (ep != nullptr && ep->U != nullptr)) && splits < 2) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
@@ -382,6 +393,7 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   a.steps_per_split = (nk + splits - 1) / splits;
   a.splits = (nk + a.steps_per_split - 1) / a.steps_per_split;  // no empty splits
   a.part = part;
+  a.addend = static_cast<const uint16_t*>(addend);
   if (a.splits > 1) {
     hipError_t e;
     if (dtype == kBF16) {

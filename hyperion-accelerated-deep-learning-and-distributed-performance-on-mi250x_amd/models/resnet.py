@@ -21,7 +21,7 @@ import torch.nn as nn
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import conv_bn_act
+from ..ops.conv import conv_bn_act, residual_link
 
 
 def _downsample(ds: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
@@ -51,8 +51,9 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else _downsample(self.downsample, x)
-        out = conv_bn_act(self.conv1, self.bn1, x)
-        return conv_bn_act(self.conv2, self.bn2, out, residual=identity)
+        link = residual_link(x) if self.downsample is None else None  # shortcut grad -> conv1 dgrad
+        out = conv_bn_act(self.conv1, self.bn1, x, link=link)
+        return conv_bn_act(self.conv2, self.bn2, out, residual=identity, link=link)
 
 
 class Bottleneck(nn.Module):
@@ -72,9 +73,10 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = x if self.downsample is None else _downsample(self.downsample, x)
-        out = conv_bn_act(self.conv1, self.bn1, x)
+        link = residual_link(x) if self.downsample is None else None  # shortcut grad -> conv1 dgrad
+        out = conv_bn_act(self.conv1, self.bn1, x, link=link)
         out = conv_bn_act(self.conv2, self.bn2, out)
-        return conv_bn_act(self.conv3, self.bn3, out, residual=identity)
+        return conv_bn_act(self.conv3, self.bn3, out, residual=identity, link=link)
 
 
 class ResNet(nn.Module):

@@ -48,16 +48,48 @@ def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     )
 
 
-def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
+           addend: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dX (+ addend: the identity-shortcut gradient of a residual block, fused into the store)."""
     R, S = w.shape[2], w.shape[3]
     if (tuple(stride) == (1, 1) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0 and padding[0] <= R - 1
             and padding[1] <= S - 1 and _native.use_native(dy, op="dgrad")):
         # dX = conv(dY, flip(W) with C <-> K), stride 1, padding R-1-p: conv_igemm.hip's DGRAD mode
         # reads the forward filter flipped and transposed in-kernel (no filter copy)
         dyc = dy.contiguous(memory_format=torch.channels_last)
-        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1])
-    return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
-                                               [True, False, False])[0]
+        if addend is not None:
+            addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
+        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend)
+    dx = torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
+                                             [True, False, False])[0]
+    return dx if addend is None else dx + addend
+
+
+FUSE_SHORTCUT_GRAD = True  # models create ResidualLinks only when set (A/B switch for tests)
+
+
+def residual_link(x: torch.Tensor) -> Optional["ResidualLink"]:
+    return ResidualLink(x) if FUSE_SHORTCUT_GRAD else None
+
+
+class ResidualLink:
+    """Carries a bottleneck's identity-shortcut gradient from its last conv/BN (which would return
+    it as the residual input's gradient) to its first conv's data gradient, where the conv kernel
+    adds it in the store epilogue — autograd's separate ``dx_conv1 + d_identity`` add kernel (one
+    launch and two extra passes over the block input per block) disappears.
+
+    Valid because both ops consume the SAME tensor (the block input) and the first op's backward
+    always runs after the last op's (it depends on it through the main branch): the gradient only
+    moves between two paths that autograd would have summed.  ``armed`` is set only when the
+    first op took the fused path, so a fallback op never drops the gradient.
+    """
+
+    __slots__ = ("src", "armed", "dres")
+
+    def __init__(self, src: torch.Tensor):
+        self.src = src
+        self.armed = False
+        self.dres: Optional[torch.Tensor] = None
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
@@ -76,7 +108,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) 
 
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act):
+    def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out):
         C = _native.native()
         yc, psum, psq = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True)
         if residual is not None:
@@ -85,22 +117,34 @@ class _ConvBNActFn(torch.autograd.Function):
         # without a residual the backward recomputes the ReLU mask from yc (no need to keep `out`)
         ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
+        ctx.links = (link_in, link_out)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, w, yc, out, bn_w, bn_b, mean, invstd = ctx.saved_tensors
         stride, padding, act, has_res = ctx.cfg
+        link_in, link_out = ctx.links
         need_res = has_res and ctx.needs_input_grad[6]
         dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res)
-        dx = _dgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[0] else None
+        if need_res and link_out is not None and link_out.armed:
+            link_out.dres, dres = dres, None  # added by the block's first conv dgrad instead
+        add = None
+        if link_in is not None and link_in.dres is not None:
+            add, link_in.dres = link_in.dres, None
+        dx = _dgrad(dyc, x, w, stride, padding, addend=add) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[1] else None
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
-                dres if need_res else None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None)
 
 
-def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``bn(conv(x), residual)`` for a ``BatchNormAct2d`` ``bn``; fused on gfx950 when possible."""
+def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                link: Optional[ResidualLink] = None) -> torch.Tensor:
+    """``bn(conv(x), residual)`` for a ``BatchNormAct2d`` ``bn``; fused on gfx950 when possible.
+
+    ``link``: a ``ResidualLink`` whose ``src`` is the block input — pass it to the block's FIRST
+    conv (``x is link.src``) and to its LAST (``residual is link.src``) to fuse the shortcut
+    gradient into the first conv's data gradient."""
     use = (
         bn.training
         and bn.track_running_stats
@@ -113,5 +157,13 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
     if not use:
         return bn(conv(x), residual=residual)
     bn._host_batches += 1  # BatchNormAct2d's host-side num_batches_tracked mirror
+    link_in = link_out = None
+    if link is not None:
+        if x is link.src and residual is None:
+            link.armed = True  # the first conv runs fused: its dgrad can take the shortcut gradient
+            link_in = link
+        elif residual is link.src and link.armed:
+            link_out = link
     return _ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
-                              tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act))
+                              tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
+                              link_in, link_out)

@@ -158,3 +158,53 @@ def test_conv_splitk_fwd_stats_and_dgrad(shape, splits):
         dref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=1, padding=p)
         err = (dx.float() - dref).norm() / dref.norm()
         assert err < 1e-2, f"rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("shape,splits", [((4, 256, 14, 14, 64, 1, 1, 0), 1), ((8, 64, 14, 14, 64, 3, 1, 1), 1),
+                                          ((4, 512, 7, 7, 512, 3, 1, 1), 3)])
+def test_conv_dgrad_addend_is_exact_separate_add(shape, splits):
+    """dgrad with the fused addend == dgrad followed by a bf16 add, bit for bit."""
+    from hyperion.ops import _native
+
+    N, C, H, W, K, R, s, p = shape
+    torch.manual_seed(0)
+    w = (torch.randn(K, C, R, R, device="cuda") / (K * R * R) ** 0.5).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    dy = torch.randn(N, K, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    add = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    C_ = _native.native()
+    ref = C_.conv_dgrad(dy, w, p, p, splits=splits) + add
+    got = C_.conv_dgrad(dy, w, p, p, splits=splits, addend=add)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("block", ["bottleneck", "basic"])
+def test_shortcut_grad_fusion_matches_autograd_add(block):
+    """ResNet blocks with the identity-shortcut gradient fused into conv1's dgrad produce the
+    same gradients as autograd's separate add (bitwise)."""
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import BasicBlock, Bottleneck
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    m = (Bottleneck(256, 64) if block == "bottleneck" else BasicBlock(64, 64)).cuda()
+    m = m.to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    cin = 256 if block == "bottleneck" else 64
+    x0 = torch.randn(8, cin, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, cin, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run(fuse):
+        hconv.FUSE_SHORTCUT_GRAD = fuse
+        try:
+            for p in m.parameters():
+                p.grad = None
+            x = x0.clone().requires_grad_(True)
+            m(x).backward(gy)
+            return [x.grad.clone()] + [p.grad.clone() for p in m.parameters()]
+        finally:
+            hconv.FUSE_SHORTCUT_GRAD = True
+
+    a, b = run(False), run(True)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
