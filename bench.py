@@ -68,7 +68,8 @@ def main(argv=None) -> int:
     from hyperion.train.step import TrainStep
     from hyperion.utils import seed_everything
 
-    env = init_from_env()
+    # HYPERION_DIST_BACKEND=gloo (+ HYPERION_COMM=torch): rehearse the N>1 path with several ranks on one GPU
+    env = init_from_env(backend=os.environ.get("HYPERION_DIST_BACKEND") or None)
     n_gpus = env.world_size
     if args.gpus is not None and args.gpus != n_gpus and env.rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={n_gpus}; using WORLD_SIZE", file=sys.stderr)
