@@ -13,6 +13,8 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
                       int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
                       float* scale, float* shift, hipStream_t stream);
 // y == nullptr with act: the ReLU mask is recomputed from x (training, no residual gradient only)
+// small-M BN fast paths (finalize folded into apply / one-launch backward); 0 disables (A/B, tests)
+void bn_set_small_paths(int on);
 hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
                        const float* weight, const float* bias, const float* save_mean, const float* save_invstd,
                        int training, int act, float* pdz, float* pdzx, float* dweight, float* dbias, float* kA,

@@ -445,9 +445,317 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, 
   }
 }
 
+// ---------------------------------------------------------------- small-M fused paths
+// Below ~8K rows (ResNet-50 layer3/layer4 at batch 32: M = 6272 / 1568) every BN kernel is
+// launch/latency-bound (~4-5 us each on MI355X whatever its size), so the separate finalize
+// launches are folded away:
+//  * forward: each apply block re-derives scale/shift for ITS 64 channels from the P partial rows
+//    (P <= 128, L2-resident) — the same double-precision finalize arithmetic, blockIdx.y == 0
+//    also writes save_mean / save_invstd / running stats — then applies;
+//  * backward (M <= 2048: layer4): one block owns 8 channels over ALL M rows, register-resident:
+//    Σdz, Σdz·x, in-block finalize, dx — reduce + finalize + dx in one launch.
+int g_bn_small = 1;  // small-M fused paths on (bn_set_small_paths: A/B and tests)
+constexpr int kSmallFinP = 128;
+constexpr int64_t kSmallBwdM = 8192;
+
+struct StatsFin {  // forward finalize inputs / outputs (bn_stats_finalize_k's arguments)
+  const float* weight;
+  const float* bias;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;
+  float* save_invstd;
+};
+
+struct BwdFin {  // backward finalize inputs / outputs (bn_bwd_finalize_k's arguments)
+  const float* weight;
+  const float* mean;
+  const float* invstd;
+  int training;
+  float* dweight;
+  float* dbias;
+};
+
+template <typename T, bool ACT, bool RES>
+__global__ __launch_bounds__(kBlock) void bn_fin_apply_k(const T* __restrict__ x, const T* __restrict__ res,
+                                                         T* __restrict__ y, const float* __restrict__ psum,
+                                                         const float* __restrict__ psq, int P, int64_t M, int C,
+                                                         int64_t rpb, StatsFin fin) {
+  __shared__ double red[2][32][64];
+  __shared__ float s_sc[64], s_sh[64];
+  const int tid = threadIdx.x, cx = tid & 7, ry = tid >> 3;
+  const int cb = blockIdx.x * 64, c0 = cb + cx * 8;
+  // ---- finalize this block's 64 channels (fixed summation order: identical in every block)
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  for (int p = ry; p < P; p += 32) {
+    const float4* ps = reinterpret_cast<const float4*>(psum + (int64_t)p * C + c0);
+    const float4* pq = reinterpret_cast<const float4*>(psq + (int64_t)p * C + c0);
+    const float4 s0 = ps[0], s1 = ps[1], q0 = pq[0], q1 = pq[1];
+    a[0] += s0.x; a[1] += s0.y; a[2] += s0.z; a[3] += s0.w; a[4] += s1.x; a[5] += s1.y; a[6] += s1.z; a[7] += s1.w;
+    b[0] += q0.x; b[1] += q0.y; b[2] += q0.z; b[3] += q0.w; b[4] += q1.x; b[5] += q1.y; b[6] += q1.z; b[7] += q1.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][ry][cx * 8 + j] = a[j];
+    red[1][ry][cx * 8 + j] = b[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    double sa = 0.0, sb = 0.0;
+    for (int i = 0; i < 32; ++i) {
+      sa += red[0][i][tid];
+      sb += red[1][i][tid];
+    }
+    const int c = cb + tid;
+    const double mean = sa / (double)M;
+    double var = sb / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
+    const float w = fin.weight ? fin.weight[c] : 1.f;
+    const float bb = fin.bias ? fin.bias[c] : 0.f;
+    const float sc = w * invstd;
+    s_sc[tid] = sc;
+    s_sh[tid] = bb - (float)mean * sc;
+    if (blockIdx.y == 0) {
+      fin.save_mean[c] = (float)mean;
+      fin.save_invstd[c] = invstd;
+      if (fin.running_mean != nullptr) {
+        const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        fin.running_mean[c] = (float)((1.0 - fin.momentum) * fin.running_mean[c] + fin.momentum * mean);
+        fin.running_var[c] = (float)((1.0 - fin.momentum) * fin.running_var[c] + fin.momentum * unbiased);
+      }
+    }
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = s_sc[cx * 8 + j];
+    sh[j] = s_sh[cx * 8 + j];
+  }
+  // ---- apply rows [y*rpb, +rpb)
+  const int64_t row1 = min(M, (int64_t)(blockIdx.y + 1) * rpb);
+  for (int64_t row = (int64_t)blockIdx.y * rpb + ry; row < row1; row += 32) {
+    const int64_t off = row * C + c0;
+    float v[8], rr[8];
+    Vec8<T>::load(x + off, v);
+    if (RES) Vec8<T>::load(res + off, rr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = fmaf(v[j], sc[j], sh[j]);
+      if (RES) t += rr[j];
+      if (ACT) t = fmaxf(t, 0.f);
+      v[j] = t;
+    }
+    Vec8<T>::store(y + off, v);
+  }
+}
+
+// grid C/8, block 256: 8 channels (one 16-byte vector per row) x all M <= 2048 rows.  Every
+// thread loads its <= 8 rows of dy / x (/ y) ONCE, in one burst (all loads in flight), keeps
+// them packed in registers across the block reduction and the in-block finalize, and writes
+// dx from them: one memory round trip per tensor (a row loop re-reading the data was
+// latency-bound: 47-100 us at M = 6272).
+constexpr int kBwdRows = 8;
+
+template <typename T>
+__device__ __forceinline__ void unpack8(const uint4& raw, float (&v)[8]) {
+  Vec8<T>::load(reinterpret_cast<const T*>(&raw), v);
+}
+
+template <typename T, bool ACT, bool RES, bool MASKX, int NT, int ROWS>
+__global__ __launch_bounds__(NT) void bn_bwd_small_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                         const T* __restrict__ y, T* __restrict__ dx,
+                                                         T* __restrict__ dres, int64_t M, int C, BwdFin fin,
+                                                         const float* __restrict__ bn_b) {
+  static_assert(sizeof(T) == 2, "packed 16-bit rows");
+  __shared__ float red[2][NT / 64][8];
+  __shared__ float kk[3][8];
+  __shared__ double ksum[2][8];
+  const int tid = threadIdx.x;
+  // XCD-aware slice order: blocks b, b+8, ... share an XCD (round-robin dispatch), so give them
+  // ADJACENT 8-channel slices — 8 slices = one 128-byte row segment is then fetched into one
+  // L2 once instead of into 8 (the 16-byte-per-row access otherwise moves 8x the bytes)
+  const int G = gridDim.x;
+  int slice = blockIdx.x;
+  if ((G & 7) == 0) slice = (slice & 7) * (G >> 3) + (slice >> 3);
+  const int c0 = slice * 8;
+  ReluMask<T, ACT, MASKX> mk;
+  mk.init(fin.weight, bn_b, fin.mean, fin.invstd, c0);
+  uint4 rg[ROWS], rx[ROWS], ryv[ROWS];
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) {
+    const int64_t row = tid + (int64_t)i * NT;
+    if (row < M) {
+      const int64_t off = row * C + c0;
+      rg[i] = *reinterpret_cast<const uint4*>(dy + off);
+      rx[i] = *reinterpret_cast<const uint4*>(x + off);
+      if (ACT && !MASKX) ryv[i] = *reinterpret_cast<const uint4*>(y + off);
+    }
+  }
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) {
+    if (tid + (int64_t)i * NT < M) {
+      float g[8], xv[8], yv[8];
+      unpack8<T>(rg[i], g);
+      unpack8<T>(rx[i], xv);
+      if (ACT && !MASKX) unpack8<T>(ryv[i], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = mk.keep(xv, yv, j) ? g[j] : 0.f;
+        s[j] += d;
+        q[j] += d * xv[j];
+      }
+    }
+  }
+  // 8 channels x {Σdz, Σdz·x}: wave tree sums, then the 4 waves in fixed order (deterministic)
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float ws = wave_sum(s[j]), wq = wave_sum(q[j]);
+    if (lane == 0) {
+      red[0][wv][j] = ws;
+      red[1][wv][j] = wq;
+    }
+  }
+  __syncthreads();
+  if (tid < 16) {
+    const int j = tid & 7, which = tid >> 3;
+    double acc = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) acc += red[which][w][j];
+    ksum[which][j] = acc;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    const int c = c0 + tid;
+    const double a = ksum[0][tid], b = ksum[1][tid];
+    const double mu = fin.mean[c], is = fin.invstd[c];
+    const double sum_dz_xhat = is * (b - mu * a);
+    if (fin.dweight) fin.dweight[c] = (float)sum_dz_xhat;
+    if (fin.dbias) fin.dbias[c] = (float)a;
+    const double g = fin.weight ? fin.weight[c] : 1.0;
+    const double A = g * is;
+    const double Bc = fin.training ? -A * is * sum_dz_xhat / (double)M : 0.0;
+    const double Cc = fin.training ? -A * a / (double)M - Bc * mu : 0.0;
+    kk[0][tid] = (float)A;
+    kk[1][tid] = (float)Bc;
+    kk[2][tid] = (float)Cc;
+  }
+  __syncthreads();
+  float A[8], B[8], Cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A[j] = kk[0][j];
+    B[j] = kk[1][j];
+    Cc[j] = kk[2][j];
+  }
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) {
+    const int64_t row = tid + (int64_t)i * NT;
+    if (row < M) {
+      const int64_t off = row * C + c0;
+      float g[8], xv[8], yv[8];
+      unpack8<T>(rg[i], g);
+      unpack8<T>(rx[i], xv);
+      if (ACT && !MASKX) unpack8<T>(ryv[i], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = mk.keep(xv, yv, j) ? g[j] : 0.f;
+        g[j] = d;
+        xv[j] = fmaf(A[j], d, fmaf(B[j], xv[j], Cc[j]));
+      }
+      Vec8<T>::store(dx + off, xv);
+      if (RES) Vec8<T>::store(dres + off, g);
+    }
+  }
+}
+
+// small-M forward: finalize folded into the apply (returns false when the shape is not covered)
+bool launch_fin_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* psum,
+                      const float* psq, int P, const float* weight, const float* bias, float* running_mean,
+                      float* running_var, float momentum, float eps, int act, float* save_mean, float* save_invstd,
+                      hipStream_t stream) {
+  if (g_bn_small == 0 || P > kSmallFinP || M > 2 * kSmallBwdM || C % 64 != 0 || (dtype != kBF16 && dtype != kF16))
+    return false;
+  const int groups = C / 64;
+  int64_t R = (M + 127) / 128;  // >= 4 rows per thread-lane (32 lanes)
+  const int64_t cap = 512 / groups > 0 ? 512 / groups : 1;
+  if (R > cap) R = cap;
+  if (R < 1) R = 1;
+  const int64_t rpb = (M + R - 1) / R;
+  R = (M + rpb - 1) / rpb;
+  const StatsFin fin{weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd};
+  const dim3 grid(groups, (unsigned)R);
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    const T* xt = static_cast<const T*>(x);
+    const T* rt = static_cast<const T*>(res);
+    T* yt = static_cast<T*>(y);
+    if (act && res)
+      hipLaunchKernelGGL((bn_fin_apply_k<T, true, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P, M,
+                         C, rpb, fin);
+    else if (act)
+      hipLaunchKernelGGL((bn_fin_apply_k<T, true, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P, M,
+                         C, rpb, fin);
+    else if (res)
+      hipLaunchKernelGGL((bn_fin_apply_k<T, false, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P, M,
+                         C, rpb, fin);
+    else
+      hipLaunchKernelGGL((bn_fin_apply_k<T, false, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P,
+                         M, C, rpb, fin);
+  });
+  return true;
+}
+
+// small-M backward: reduce + finalize + dx in one launch (false when not covered)
+bool launch_bwd_small(int dtype, bool maskx, bool act, const void* dy, const void* x, const void* y, void* dx,
+                      void* dres, int64_t M, int C, const BwdFin& fin, const float* bias, hipStream_t stream) {
+  if (g_bn_small == 0 || M > (int64_t)kBwdRows * kBlock || C % 8 != 0 || (dtype != kBF16 && dtype != kF16))
+    return false;
+  const dim3 grid(C / 8);
+  // 256 threads x 8 register-resident rows (M <= 2048: layer4).  Wider blocks for layer3's 6272
+  // rows (512 x 13, 1024 x 8) spill VGPRs: that case keeps the 3-kernel path.
+#define HYP_BN_SMALL(ACTV, RESV, MX)                                                                               \
+  hipLaunchKernelGGL((bn_bwd_small_k<T, ACTV, RESV, MX, kBlock, kBwdRows>), grid, dim3(kBlock), 0, stream, dyt, xt, \
+                     yt, dxt, drt, M, C, fin, bias)
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    const T* dyt = static_cast<const T*>(dy);
+    const T* xt = static_cast<const T*>(x);
+    const T* yt = static_cast<const T*>(y);
+    T* dxt = static_cast<T*>(dx);
+    T* drt = static_cast<T*>(dres);
+    if (maskx) {
+      HYP_BN_SMALL(true, false, true);
+    } else if (act && dres) {
+      HYP_BN_SMALL(true, true, false);
+    } else if (act) {
+      HYP_BN_SMALL(true, false, false);
+    } else if (dres) {
+      HYP_BN_SMALL(false, true, false);
+    } else {
+      HYP_BN_SMALL(false, false, false);
+    }
+  };
+  if (dtype == kBF16)
+    go(bf16_t{});
+  else
+    go(f16_t{});
+#undef HYP_BN_SMALL
+  return true;
+}
+
 }  // namespace
 
 // ======================================================================== host launchers
+void bn_set_small_paths(int on) { g_bn_small = on ? 1 : 0; }
+
 hipError_t bn_workspace_rows(int64_t M, int C, int* P_out) {
   BnGeom g;
   if (!bn_geom(M, C, kStatsBlocks, g)) return hipErrorInvalidValue;
@@ -466,6 +774,9 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
     if (training) {
       hipLaunchKernelGGL(bn_stats_partial_k<T>, dim3(gs.P, gs.gy), dim3(kBlock), 0, stream, xt, M, C, gs.tpr, gs.rpi,
                          gs.rows_per_block, psum, psq);
+      if (launch_fin_apply(dtype, x, res, y, M, C, psum, psq, gs.P, weight, bias, running_mean, running_var, momentum,
+                           eps, act, save_mean, save_invstd, stream))
+        return hipGetLastError();
       hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum, psq, gs.P, C, M,
                          weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
     } else {
@@ -521,6 +832,9 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
   // eval-mode constants are running stats, which the mask recomputation below does not model)
   const bool maskx = act && y == nullptr;
   if (maskx && (!training || dres != nullptr)) return hipErrorInvalidValue;
+  if (launch_bwd_small(dtype, maskx, act != 0, dy, x, y, dx, dres, M, C,
+                       BwdFin{weight, save_mean, save_invstd, training, dweight, dbias}, bias, stream))
+    return hipGetLastError();
   HYP_DISPATCH_FLOAT(dtype, T, {
     const T* dyt = static_cast<const T*>(dy);
     const T* xt = static_cast<const T*>(x);
@@ -556,6 +870,9 @@ hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, v
                                     hipStream_t stream) {
   BnGeom ga;
   if (!bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  if (launch_fin_apply(dtype, x, res, y, M, C, psum, psq, P, weight, bias, running_mean, running_var, momentum, eps,
+                       act, save_mean, save_invstd, stream))
+    return hipGetLastError();
   hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum, psq,
                      P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale,
                      shift);

@@ -234,3 +234,48 @@ def test_bn_combine_multichunk_matches_and_is_deterministic(C):
     M = N * H * W
     torch.testing.assert_close(gw, wr.grad, atol=1e-3 * M ** 0.5, rtol=2e-2)
     torch.testing.assert_close(gb, br.grad, atol=1e-3 * M ** 0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("shape", [(32, 512, 7, 7), (32, 2048, 7, 7), (32, 256, 14, 14), (32, 1024, 14, 14),
+                                   (3, 64, 5, 5)])
+@pytest.mark.parametrize("act,use_res", [(True, False), (True, True), (False, False)])
+def test_bn_small_m_paths_match_general_path(shape, act, use_res):
+    """Small-M fast paths (finalize folded into the apply; one-launch backward) vs the general
+    3-kernel paths and the fp32 reference, through the conv-partials entry (ResNet layer3/4)."""
+    from hyperion.ops import _native
+    from hyperion.ops.batchnorm import _BNActFn
+
+    C_ = _native.native()
+    N, C, H, W = shape
+    torch.manual_seed(2)
+    x = (torch.randn(N, C, H, W, device="cuda") * 1.3 + 0.2).bfloat16().contiguous(memory_format=torch.channels_last)
+    res = torch.randn_like(x) if use_res else None
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+    gy = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run(small):
+        C_.bn_set_small_paths(small)
+        try:
+            rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+            xn = x.detach().requires_grad_(True)
+            rn = res.detach().requires_grad_(True) if use_res else None
+            wn, bn = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+            yn = _BNActFn.apply(xn, rn, wn, bn, rm, rv, 0.1, 1e-5, True, act)
+            yn.backward(gy)
+            return [yn, xn.grad, wn.grad, bn.grad, rm, rv] + ([rn.grad] if use_res else [])
+        finally:
+            C_.bn_set_small_paths(True)
+
+    fast, slow = run(True), run(False)
+    M = N * H * W
+    for i, (a, c) in enumerate(zip(fast, slow)):
+        tol = 1e-3 * M ** 0.5 if i in (2, 3) else 2e-2
+        torch.testing.assert_close(a.float(), c.float(), atol=tol, rtol=2e-2, msg=f"output {i}")
+    xr = x.detach().float().requires_grad_(True)
+    rr = res.detach().float().requires_grad_(True) if use_res else None
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = _ref_bn(xr, rr, wr, br, torch.zeros(C, device="cuda"), torch.ones(C, device="cuda"), True, 0.1, 1e-5, act)
+    yr.backward(gy.float())
+    torch.testing.assert_close(fast[0].float(), yr, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(fast[1].float(), xr.grad, atol=6e-2, rtol=6e-2)
