@@ -301,6 +301,29 @@ at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H,
   return dx;
 }
 
+// comp [N, C, P, Q] channels-last -> [N, C, H, W]: comp scattered to (p*sh, q*sw) (+ addend)
+at::Tensor upsample_add(const at::Tensor& comp, const c10::optional<at::Tensor>& addend, int64_t H, int64_t W,
+                        int64_t sh, int64_t sw) {
+  HYP_CHECK_CUDA_TENSOR(comp);
+  TORCH_CHECK(comp.dim() == 4 && comp.is_contiguous(at::MemoryFormat::ChannelsLast) && comp.size(1) % 8 == 0,
+              "upsample_add: channels-last [N, C, P, Q] with C % 8 == 0");
+  const int N = comp.size(0), C = comp.size(1), P = comp.size(2), Q = comp.size(3);
+  TORCH_CHECK(sh >= 1 && sw >= 1 && (P - 1) * sh < H && (Q - 1) * sw < W, "upsample_add: bad geometry");
+  const at::DeviceGuard guard(comp.device());
+  auto out = at::empty({N, C, H, W}, comp.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const void* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    const auto& a = *addend;
+    TORCH_CHECK(a.sizes() == out.sizes() && a.scalar_type() == comp.scalar_type() &&
+                    a.is_contiguous(at::MemoryFormat::ChannelsLast) && a.device() == comp.device(),
+                "upsample_add: addend must match the output (shape, dtype, channels-last)");
+    add = a.data_ptr();
+  }
+  HYP_CHECK_HIP(hyp::upsample_add(dtype_code(comp), comp.data_ptr(), add, out.data_ptr(), N, (int)H, (int)W, C, P, Q,
+                                  (int)sh, (int)sw, cur_stream()));
+  return out;
+}
+
 // x [N, C, H, W] channels-last -> [N, C]
 at::Tensor global_avgpool_fwd(const at::Tensor& x) {
   HYP_CHECK_CUDA_TENSOR(x);
@@ -344,6 +367,9 @@ void register_conv_ops(pybind11::module& m) {
   m.def("maxpool2d_fwd", &maxpool2d_fwd, "NHWC max pool (+ window-tap index)");
   m.def("maxpool2d_bwd", &maxpool2d_bwd, "NHWC max pool backward (gather, deterministic)");
   m.def("global_avgpool_fwd", &global_avgpool_fwd, "NHWC global average pool");
+  m.def("upsample_add", &upsample_add, "strided dgrad completion: comp scattered to every s-th pixel (+ addend)",
+        pybind11::arg("comp"), pybind11::arg("addend"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("sh"),
+        pybind11::arg("sw"));
   m.def("global_avgpool_bwd", &global_avgpool_bwd, "NHWC global average pool backward");
   m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

@@ -184,6 +184,9 @@ hipError_t maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, in
 hipError_t maxpool2d_backward(int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C,
                               int k, int s, int pad, hipStream_t st);
 hipError_t global_avgpool_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t st);
+// out[N,H,W,C] = addend (optional) + comp[N,P,Q,C] scattered to pixels (p*sh, q*sw), zeros elsewhere
+hipError_t upsample_add(int dtype, const void* comp, const void* addend, void* out, int N, int H, int W, int C, int P,
+                        int Q, int sh, int sw, hipStream_t st);
 hipError_t global_avgpool_backward(int dtype, const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
 }  // namespace hyp
 

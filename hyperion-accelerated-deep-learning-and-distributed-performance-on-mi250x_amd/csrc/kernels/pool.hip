@@ -147,6 +147,42 @@ __global__ __launch_bounds__(256) void gap_bwd_k(const T* __restrict__ dy, T* __
   Vec8<T>::store(dx + (t / cv) * C + c0, g);
 }
 
+// Strided-conv data gradient completion: out[n, h, w] = addend[n, h, w] + (h % sh == 0 && w % sw == 0 ?
+// comp[n, h / sh, w / sw] : 0).  A 1x1 stride-s convolution's dX is dY·W on the output grid
+// scattered to every s-th input pixel (zeros elsewhere); `comp` is that GEMM (conv_igemm.hip,
+// DGRAD, stride-1 geometry) and this one pass writes the zero-upsampled result — plus, when given,
+// the other branch's gradient of the same block input (ResNet downsample + conv1), so neither the
+// vendor kernel's zero fill nor autograd's separate add runs.  Sum rounded once, like the add.
+template <typename T, bool ADD>
+__global__ __launch_bounds__(256) void upsample_add_k(const T* __restrict__ comp, const T* __restrict__ addend,
+                                                      T* __restrict__ out, int N, int H, int W, int C, int P, int Q,
+                                                      int sh, int sw) {
+  const int cv = C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * H * W * cv) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int w = (int)(pix % W);
+  pix /= W;
+  const int h = (int)(pix % H);
+  const int n = (int)(pix / H);
+  float v[8];
+  const int p = h / sh, q = w / sw;
+  if (p * sh == h && q * sw == w && p < P && q < Q) {
+    Vec8<T>::load(comp + (((int64_t)n * P + p) * Q + q) * C + c0, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
+  if (ADD) {
+    float a[8];
+    Vec8<T>::load(addend + t * 8, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += a[j];
+  }
+  Vec8<T>::store(out + t * 8, v);
+}
+
 inline int blocks_for(int64_t n) { return (int)((n + 255) / 256); }
 
 }  // namespace
@@ -169,6 +205,21 @@ hipError_t maxpool2d_backward(int dtype, const void* dy, const uint8_t* idx, voi
   const int64_t total = (int64_t)N * H * W * (C / 8);
   HYP_DISPATCH_FLOAT(dtype, T, {
     hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(blocks_for(total)), dim3(256), 0, st, (const T*)dy, idx, (T*)dx, g);
+  });
+  return hipGetLastError();
+}
+
+hipError_t upsample_add(int dtype, const void* comp, const void* addend, void* out, int N, int H, int W, int C, int P,
+                        int Q, int sh, int sw, hipStream_t st) {
+  if (C % 8 != 0 || sh < 1 || sw < 1 || P < 1 || Q < 1) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    if (addend)
+      hipLaunchKernelGGL((upsample_add_k<T, true>), dim3(blocks_for(total)), dim3(256), 0, st, (const T*)comp,
+                         (const T*)addend, (T*)out, N, H, W, C, P, Q, sh, sw);
+    else
+      hipLaunchKernelGGL((upsample_add_k<T, false>), dim3(blocks_for(total)), dim3(256), 0, st, (const T*)comp,
+                         (const T*)addend, (T*)out, N, H, W, C, P, Q, sh, sw);
   });
   return hipGetLastError();
 }

@@ -21,12 +21,12 @@ import torch.nn as nn
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import conv_bn_act, residual_link
+from ..ops.conv import branch_sum_link, conv_bn_act, residual_link
 
 
-def _downsample(ds: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+def _downsample(ds: nn.Sequential, x: torch.Tensor, branch=None) -> torch.Tensor:
     """``downsample = Sequential(conv1x1, BatchNormAct2d)`` (torchvision keys ``downsample.0/1``)."""
-    return conv_bn_act(ds[0], ds[1], x)
+    return conv_bn_act(ds[0], ds[1], x, branch=branch)
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -50,9 +50,12 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else _downsample(self.downsample, x)
-        link = residual_link(x) if self.downsample is None else None  # shortcut grad -> conv1 dgrad
-        out = conv_bn_act(self.conv1, self.bn1, x, link=link)
+        # identity shortcut: its gradient goes to conv1's dgrad store; downsample: the two data
+        # gradients of x (downsample, conv1) are summed in-kernel
+        branch = branch_sum_link(x) if self.downsample is not None else None
+        identity = x if self.downsample is None else _downsample(self.downsample, x, branch)
+        link = residual_link(x) if self.downsample is None else None
+        out = conv_bn_act(self.conv1, self.bn1, x, link=link, branch=branch)
         return conv_bn_act(self.conv2, self.bn2, out, residual=identity, link=link)
 
 
@@ -72,9 +75,12 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else _downsample(self.downsample, x)
-        link = residual_link(x) if self.downsample is None else None  # shortcut grad -> conv1 dgrad
-        out = conv_bn_act(self.conv1, self.bn1, x, link=link)
+        # identity shortcut: its gradient goes to conv1's dgrad store; downsample: the two data
+        # gradients of x (downsample, conv1) are summed in-kernel
+        branch = branch_sum_link(x) if self.downsample is not None else None
+        identity = x if self.downsample is None else _downsample(self.downsample, x, branch)
+        link = residual_link(x) if self.downsample is None else None
+        out = conv_bn_act(self.conv1, self.bn1, x, link=link, branch=branch)
         out = conv_bn_act(self.conv2, self.bn2, out)
         return conv_bn_act(self.conv3, self.bn3, out, residual=identity, link=link)
 

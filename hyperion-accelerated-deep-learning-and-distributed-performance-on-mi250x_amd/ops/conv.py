@@ -14,8 +14,9 @@ SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
 * backward — the fused BN/ReLU/residual backward (``bn_act.hip``) produces dconv; the data
   gradient of a stride-1 convolution is the same implicit-GEMM kernel in DGRAD mode (the forward
   filter read flipped and channel-transposed through ds_read_b64_tr_b16, no filter copy); weight
-  gradients run on ``conv_wgrad.hip`` (split-K MFMA over the output pixels); strided data
-  gradients use the vendor kernels (``aten.convolution_backward``).
+  gradients run on ``conv_wgrad.hip`` (split-K MFMA over the output pixels); a 1x1 strided data
+  gradient is the same DGRAD GEMM on the output grid plus one scatter(+add) pass; other strided
+  data gradients use the vendor kernels (``aten.convolution_backward``).
 
 Anything outside the kernel's envelope (fp32, C % 64 != 0 such as the RGB stem, groups, dilation,
 eval mode) falls back to ``bn(conv(x), residual)`` — the same math.
@@ -60,6 +61,16 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
         return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend)
+    if (R == 1 and S == 1 and tuple(padding) == (0, 0) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0
+            and _native.use_native(dy, op="dgrad")):
+        # 1x1 stride-s (ResNet downsample): dY·W on the output grid is the stride-1 DGRAD GEMM; one
+        # pass scatters it to every s-th input pixel, zeros elsewhere, + addend (the vendor path
+        # ran a zero-fill kernel, its own dgrad, and autograd a separate add)
+        Cn = _native.native()
+        comp = Cn.conv_dgrad(dy.contiguous(memory_format=torch.channels_last), w, 0, 0)
+        if addend is not None:
+            addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
+        return Cn.upsample_add(comp, addend, x.shape[2], x.shape[3], stride[0], stride[1])
     dx = torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                              [True, False, False])[0]
     return dx if addend is None else dx + addend
@@ -92,6 +103,29 @@ class ResidualLink:
         self.dres: Optional[torch.Tensor] = None
 
 
+class BranchSumLink:
+    """Sums the two data gradients of a downsampling block's input — its ``downsample`` conv and
+    its first conv both read the block input, and autograd would add their gradients with a
+    separate kernel (two full passes over the block input).  Whichever of the two backward calls
+    runs first parks its dX here; the second one adds it in its own store (the conv kernel's
+    addend epilogue, or the strided-dgrad scatter pass) and returns the sum, the first returns
+    None.  Armed only when BOTH convs took the fused path in the forward (``users == 2``), so a
+    fallback op never loses its gradient; both backward calls always run (they depend on the
+    same block output).  Reference: torchvision ``Bottleneck.forward`` (``out += identity``).
+    """
+
+    __slots__ = ("src", "users", "pending")
+
+    def __init__(self, src: torch.Tensor):
+        self.src = src
+        self.users = 0
+        self.pending: Optional[torch.Tensor] = None
+
+
+def branch_sum_link(x: torch.Tensor) -> Optional[BranchSumLink]:
+    return BranchSumLink(x) if FUSE_SHORTCUT_GRAD else None
+
+
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
     # csrc/kernels/conv_wgrad.hip: split-K MFMA GEMM over the output pixels with transposed LDS
     # reads (one kernel + one deterministic partial-sum/cast kernel; MIOpen used 3-4 launches).
@@ -108,7 +142,8 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) 
 
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out):
+    def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out,
+                branch):
         C = _native.native()
         yc, psum, psq = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True)
         if residual is not None:
@@ -117,14 +152,14 @@ class _ConvBNActFn(torch.autograd.Function):
         # without a residual the backward recomputes the ReLU mask from yc (no need to keep `out`)
         ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
-        ctx.links = (link_in, link_out)
+        ctx.links = (link_in, link_out, branch)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, w, yc, out, bn_w, bn_b, mean, invstd = ctx.saved_tensors
         stride, padding, act, has_res = ctx.cfg
-        link_in, link_out = ctx.links
+        link_in, link_out, branch = ctx.links
         need_res = has_res and ctx.needs_input_grad[6]
         dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res)
         if need_res and link_out is not None and link_out.armed:
@@ -132,19 +167,29 @@ class _ConvBNActFn(torch.autograd.Function):
         add = None
         if link_in is not None and link_in.dres is not None:
             add, link_in.dres = link_in.dres, None
-        dx = _dgrad(dyc, x, w, stride, padding, addend=add) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if branch is not None and branch.users == 2:
+                other, branch.pending = branch.pending, None
+                if other is None:  # first of the block input's two consumers: park dX for the second
+                    branch.pending = _dgrad(dyc, x, w, stride, padding, addend=add)
+                else:
+                    dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add)
+            else:
+                dx = _dgrad(dyc, x, w, stride, padding, addend=add)
         dw = _wgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[1] else None
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
-                dres, None, None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None, None)
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                link: Optional[ResidualLink] = None) -> torch.Tensor:
+                link: Optional[ResidualLink] = None, branch: Optional[BranchSumLink] = None) -> torch.Tensor:
     """``bn(conv(x), residual)`` for a ``BatchNormAct2d`` ``bn``; fused on gfx950 when possible.
 
     ``link``: a ``ResidualLink`` whose ``src`` is the block input — pass it to the block's FIRST
     conv (``x is link.src``) and to its LAST (``residual is link.src``) to fuse the shortcut
-    gradient into the first conv's data gradient."""
+    gradient into the first conv's data gradient.  ``branch``: a ``BranchSumLink`` on the block
+    input, passed to the downsample conv and the first conv (sums their data gradients in-kernel)."""
     use = (
         bn.training
         and bn.track_running_stats
@@ -164,6 +209,11 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
             link_in = link
         elif residual is link.src and link.armed:
             link_out = link
+    if branch is not None:
+        if x is branch.src and branch.users < 2:
+            branch.users += 1
+        else:
+            branch = None
     return _ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
                               tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
-                              link_in, link_out)
+                              link_in, link_out, branch)

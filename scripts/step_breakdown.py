@@ -1,4 +1,4 @@
-"""Per-step kernel breakdown of a rocprofv3 kernel trace of bench.py (the adam_mt_k launch pair marks a step end).
+"""Per-step kernel breakdown of a rocprofv3 kernel trace of bench.py (a group of adam_mt_k launches marks a step end).
 
 Usage: python scripts/step_breakdown.py <run_kernel_trace.csv> [n_steps] [top]
 """
@@ -24,7 +24,7 @@ def short(name: str) -> str:
 def main(path, n=5, top=40):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     adam = [i for i, r in enumerate(rows) if "adam_mt_k" in r["Kernel_Name"]]
-    ends = [i for j, i in enumerate(adam) if j + 1 == len(adam) or adam[j + 1] != i + 1]
+    ends = [i for j, i in enumerate(adam) if j + 1 == len(adam) or adam[j + 1] > i + 16]  # one group per step
     a, b = ends[-n - 1], ends[-1]
     w = rows[a + 1:b + 1]
     span = (int(w[-1]["End_Timestamp"]) - int(w[0]["Start_Timestamp"])) / n / 1e3

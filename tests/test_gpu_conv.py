@@ -208,3 +208,91 @@ def test_shortcut_grad_fusion_matches_autograd_add(block):
     a, b = run(False), run(True)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 14, 14, 2, 2), (2, 64, 7, 9, 2, 2), (3, 128, 8, 8, 1, 1), (2, 8, 6, 6, 3, 2)])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_upsample_add_matches_reference(shape, with_add):
+    """comp scattered to every s-th pixel (+ addend) == zeros / strided assign / bf16 add, bit for bit."""
+    from hyperion.ops import _native
+
+    N, C, H, W, sh, sw = shape
+    P, Q = (H - 1) // sh + 1, (W - 1) // sw + 1
+    torch.manual_seed(0)
+    comp = torch.randn(N, C, P, Q, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    add = (torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+           if with_add else None)
+    ref = torch.zeros(N, C, H, W, device="cuda", dtype=torch.bfloat16)
+    ref[:, :, ::sh, ::sw] = comp
+    if with_add:
+        ref = ref + add
+    got = _native.native().upsample_add(comp, add, H, W, sh, sw)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 28, 28, 512), (8, 1024, 14, 14, 2048), (2, 64, 7, 7, 128)])
+def test_strided_1x1_dgrad_matches_fp32(shape):
+    """1x1 stride-2 data gradient (DGRAD GEMM on the output grid + scatter) vs the fp32 reference."""
+    from hyperion.ops.conv import _dgrad
+
+    N, C, H, W, K = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 1, 1, device="cuda") / C ** 0.5).bfloat16().contiguous(memory_format=torch.channels_last)
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dy = torch.randn(N, K, P, Q, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    dx = _dgrad(dy, x, w, (2, 2), (0, 0))
+    dref = torch.nn.grad.conv2d_input((N, C, H, W), w.float(), dy.float(), stride=2, padding=0)
+    err = (dx.float() - dref).norm() / dref.norm()
+    assert err < 1e-2, f"rel err {err:.3e}"
+    assert torch.all(dx[:, :, 1::2, :] == 0) and torch.all(dx[:, :, :, 1::2] == 0)
+
+
+@pytest.mark.parametrize("block", ["bottleneck_s2", "bottleneck_s1", "basic_s2"])
+def test_downsample_branch_grad_fusion_matches_autograd_add(block):
+    """Downsampling blocks with the two data gradients of the block input summed in-kernel
+    (BranchSumLink) produce the same gradients as autograd's separate add (bitwise)."""
+    import torch.nn as nn
+
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import BasicBlock, Bottleneck, conv1x1
+    from hyperion.ops.batchnorm import BatchNormAct2d
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    if block == "bottleneck_s2":
+        cin, cout, s, HW = 256, 512, 2, 14
+        m = Bottleneck(cin, 128, 2, nn.Sequential(conv1x1(cin, cout, 2), BatchNormAct2d(cout)))
+    elif block == "bottleneck_s1":
+        cin, cout, s, HW = 64, 256, 1, 14
+        m = Bottleneck(cin, 64, 1, nn.Sequential(conv1x1(cin, cout, 1), BatchNormAct2d(cout)))
+    else:
+        cin, cout, s, HW = 64, 128, 2, 14
+        m = BasicBlock(cin, 128, 2, nn.Sequential(conv1x1(cin, cout, 2), BatchNormAct2d(cout)))
+    m = m.cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    x0 = torch.randn(8, cin, HW, HW, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, cout, HW // s, HW // s, device="cuda").bfloat16().contiguous(
+        memory_format=torch.channels_last)
+
+    def run(fuse):
+        hconv.FUSE_SHORTCUT_GRAD = fuse
+        try:
+            for p in m.parameters():
+                p.grad = None
+            x = x0.clone().requires_grad_(True)
+            m(x).backward(gy)
+            return [x.grad.clone()] + [p.grad.clone() for p in m.parameters()]
+        finally:
+            hconv.FUSE_SHORTCUT_GRAD = True
+
+    # the strided 3x3 conv's data gradient is MIOpen's: pin its deterministic algorithm
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        a, b = run(False), run(True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
