@@ -87,8 +87,9 @@ def main(argv=None) -> int:
 
         cast_for_compute(model, amp)
     if n_gpus > 1:
+        # fp32 gradient buckets by default (the reference reduced fp32 grads); --comm-dtype bf16 opt-in
         model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
-                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None)
+                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
     opt = FusedAdam(model.parameters(), lr=1e-3, zero_grad_in_step=True)
     loss_fn = nn.MSELoss()
 
@@ -130,6 +131,15 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.float().item())
+    replicas = None
+    if n_gpus > 1:
+        # correctness self-check after the timed loop: every rank must hold bit-identical weights
+        from hyperion.parallel.debug import assert_replicas_in_sync
+
+        try:
+            replicas = {"in_sync": True, "tensors": assert_replicas_in_sync(model)}
+        except RuntimeError as e:
+            replicas = {"in_sync": False, "error": str(e)[:300]}
     ms = elapsed / args.steps * 1e3
     value = n_gpus * B * args.steps / elapsed
     if env.rank == 0:
@@ -166,10 +176,13 @@ def main(argv=None) -> int:
                 "kernels": _native.backend(),
                 "native_so": _native.loaded_path(),
                 "channels_last": bool(args.channels_last),
+                "grad_allreduce_dtype": (None if n_gpus == 1 else args.comm_dtype),
             },
             "baseline": {"value": BASELINE_SAMPLES_PER_S, "ms_per_step": 56.32, "hw": "1x MI250X GCD, fp32"},
             "final_loss": round(final_loss, 6),
         }
+        if replicas is not None:
+            rec["replicas"] = replicas
         if smi is not None:
             rec["smi"] = smi.summary()
         line = json.dumps(rec)

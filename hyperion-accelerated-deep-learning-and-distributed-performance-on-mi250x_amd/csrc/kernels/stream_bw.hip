@@ -63,9 +63,12 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
                      int blocks, hipStream_t stream) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
-  int grid = blocks > 0 ? blocks : 2048;  // 8 x 256-thread WGs per CU
+  // blocks > 0: grid-stride over that many workgroups; 0: 2048 (8 x 256-thread WGs per CU);
+  // < 0: one tile per workgroup (a full grid, every workgroup exits after its tile)
   const int64_t need = (n4 + 256 * kUnroll - 1) / (256 * kUnroll);
-  if (need < grid) grid = (int)need;
+  int64_t grid = blocks > 0 ? blocks : (blocks < 0 ? need : 2048);
+  if (need < grid) grid = need;
+  if (grid > INT32_MAX) return hipErrorInvalidValue;
   if (grid < 1) grid = 1;
   auto A = reinterpret_cast<const float4*>(a);
   auto B = reinterpret_cast<const float4*>(b);
@@ -73,9 +76,9 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
 #define HYP_STREAM_CASE(OPV)                                                                                     \
   case OPV:                                                                                                      \
     if (nontemporal)                                                                                             \
-      hipLaunchKernelGGL((stream_k<OPV, true>), dim3(grid), dim3(256), 0, stream, A, B, C, s, n4);               \
+      hipLaunchKernelGGL((stream_k<OPV, true>), dim3((unsigned)grid), dim3(256), 0, stream, A, B, C, s, n4);               \
     else                                                                                                         \
-      hipLaunchKernelGGL((stream_k<OPV, false>), dim3(grid), dim3(256), 0, stream, A, B, C, s, n4);              \
+      hipLaunchKernelGGL((stream_k<OPV, false>), dim3((unsigned)grid), dim3(256), 0, stream, A, B, C, s, n4);              \
     break;
   switch (op) {
     HYP_STREAM_CASE(0)

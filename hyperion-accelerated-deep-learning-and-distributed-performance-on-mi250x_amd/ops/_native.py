@@ -79,6 +79,24 @@ def use_native(*tensors: torch.Tensor, op: Optional[str] = None) -> bool:
     return True
 
 
+_COUNTS: dict = {}
+
+
+def count(op: str, n: int = 1) -> None:
+    """Dispatch counter: ops record which path ran (``conv_bn_act``, ``dgrad``, ``dgrad_vendor``,
+    ...), so GPU tests assert the native kernels were actually reached rather than a silent
+    fallback that computes the same numbers (host-side only; one dict update per op call)."""
+    _COUNTS[op] = _COUNTS.get(op, 0) + n
+
+
+def counters() -> dict:
+    return dict(_COUNTS)
+
+
+def reset_counters() -> None:
+    _COUNTS.clear()
+
+
 def loaded_path() -> Optional[str]:
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None

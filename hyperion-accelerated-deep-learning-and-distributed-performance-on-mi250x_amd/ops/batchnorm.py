@@ -134,6 +134,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
             self._host_batches = 0
         super()._save_to_state_dict(destination, prefix, keep_vars)
 
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        # the loaded num_batches_tracked is the whole count: drop any un-flushed host increments
+        self._host_batches = 0
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:  # type: ignore[override]
         use_batch_stats = self.training or not self.track_running_stats
         momentum = 0.0 if self.momentum is None else self.momentum
@@ -146,6 +151,29 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         return bn_act(x, residual, self.weight, self.bias, rm, rv, use_batch_stats, momentum, self.eps, self.act)
+
+
+class HostCounterReplay:
+    """Keeps ``BatchNormAct2d``'s host-side ``num_batches_tracked`` mirror right under hipGraph
+    replay: a captured step increments the mirror once in Python while recording (a forward that
+    never ran on the device) and never again, so ``TrainStep`` / ``GraphedClosure`` snapshot the
+    mirrors around the capture, undo the recording pass, and add the per-step delta on every
+    replay — checkpoints then store the true count, like torch's BatchNorm."""
+
+    def __init__(self, module: nn.Module):
+        self.mods = [m for m in module.modules() if hasattr(m, "_host_batches")]
+        self.before = [m._host_batches for m in self.mods]
+        self.delta: list = []
+
+    def captured(self) -> "HostCounterReplay":
+        self.delta = [(m, m._host_batches - b) for m, b in zip(self.mods, self.before) if m._host_batches != b]
+        for m, d in self.delta:
+            m._host_batches -= d
+        return self
+
+    def replayed(self, n: int = 1) -> None:
+        for m, d in self.delta:
+            m._host_batches += n * d
 
 
 class BatchNormAct1d(BatchNormAct2d):

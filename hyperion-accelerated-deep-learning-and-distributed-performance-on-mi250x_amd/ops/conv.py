@@ -23,6 +23,7 @@ eval mode) falls back to ``bn(conv(x), residual)`` — the same math.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional
 
 import torch
@@ -60,6 +61,7 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         dyc = dy.contiguous(memory_format=torch.channels_last)
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
+        _native.count("dgrad")
         return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend)
     if (R == 1 and S == 1 and tuple(padding) == (0, 0) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0
             and _native.use_native(dy, op="dgrad")):
@@ -67,10 +69,12 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         # pass scatters it to every s-th input pixel, zeros elsewhere, + addend (the vendor path
         # ran a zero-fill kernel, its own dgrad, and autograd a separate add)
         Cn = _native.native()
+        _native.count("dgrad_strided1x1")
         comp = Cn.conv_dgrad(dy.contiguous(memory_format=torch.channels_last), w, 0, 0)
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
         return Cn.upsample_add(comp, addend, x.shape[2], x.shape[3], stride[0], stride[1])
+    _native.count("dgrad_vendor")
     dx = torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                              [True, False, False])[0]
     return dx if addend is None else dx + addend
@@ -92,34 +96,42 @@ class ResidualLink:
     Valid because both ops consume the SAME tensor (the block input) and the first op's backward
     always runs after the last op's (it depends on it through the main branch): the gradient only
     moves between two paths that autograd would have summed.  ``armed`` is set only when the
-    first op took the fused path, so a fallback op never drops the gradient.
+    first op took the fused path, so a fallback op never drops the gradient; and the last op
+    parks its gradient only when the engine WILL run the first op's node in the same backward
+    (``torch._C._will_engine_execute_node``) — a partial backward (``autograd.grad`` w.r.t. some
+    leaves only, ``retain_graph=True``) gets the plain per-op gradients.
     """
 
-    __slots__ = ("src", "armed", "dres")
+    __slots__ = ("src", "armed", "dres", "first_node")
 
     def __init__(self, src: torch.Tensor):
         self.src = src
         self.armed = False
         self.dres: Optional[torch.Tensor] = None
+        self.first_node = None
 
 
 class BranchSumLink:
     """Sums the two data gradients of a downsampling block's input — its ``downsample`` conv and
     its first conv both read the block input, and autograd would add their gradients with a
     separate kernel (two full passes over the block input).  Whichever of the two backward calls
-    runs first parks its dX here; the second one adds it in its own store (the conv kernel's
-    addend epilogue, or the strided-dgrad scatter pass) and returns the sum, the first returns
-    None.  Armed only when BOTH convs took the fused path in the forward (``users == 2``), so a
-    fallback op never loses its gradient; both backward calls always run (they depend on the
-    same block output).  Reference: torchvision ``Bottleneck.forward`` (``out += identity``).
+    runs first parks its dX here (tagged with its consumer index); the second one adds it in its
+    own store (the conv kernel's addend epilogue, or the strided-dgrad scatter pass) and returns
+    the sum, the first returns None.  Armed only when BOTH convs took the fused path in the
+    forward (``users == 2``), so a fallback op never loses its gradient, and a node parks only
+    when the engine will run the OTHER consumer's node in the same backward (a partial
+    ``autograd.grad`` that reaches one consumer returns plain per-op gradients; a parked tensor
+    from an earlier, abandoned pass is dropped by its own owner).  Reference: torchvision
+    ``Bottleneck.forward`` (``out += identity``).
     """
 
-    __slots__ = ("src", "users", "pending")
+    __slots__ = ("src", "users", "pending", "nodes")
 
     def __init__(self, src: torch.Tensor):
         self.src = src
         self.users = 0
-        self.pending: Optional[torch.Tensor] = None
+        self.pending = None  # (owner consumer index, dX)
+        self.nodes = [None, None]  # grad_fn of each consumer's output
 
 
 def branch_sum_link(x: torch.Tensor) -> Optional[BranchSumLink]:
@@ -135,15 +147,23 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) 
     if (x.shape[1] % 64 == 0 and dy.shape[1] % 8 == 0 and P * Q < (1 << 14) and dy.shape[0] * P * Q < (1 << 22)
             and _native.use_native(x, op="wgrad")):
         dyc = dy.contiguous(memory_format=torch.channels_last)
+        _native.count("wgrad")
         return _native.native().conv_wgrad(dyc, x, R, S, stride[0], stride[1], padding[0], padding[1])
+    _native.count("wgrad_vendor")
     return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
+
+
+def _will_run(ref) -> bool:
+    """``ref``: a weakref to a consumer's backward node (weak: the node's ctx holds the link)."""
+    node = ref() if ref is not None else None
+    return node is not None and torch._C._will_engine_execute_node(node)
 
 
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out,
-                branch):
+                branch, bidx):
         C = _native.native()
         yc, psum, psq = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True)
         if residual is not None:
@@ -152,34 +172,37 @@ class _ConvBNActFn(torch.autograd.Function):
         # without a residual the backward recomputes the ReLU mask from yc (no need to keep `out`)
         ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
-        ctx.links = (link_in, link_out, branch)
+        ctx.links = (link_in, link_out, branch, bidx)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, w, yc, out, bn_w, bn_b, mean, invstd = ctx.saved_tensors
         stride, padding, act, has_res = ctx.cfg
-        link_in, link_out, branch = ctx.links
+        link_in, link_out, branch, bidx = ctx.links
         need_res = has_res and ctx.needs_input_grad[6]
         dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res)
-        if need_res and link_out is not None and link_out.armed:
+        if need_res and link_out is not None and link_out.armed and _will_run(link_out.first_node):
             link_out.dres, dres = dres, None  # added by the block's first conv dgrad instead
         add = None
         if link_in is not None and link_in.dres is not None:
             add, link_in.dres = link_in.dres, None
         dx = None
         if ctx.needs_input_grad[0]:
-            if branch is not None and branch.users == 2:
-                other, branch.pending = branch.pending, None
-                if other is None:  # first of the block input's two consumers: park dX for the second
-                    branch.pending = _dgrad(dyc, x, w, stride, padding, addend=add)
+            if branch is not None and branch.users == 2 and _will_run(branch.nodes[1 - bidx]):
+                pend, branch.pending = branch.pending, None
+                if pend is not None and pend[0] == bidx:
+                    pend = None  # our own dX from an abandoned pass (its partner never ran): stale
+                if pend is None:  # first of the block input's two consumers: park dX for the second
+                    branch.pending = (bidx, _dgrad(dyc, x, w, stride, padding, addend=add))
                 else:
+                    other = pend[1]
                     dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add)
             else:
                 dx = _dgrad(dyc, x, w, stride, padding, addend=add)
         dw = _wgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[1] else None
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
-                dres, None, None, None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None, None, None)
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
@@ -200,7 +223,9 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
         and _native_conv_ok(x, conv)
     )
     if not use:
+        _native.count("conv_bn_act_fallback")
         return bn(conv(x), residual=residual)
+    _native.count("conv_bn_act")
     bn._host_batches += 1  # BatchNormAct2d's host-side num_batches_tracked mirror
     link_in = link_out = None
     if link is not None:
@@ -209,11 +234,18 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
             link_in = link
         elif residual is link.src and link.armed:
             link_out = link
+    bidx = -1
     if branch is not None:
         if x is branch.src and branch.users < 2:
+            bidx = branch.users
             branch.users += 1
         else:
             branch = None
-    return _ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
-                              tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
-                              link_in, link_out, branch)
+    out = _ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
+                             tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
+                             link_in, link_out, branch, bidx)
+    if branch is not None:
+        branch.nodes[bidx] = weakref.ref(out.grad_fn)
+    if link_in is not None:
+        link_in.first_node = weakref.ref(out.grad_fn)
+    return out

@@ -28,6 +28,14 @@ from . import _native
 from .multi_tensor import TableCache
 
 
+def grad_of(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The gradient the optimizer should consume: ``p.main_grad`` (an fp32 reduced-gradient view
+    that data-parallel wrappers attach to low-precision parameters, ``parallel/ddp.py``) when set,
+    else ``p.grad``."""
+    g = getattr(p, "main_grad", None)
+    return g if g is not None else p.grad
+
+
 def _dense(t: torch.Tensor) -> bool:
     return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 
@@ -83,7 +91,7 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._host_step += 1
-        first = next((p for g in self.param_groups for p in g["params"] if p.grad is not None), None)
+        first = next((p for g in self.param_groups for p in g["params"] if grad_of(p) is not None), None)
         if first is None:
             return loss
         native = _native.use_native(first, op="adam")
@@ -92,14 +100,15 @@ class FusedAdam(torch.optim.Optimizer):
                 self._step_t = torch.full((), float(self._host_step - 1), dtype=torch.float32, device=first.device)
             self._step_t.add_(1.0)
         for gi, group in enumerate(self.param_groups):
-            params = [p for p in group["params"] if p.grad is not None]
-            # partition by (param dtype, grad dtype): one launch per partition
+            params = [p for p in group["params"] if grad_of(p) is not None]
+            # partition by (param dtype, grad dtype): one launch per partition (an fp32 main_grad
+            # of a bf16 parameter is its own partition: fp32 grads, bf16 params + fp32 masters)
             parts = {}
             for p in params:
-                parts.setdefault((p.dtype, p.grad.dtype), []).append(p)
+                parts.setdefault((p.dtype, grad_of(p).dtype), []).append(p)
             for (pdt, gdt), ps in parts.items():
                 sts = [self._state(p) for p in ps]
-                gs = [p.grad for p in ps]
+                gs = [grad_of(p) for p in ps]
                 ms = [s["exp_avg"] for s in sts]
                 vs = [s["exp_avg_sq"] for s in sts]
                 masters = [s["master"] for s in sts] if pdt != torch.float32 else None
@@ -191,7 +200,7 @@ def clip_grad_norm_(
     is all-reduced over ``group`` before clipping — the reference's ``clip_grad_norm_`` on FSDP
     modules skipped this and clipped by the local shard norm.
     """
-    grads: List[torch.Tensor] = [p.grad for p in parameters if p.grad is not None]
+    grads: List[torch.Tensor] = [g for g in (grad_of(p) for p in parameters) if g is not None]
     if not grads:
         return torch.zeros(())
     dev = grads[0].device

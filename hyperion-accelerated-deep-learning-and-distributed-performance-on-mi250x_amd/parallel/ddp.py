@@ -4,17 +4,24 @@ Reference: ``torch.nn.parallel.DistributedDataParallel`` wrapped around every tr
 (``distributed_utils.py:159,229,475``; SURVEY §2.2 "DP: DDP", K2-K6).
 
 MI355X design:
-* gradients are packed (and pre-scaled by 1/world) into persistent flat buckets the moment each
-  parameter's gradient is final (``post_accumulate_grad`` hook), and a bucket's all-reduce is
-  issued as soon as it is complete — in bucket order on every rank — so RCCL traffic over xGMI
-  overlaps the rest of the backward pass;
+* gradients are packed into persistent flat buckets the moment each parameter's gradient is
+  final (``post_accumulate_grad`` hook), and a bucket's all-reduce (RCCL ``avg``) is issued as
+  soon as it is complete — in bucket order on every rank — so RCCL traffic over xGMI overlaps the
+  rest of the backward pass;
+* buckets are **fp32 by default** whatever the compute dtype: the reference reduced fp32
+  gradients, and a bf16 sum over 8 ranks keeps 8 significant bits.  A bf16/fp16
+  parameter's gradient is up-converted by the pack copy and handed to the optimizer as
+  ``param.main_grad`` (an fp32 bucket view; ``param.grad`` is released after packing, so the
+  next backward's AccumulateGrad steals its fresh gradient instead of adding into it).
+  ``comm_dtype=torch.bfloat16`` (opt-in) halves the bytes on the wire; ``comm_dtype=None`` uses
+  each parameter's own dtype;
 * bucket sizes default to 64 MiB (first bucket 4 MiB): with 288 GB HBM per GPU memory is no
   constraint, and on a fully-connected 8-GPU xGMI mesh RCCL's ring/direct algorithms reach
   their bus bandwidth only at tens of MiB per call, while a small first bucket
   lets the first all-reduce start early in backward;
-* after backward, ``param.grad`` is re-pointed at its bucket slice, so the fused optimizer reads
-  the reduced gradient in place (no copy back) and its pointer table stays valid across steps;
-* ``comm_dtype=torch.bfloat16`` halves the bytes on the wire (the reduction runs in RCCL);
+* after backward, ``param.grad`` (same dtype) or ``param.main_grad`` (fp32 bucket, low-precision
+  parameter) points at the bucket slice, so the fused optimizer reads the reduced gradient in
+  place (no copy back) and its pointer table stays valid across steps;
 * ``broadcast_buffers`` reproduces the reference's per-forward BN buffer broadcast (K5);
 * ``defer_allreduce`` (set by ``TrainStep`` for hipGraph replay): backward only packs the buckets
   and ``allreduce_buckets()`` reduces them afterwards — the captured fwd+bwd graph and the
@@ -93,14 +100,15 @@ class DistributedDataParallel(nn.Module):
         bucket_cap_mb: float = 64.0,
         first_bucket_mb: float = 4.0,
         broadcast_buffers: bool = True,
-        comm_dtype: Optional[torch.dtype] = None,
+        comm_dtype: Optional[torch.dtype] = torch.float32,
         device_ids=None,  # accepted for API compatibility with torch DDP
         find_unused_parameters: bool = False,
         comm=None,
         buckets_at_world_1: bool = False,
     ):
-        """``buckets_at_world_1``: build the bucket machinery even for a single rank (tests of the
-        bucket / deferred-all-reduce / graph paths on a one-GPU box)."""
+        """``comm_dtype``: gradient bucket / all-reduce dtype (fp32 default; ``None`` = each
+        parameter's dtype).  ``buckets_at_world_1``: build the bucket machinery even for a single
+        rank (tests of the bucket / deferred-all-reduce / graph paths on a one-GPU box)."""
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -149,7 +157,7 @@ class DistributedDataParallel(nn.Module):
         cur_key = None
         limit = first_mb * 2**20
         for p in params:
-            dt = comm_dtype or p.dtype
+            dt = comm_dtype if (comm_dtype is not None and p.is_floating_point()) else p.dtype
             key = (dt, p.device, stage_of.get(id(p), -1))
             nbytes = p.numel() * torch.empty((), dtype=dt).element_size()
             if cur and (key != cur_key or cur_bytes + nbytes > limit):
@@ -182,12 +190,12 @@ class DistributedDataParallel(nn.Module):
             return
         off, n = b.offsets[i], p.numel()
         slot = _param_view(b.buf[off : off + n], p)
-        with torch.no_grad():
-            g = p.grad
-            if g.dtype == slot.dtype:
-                torch.mul(g, 1.0 / self.world, out=slot)  # pack + pre-scale in one pass
-            else:
-                slot.copy_(g * (1.0 / self.world))
+        g = p.grad
+        if g.data_ptr() != slot.data_ptr():  # else AccumulateGrad already summed into the slot
+            with torch.no_grad():
+                slot.copy_(g)  # pack (+ up-convert into an fp32 bucket); the all-reduce averages
+        if slot.dtype != p.dtype:
+            p.grad = None  # consumed: the optimizer reads p.main_grad; the next backward steals
         b.got[i] = True
         b.ready += 1
         if b.ready == len(b.params) and not self.defer_allreduce:
@@ -199,7 +207,7 @@ class DistributedDataParallel(nn.Module):
             if b.ready < len(b.params):
                 break
             range_push(f"ddp_allreduce_b{b.index}")
-            b.work = self.comm.all_reduce(b.buf, "sum")
+            b.work = self.comm.all_reduce(b.buf, "avg")
             range_pop()
             b.launched = True
             self._next_launch += 1
@@ -227,10 +235,9 @@ class DistributedDataParallel(nn.Module):
                 view = _param_view(b.buf[off : off + p.numel()], p)
                 if view.dtype == p.dtype:
                     p.grad = view
-                elif p.grad is not None:
-                    p.grad.copy_(view)
                 else:
-                    p.grad = view.to(p.dtype)
+                    p.grad = None
+                    p.main_grad = view  # fp32 reduced gradient of a low-precision parameter
             b.ready = 0
             b.got = [False] * len(b.params)
             b.launched = False
@@ -244,8 +251,8 @@ class DistributedDataParallel(nn.Module):
     def allreduce_buckets(self, indices: Optional[List[int]] = None, wait: bool = True) -> list:
         """Reduce the given buckets (default: all) now (``defer_allreduce`` mode).
 
-        The gradients already point at their bucket slices (pre-scaled by 1/world), so after this
-        the optimizer reads the averaged gradients in place.  ``wait=False`` returns the work
+        The gradients already point at their bucket slices, so after this (an RCCL ``avg``) the
+        optimizer reads the averaged gradients in place.  ``wait=False`` returns the work
         handles instead of ordering the current stream after them, so compute issued next (the
         second half of a split backward) overlaps the collectives on the comm stream; every rank
         must pass the same ``indices`` in the same order."""
@@ -254,7 +261,7 @@ class DistributedDataParallel(nn.Module):
         works = []
         for b in self._buckets if indices is None else [self._buckets[i] for i in indices]:
             range_push(f"ddp_allreduce_b{b.index}")
-            works.append(self.comm.all_reduce(b.buf, "sum"))
+            works.append(self.comm.all_reduce(b.buf, "avg"))
             range_pop()
         if wait:
             for w in works:

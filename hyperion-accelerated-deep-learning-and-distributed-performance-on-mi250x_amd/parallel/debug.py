@@ -18,13 +18,19 @@ import torch.nn as nn
 
 
 def replica_checksums(params: Iterable[torch.Tensor]) -> torch.Tensor:
-    sums = [p.detach().double().sum() for p in params]
-    return torch.stack(sums) if sums else torch.zeros(0, dtype=torch.float64)
+    """[n_params, 2] fp64 (Σx, Σx²) per tensor: identical replicas give identical rows (the sums run
+    in one fixed order on one device type), and a differing element moves at least one of them."""
+    rows = []
+    for p in params:
+        d = p.detach().double()
+        rows.append(torch.stack([d.sum(), (d * d).sum()]))
+    return torch.stack(rows) if rows else torch.zeros(0, 2, dtype=torch.float64)
 
 
-def assert_replicas_in_sync(model: nn.Module, group=None, atol: float = 0.0) -> None:
+def assert_replicas_in_sync(model: nn.Module, group=None, atol: float = 0.0) -> int:
+    """Raise if any parameter differs between ranks; returns the number of tensors compared."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        return
+        return 0
     inner = getattr(model, "module", model)
     cs = replica_checksums(inner.parameters())
     dev = next(inner.parameters()).device
@@ -34,11 +40,12 @@ def assert_replicas_in_sync(model: nn.Module, group=None, atol: float = 0.0) -> 
     dist.all_gather(out, cs, group=group)
     names = [n for n, _ in inner.named_parameters()]
     for r in range(1, world):
-        diff = (out[r] - out[0]).abs()
+        diff = (out[r] - out[0]).abs().amax(dim=1) if cs.dim() == 2 else (out[r] - out[0]).abs()
         bad = (diff > atol).nonzero().flatten().tolist()
         if bad:
             raise RuntimeError(f"replica desync: rank {r} differs from rank 0 in {[names[i] for i in bad[:5]]}"
                                f"{' ...' if len(bad) > 5 else ''}")
+    return len(names)
 
 
 def assert_same_collective_sequence(tag: str, group=None, device: Optional[torch.device] = None) -> None:

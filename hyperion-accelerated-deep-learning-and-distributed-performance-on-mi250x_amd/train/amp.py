@@ -76,7 +76,9 @@ class LossScaler:
             return
         self._unscaled = True  # GradScaler semantics: one unscale per step (clip may call it early)
         self.found_inf_t.zero_()
-        grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+        from ..ops.optim import grad_of
+
+        grads = [gr for g in optimizer.param_groups for gr in (grad_of(p) for p in g["params"]) if gr is not None]
         if not grads:
             return
         by_dtype: Dict[torch.dtype, list] = {}

@@ -39,6 +39,9 @@ def save_checkpoint(path: str, model: nn.Module, optimizer: Optional[torch.optim
     """Write a checkpoint; returns the path written on this rank (None on non-writing ranks)."""
     rank = _rank()
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    # every rank, before any branch: the FSDP paths write per-rank files (and the full path only
+    # after its all-ranks gather), so a missing directory must not fail there
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     meta = {"epoch": epoch, "step": step, "world_size": world}
     if extra:
         meta.update(extra)
@@ -71,7 +74,6 @@ def save_checkpoint(path: str, model: nn.Module, optimizer: Optional[torch.optim
         doc["optimizer_state_dict"] = optimizer.state_dict()
     if scaler is not None:
         doc["scaler_state_dict"] = scaler.state_dict()
-    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     torch.save(doc, path)
     return path
 

@@ -15,7 +15,7 @@ RCCL call is ever recorded into a graph, and the ~500 per-step kernel launches s
 graph launches.
 
 When the model exposes ``graph_stages()`` (``[bottom, top]`` with ``forward == top∘bottom``;
-ResNet splits after layer2), the backward itself is cut in two graphs at that boundary: graph 1 =
+ResNet splits after layer1), the backward itself is cut in two graphs at that boundary: graph 1 =
 forward + backward of the top (its buckets — ~85% of ResNet-50's gradient bytes — are complete),
 then those buckets' all-reduces are issued on the comm stream WITHOUT ordering the compute
 stream after them, graph 2 = backward of the bottom (overlapping the collectives), the remaining
@@ -70,6 +70,7 @@ class TrainStep:
         self._phase1: list = []
         self._phase2: list = []
         self._keep = None
+        self._counters = None  # BatchNormAct2d num_batches_tracked mirrors under replay
 
     def _ddp(self):
         """The model if it is a bucketed Hyperion DDP whose step can be split around its collectives."""
@@ -172,6 +173,15 @@ class TrainStep:
                 self._body(self.static_x, self.static_y, zero_in_place=True)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        from ..ops.batchnorm import HostCounterReplay
+
+        counters = HostCounterReplay(self.model)
+        try:
+            self._capture_graphs()
+        finally:
+            self._counters = counters.captured()
+
+    def _capture_graphs(self) -> None:
         ddp = self._ddp()
         stages = self._stages()
         if ddp is not None and stages is not None:  # three graphs: top fwd+bwd | bottom bwd | optimizer
@@ -216,6 +226,7 @@ class TrainStep:
         if y.data_ptr() != self.static_y.data_ptr():
             self.static_y.copy_(y, non_blocking=True)
         self.graph.replay()
+        self._counters.replayed()
         if self.graph3 is not None:
             # top buckets reduce on the comm stream while the bottom backward replays
             works = self.model.allreduce_buckets(self._phase1, wait=False)
@@ -239,9 +250,12 @@ class GraphedClosure:
     ``loss_fn(model(x), y)`` (Llama with masks and labels, the LM with its fused head).
     """
 
-    def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3):
+    def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, module: Optional[nn.Module] = None):
+        """``module``: the model the closure trains (its BatchNormAct2d counters follow replays)."""
         self.fn = fn
         self.warmup = warmup
+        self.module = module
+        self.counters = None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.out: Optional[torch.Tensor] = None
 
@@ -254,10 +268,16 @@ class GraphedClosure:
                     self.fn()
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
+            from ..ops.batchnorm import HostCounterReplay
+
+            counters = HostCounterReplay(self.module) if self.module is not None else None
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.out = self.fn()
             torch.cuda.synchronize()
+            self.counters = counters.captured() if counters is not None else None
             self.graph = g
         self.graph.replay()
+        if self.counters is not None:
+            self.counters.replayed()
         return self.out

@@ -136,3 +136,56 @@ def test_ddp_split_backward_overlap_matches_single_process():
     for k in ref:
         torch.testing.assert_close(res[0]["sd"][k], res[1]["sd"][k], rtol=0, atol=0, msg=k)
         torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def _ddp_lowp(rank, world, comm_dtype):
+    """bf16 compute copies: the reduced gradient is the fp32 average of the ranks' bf16 gradients
+    (fp32 buckets, ``main_grad``) or its bf16 rounding (opt-in bf16 buckets, ``grad``)."""
+    import copy
+
+    import torch.distributed as dist
+
+    from hyperion.ops.optim import FusedAdam, grad_of
+    from hyperion.parallel import DDP
+    from hyperion.train.amp import cast_for_compute
+
+    base = cast_for_compute(_model(seed=0), torch.bfloat16)
+    plain = copy.deepcopy(base)
+    x, y = _data(0)
+    x, y = x[rank * 4:(rank + 1) * 4].to(torch.bfloat16), y[rank * 4:(rank + 1) * 4]
+    torch.nn.functional.cross_entropy(plain(x).float(), y).backward()
+    local = [p.grad.float() for p in plain.parameters()]
+    gathered = []
+    for g in local:
+        out = [torch.empty_like(g) for _ in range(world)]
+        dist.all_gather(out, g)
+        gathered.append(sum(out) / world)
+    m = DDP(base, bucket_cap_mb=1.0, first_bucket_mb=0.1, broadcast_buffers=False, comm_dtype=comm_dtype)
+    torch.nn.functional.cross_entropy(m(x).float(), y).backward()
+    got = [grad_of(p) for p in m.parameters()]
+    dtypes = sorted({str(g.dtype) for g in got})
+    err = max(float((g.float() - e).abs().max()) for g, e in zip(got, gathered))
+    err_bf16 = max(float((g.float() - e.to(torch.bfloat16).float()).abs().max()) for g, e in zip(got, gathered))
+    has_main = any(getattr(p, "main_grad", None) is not None for p in m.parameters())
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    opt.step()
+    return {"err": err, "err_bf16": err_bf16, "dtypes": dtypes, "has_main": has_main,
+            "params": [p.detach().float().clone() for p in m.parameters()]}
+
+
+def test_ddp_bf16_compute_reduces_in_fp32_by_default():
+    res = run_world(_ddp_lowp, 2, (torch.float32,))
+    for r in (0, 1):
+        assert res[r]["has_main"] and "torch.float32" in res[r]["dtypes"]
+        assert res[r]["err"] == 0.0  # exactly the fp32 average of the bf16 rank gradients
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_ddp_bf16_buckets_opt_in():
+    res = run_world(_ddp_lowp, 2, (torch.bfloat16,))
+    for r in (0, 1):
+        assert res[r]["dtypes"] == ["torch.bfloat16"]  # every bucket on the wire in bf16
+        assert res[r]["err_bf16"] <= 1e-2  # gloo's bf16 sum: one rounding of the fp32 average
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)

@@ -38,11 +38,13 @@ def test_conv_fwd_and_stats_match_fp32(shape, dtype):
 @pytest.mark.parametrize("shape", SHAPES[:5])
 @pytest.mark.parametrize("act,res", [(True, False), (True, True), (False, False)])
 def test_conv_bn_act_fwd_bwd_match_reference(shape, act, res):
+    from hyperion.ops import _native
     from hyperion.ops.batchnorm import BatchNormAct2d
     from hyperion.ops.conv import conv_bn_act
 
     N, C, H, W, K, R, s, p = shape
     torch.manual_seed(0)
+    _native.reset_counters()
     conv = torch.nn.Conv2d(C, K, R, stride=s, padding=p, bias=False).cuda()
     bn = BatchNormAct2d(K, act=act).cuda()
     with torch.no_grad():
@@ -58,6 +60,11 @@ def test_conv_bn_act_fwd_bwd_match_reference(shape, act, res):
     out = conv_bn_act(conv_l, bn, x, r)
     g = torch.randn_like(out)
     out.backward(g)
+    cnt = _native.counters()  # the fused kernels ran (a bn(conv(x)) fallback computes the same numbers)
+    assert cnt.get("conv_bn_act") == 1 and "conv_bn_act_fallback" not in cnt, cnt
+    assert cnt.get("wgrad") == 1 and "wgrad_vendor" not in cnt, cnt
+    if s == 1 or R == 1:
+        assert "dgrad_vendor" not in cnt, cnt
     # fp32 reference on the CPU: MIOpen's fp32 conv backward segfaults on the host for the
     # N=1, C=256, 7x7, K=2048 1x1 shape (ROCm 7 / torch 2.10; reproduced in isolation), so the
     # oracle does not touch the vendor GPU path at all
@@ -296,3 +303,50 @@ def test_downsample_branch_grad_fusion_matches_autograd_add(block):
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("block", ["bottleneck_s2", "bottleneck_id"])
+def test_partial_backward_with_gradient_links(block):
+    """A partial ``autograd.grad`` (retain_graph) that reaches only one consumer of a block input
+    must not park a gradient for a partner that never runs: the following full backward still
+    matches the unfused gradients bitwise (BranchSumLink / ResidualLink staleness)."""
+    import torch.nn as nn
+
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import Bottleneck, conv1x1
+    from hyperion.ops.batchnorm import BatchNormAct2d
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    if block == "bottleneck_s2":
+        cin, cout, s = 256, 512, 2
+        m = Bottleneck(cin, 128, 2, nn.Sequential(conv1x1(cin, cout, 2), BatchNormAct2d(cout)))
+        probe = m.downsample[0].weight
+    else:
+        cin, cout, s = 256, 256, 1
+        m = Bottleneck(cin, 64)
+        probe = m.conv3.weight
+    m = m.cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    x0 = torch.randn(8, cin, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, cout, 14 // s, 14 // s, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run(fuse, partial):
+        hconv.FUSE_SHORTCUT_GRAD = fuse
+        try:
+            x = x0.clone().requires_grad_(True)
+            out = m(x)
+            if partial:  # reaches the probe's consumer only
+                torch.autograd.grad(out, [probe], gy, retain_graph=True)
+            return torch.autograd.grad(out, [x], gy)[0]
+        finally:
+            hconv.FUSE_SHORTCUT_GRAD = True
+
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        ref = run(False, False)
+        got = run(True, True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+    assert torch.equal(ref, got)
