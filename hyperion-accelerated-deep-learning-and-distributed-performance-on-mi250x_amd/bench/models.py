@@ -55,7 +55,7 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
 
     from ..train.step import GraphedClosure
 
-    step = GraphedClosure(body, warmup=2) if graph else body
+    step = GraphedClosure(body, warmup=2, module=m) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
     return {"model": model, "batch": batch, "seq": seq, "precision": precision, "graph": graph, "ms_per_step": t * 1e3,
@@ -127,7 +127,7 @@ def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmu
         opt.step()
         return loss.detach()
 
-    step = GraphedClosure(body, warmup=2) if graph else body
+    step = GraphedClosure(body, warmup=2, module=m) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
     return {"model": "llama2_7b" if config is None else "llama_custom", "lora": lora, "graph": graph, "batch": batch,

@@ -148,6 +148,8 @@ void stream(int64_t op, const at::Tensor& a, const c10::optional<at::Tensor>& b,
 
 void register_norm_ops(pybind11::module& m) {
   m.def("bn_fwd", &bn_fwd, "fused NHWC batch-norm (+residual)(+relu) forward");
+  m.def("bn_set_fin2", [](bool on) { hyp::bn_set_fin2(on ? 1 : 0); },
+        "wide one-round BN finalize on/off (A/B and tests)");
   m.def("bn_set_small_paths", [](bool on) { hyp::bn_set_small_paths(on ? 1 : 0); },
         "small-M BN fast paths: finalize folded into the apply, one-launch backward (default on)");
   m.def("bn_bwd", &bn_bwd, "fused NHWC batch-norm (+residual)(+relu) backward");

@@ -12,6 +12,8 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
                       const float* bias, float* running_mean, float* running_var, float momentum, float eps,
                       int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
                       float* scale, float* shift, hipStream_t stream);
+// wide (one-round, 1024-thread) BN finalize on/off: A/B against the one-level kernels
+void bn_set_fin2(int on);
 // y == nullptr with act: the ReLU mask is recomputed from x (training, no residual gradient only)
 // small-M BN fast paths (finalize folded into apply / one-launch backward); 0 disables (A/B, tests)
 void bn_set_small_paths(int on);

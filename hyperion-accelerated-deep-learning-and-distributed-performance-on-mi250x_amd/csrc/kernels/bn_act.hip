@@ -25,6 +25,17 @@ constexpr int kStatsBlocks = 512;  // partial rows per reduction: keeps the comb
 constexpr int kFinCh = 8;          // finalize block: 8 channels x 32 partial-row groups
 constexpr int kFinGr = 32;
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct BwdFin {  // backward finalize inputs / outputs (bn_bwd_finalize_k's arguments)
+  const float* weight;
+  const float* mean;
+  const float* invstd;
+  int training;
+  float* dweight;
+  float* dbias;
+};
+
 struct BnGeom {
   int tpr;   // threads per row (each owns 8 channels)
   int rpi;   // rows per block-iteration
@@ -403,6 +414,103 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------- wide finalize
+// The conv epilogue (forward) and bn_bwd_reduce_k (backward) leave P partial rows [P, C] — up to
+// 784 for ResNet-50 layer1.  The finalize kernels above give each of C/8 blocks P/32 scalar loads
+// per thread, issued 8 at a time: three or four dependent memory round trips, a 5-7 us
+// latency-bound launch (8 blocks at C = 64; 75 such launches per ResNet-50 step).  A ticketed
+// two-level variant (last arriver combines) measured 10-14 us: the agent-scope release/acquire
+// fences and the winner's serial second pass cost more than they save (MI355X_MICROARCH.md
+// "splitk-seam").  Here one 1024-thread block owns 16 channels (4 float4 lanes) x 256 row lanes:
+// every partial is read by ONE round of independent 16-byte loads (<= 4 per thread for P <= 1024),
+// then a fixed-order LDS tree over the 256 row lanes (deterministic) and the fp64 finalize.
+struct Fin2Fwd {  // forward: statistics -> mean / invstd / running stats / scale / shift
+  const float* weight;
+  const float* bias;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;
+  float* save_invstd;
+  float* scale;
+  float* shift;
+};
+
+constexpr int kWideRows = 256;  // row lanes per block
+constexpr int kWideUnroll = 4;  // partial rows per thread per round
+
+template <bool BWD>
+__global__ __launch_bounds__(1024) void bn_fin_wide_k(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                       int P, int C, int64_t M, Fin2Fwd ff, BwdFin bf,
+                                                       float* __restrict__ kA, float* __restrict__ kB,
+                                                       float* __restrict__ kC) {
+  __shared__ f32x4 red[2][kWideRows][4];
+  const int tid = threadIdx.x, q = tid & 3, ry = tid >> 2;
+  const int c = blockIdx.x * 16 + q * 4;
+  f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = sa;
+  for (int r0 = ry; r0 < P; r0 += kWideRows * kWideUnroll) {
+    f32x4 va[kWideUnroll], vb[kWideUnroll];
+#pragma unroll
+    for (int u = 0; u < kWideUnroll; ++u) {  // all loads of the round in flight before any add
+      const int r = r0 + u * kWideRows;
+      const bool ok = r < P;
+      va[u] = ok ? *reinterpret_cast<const f32x4*>(pa + (int64_t)r * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      vb[u] = ok ? *reinterpret_cast<const f32x4*>(pb + (int64_t)r * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < kWideUnroll; ++u) {
+      sa += va[u];
+      sb += vb[u];
+    }
+  }
+  red[0][ry][q] = sa;
+  red[1][ry][q] = sb;
+  __syncthreads();
+  for (int h = kWideRows / 2; h >= 1; h >>= 1) {  // fixed pairing: deterministic
+    if (ry < h) {
+      red[0][ry][q] += red[0][ry + h][q];
+      red[1][ry][q] += red[1][ry + h][q];
+    }
+    __syncthreads();
+  }
+  if (tid < 16) {
+    const int ch = blockIdx.x * 16 + tid;
+    if (ch < C) {
+      const double a = red[0][0][tid >> 2][tid & 3], b = red[1][0][tid >> 2][tid & 3];
+      if (!BWD) {
+        const double mean = a / (double)M;
+        double var = b / (double)M - mean * mean;
+        if (var < 0.0) var = 0.0;
+        const float invstd = (float)(1.0 / sqrt(var + (double)ff.eps));
+        ff.save_mean[ch] = (float)mean;
+        ff.save_invstd[ch] = invstd;
+        if (ff.running_mean != nullptr) {
+          const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+          ff.running_mean[ch] = (float)((1.0 - ff.momentum) * ff.running_mean[ch] + ff.momentum * mean);
+          ff.running_var[ch] = (float)((1.0 - ff.momentum) * ff.running_var[ch] + ff.momentum * unbiased);
+        }
+        const float w = ff.weight ? ff.weight[ch] : 1.f;
+        const float bb = ff.bias ? ff.bias[ch] : 0.f;
+        const float sc = w * invstd;
+        ff.scale[ch] = sc;
+        ff.shift[ch] = bb - (float)mean * sc;
+      } else {
+        const double mu = bf.mean[ch], is = bf.invstd[ch];
+        const double sum_dz_xhat = is * (b - mu * a);
+        if (bf.dweight) bf.dweight[ch] = (float)sum_dz_xhat;
+        if (bf.dbias) bf.dbias[ch] = (float)a;
+        const double gw = bf.weight ? bf.weight[ch] : 1.0;
+        const double A = gw * is;
+        const double Bc = bf.training ? -A * is * sum_dz_xhat / (double)M : 0.0;
+        const double Cc = bf.training ? -A * a / (double)M - Bc * mu : 0.0;
+        kA[ch] = (float)A;
+        kB[ch] = (float)Bc;
+        kC[ch] = (float)Cc;
+      }
+    }
+  }
+}
+
 template <typename T, bool ACT, bool RES, bool MASKX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const T* __restrict__ y, T* __restrict__ dx,
@@ -466,15 +574,6 @@ struct StatsFin {  // forward finalize inputs / outputs (bn_stats_finalize_k's a
   float momentum, eps;
   float* save_mean;
   float* save_invstd;
-};
-
-struct BwdFin {  // backward finalize inputs / outputs (bn_bwd_finalize_k's arguments)
-  const float* weight;
-  const float* mean;
-  const float* invstd;
-  int training;
-  float* dweight;
-  float* dbias;
 };
 
 template <typename T, bool ACT, bool RES>
@@ -677,6 +776,17 @@ __global__ __launch_bounds__(NT) void bn_bwd_small_k(const T* __restrict__ dy, c
   }
 }
 
+int g_fin2 = 1;  // wide finalize on (bn_set_fin2: A/B against the one-level kernels)
+
+// Wide finalize launch (false: not applicable — C % 16, or disabled)
+template <bool BWD>
+bool launch_fin_wide(const float* pa, const float* pb, int P, int C, int64_t M, const Fin2Fwd& ff, const BwdFin& bf,
+                     float* kA, float* kB, float* kC, hipStream_t stream) {
+  if (!g_fin2 || C % 16 != 0) return false;
+  hipLaunchKernelGGL((bn_fin_wide_k<BWD>), dim3(C / 16), dim3(1024), 0, stream, pa, pb, P, C, M, ff, bf, kA, kB, kC);
+  return true;
+}
+
 // small-M forward: finalize folded into the apply (returns false when the shape is not covered)
 bool launch_fin_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* psum,
                       const float* psq, int P, const float* weight, const float* bias, float* running_mean,
@@ -763,6 +873,8 @@ hipError_t bn_workspace_rows(int64_t M, int C, int* P_out) {
   return hipSuccess;
 }
 
+void bn_set_fin2(int on) { g_fin2 = on ? 1 : 0; }
+
 hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* weight,
                       const float* bias, float* running_mean, float* running_var, float momentum, float eps,
                       int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
@@ -777,8 +889,11 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
       if (launch_fin_apply(dtype, x, res, y, M, C, psum, psq, gs.P, weight, bias, running_mean, running_var, momentum,
                            eps, act, save_mean, save_invstd, stream))
         return hipGetLastError();
-      hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum, psq, gs.P, C, M,
-                         weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+      const Fin2Fwd ff{weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift};
+      if (!launch_fin_wide<false>(psum, psq, gs.P, C, M, ff, BwdFin{}, nullptr, nullptr, nullptr, stream))
+        hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum,
+                           psq, gs.P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean,
+                           save_invstd, scale, shift);
     } else {
       hipLaunchKernelGGL(bn_eval_consts_k, dim3((C + 255) / 256), dim3(256), 0, stream, C, weight, bias, running_mean,
                          running_var, eps, save_mean, save_invstd, scale, shift);
@@ -849,8 +964,10 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
     else
       hipLaunchKernelGGL((bn_bwd_reduce_k<T, false, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
                          gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
-    hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, pdz, pdzx,
-                       gs.P, C, M, weight, save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
+    const BwdFin bf{weight, save_mean, save_invstd, training, dweight, dbias};
+    if (!launch_fin_wide<true>(pdz, pdzx, gs.P, C, M, Fin2Fwd{}, bf, kA, kB, kC, stream))
+      hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, pdz,
+                         pdzx, gs.P, C, M, weight, save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
     launch_bn_dx<T>(maskx, act, dres != nullptr, dim3(ga.P, ga.gy), stream, dyt, xt, yt, static_cast<T*>(dx),
                     static_cast<T*>(dres), kA, kB, kC, M, C, ga, weight, bias, save_mean, save_invstd);
   });
@@ -873,9 +990,11 @@ hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, v
   if (launch_fin_apply(dtype, x, res, y, M, C, psum, psq, P, weight, bias, running_mean, running_var, momentum, eps,
                        act, save_mean, save_invstd, stream))
     return hipGetLastError();
-  hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum, psq,
-                     P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale,
-                     shift);
+  const Fin2Fwd ff{weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift};
+  if (!launch_fin_wide<false>(psum, psq, P, C, M, ff, BwdFin{}, nullptr, nullptr, nullptr, stream))
+    hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum,
+                       psq, P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd,
+                       scale, shift);
   HYP_DISPATCH_FLOAT(dtype, T, {
     const T* xt = static_cast<const T*>(x);
     const T* rt = static_cast<const T*>(res);

@@ -31,11 +31,9 @@ __device__ __forceinline__ void stream_store(float4* p, float4 r) {
   }
 }
 
-// Each thread moves kUnroll float4 per trip with all loads issued before any store (≥ 4 × 16 B per
+// Each thread moves kUnroll float4 per trip with all loads issued before any store (≥ U × 16 B per
 // operand in flight per lane: HBM latency is hidden by memory-level parallelism, not occupancy).
-constexpr int kUnroll = 4;
-
-template <int OP, bool NT>
+template <int OP, bool NT, int kUnroll>
 __global__ __launch_bounds__(256) void stream_k(const float4* __restrict__ a, const float4* __restrict__ b,
                                                 float4* __restrict__ c, float s, int64_t n4) {
   const int64_t tile = (int64_t)blockDim.x * kUnroll;
@@ -63,22 +61,35 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
                      int blocks, hipStream_t stream) {
   if (n % 4 != 0) return hipErrorInvalidValue;
   const int64_t n4 = n / 4;
-  // blocks > 0: grid-stride over that many workgroups; 0: 2048 (8 x 256-thread WGs per CU);
-  // < 0: one tile per workgroup (a full grid, every workgroup exits after its tile)
-  const int64_t need = (n4 + 256 * kUnroll - 1) / (256 * kUnroll);
-  int64_t grid = blocks > 0 ? blocks : (blocks < 0 ? need : 2048);
+  // blocks > 0: grid-stride over that many workgroups (4 float4 per lane per trip);
+  // blocks = -U (U in 1, 2, 4, 8): one tile of U float4 per lane per workgroup (a full grid, every
+  // workgroup exits after its tile); 0: the default — full grid, U = 1, measured best on MI355X
+  // (add, 500M fp32: 6175 GB/s with non-temporal stores vs 6109 for torch's add, 5944 for the
+  // grid-stride form; profiles/hardware_r02/stream_sweep.json)
+  if (blocks == 0) blocks = -1;
+  const int U = blocks < 0 ? -blocks : 4;
+  if (U != 1 && U != 2 && U != 4 && U != 8) return hipErrorInvalidValue;
+  const int64_t need = (n4 + 256 * U - 1) / (256 * U);
+  int64_t grid = blocks > 0 ? blocks : need;
   if (need < grid) grid = need;
   if (grid > INT32_MAX) return hipErrorInvalidValue;
   if (grid < 1) grid = 1;
   auto A = reinterpret_cast<const float4*>(a);
   auto B = reinterpret_cast<const float4*>(b);
   auto C = reinterpret_cast<float4*>(c);
-#define HYP_STREAM_CASE(OPV)                                                                                     \
-  case OPV:                                                                                                      \
-    if (nontemporal)                                                                                             \
-      hipLaunchKernelGGL((stream_k<OPV, true>), dim3((unsigned)grid), dim3(256), 0, stream, A, B, C, s, n4);               \
-    else                                                                                                         \
-      hipLaunchKernelGGL((stream_k<OPV, false>), dim3((unsigned)grid), dim3(256), 0, stream, A, B, C, s, n4);              \
+#define HYP_STREAM_U(OPV, UV)                                                                                      \
+  if (U == UV) {                                                                                                   \
+    if (nontemporal)                                                                                               \
+      hipLaunchKernelGGL((stream_k<OPV, true, UV>), dim3((unsigned)grid), dim3(256), 0, stream, A, B, C, s, n4);   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((stream_k<OPV, false, UV>), dim3((unsigned)grid), dim3(256), 0, stream, A, B, C, s, n4);  \
+  }
+#define HYP_STREAM_CASE(OPV) \
+  case OPV:                  \
+    HYP_STREAM_U(OPV, 1)     \
+    HYP_STREAM_U(OPV, 2)     \
+    HYP_STREAM_U(OPV, 4)     \
+    HYP_STREAM_U(OPV, 8)     \
     break;
   switch (op) {
     HYP_STREAM_CASE(0)
@@ -89,6 +100,7 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
       return hipErrorInvalidValue;
   }
 #undef HYP_STREAM_CASE
+#undef HYP_STREAM_U
   return hipGetLastError();
 }
 

@@ -1,8 +1,15 @@
 """Multi-tensor launch tables for the gfx950 multi-tensor kernels (``csrc/kernels/adam.hip``).
 
-A table is built once per set of tensor pointers and reused while the pointers stay the same
-(always, inside a captured hipGraph — tables are built during warm-up, never during capture).  Each row of the block table is (tensor id, chunk id); one
-256-thread block processes ``chunk`` elements.
+A table is built once per set of tensor pointers and reused while the pointers stay the same.
+Each row of the block table is (tensor id, chunk id); one 256-thread block processes ``chunk``
+elements.
+
+hipGraph capture: a table is never ALLOCATED during capture (see ``MultiTensorTable``), but one
+built during warm-up can be RE-POINTED there — same tensor count and sizes, new addresses (the
+captured step's gradients: ``TrainStep`` lets autograd steal the fresh weight gradients instead of
+adding them into kept ``.grad`` buffers, which cost one add kernel per parameter per step).  The
+captured kernel reads the table's device buffer at replay time, so the new pointers are written
+into that (pre-capture) buffer right after capture ends: ``flush_pending()``.
 """
 from __future__ import annotations
 
@@ -14,15 +21,24 @@ CHUNK = 8192  # elements per block (multiple of 4 for the float4 body)
 
 
 
+_PENDING: List[Tuple[torch.Tensor, torch.Tensor]] = []  # (device pointer table, host pointers)
+
+
 def flush_pending() -> int:
-    """Kept for API compatibility: tables are never built during capture (see below)."""
-    return 0
+    """Write the pointer updates recorded during a hipGraph capture (call after the capture ends,
+    before the first replay); returns how many tables were updated."""
+    n = len(_PENDING)
+    for dev_t, host_t in _PENDING:
+        dev_t.copy_(host_t)
+    _PENDING.clear()
+    return n
 
 
 class MultiTensorTable:
     def __init__(self, groups: Sequence[Sequence[torch.Tensor]], chunk: int = CHUNK):
         """``groups``: K lists of T tensors each (e.g. [params, grads, exp_avg, exp_avg_sq])."""
         assert groups and all(len(g) == len(groups[0]) for g in groups)
+        self.layout = self.layout_of(groups)
         self.T = len(groups[0])
         self.chunk = chunk
         dev = groups[0][0].device
@@ -63,6 +79,23 @@ class MultiTensorTable:
     def key_of(groups: Sequence[Sequence[torch.Tensor]]) -> Tuple[int, ...]:
         return tuple(t.data_ptr() for g in groups for t in g)
 
+    @staticmethod
+    def layout_of(groups: Sequence[Sequence[torch.Tensor]]) -> Tuple:
+        return (len(groups),) + tuple(t.numel() for t in groups[0])
+
+    def repoint(self, groups: Sequence[Sequence[torch.Tensor]]) -> None:
+        """Same tensor count and sizes, new addresses: rewrite the pointer table in place (the
+        block table depends on sizes only).  Deferred to ``flush_pending`` under capture."""
+        ptrs = [t.data_ptr() for g in groups for t in g]
+        if any(p % 16 for p in ptrs):
+            raise ValueError("multi-tensor kernels need 16-byte aligned tensors")
+        host = torch.tensor(ptrs, dtype=torch.int64)
+        if self.ptrs.is_cuda and torch.cuda.is_current_stream_capturing():
+            _PENDING.append((self.ptrs, host))
+        else:
+            self.ptrs.copy_(host)
+        self.key = self.key_of(groups)
+
 
 class TableCache:
     """Keeps the most recent table per role; rebuilds when pointers change."""
@@ -73,7 +106,9 @@ class TableCache:
     def get(self, role: str, groups: Sequence[Sequence[torch.Tensor]]) -> MultiTensorTable:
         key = MultiTensorTable.key_of(groups)
         t = self._tables.get(role)
-        if t is None or t.key != key:
+        if t is not None and t.key != key and t.layout == MultiTensorTable.layout_of(groups):
+            t.repoint(groups)
+        elif t is None or t.key != key:
             t = MultiTensorTable(groups)
             self._tables[role] = t
         return t

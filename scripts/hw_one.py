@@ -51,7 +51,7 @@ else:
     for n in (100_000_000, 500_000_000):
         x, y, z = torch.rand(n, device="cuda"), torch.rand(n, device="cuda"), torch.empty(n, device="cuda")
         rows.append({"n": n, "kernel": "torch_add", "GBps": 12 * n / ev(lambda: torch.add(x, y, out=z)) / 1e9})
-        for blocks in (0, 1024, 4096, -1):
+        for blocks in (0, 2048, -1, -2, -4, -8):
             for nt in (True, False):
                 t = ev(lambda: C.stream(2, x, y, z, 3.0, nt, blocks))
                 rows.append({"n": n, "kernel": f"hyp_add_blocks{blocks}_nt{int(nt)}", "GBps": 12 * n / t / 1e9})

@@ -279,3 +279,49 @@ def test_bn_small_m_paths_match_general_path(shape, act, use_res):
     yr.backward(gy.float())
     torch.testing.assert_close(fast[0].float(), yr, atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(fast[1].float(), xr.grad, atol=6e-2, rtol=6e-2)
+
+
+@pytest.mark.parametrize("shape", [(32, 64, 56, 56), (32, 256, 56, 56), (8, 128, 28, 28), (4, 2048, 7, 7)])
+@pytest.mark.parametrize("act,use_res", [(True, False), (True, True)])
+def test_bn_wide_finalize_matches_one_level(shape, act, use_res):
+    """Wide one-round finalize (1024-thread blocks of 16 channels x 256 row lanes, fixed-order LDS
+    tree) vs the one-level finalize kernels: same results to rounding, bitwise deterministic."""
+    from hyperion.ops import _native
+    from hyperion.ops.batchnorm import _BNActFn
+
+    C_ = _native.native()
+    N, C, H, W = shape
+    torch.manual_seed(3)
+    x = (torch.randn(N, C, H, W, device="cuda") * 1.1 - 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
+    res = torch.randn_like(x) if use_res else None
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+    gy = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run(two):
+        C_.bn_set_fin2(two)
+        C_.bn_set_small_paths(False)  # the general (large-M) paths, where the finalize runs
+        try:
+            rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+            xn = x.detach().requires_grad_(True)
+            rn = res.detach().requires_grad_(True) if use_res else None
+            wn, bn = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+            yn = _BNActFn.apply(xn, rn, wn, bn, rm, rv, 0.1, 1e-5, True, act)
+            yn.backward(gy)
+            torch.cuda.synchronize()
+            return [yn, xn.grad, wn.grad, bn.grad, rm, rv] + ([rn.grad] if use_res else [])
+        finally:
+            C_.bn_set_fin2(True)
+            C_.bn_set_small_paths(True)
+
+    two = [run(True) for _ in range(3)]
+    one = run(False)
+    for r in two[1:]:
+        for a, c in zip(two[0], r):
+            assert torch.equal(a, c), "wide finalize must be deterministic"
+    M = N * H * W
+    for i, (a, c) in enumerate(zip(two[0], one)):
+        tol = 1e-3 * M ** 0.5 if i in (2, 3) else 2e-2
+        torch.testing.assert_close(a.float(), c.float(), atol=tol, rtol=2e-2, msg=f"output {i}")
+    torch.testing.assert_close(two[0][4], one[4], atol=1e-5, rtol=1e-4)  # running mean
+    torch.testing.assert_close(two[0][5], one[5], atol=1e-5, rtol=1e-4)  # running var
