@@ -202,6 +202,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       for (int j = 0; j < FN; ++j)
         fb[j] = DGRAD ? mfl::frag_tr<BN>(bs, ks * 32, wn * (BN / 2) + j * 16, lane)
                       : frag(bs, wn * (BN / 2) + j * 16 + r16, ks * 4 + c4);
+      if (DGRAD) mfl::lds_reads_done();  // the asm transposed reads (see mfma_lds.h) have returned
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
       for (int i = 0; i < FM; ++i) fa[i] = frag_tr<BM>(as, ks * 32, wm * (BM / 2) + i * 16, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[j] = frag_tr<BN>(bs, ks * 32, wn * (BN / 2) + j * 16, lane);
+      lds_reads_done();  // the asm transposed reads (see mfma_lds.h) have returned
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

@@ -59,6 +59,26 @@ __device__ __forceinline__ int tr_row_to_k(int row) {
   return (row & ~31) | (((row >> 2) & 3) << 3) | (((row >> 4) & 1) << 2) | (row & 3);
 }
 
+// ds_read_b64_tr_b16 as inline asm.  The builtin form makes hipcc (ROCm 7.2) wait vmcnt(0) before
+// the read whenever a global_load_lds is in flight — it cannot prove the DMA's LDS destination does
+// not alias — which drained the NEXT stage's prefetch before every k-step of the weight-gradient
+// and data-gradient kernels (load and compute fully serialized).  The asm read is invisible to that
+// pass; the caller orders it: the stage it reads was retired by wait_stage + barrier, and
+// lds_reads_done() (lgkmcnt(0) + sched_barrier) precedes the MFMAs that consume the fragments.
+__device__ __forceinline__ s16x4 ds_read_tr16_asm(const uint16_t* addr) {
+  typedef short s16x4_t __attribute__((ext_vector_type(4)));
+  s16x4_t v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)addr;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+// every LDS read issued so far (asm ones included) has returned; no instruction moves across
+__device__ __forceinline__ void lds_reads_done() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int W>
 __device__ __forceinline__ u16x8 frag_tr(const uint16_t* img, int r0, int cb, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -68,7 +88,7 @@ __device__ __forceinline__ u16x8 frag_tr(const uint16_t* img, int r0, int cb, in
   for (int t = 0; t < 2; ++t) {
     const int row = r0 + 16 * t + 4 * g + q;
     const uint16_t* addr = img + row * W + ((chunk ^ swz_tr<W>(row)) << 3) + ((p & 1) << 2);
-    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)addr);
+    const s16x4 v = ds_read_tr16_asm(addr);
 #pragma unroll
     for (int e = 0; e < 4; ++e) out[4 * t + e] = (uint16_t)v[e];
   }

@@ -30,6 +30,7 @@ import torch
 import torch.nn as nn
 
 from . import _native
+from . import streams as _streams
 
 
 def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -187,6 +188,10 @@ class _ConvBNActFn(torch.autograd.Function):
         add = None
         if link_in is not None and link_in.dres is not None:
             add, link_in.dres = link_in.dres, None
+        dw = None
+        if ctx.needs_input_grad[1] and _streams.use_side_for(w):
+            # off the critical path: forked BEFORE the data gradient, so the two overlap
+            dw = _streams.run_on_side(lambda: _wgrad(dyc, x, w, stride, padding), [dyc, x], dyc.device)
         dx = None
         if ctx.needs_input_grad[0]:
             if branch is not None and branch.users == 2 and _will_run(branch.nodes[1 - bidx]):
@@ -200,7 +205,8 @@ class _ConvBNActFn(torch.autograd.Function):
                     dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add)
             else:
                 dx = _dgrad(dyc, x, w, stride, padding, addend=add)
-        dw = _wgrad(dyc, x, w, stride, padding) if ctx.needs_input_grad[1] else None
+        if dw is None and ctx.needs_input_grad[1]:
+            dw = _wgrad(dyc, x, w, stride, padding)
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
                 dres, None, None, None, None, None, None, None, None, None)
 

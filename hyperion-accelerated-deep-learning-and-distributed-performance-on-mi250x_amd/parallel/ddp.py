@@ -40,6 +40,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops import streams as _streams
 from ..utils.nvtx import range_push, range_pop
 from .comm import get_comm
 
@@ -193,7 +194,16 @@ class DistributedDataParallel(nn.Module):
         g = p.grad
         if g.data_ptr() != slot.data_ptr():  # else AccumulateGrad already summed into the slot
             with torch.no_grad():
-                slot.copy_(g)  # pack (+ up-convert into an fp32 bucket); the all-reduce averages
+                if g.is_cuda and _streams.pending(g.device):
+                    # the gradient may still be in flight on the weight-gradient side stream: pack
+                    # it there (the bucket's all-reduce joins that stream first)
+                    side = _streams.side_stream(g.device)
+                    side.wait_stream(torch.cuda.current_stream(g.device))  # g may be a main-stream result
+                    with torch.cuda.stream(side):
+                        slot.copy_(g)
+                    g.record_stream(side)
+                else:
+                    slot.copy_(g)  # pack (+ up-convert into an fp32 bucket); the all-reduce averages
         if slot.dtype != p.dtype:
             p.grad = None  # consumed: the optimizer reads p.main_grad; the next backward steals
         b.got[i] = True
@@ -206,6 +216,8 @@ class DistributedDataParallel(nn.Module):
             b = self._buckets[self._next_launch]
             if b.ready < len(b.params):
                 break
+            if b.buf.is_cuda:
+                _streams.join(b.buf.device)  # packs issued on the weight-gradient side stream
             range_push(f"ddp_allreduce_b{b.index}")
             b.work = self.comm.all_reduce(b.buf, "avg")
             range_pop()
@@ -258,6 +270,8 @@ class DistributedDataParallel(nn.Module):
         must pass the same ``indices`` in the same order."""
         if not self._buckets or not self._sync:
             return []
+        if self._buckets[0].buf.is_cuda:
+            _streams.join(self._buckets[0].buf.device)
         works = []
         for b in self._buckets if indices is None else [self._buckets[i] for i in indices]:
             range_push(f"ddp_allreduce_b{b.index}")

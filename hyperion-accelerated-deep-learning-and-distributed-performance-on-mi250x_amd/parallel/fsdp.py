@@ -46,6 +46,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops import streams as _streams
 from ..ops.optim import clip_grad_norm_
 from .comm import get_comm
 
@@ -194,6 +195,8 @@ class _FlatGroup:
             return False
         buf = self._grad_buf()
         o, n = self.offsets[i], self.numels[i]
+        if p.grad.is_cuda:
+            _streams.join(p.grad.device)  # produced on the weight-gradient side stream
         with torch.no_grad():
             buf[o : o + n].copy_(p.grad.reshape(-1))
         p.grad = None

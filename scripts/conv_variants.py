@@ -18,6 +18,7 @@ from hyperion.ops import _native  # noqa: E402
 C_ = _native.native()
 what = (sys.argv[1] if len(sys.argv) > 1 else "fwd,dgrad,wgrad").split(",")
 quick = "--quick" in sys.argv
+stages = "--stages" in sys.argv  # automatic plan at LDS ring depths 2, 3, 4
 
 
 def gtime(fn, n=20, reps=10):
@@ -51,7 +52,19 @@ for sh in resnet50_convs(32):
     dy = torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     gf = 2.0 * N * P * P * K * C * R * R / 1e9
     r = dict(sh, P=P, gflop=gf)
-    tiles = [(0, 0, -1)] + ([] if quick else [(64, 64, 1), (128, 64, 1), (128, 128, 1), (64, 64, -1), (128, 64, -1)])
+    tiles = [(0, 0, -1)] + ([] if quick or stages else [(64, 64, 1), (128, 64, 1), (128, 128, 1), (64, 64, -1),
+                                                         (128, 64, -1)])
+    if stages:
+        for nb in (2, 3, 4):
+            C_.conv_set_stages(nb, nb)
+            r[f"fwd_nb{nb}"] = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True))
+            if s == 1 and K % 64 == 0:
+                r[f"dgrad_nb{nb}"] = gtime(lambda: C_.conv_dgrad(dy, w, p, p))
+            r[f"wgrad_nb{nb}"] = gtime(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p))
+        C_.conv_set_stages(0, 0)
+        rows.append(r)
+        print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
+        continue
     if "fwd" in what:
         for bm, bn, sp in tiles:
             r[f"fwd_{bm}x{bn}_s{sp}"] = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp))
