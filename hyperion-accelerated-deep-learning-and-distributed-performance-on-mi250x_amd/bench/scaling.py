@@ -23,7 +23,7 @@ import time
 from collections import defaultdict
 from typing import Dict, List, Optional, Sequence
 
-KINDS = ("language_ddp", "language_fsdp", "cifar", "llama")
+KINDS = ("language_ddp", "language_fsdp", "gpt2_fsdp", "cifar", "llama")
 
 
 def classify(filename: str) -> Optional[str]:

@@ -1,7 +1,7 @@
 """Launcher CLI, flag-compatible with the reference's ``run_distributed.py``.
 
     torchrun --standalone --nproc-per-node N -m hyperion.cli.run_distributed \
-        --model {language_ddp,cifar,language_fsdp,llama,all,scaling} --epochs 5 --base_dir . \
+        --model {language_ddp,cifar,language_fsdp,gpt2_fsdp,llama,all,scaling} --epochs 5 --base_dir . \
         [--hf_token T] [--model_id ID] [--lora] [--batch_size 1] [--progress_every 50] [--scaling_gpus 1,2,4,8]
 
 Reference behaviour (``run_distributed.py:38-149``): reads RANK/WORLD_SIZE/LOCAL_RANK from the env,
@@ -22,13 +22,15 @@ import sys
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(description="Hyperion-MI355X distributed training launcher")
     ap.add_argument("--model", default="language_ddp",
-                    choices=["language_ddp", "cifar", "language_fsdp", "llama", "all", "scaling"])
+                    choices=["language_ddp", "cifar", "language_fsdp", "gpt2_fsdp", "llama", "all", "scaling"],
+                    help="gpt2_fsdp: GPT-2-small causal LM, FSDP with per-layer units (BASELINE config 4)")
     ap.add_argument("--epochs", type=int, default=5)
     ap.add_argument("--base_dir", default=os.getcwd())
     ap.add_argument("--hf_token", default=None)
     ap.add_argument("--model_id", default="NousResearch/Llama-2-7b-hf")
     ap.add_argument("--lora", action="store_true")
     ap.add_argument("--batch_size", type=int, default=1, help="Llama per-rank batch (reference default 1)")
+    ap.add_argument("--lm_batch_size", type=int, default=None, help="gpt2_fsdp per-rank batch (default 32)")
     ap.add_argument("--progress_every", type=int, default=50)
     ap.add_argument("--scaling_gpus", default="1,2,4,8")
     # hyperion extensions
@@ -39,7 +41,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--kernels", default=None, choices=["hyperion", "torch"])
     ap.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch")
     ap.add_argument("--dataset_size", type=int, default=None)
-    ap.add_argument("--resume", default=None)
+    ap.add_argument("--resume", default=None, help="checkpoint path, or 'auto' = this run kind's latest checkpoint")
+    ap.add_argument("--ckpt_every", type=int, default=None, help="write the latest checkpoint every N steps")
+    ap.add_argument("--max_restarts", type=int, default=0,
+                    help="single process: re-run a failed trainer up to N times with --resume auto (multi-process: "
+                         "use torchrun --max-restarts N together with --resume auto)")
     ap.add_argument("--ckpt_mode", default="full", choices=["full", "sharded"])
     ap.add_argument("--lora_parallel", default="fsdp", choices=["fsdp", "ddp"])
     ap.add_argument("--seed", type=int, default=0)
@@ -66,8 +72,7 @@ def main(argv=None) -> int:
     if args.hf_token:
         os.environ.setdefault("HF_TOKEN", args.hf_token)  # accepted; nothing is downloaded
     from hyperion.bench.scaling import create_scaling_report, run_scaling_experiment
-    from hyperion.train.distributed import (RunOptions, train_cifar_model_ddp, train_language_model_ddp,
-                                            train_language_model_fsdp, train_llama_fsdp)
+    from hyperion.train.distributed import RunOptions
 
     env = _env()
     if args.model == "scaling":
@@ -88,22 +93,42 @@ def main(argv=None) -> int:
     rank, world, _local = env
     opts = RunOptions(synthetic=args.synthetic, dataset_size=args.dataset_size, max_steps_per_epoch=args.max_steps,
                       precision=args.precision, seed=args.seed, save=not args.no_save, ckpt_mode=args.ckpt_mode,
-                      resume=args.resume, causal=args.causal)
+                      resume=args.resume, causal=args.causal, ckpt_every=args.ckpt_every)
     todo = ["language_ddp", "cifar", "language_fsdp", "llama"] if args.model == "all" else [args.model]
     for m in todo:
-        if m == "language_ddp":
-            train_language_model_ddp(rank, world, args.epochs, args.base_dir, opts)
-        elif m == "cifar":
-            train_cifar_model_ddp(rank, world, args.epochs, args.base_dir, opts)
-        elif m == "language_fsdp":
-            train_language_model_fsdp(rank, world, args.epochs, args.base_dir, opts)
-        elif m == "llama":
-            train_llama_fsdp(rank, world, epochs=args.epochs, base_dir=args.base_dir, hf_token=args.hf_token,
-                             model_id=args.model_id, lora=args.lora, batch_size=args.batch_size,
-                             progress_every=args.progress_every, opts=opts, lora_parallel=args.lora_parallel)
+        attempt = 0
+        while True:
+            try:
+                _run_one(m, rank, world, args, opts)
+                break
+            except Exception as e:  # noqa: BLE001 - restart policy
+                if world > 1 or attempt >= args.max_restarts:
+                    raise
+                attempt += 1
+                print(f"[run_distributed] {m} failed ({e!r}); restart {attempt}/{args.max_restarts} from the latest "
+                      "checkpoint", file=sys.stderr, flush=True)
+                opts.resume = "auto"
     if rank == 0:
         create_scaling_report(os.path.join(args.base_dir, "data", "distributed"))
     return 0
+
+
+def _run_one(m: str, rank: int, world: int, args, opts) -> None:
+    from hyperion.train.distributed import (train_cifar_model_ddp, train_gpt2_fsdp, train_language_model_ddp,
+                                            train_language_model_fsdp, train_llama_fsdp)
+
+    if m == "language_ddp":
+        train_language_model_ddp(rank, world, args.epochs, args.base_dir, opts)
+    elif m == "cifar":
+        train_cifar_model_ddp(rank, world, args.epochs, args.base_dir, opts)
+    elif m == "language_fsdp":
+        train_language_model_fsdp(rank, world, args.epochs, args.base_dir, opts)
+    elif m == "gpt2_fsdp":
+        train_gpt2_fsdp(rank, world, args.epochs, args.base_dir, opts, batch_size=args.lm_batch_size or 32)
+    elif m == "llama":
+        train_llama_fsdp(rank, world, epochs=args.epochs, base_dir=args.base_dir, hf_token=args.hf_token,
+                         model_id=args.model_id, lora=args.lora, batch_size=args.batch_size,
+                         progress_every=args.progress_every, opts=opts, lora_parallel=args.lora_parallel)
 
 
 if __name__ == "__main__":

@@ -113,6 +113,6 @@ def simple_lm_768(vocab_size: int = GPT2_VOCAB, **kw) -> SimpleTransformerLM:
 
 def gpt2_small_lm(vocab_size: int = GPT2_VOCAB, **kw) -> SimpleTransformerLM:
     """GPT-2-small-shaped encoder LM (12 × 768, 12 heads, ff 3072, GELU, causal) for the FSDP config."""
-    kw.setdefault("causal", True)
-    kw.setdefault("dropout", 0.1)
-    return SimpleTransformerLM(vocab_size, emb_dim=768, n_heads=12, n_layers=12, ff_dim=3072, activation="gelu", **kw)
+    cfg = dict(emb_dim=768, n_heads=12, n_layers=12, ff_dim=3072, activation="gelu", causal=True, dropout=0.1)
+    cfg.update(kw)
+    return SimpleTransformerLM(vocab_size, **cfg)

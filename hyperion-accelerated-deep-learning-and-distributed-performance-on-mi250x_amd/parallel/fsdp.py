@@ -133,9 +133,17 @@ class _FlatGroup:
         self._grad_bytes = self.full_grad.untyped_storage().nbytes() if trainable else 0
         self.gathered = True
         self.gather_work = None
-        self._send = None
+        # persistent all-gather source in the compute dtype: cast ONCE per optimizer step (the
+        # forward gather), reused by the backward re-gather; None when the shard already has it
+        self._send_buf = (torch.empty(self.shard_numel, dtype=self.cdtype, device=dev)
+                          if self.flat_param.dtype != self.cdtype else None)
+        self.send_valid = False
         self.rs_work = None
         self.rs_out: Optional[torch.Tensor] = None
+        # persistent reduce-scatter output / fp32 shard gradient (no per-step allocation or .to())
+        self._rs_buf = (torch.empty(self.shard_numel, dtype=self.rdtype, device=dev)
+                        if trainable and self.rdtype != torch.float32 else None)
+        self._grad_shard = torch.empty(self.shard_numel, dtype=torch.float32, device=dev) if trainable else None
         self.grad_ready: Set[int] = set()
         self.reduced = False
         # module parameters become views of the full buffer (the same Parameter objects)
@@ -159,13 +167,19 @@ class _FlatGroup:
         st = self.full.untyped_storage()
         if st.nbytes() != self._full_bytes:
             st.resize_(self._full_bytes)
-        send = self.flat_param.detach().to(self.cdtype)
+        if self._send_buf is None:
+            send = self.flat_param.detach()
+        else:
+            if not self.send_valid:  # params changed since the last cast (an optimizer step)
+                with torch.no_grad():
+                    self._send_buf.copy_(self.flat_param.detach())
+                self.send_valid = True
+            send = self._send_buf
         out = self.full.data  # fresh version counter: autograd's saved views stay valid
         if self.fsdp.world == 1:
             out.copy_(send)
             self.gathered = True
             return
-        self._send = send
         self.gather_work = self.fsdp.comm.all_gather(out, send)
         if not async_op:
             self.wait_gather()
@@ -174,7 +188,6 @@ class _FlatGroup:
         if self.gather_work is not None:
             self.gather_work.wait()
             self.gather_work = None
-            self._send = None
             self.gathered = True
 
     # -- gradients ------------------------------------------------------------------------
@@ -211,13 +224,16 @@ class _FlatGroup:
         for i, (o, n) in enumerate(zip(self.offsets, self.numels)):
             if i not in self.grad_ready:  # unused this step: contributes zeros
                 buf[o : o + n].zero_()
-        W = self.fsdp.world
-        buf.mul_(1.0 / W)  # AVG semantics; pre-divided so a bf16 sum cannot overflow
-        if W == 1:
+        if self.fsdp.world == 1:
             self.rs_out, self.rs_work = buf, None
+            return
+        # AVG in RCCL; the output lands in a persistent buffer — straight in the fp32 shard
+        # gradient when the reduction runs in fp32 and nothing is being accumulated
+        if self._rs_buf is None and self.flat_param.grad is None:
+            self.rs_out = self._grad_shard
         else:
-            self.rs_out = torch.empty(self.shard_numel, dtype=self.rdtype, device=buf.device)
-            self.rs_work = self.fsdp.comm.reduce_scatter(self.rs_out, buf, "sum")
+            self.rs_out = self._rs_buf if self._rs_buf is not None else torch.empty_like(self._grad_shard)
+        self.rs_work = self.fsdp.comm.reduce_scatter(self.rs_out, buf, "avg")
 
     def finish_reduce(self) -> None:
         if not self.reduced:
@@ -225,11 +241,16 @@ class _FlatGroup:
         if self.rs_work is not None:
             self.rs_work.wait()
             self.rs_work = None
-        g = self.rs_out.to(torch.float32)
-        if self.flat_param.grad is None:
-            self.flat_param.grad = g if g.data_ptr() != self.full_grad.data_ptr() else g.clone()
-        else:
-            self.flat_param.grad.add_(g)
+        g = self.rs_out
+        if self.fsdp.world == 1:  # rs_out is the full flat gradient buffer (released below)
+            g = g[: self.shard_numel]
+        with torch.no_grad():
+            if self.flat_param.grad is None:
+                if g.data_ptr() != self._grad_shard.data_ptr():
+                    self._grad_shard.copy_(g)  # (+ bf16 -> fp32)
+                self.flat_param.grad = self._grad_shard
+            else:
+                self.flat_param.grad.add_(g)
         self.rs_out = None
         self.full_grad.untyped_storage().resize_(0)
 
@@ -450,7 +471,14 @@ class FullyShardedDataParallel(nn.Module):
     def _post_backward(self) -> None:
         for u in self.units:
             u.finish()
+            for g in u.groups:
+                g.send_valid = False  # the optimizer steps next: recast on the next forward gather
         self._in_backward = False
+
+    def invalidate_gather_cache(self) -> None:
+        """Call after changing the flat shards outside an optimizer step that follows backward."""
+        for g in self.flat_groups():
+            g.send_valid = False
 
     # -- forward ----------------------------------------------------------------------------
     def _root_pre(self) -> None:
@@ -530,6 +558,7 @@ class FullyShardedDataParallel(nn.Module):
             for p, o, n in zip(g.params, g.offsets, g.numels):
                 flat[o : o + n].copy_(sd[names[id(p)]].reshape(-1).to(self.device, flat.dtype))
             g.flat_param.data.copy_(flat[self.rank * g.shard_numel : (self.rank + 1) * g.shard_numel])
+        self.invalidate_gather_cache()
         for n, t in self.module.state_dict(keep_vars=True).items():
             if id(t) not in self._unit_of_param and n in sd:
                 t.data.copy_(sd[n].to(t.device, t.dtype))
@@ -556,6 +585,7 @@ class FullyShardedDataParallel(nn.Module):
             raise ValueError(f"sharded checkpoint has world_size {sd['world_size']}, running with {self.world}")
         for g, t in zip(self.flat_groups(), sd["flat_params"]):
             g.flat_param.data.copy_(t.to(self.device))
+        self.invalidate_gather_cache()
         bufs = dict(self.module.named_buffers())
         for n, t in sd.get("buffers", {}).items():
             if n in bufs:

@@ -34,6 +34,13 @@ def _rank() -> int:
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
+def _save_atomic(doc, path: str) -> None:
+    """Write to a temporary name and rename: a crash mid-save never leaves a truncated latest file."""
+    tmp = f"{path}.tmp{os.getpid()}"
+    torch.save(doc, tmp)
+    os.replace(tmp, path)
+
+
 def save_checkpoint(path: str, model: nn.Module, optimizer: Optional[torch.optim.Optimizer] = None, scaler=None,
                     epoch: int = 0, step: int = 0, mode: str = "full", extra: Optional[Dict[str, Any]] = None) -> Optional[str]:
     """Write a checkpoint; returns the path written on this rank (None on non-writing ranks)."""
@@ -53,19 +60,19 @@ def save_checkpoint(path: str, model: nn.Module, optimizer: Optional[torch.optim
                 doc["optimizer_state_dict"] = optimizer.state_dict()
             if scaler is not None:
                 doc["scaler_state_dict"] = scaler.state_dict()
-            torch.save(doc, p)
+            _save_atomic(doc, p)
             return p
         sd = model.full_state_dict(rank0_only=True, offload_to_cpu=True)  # collective on all ranks
         # optimizer state of flat shards is per-rank: store alongside the full model per rank
         if optimizer is not None:
-            torch.save({"optimizer_state_dict": optimizer.state_dict(), **meta},
-                       path.replace(".pt", f"_optim_rank{rank}.pt"))
+            _save_atomic({"optimizer_state_dict": optimizer.state_dict(), **meta},
+                         path.replace(".pt", f"_optim_rank{rank}.pt"))
         if rank != 0:
             return None
         doc = {"model_state_dict": sd, **meta}
         if scaler is not None:
             doc["scaler_state_dict"] = scaler.state_dict()
-        torch.save(doc, path)
+        _save_atomic(doc, path)
         return path
     if rank != 0:
         return None
@@ -74,8 +81,23 @@ def save_checkpoint(path: str, model: nn.Module, optimizer: Optional[torch.optim
         doc["optimizer_state_dict"] = optimizer.state_dict()
     if scaler is not None:
         doc["scaler_state_dict"] = scaler.state_dict()
-    torch.save(doc, path)
+    _save_atomic(doc, path)
     return path
+
+
+def rng_state() -> Dict[str, torch.Tensor]:
+    """CPU (+ current GPU) generator states, for bit-exact resume of dropout streams."""
+    st = {"rng_cpu": torch.get_rng_state()}
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        st["rng_cuda"] = torch.cuda.get_rng_state()
+    return st
+
+
+def restore_rng(meta: Dict[str, Any]) -> None:
+    if isinstance(meta.get("rng_cpu"), torch.Tensor):
+        torch.set_rng_state(meta["rng_cpu"])
+    if isinstance(meta.get("rng_cuda"), torch.Tensor) and torch.cuda.is_available():
+        torch.cuda.set_rng_state(meta["rng_cuda"])
 
 
 def load_checkpoint(path: str, model: nn.Module, optimizer: Optional[torch.optim.Optimizer] = None, scaler=None,

@@ -39,7 +39,7 @@ from ..parallel.launch import cleanup, setup
 from ..utils.fault import maybe_inject
 from ..utils.seed import seed_everything
 from .amp import LossScaler
-from .checkpoint import load_checkpoint, save_checkpoint
+from .checkpoint import load_checkpoint, restore_rng, rng_state, save_checkpoint
 from .metrics import SCHEMAS, MetricsCSV, make_run_id, write_manifest
 
 DEFAULT_BASE_DIR = os.environ.get("HYPERION_BASE_DIR", os.getcwd())
@@ -56,7 +56,8 @@ class RunOptions:
     seed: int = 0
     save: bool = True
     ckpt_mode: str = "full"                 # full | sharded (FSDP)
-    resume: Optional[str] = None
+    resume: Optional[str] = None            # checkpoint path, or "auto" = this run kind's latest checkpoint
+    ckpt_every: Optional[int] = None        # also write the latest checkpoint every N steps (restartable)
     num_workers: int = 2
     causal: bool = False                    # reference LM had no causal mask
     timeout_s: float = 600.0
@@ -105,6 +106,12 @@ class _EpochRunner:
         self.clip, self.sharded_clip = clip, sharded_clip
         self.opts = opts
         self.global_step = 0
+        self.save_latest: Optional[Callable[[int, int], None]] = None  # (epoch, batches done in it)
+
+    def after_step(self, epoch: int, done_in_epoch: int) -> None:
+        """Periodic latest checkpoint (``RunOptions.ckpt_every``): collective for FSDP, every rank calls."""
+        if self.save_latest is not None and self.opts.ckpt_every and self.global_step % self.opts.ckpt_every == 0:
+            self.save_latest(epoch, done_in_epoch)
 
     def step(self, loss_fn) -> torch.Tensor:
         self.opt.zero_grad(set_to_none=True)
@@ -149,9 +156,7 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
     opts = opts or RunOptions()
     device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
     seed_everything(opts.seed, 0)  # identical init on every rank (DDP also broadcasts)
-    run_id = make_run_id("language_ddp", world)
     out = _out_dir(base_dir)
-    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["language_ddp"], enabled=rank == 0)
     ds = _wikitext(opts, base_dir)
     sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
     model = simple_lm_256(GPT2_VOCAB, causal=opts.causal).to(device)
@@ -161,9 +166,14 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
     scaler = LossScaler(enabled=precision == "fp16", device=device)
     runner = _EpochRunner(rank, world, device, model, opt, scaler, _amp(precision), None, False, opts)
     inner = model.module if hasattr(model, "module") else model
-    start_epoch = _maybe_resume(opts, model, opt, scaler)
+    res = _maybe_resume(opts, model, opt, scaler, out, "language_ddp")
+    run_id = res.run_id or make_run_id("language_ddp", world)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["language_ddp"], enabled=rank == 0,
+                     append=res.run_id is not None)
+    runner.global_step = res.global_step
+    _latest_saver(opts, out, "language_ddp", run_id, model, opt, scaler, runner)
     history = []
-    for ep in range(start_epoch, epochs):
+    for ep in range(res.start_epoch, epochs):
         sampler.set_epoch(ep)
         _sync(device)
         t0 = time.time()
@@ -172,6 +182,8 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
         for i, (ids, _mask) in enumerate(loader):
             if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
                 break
+            if res.skip_batch(ep, i):
+                continue  # done before the checkpoint this run resumed from
             x, y = ids[:, :-1], ids[:, 1:]
             ddp_fwd = model if world > 1 else None
 
@@ -183,11 +195,14 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
             loss, _ = runner.step(lm_loss)
             loss_sum += loss
             n += 1
+            runner.after_step(ep, i + 1)
         avg = _reduce_mean(loss_sum / max(n, 1), world).item()
         _sync(device)
         dur = time.time() - t0
         csv.append(epoch=ep + 1, loss=round(avg, 6), duration=round(dur, 4), gpus=world)
         history.append({"epoch": ep + 1, "loss": avg, "duration": dur, "steps": n})
+        if runner.save_latest is not None:
+            runner.save_latest(ep + 1, 0)
         if rank == 0:
             opts.log(f"[language_ddp] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s ({n} steps)")
     ck = _finish(opts, out, run_id, model, opt, scaler, epochs, runner.global_step)
@@ -208,9 +223,7 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
     opts = opts or RunOptions()
     device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
     seed_everything(opts.seed, 0)
-    run_id = make_run_id("cifar_ddp", world)
     out = _out_dir(base_dir)
-    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["cifar"], enabled=rank == 0)
     if opts.synthetic:
         ds = SyntheticCIFAR10(seed=opts.seed, **({} if opts.dataset_size is None else {"n": opts.dataset_size}))
     else:
@@ -224,9 +237,14 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
     opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01, adamw=True)
     scaler = LossScaler(enabled=precision == "fp16", device=device)
     runner = _EpochRunner(rank, world, device, model, opt, scaler, _amp(precision), None, False, opts)
-    start_epoch = _maybe_resume(opts, model, opt, scaler)
+    res = _maybe_resume(opts, model, opt, scaler, out, "cifar_ddp")
+    run_id = res.run_id or make_run_id("cifar_ddp", world)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["cifar"], enabled=rank == 0,
+                     append=res.run_id is not None)
+    runner.global_step = res.global_step
+    _latest_saver(opts, out, "cifar_ddp", run_id, model, opt, scaler, runner)
     history = []
-    for ep in range(start_epoch, epochs):
+    for ep in range(res.start_epoch, epochs):
         sampler.set_epoch(ep)
         _sync(device)
         t0 = time.time()
@@ -236,6 +254,8 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
         for i, (img, lbl) in enumerate(loader):
             if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
                 break
+            if res.skip_batch(ep, i):
+                continue
             if device.type == "cuda":
                 img = img.contiguous(memory_format=torch.channels_last)
 
@@ -248,6 +268,7 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
             stats[1] += (logits.argmax(1) == lbl).sum()
             stats[2] += lbl.numel()
             n += 1
+            runner.after_step(ep, i + 1)
         if world > 1:
             dist.all_reduce(stats)
         loss_avg = (stats[0] / max(n, 1) / world).item()
@@ -256,6 +277,8 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
         dur = time.time() - t0
         csv.append(epoch=ep + 1, loss=round(loss_avg, 6), accuracy=round(acc, 4), duration=round(dur, 4), gpus=world)
         history.append({"epoch": ep + 1, "loss": loss_avg, "accuracy": acc, "duration": dur, "steps": n})
+        if runner.save_latest is not None:
+            runner.save_latest(ep + 1, 0)
         if rank == 0:
             opts.log(f"[cifar] epoch {ep + 1}/{epochs} loss {loss_avg:.4f} acc {acc:.2f}% {dur:.2f}s")
     ck = _finish(opts, out, run_id, model, opt, scaler, epochs, runner.global_step)
@@ -268,28 +291,37 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
 # ---------------------------------------------------------------------------------------- LM FSDP
 def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
                               opts: Optional[RunOptions] = None, batch_size: int = 32,
-                              model_fn: Optional[Callable[[], nn.Module]] = None, min_num_params: int = 100_000) -> Dict:
-    """C25: the LM under FSDP FULL_SHARD, size-based wrap, bf16 mixed precision, global clip 1.0."""
-    from ..parallel.fsdp import FSDP, MixedPrecision, size_based_auto_wrap_policy
+                              model_fn: Optional[Callable[[], nn.Module]] = None, min_num_params: int = 100_000,
+                              wrap: str = "size", run_name: str = "language_fsdp") -> Dict:
+    """C25: the LM under FSDP FULL_SHARD, size-based wrap, bf16 mixed precision, global clip 1.0.
+
+    ``model_fn`` / ``wrap='layer'`` / ``run_name``: the same trainer for other LMs — e.g.
+    :func:`train_gpt2_fsdp` (BASELINE.json config 4) wraps one FSDP unit per transformer layer."""
+    from ..models.transformer import TransformerEncoderLayer
+    from ..parallel.fsdp import FSDP, MixedPrecision, size_based_auto_wrap_policy, transformer_auto_wrap_policy
 
     opts = opts or RunOptions()
     device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
     seed_everything(opts.seed, 0)
-    run_id = make_run_id("language_fsdp", world)
     out = _out_dir(base_dir)
-    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["language_fsdp"], enabled=rank == 0)
     ds = _wikitext(opts, base_dir)
     sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
     base = (model_fn or (lambda: simple_lm_256(GPT2_VOCAB, causal=opts.causal)))()
     precision = opts.precision or ("bf16" if device.type == "cuda" else "fp32")
     pdt = _amp(precision)
-    model = FSDP(base, auto_wrap_policy=size_based_auto_wrap_policy(min_num_params), device_id=device,
-                 mixed_precision=MixedPrecision(pdt, pdt, pdt))
+    policy = (transformer_auto_wrap_policy({TransformerEncoderLayer}) if wrap == "layer"
+              else size_based_auto_wrap_policy(min_num_params))
+    model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt))
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, True, opts)
-    start_epoch = _maybe_resume(opts, model, opt, None)
+    res = _maybe_resume(opts, model, opt, None, out, run_name)
+    run_id = res.run_id or make_run_id(run_name, world)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS.get(run_name, SCHEMAS["language_fsdp"]),
+                     enabled=rank == 0, append=res.run_id is not None)
+    runner.global_step = res.global_step
+    _latest_saver(opts, out, run_name, run_id, model, opt, None, runner)
     history = []
-    for ep in range(start_epoch, epochs):
+    for ep in range(res.start_epoch, epochs):
         sampler.set_epoch(ep)
         _sync(device)
         t0 = time.time()
@@ -298,17 +330,22 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
         for i, (ids, _mask) in enumerate(loader):
             if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
                 break
+            if res.skip_batch(ep, i):
+                continue
             x, y = ids[:, :-1], ids[:, 1:]
             loss, _ = runner.step(lambda: (model.forward_loss(x, y, ignore_index=GPT2_PAD), None))
             loss_sum += loss
             n += 1
+            runner.after_step(ep, i + 1)
         avg = _reduce_mean(loss_sum / max(n, 1), world).item()
         _sync(device)
         dur = time.time() - t0
         csv.append(epoch=ep + 1, loss=round(avg, 6), duration=round(dur, 4), gpus=world)
         history.append({"epoch": ep + 1, "loss": avg, "duration": dur, "steps": n})
+        if runner.save_latest is not None:
+            runner.save_latest(ep + 1, 0)
         if rank == 0:
-            opts.log(f"[language_fsdp] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s")
+            opts.log(f"[{run_name}] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s")
     if world > 1:
         dist.barrier()
     ck = _finish(opts, out, run_id, model, opt, None, epochs, runner.global_step)
@@ -316,6 +353,19 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
     if world > 1:
         cleanup()
     return {"run_id": run_id, "history": history, "checkpoint": ck}
+
+
+def train_gpt2_fsdp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
+                    opts: Optional[RunOptions] = None, batch_size: int = 32) -> Dict:
+    """BASELINE.json config 4: GPT-2-small-shaped causal LM (12 x 768, 12 heads, ff 3072, GELU,
+    124M parameters with the tied-size head) under FSDP FULL_SHARD with one unit per transformer
+    layer, bf16 mixed precision, global clip 1.0, on WikiText-2-shaped data (128 tokens).  The
+    reference's FSDP run used the 2-layer 256-d LM (``distributed_utils.py:290-406``); this is the
+    same trainer (:func:`train_language_model_fsdp`) on the larger model."""
+    from ..models.simple_lm import gpt2_small_lm
+
+    return train_language_model_fsdp(rank, world, epochs, base_dir, opts, batch_size,
+                                     model_fn=lambda: gpt2_small_lm(GPT2_VOCAB), wrap="layer", run_name="gpt2_fsdp")
 
 
 # ---------------------------------------------------------------------------------------- Llama
@@ -340,9 +390,7 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
     opts = opts or RunOptions()
     device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
     seed_everything(opts.seed, 0)
-    run_id = make_run_id("llama", world)
     out = _out_dir(base_dir)
-    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["llama"], enabled=rank == 0)
     cfg = config or LlamaConfig.llama2_7b()
     ds = _wikitext(opts, base_dir)
     sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
@@ -363,9 +411,14 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
         model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt))
     opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, isinstance(model, FSDP), opts)
-    start_epoch = _maybe_resume(opts, model, opt, None)
+    res = _maybe_resume(opts, model, opt, None, out, "llama")
+    run_id = res.run_id or make_run_id("llama", world)
+    csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["llama"], enabled=rank == 0,
+                     append=res.run_id is not None)
+    runner.global_step = res.global_step
+    _latest_saver(opts, out, "llama", run_id, model, opt, None, runner)
     history = []
-    for ep in range(start_epoch, epochs):
+    for ep in range(res.start_epoch, epochs):
         sampler.set_epoch(ep)
         _sync(device)
         t0 = time.time()
@@ -374,6 +427,8 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
         for i, (ids, msk) in enumerate(loader):
             if opts.max_steps_per_epoch is not None and i >= opts.max_steps_per_epoch:
                 break
+            if res.skip_batch(ep, i):
+                continue
             ids = ids % cfg.vocab_size  # GPT-2-tokenized synthetic ids folded into the Llama vocab
             labels = ids.masked_fill(msk == 0, -100) if mask_pad_labels else ids.clone()
 
@@ -383,6 +438,7 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
             loss, _ = runner.step(llama_loss)
             loss_sum += loss
             n += 1
+            runner.after_step(ep, i + 1)
             if rank == 0 and progress_every and n % progress_every == 0:
                 opts.log(f"[llama] epoch {ep + 1} step {n} loss {loss.item():.4f}")
         avg = _reduce_mean(loss_sum / max(n, 1), world).item()
@@ -390,6 +446,8 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
         dur = time.time() - t0
         csv.append(epoch=ep + 1, loss=round(avg, 6), duration_s=round(dur, 4), gpus=world, mode=mode)
         history.append({"epoch": ep + 1, "loss": avg, "duration_s": dur, "steps": n, "mode": mode})
+        if runner.save_latest is not None:
+            runner.save_latest(ep + 1, 0)
         if rank == 0:
             opts.log(f"[llama] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s mode {mode}")
     ck = None
@@ -438,11 +496,61 @@ def _single_device() -> torch.device:
     return d
 
 
-def _maybe_resume(opts: RunOptions, model, opt, scaler) -> int:
-    if not opts.resume:
-        return 0
-    meta = load_checkpoint(opts.resume, model, opt, scaler)
-    return int(meta.get("epoch", 0))
+@dataclass
+class _Resume:
+    """Where a resumed run picks up: epoch (completed epochs), batches already done in it."""
+
+    start_epoch: int = 0
+    skip: int = 0
+    run_id: Optional[str] = None
+    global_step: int = 0
+    rng: Optional[Dict] = None
+
+    def skip_batch(self, epoch: int, i: int) -> bool:
+        """True for batches done before the checkpoint.  The generator states are restored at the
+        first batch that runs: creating the epoch's DataLoader iterator draws from the global
+        generator, so restoring earlier would shift every later dropout mask."""
+        if epoch != self.start_epoch:
+            return False
+        if i < self.skip:
+            return True
+        if self.rng is not None:
+            restore_rng(self.rng)
+            self.rng = None
+        return False
+
+
+def _latest_path(out: str, run_name: str) -> str:
+    return os.path.join(out, f"{run_name}_latest.pt")
+
+
+def _maybe_resume(opts: RunOptions, model, opt, scaler, out: Optional[str] = None,
+                  run_name: Optional[str] = None) -> _Resume:
+    """Restore from ``opts.resume`` (a path, or ``"auto"`` = the latest checkpoint of this run kind
+    in ``out`` if one exists): model / optimizer / scaler / RNG state and the position in the data
+    stream, so an interrupted run continues bit-for-bit where its last checkpoint was taken."""
+    path = opts.resume
+    if path == "auto":
+        path = _latest_path(out, run_name) if out and run_name else None
+        if path is None or not os.path.exists(path):
+            return _Resume()
+    if not path:
+        return _Resume()
+    meta = load_checkpoint(path, model, opt, scaler)
+    rng = {k: v for k, v in meta.items() if k.startswith("rng_")} or None
+    return _Resume(int(meta.get("epoch", 0)), int(meta.get("step_in_epoch", 0)), meta.get("run_id"),
+                   int(meta.get("step", 0)), rng)
+
+
+def _latest_saver(opts: RunOptions, out: str, run_name: str, run_id: str, model, opt, scaler, runner) -> None:
+    if not opts.ckpt_every:
+        return
+
+    def save(epoch: int, done: int) -> None:
+        save_checkpoint(_latest_path(out, run_name), model, opt, scaler, epoch, runner.global_step,
+                        mode=opts.ckpt_mode, extra={"step_in_epoch": done, "run_id": run_id, **rng_state()})
+
+    runner.save_latest = save
 
 
 def _finish(opts: RunOptions, out: str, run_id: str, model, opt, scaler, epoch: int, step: int):

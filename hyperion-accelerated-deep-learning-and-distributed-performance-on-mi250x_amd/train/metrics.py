@@ -23,6 +23,7 @@ from typing import Dict, List, Optional
 SCHEMAS: Dict[str, List[str]] = {
     "language_ddp": ["epoch", "loss", "duration", "gpus"],
     "language_fsdp": ["epoch", "loss", "duration", "gpus"],
+    "gpt2_fsdp": ["epoch", "loss", "duration", "gpus"],
     "cifar": ["epoch", "loss", "accuracy", "duration", "gpus"],
     "llama": ["epoch", "loss", "duration_s", "gpus", "mode"],
 }
@@ -33,11 +34,12 @@ def make_run_id(model: str, world: int, when: Optional[float] = None) -> str:
 
 
 class MetricsCSV:
-    def __init__(self, path: str, columns: List[str], enabled: bool = True):
+    def __init__(self, path: str, columns: List[str], enabled: bool = True, append: bool = False):
+        """``append``: continue an existing file (a resumed run keeps its run_id and CSV)."""
         self.path = path
         self.columns = columns
         self.enabled = enabled
-        if enabled:
+        if enabled and not (append and os.path.exists(path)):
             os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
             with open(path, "w", newline="") as f:
                 csv.writer(f).writerow(columns)

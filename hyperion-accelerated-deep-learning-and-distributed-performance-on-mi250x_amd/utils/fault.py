@@ -6,6 +6,10 @@ the process-group timeout), ``nan`` (returns True so the caller poisons its loss
 :func:`maybe_inject` once per step; tests assert that the surviving ranks fail within the
 configured timeout instead of hanging (the reference disabled the watchdog:
 ``TORCH_NCCL_ASYNC_ERROR_HANDLING=0``, ``run_language_fsdp.sh:10``).
+
+``HYPERION_FAULT_MARKER=path`` makes the fault one-shot across restarts: it fires only while the
+marker file does not exist and creates it when it fires (restart + auto-resume tests: the resumed
+run replays the same step numbers and must not fail again).
 """
 from __future__ import annotations
 
@@ -33,6 +37,12 @@ def maybe_inject(rank: int, step: int, spec: Optional[str] = None) -> bool:
     f = parse(spec)
     if f is None or f[0] != rank or f[1] != step:
         return False
+    marker = os.environ.get("HYPERION_FAULT_MARKER")
+    if marker:
+        if os.path.exists(marker):
+            return False
+        with open(marker, "w") as fh:
+            fh.write(f"{rank}:{step}\n")
     kind = f[2]
     if kind == "exit":
         sys.stderr.write(f"[hyperion] injected fault: rank {rank} exits at step {step}\n")

@@ -92,3 +92,64 @@ def test_llama_full_fsdp_single_process(tmp_path):
     r = train_llama_fsdp(0, 1, epochs=1, base_dir=str(tmp_path), lora=False, batch_size=2, progress_every=0,
                          opts=_opts(), config=LlamaConfig.tiny())
     assert r["mode"] == "fsdp_fp32" and r["history"][0]["steps"] == 2
+
+
+def _final_params(base, **kw):
+    from hyperion.train.distributed import train_language_model_ddp
+
+    r = train_language_model_ddp(0, 1, epochs=2, base_dir=base, opts=_opts(**kw), batch_size=4)
+    ck = torch.load(r["checkpoint"], weights_only=True)
+    return r, ck
+
+
+def test_restart_auto_resume_replays_the_lost_steps_bit_exact(tmp_path, monkeypatch):
+    """Checkpoint every step; an injected failure at global step 3 kills the first run; a second
+    run with resume='auto' continues from the latest checkpoint (epoch 1, batch 1) and ends with
+    exactly the weights and optimizer state of an uninterrupted run (data position + RNG restored)."""
+    from hyperion.utils.fault import InjectedFault
+
+    ref_dir, run_dir = tmp_path / "ref", tmp_path / "run"
+    _, ref = _final_params(str(ref_dir), ckpt_every=1)
+    monkeypatch.setenv("HYPERION_FAULT", "0:3:raise")
+    monkeypatch.setenv("HYPERION_FAULT_MARKER", str(tmp_path / "fault.marker"))
+    import pytest
+
+    with pytest.raises(InjectedFault):
+        _final_params(str(run_dir), ckpt_every=1)
+    latest = torch.load(run_dir / "data" / "distributed" / "language_ddp_latest.pt", weights_only=True)
+    assert latest["step"] == 3 and latest["epoch"] == 1 and latest["step_in_epoch"] == 1
+    r, got = _final_params(str(run_dir), ckpt_every=1, resume="auto")  # marker set: no second fault
+    assert [h["steps"] for h in r["history"]] == [1]  # only the remaining step of epoch 2 re-ran
+    for k, v in ref["model_state_dict"].items():
+        assert torch.equal(v, got["model_state_dict"][k]), k
+    rows = list(csv.reader(open(run_dir / "data" / "distributed" / f"{r['run_id']}_metrics.csv")))
+    assert rows[0] == ["epoch", "loss", "duration", "gpus"] and [row[0] for row in rows[1:]] == ["1", "2"]
+
+
+def test_cli_max_restarts_recovers_single_process(tmp_path, monkeypatch):
+    from hyperion.cli.run_distributed import main
+
+    monkeypatch.setenv("HYPERION_FAULT", "0:2:raise")
+    monkeypatch.setenv("HYPERION_FAULT_MARKER", str(tmp_path / "m"))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    rc = main(["--model", "language_ddp", "--epochs", "2", "--max_steps", "2", "--dataset_size", "64", "--base_dir",
+               str(tmp_path), "--ckpt_every", "1", "--max_restarts", "1"])
+    assert rc == 0 and (tmp_path / "m").exists()
+    assert (tmp_path / "data" / "distributed" / "language_ddp_latest.pt").exists()
+
+
+def _gpt2_fsdp(rank, world, base):
+    from hyperion.train.distributed import train_language_model_fsdp
+    from hyperion.models.simple_lm import gpt2_small_lm
+
+    tiny = lambda: gpt2_small_lm(vocab_size=50257, emb_dim=32, n_heads=2, n_layers=2, ff_dim=64)  # noqa: E731
+    return train_language_model_fsdp(rank, world, epochs=1, base_dir=base, opts=_opts(), batch_size=4, model_fn=tiny,
+                                     wrap="layer", run_name="gpt2_fsdp")
+
+
+def test_gpt2_fsdp_layer_units_world2(tmp_path):
+    res = run_world(_gpt2_fsdp, 2, (str(tmp_path),))
+    assert res[0]["run_id"].startswith("gpt2_fsdp_2gpus_")
+    rows = list(csv.reader(open(tmp_path / "data" / "distributed" / f"{res[0]['run_id']}_metrics.csv")))
+    assert rows[0] == ["epoch", "loss", "duration", "gpus"] and len(rows) == 2
