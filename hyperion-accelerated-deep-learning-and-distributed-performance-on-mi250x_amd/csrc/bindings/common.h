@@ -49,4 +49,16 @@ inline bool is_rows_by_channels(const at::Tensor& x) {
   return false;
 }
 
+// A zeroed fp64 [kStatSlots, 2, C] statistics accumulator (the BN kernels ADD into it with
+// atomics): the caller's (a slice of a pre-zeroed arena, ops/_native.py) or a fresh zeroed one.
+inline at::Tensor stats_sums(const c10::optional<at::Tensor>& sums, int64_t C, const at::Tensor& like) {
+  if (sums.has_value() && sums->defined()) {
+    TORCH_CHECK(sums->scalar_type() == at::kDouble && sums->is_contiguous() &&
+                    sums->numel() == 2 * C * hyp::kStatSlots && sums->device() == like.device(),
+                "stats sums: a contiguous fp64 [kStatSlots * 2 * C] tensor on the input's device (zeroed)");
+    return sums->view({hyp::kStatSlots, 2, C});
+  }
+  return at::zeros({hyp::kStatSlots, 2, C}, like.options().dtype(at::kDouble));
+}
+
 }  // namespace hypbind

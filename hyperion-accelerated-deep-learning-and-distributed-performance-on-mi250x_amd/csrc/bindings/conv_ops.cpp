@@ -14,7 +14,6 @@ at::Tensor& zero_page(const at::Device& dev) {
   return z[i];
 }
 
-// x [N,C,H,W] channels-last, w [K,C,R,S] channels-last -> (y [N,K,P,Q] channels-last, psum, psq)
 // Effective split-K count for a conv of nk reduction steps (conv_fwd's own rounding: no empty splits).
 int plan_splits(int M, int K, int nk, int bm, int bn, int64_t splits_req) {
   int sp = splits_req > 0 ? (int)splits_req : (splits_req == 0 ? 1 : hyp::conv_fwd_splits(M, K, nk, bm, bn));
@@ -23,8 +22,11 @@ int plan_splits(int M, int K, int nk, int bm, int bn, int64_t splits_req) {
   return (nk + steps - 1) / steps;
 }
 
+// x [N,C,H,W] channels-last, w [K,C,R,S] channels-last -> (y [N,K,P,Q] channels-last, Σy, Σy² as
+// [kStatSlots, K] slot partials).  The statistics are ADDED into `sums` ([kStatSlots*2*K] fp64, zeroed).
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t sh, int64_t sw, int64_t ph,
-                                 int64_t pw, bool stats, int64_t bm_req, int64_t bn_req, int64_t splits_req) {
+                                 int64_t pw, bool stats, int64_t bm_req, int64_t bn_req, int64_t splits_req,
+                                 const c10::optional<at::Tensor>& sums) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: 4D tensors");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -46,21 +48,17 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   if (bn_req > 0) bn = (int)bn_req;
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
               "conv_fwd: tiles 64x64, 128x64 or 128x128");
-  // split-K below ~2 workgroups per CU (the stats then come from the reduce, kStatRows-row partials)
+  // split-K below ~2 workgroups per CU (the stats then come from the reduce)
   const int splits = plan_splits(M, K, R * S * (C / 64), bm, bn, splits_req);
-  at::Tensor psum, psq, slabs;
-  if (stats) {
-    const int mt = splits > 1 ? (M + hyp::kStatRows - 1) / hyp::kStatRows : (M + bm - 1) / bm;
-    auto part = at::empty({2, mt, K}, x.options().dtype(at::kFloat));
-    psum = part[0];
-    psq = part[1];
-  }
+  at::Tensor acc, slabs;
+  if (stats) acc = stats_sums(sums, K, x);
   if (splits > 1) slabs = at::empty({splits, M, K}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
-                              stats ? psum.data_ptr<float>() : nullptr, stats ? psq.data_ptr<float>() : nullptr, N, H, W,
-                              C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, splits,
+                              stats ? acc.data_ptr<double>() : nullptr, stats ? acc.data_ptr<double>() + K : nullptr, N, H,
+                              W, C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, splits,
                               splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream()));
-  return {y, psum, psq};
+  if (!stats) return {y, at::Tensor(), at::Tensor()};
+  return {y, acc.select(1, 0), acc.select(1, 1)};  // [kStatSlots, K] each: .sum(0) = per-channel totals
 }
 
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
@@ -242,31 +240,29 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int6
   return dw;
 }
 
-// BN forward (training) given conv-epilogue partials: returns (y, save_mean, save_invstd)
-std::vector<at::Tensor> bn_fwd_partials(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
-                                        const at::Tensor& psum, const at::Tensor& psq,
-                                        const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
-                                        const c10::optional<at::Tensor>& running_mean,
-                                        const c10::optional<at::Tensor>& running_var, double momentum, double eps,
-                                        bool act) {
+// BN forward (training) given the statistics sums [2, C] of x (conv epilogue): (y, save_mean, save_invstd)
+std::vector<at::Tensor> bn_fwd_sums(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
+                                    const at::Tensor& sums, const c10::optional<at::Tensor>& weight,
+                                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& running_mean,
+                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps,
+                                    bool act) {
   HYP_CHECK_CUDA_TENSOR(x);
-  TORCH_CHECK(is_rows_by_channels(x), "bn_fwd_partials: x must be channels-last");
+  TORCH_CHECK(is_rows_by_channels(x), "bn_fwd_sums: x must be channels-last");
   const int64_t C = x.size(1), M = x.numel() / C;
-  TORCH_CHECK(psum.dim() == 2 && psum.size(1) == C && psq.sizes() == psum.sizes(), "bn_fwd_partials: partials shape");
+  TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.is_contiguous() && sums.numel() == 2 * C * hyp::kStatSlots,
+              "bn_fwd_sums: sums must be a contiguous fp64 [kStatSlots * 2 * C] tensor");
   if (residual.has_value() && residual->defined())
     TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type() &&
                     is_rows_by_channels(*residual),
-                "bn_fwd_partials: residual shape/dtype/layout mismatch");
+                "bn_fwd_sums: residual shape/dtype/layout mismatch");
   const at::DeviceGuard guard(x.device());
   auto y = at::empty_like(x);
-  auto fopt = x.options().dtype(at::kFloat);
-  auto stats = at::empty({2, C}, fopt);
-  auto ws = at::empty({2 * C}, fopt);
-  HYP_CHECK_HIP(hyp::bn_forward_from_partials(
+  auto stats = at::empty({2, C}, x.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::bn_forward_from_sums(
       dtype_code(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, (int)C, ptr_or_null<float>(weight),
       ptr_or_null<float>(bias), ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var), (float)momentum,
-      (float)eps, act ? 1 : 0, psum.data_ptr<float>(), psq.data_ptr<float>(), (int)psum.size(0), stats.data_ptr<float>(),
-      stats.data_ptr<float>() + C, ws.data_ptr<float>(), ws.data_ptr<float>() + C, cur_stream()));
+      (float)eps, act ? 1 : 0, sums.data_ptr<double>(), stats.data_ptr<float>(), stats.data_ptr<float>() + C,
+      cur_stream()));
   return {y, stats[0], stats[1]};
 }
 
@@ -351,7 +347,8 @@ at::Tensor global_avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
 void register_conv_ops(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)", pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
-        pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1, pybind11::arg("splits") = -1);
+        pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1, pybind11::arg("splits") = -1,
+        pybind11::arg("sums") = pybind11::none());
   m.def("conv_set_stages", [](int64_t fwd, int64_t wgrad) {
     hyp::conv_set_stages((int)fwd);
     hyp::conv_wgrad_set_stages((int)wgrad);
@@ -378,7 +375,7 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
         pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("alpha") = 1.0);
-  m.def("bn_fwd_partials", &bn_fwd_partials, "BN finalize + apply from conv-epilogue partials");
+  m.def("bn_fwd_sums", &bn_fwd_sums, "BN apply (inline finalize) from conv-epilogue statistics sums");
 }
 
 }  // namespace hypbind

@@ -5,12 +5,13 @@
 namespace hypbind {
 namespace {
 
-// x: [N,C,H,W] channels-last or [M,C]; returns (y, save_mean, save_invstd)
+// x: [N,C,H,W] channels-last or [M,C]; returns (y, save_mean, save_invstd).  sums: optional zeroed
+// fp64 [2, C] statistics accumulator (training).
 std::vector<at::Tensor> bn_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
                                const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
                                const c10::optional<at::Tensor>& running_mean,
                                const c10::optional<at::Tensor>& running_var, double momentum, double eps, bool training,
-                               bool act) {
+                               bool act, const c10::optional<at::Tensor>& sums) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(is_rows_by_channels(x), "bn_fwd: x must be channels-last 4D or contiguous 2D");
   const int64_t C = x.size(1);
@@ -25,27 +26,28 @@ std::vector<at::Tensor> bn_fwd(const at::Tensor& x, const c10::optional<at::Tens
   const at::DeviceGuard guard(x.device());
   auto y = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
-  int P = 1;
-  HYP_CHECK_HIP(hyp::bn_workspace_rows(M, (int)C, &P));
-  auto ws = at::empty({training ? 2 * P * C + 4 * C : 4 * C}, fopt);
-  float* base = ws.data_ptr<float>();
   auto stats = at::empty({2, C}, fopt);
-  float* psum = training ? base + 4 * C : nullptr;
-  float* psq = training ? base + 4 * C + (int64_t)P * C : nullptr;
+  at::Tensor acc, consts;
+  if (training)
+    acc = stats_sums(sums, C, x);
+  else
+    consts = at::empty({2, C}, fopt);
   HYP_CHECK_HIP(hyp::bn_forward(dtype_code(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, (int)C,
                                 ptr_or_null<float>(weight), ptr_or_null<float>(bias), ptr_or_null<float>(running_mean),
                                 ptr_or_null<float>(running_var), (float)momentum, (float)eps, training ? 1 : 0,
-                                act ? 1 : 0, psum, psq, stats.data_ptr<float>(), stats.data_ptr<float>() + C, base,
-                                base + C, cur_stream()));
+                                act ? 1 : 0, training ? acc.data_ptr<double>() : nullptr, stats.data_ptr<float>(),
+                                stats.data_ptr<float>() + C, training ? nullptr : consts.data_ptr<float>(),
+                                training ? nullptr : consts.data_ptr<float>() + C, cur_stream()));
   return {y, stats[0], stats[1]};
 }
 
 // returns (dx, dres or undefined, dweight, dbias)
-// y may be None with act (training, no residual): the ReLU mask is recomputed from x, weight, bias
+// y may be None with act (training, no residual): the ReLU mask is recomputed from x, weight, bias.
+// sums: optional zeroed fp64 [2, C] accumulator for Σdz, Σdz·x.
 std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& y,
                                const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
                                const at::Tensor& save_mean, const at::Tensor& save_invstd, bool training, bool act,
-                               bool has_res) {
+                               bool has_res, const c10::optional<at::Tensor>& sums) {
   HYP_CHECK_CUDA_TENSOR(x);
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
@@ -59,19 +61,13 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const 
   auto dx = at::empty_like(x);
   at::Tensor dres;
   if (has_res) dres = at::empty_like(x);
-  auto fopt = x.options().dtype(at::kFloat);
-  int P = 1;
-  HYP_CHECK_HIP(hyp::bn_workspace_rows(M, (int)C, &P));
-  auto ws = at::empty({2 * (int64_t)P * C + 3 * C}, fopt);
-  float* base = ws.data_ptr<float>();
-  auto dwb = at::empty({2, C}, fopt);
+  auto acc = stats_sums(sums, C, x);
+  auto dwb = at::empty({2, C}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::bn_backward(dtype_code(x), dyc.data_ptr(), x.data_ptr(), (act && have_y) ? y->data_ptr() : nullptr,
                                  dx.data_ptr(), has_res ? dres.data_ptr() : nullptr, M, (int)C,
                                  ptr_or_null<float>(weight), ptr_or_null<float>(bias), save_mean.data_ptr<float>(),
-                                 save_invstd.data_ptr<float>(),
-                                 training ? 1 : 0, act ? 1 : 0, base + 3 * C, base + 3 * C + (int64_t)P * C,
-                                 dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, base, base + C, base + 2 * C,
-                                 cur_stream()));
+                                 save_invstd.data_ptr<float>(), training ? 1 : 0, act ? 1 : 0, acc.data_ptr<double>(),
+                                 dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, cur_stream()));
   return {dx, dres, dwb[0], dwb[1]};
 }
 
@@ -147,12 +143,16 @@ void stream(int64_t op, const at::Tensor& a, const c10::optional<at::Tensor>& b,
 }  // namespace
 
 void register_norm_ops(pybind11::module& m) {
-  m.def("bn_fwd", &bn_fwd, "fused NHWC batch-norm (+residual)(+relu) forward");
-  m.def("bn_set_fin2", [](bool on) { hyp::bn_set_fin2(on ? 1 : 0); },
-        "wide one-round BN finalize on/off (A/B and tests)");
+  m.def("bn_fwd", &bn_fwd, "fused NHWC batch-norm (+residual)(+relu) forward", pybind11::arg("x"),
+        pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
+        pybind11::arg("running_var"), pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("training"),
+        pybind11::arg("act"), pybind11::arg("sums") = pybind11::none());
   m.def("bn_set_small_paths", [](bool on) { hyp::bn_set_small_paths(on ? 1 : 0); },
-        "small-M BN fast paths: finalize folded into the apply, one-launch backward (default on)");
-  m.def("bn_bwd", &bn_bwd, "fused NHWC batch-norm (+residual)(+relu) backward");
+        "small-M BN one-launch backward (default on)");
+  m.def("bn_bwd", &bn_bwd, "fused NHWC batch-norm (+residual)(+relu) backward", pybind11::arg("dy"), pybind11::arg("x"),
+        pybind11::arg("y"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("save_mean"),
+        pybind11::arg("save_invstd"), pybind11::arg("training"), pybind11::arg("act"), pybind11::arg("has_res"),
+        pybind11::arg("sums") = pybind11::none());
   m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());

@@ -7,20 +7,33 @@
 namespace hyp {
 
 // ---- bn_act.hip ----------------------------------------------------------------------------
-hipError_t bn_workspace_rows(int64_t M, int C, int* P_out);
+// Statistics sums are [kStatSlots][2][C] fp64: producer block / tile b adds into slot b % kStatSlots,
+// so a burst of tiles finishing together queues <= 1/kStatSlots of its atomics on any one 64-byte
+// line (the memory-side atomic unit serializes per line: 784 layer1 tiles on one slot cost ~13 us);
+// consumers sum the slots in fixed order.
+constexpr int kStatSlots = 8;
+// Training statistics are per-channel fp64 sums [kStatSlots][2][C] (Σx, Σx²) accumulated with atomics: every
+// `sums` argument must point at ZEROED memory before its producer runs.  Consumers finalize inline.
+hipError_t bn_stats(int dtype, const void* x, int64_t M, int C, double* sums, hipStream_t stream);
 hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* weight,
                       const float* bias, float* running_mean, float* running_var, float momentum, float eps,
-                      int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
-                      float* scale, float* shift, hipStream_t stream);
-// wide (one-round, 1024-thread) BN finalize on/off: A/B against the one-level kernels
-void bn_set_fin2(int on);
-// y == nullptr with act: the ReLU mask is recomputed from x (training, no residual gradient only)
-// small-M BN fast paths (finalize folded into apply / one-launch backward); 0 disables (A/B, tests)
+                      int training, int act, double* sums, float* save_mean, float* save_invstd, float* scale,
+                      float* shift, hipStream_t stream);
+hipError_t bn_forward_from_sums(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                                const float* weight, const float* bias, float* running_mean, float* running_var,
+                                float momentum, float eps, int act, const double* sums, float* save_mean,
+                                float* save_invstd, hipStream_t stream);
+// small-M one-launch backward (M <= 2048); 0 disables (A/B, tests)
 void bn_set_small_paths(int on);
+// y == nullptr with act: the ReLU mask is recomputed from x (training, no residual gradient only).
+// sums: zeroed [kStatSlots][2][C] workspace for Σdz, Σdz·x.
 hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
                        const float* weight, const float* bias, const float* save_mean, const float* save_invstd,
-                       int training, int act, float* pdz, float* pdzx, float* dweight, float* dbias, float* kA,
-                       float* kB, float* kC, hipStream_t stream);
+                       int training, int act, double* sums, float* dweight, float* dbias, hipStream_t stream);
+// dz already masked and its sums [kStatSlots][2][C] (Σdz, Σdz·x) complete: the dx pass only.
+hipError_t bn_backward_dx(int dtype, const void* dz, const void* x, void* dx, int64_t M, int C, const float* weight,
+                          const float* save_mean, const float* save_invstd, int training, const double* sums,
+                          float* dweight, float* dbias, hipStream_t stream);
 
 // ---- adam.hip ------------------------------------------------------------------------------
 // param_dtype kF32: ptrs = [param, grad, m, v]; kBF16/kF16: ptrs = [lowp param, grad, m, v, fp32 master]
@@ -116,8 +129,9 @@ hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, vo
 
 namespace hyp {
 // ---- conv_igemm.hip --------------------------------------------------------------------------
-// NHWC implicit-GEMM conv (bf16/f16), optional BN-statistics epilogue (psum/psq: [ceil(M/bm), K];
-// with splits > 1 the stats come from the split-K reduce: [ceil(M/kStatRows), K]).
+// NHWC implicit-GEMM conv (bf16/f16), optional BN-statistics epilogue: per-channel Σy (psum[K]) and
+// Σy² (psq = psum + K; fp64, slots of stride 2K: bn_act.hip layout) of the rounded outputs, ADDED atomically (zero them first); with splits > 1 the
+// stats come from the split-K reduce.
 bool conv_fwd_supported(int C, int K);
 void conv_set_stages(int nb);        // LDS pipeline depth 2..4 (0 = automatic); tuning only
 void conv_wgrad_set_stages(int nb);
@@ -125,7 +139,7 @@ void conv_fwd_tile(int M, int K, int* bm, int* bn);
 // addend (optional, splits == 1, no stats): out [M, K] += addend after rounding (fused residual grad).
 // dgrad != 0: stride-1 data gradient; "in" is dY [N,H,W,C], "w" the ORIGINAL filter [C][R][S][K]
 // (read flipped and transposed in-kernel), (ph, pw) the dgrad padding R-1-p.
-hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
+hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
                     const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr);
@@ -145,10 +159,10 @@ struct SplitkEpilogue {
 hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st,
                          float alpha = 1.f, const SplitkEpilogue* ep = nullptr);
 // Split-K reduce of a conv forward's [splits, M, K] fp32 partials into out [M, K] (T) plus the BN
-// statistics of the rounded outputs: psum/psq [ceil(M / kStatRows), K].
-constexpr int kStatRows = 16;
-hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, float* psum,
-                               float* psq, hipStream_t st);
+// statistics of the rounded outputs, added atomically into psum[K] / psq[K] (kStatRows-row blocks).
+constexpr int kStatRows = 64;  // (16 when that leaves < 512 blocks)
+hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, double* psum,
+                               double* psq, hipStream_t st);
 // Split-K plan for a convolution (forward or stride-1 dgrad) whose bm x bn tiling leaves fewer than
 // ~2 workgroups per CU: returns splits >= 1 over the nk = R*S*C/64 reduction steps.
 int conv_fwd_splits(int M, int K, int nk, int bm, int bn);
@@ -160,12 +174,6 @@ void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* s
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
                       int bn, int splits, int steps_per_split, hipStream_t st, float alpha = 1.f);
-// ---- bn_act.hip (conv-epilogue statistics) ---------------------------------------------------
-hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
-                                    const float* weight, const float* bias, float* running_mean, float* running_var,
-                                    float momentum, float eps, int act, const float* psum, const float* psq, int P,
-                                    float* save_mean, float* save_invstd, float* scale, float* shift,
-                                    hipStream_t stream);
 }  // namespace hyp
 
 namespace hyp {

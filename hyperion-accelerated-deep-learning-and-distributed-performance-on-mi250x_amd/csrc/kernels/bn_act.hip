@@ -8,12 +8,22 @@
 // 256-thread block covers `tpr` channel-vectors × `rpi` rows per iteration, so the per-channel
 // constants (scale/shift, or the backward coefficients) sit in registers for the whole loop.
 //
-// Forward (training):  stats_partial (deterministic per-block partial Σx, Σx²)
-//                      -> stats_finalize (fp64 combine, running-stat update, scale/shift)
-//                      -> apply   y = act(x*scale + shift [+ res])
-// Backward:            bwd_reduce (Σdz, Σdz·x with dz = dy·[y>0])
-//                      -> bwd_finalize (dγ, dβ, and dx = A·dz + B·x + C coefficients)
-//                      -> bwd_dx  dx = A·dz + B·x + C ; dres = dz
+// Statistics are per-channel fp64 SUMS [kStatSlots][2][C] of fp32 per-block partials, accumulated with no-return
+// global f64 atomics (channel runs per wave instruction, executed at the memory side: coherent
+// across the 8 XCD L2s) by whichever kernel produces them — the conv epilogue (conv_igemm.hip), the
+// split-K reduce, or the stats kernels below.  Every CONSUMER finalizes inline: an apply thread
+// turns the two sums of its 8 channels into mean / invstd / scale / shift in a few fp64 ops, and
+// block 0 also writes save_mean / save_invstd / running stats.  There is no finalize launch (the
+// partial-row + finalize design cost 75 latency-bound 5-7 us launches per ResNet-50 step).  The
+// sums must be zero before the producer runs: the caller hands in slices of one pre-zeroed arena
+// (one fill per forward, ops/_native.py ZeroArena).  Atomic arrival order varies, but fp32
+// partials summed in fp64 are exact while their exponents span < ~19 binades (53-bit mantissa vs
+// 24 + log2(adders)), so the finalized float mean / invstd are reproducible in practice — the
+// deterministic partial-row design's property, without its launches.
+//
+// Forward (training):  stats (atomic Σx, Σx²)  ->  apply  y = act(x*scale + shift [+ res])
+// Backward:            reduce (atomic Σdz, Σdz·x with dz = dy·[y>0])  ->  dx = A·dz + B·x + C ; dres = dz
+//                      (M <= 2048: one register-resident launch does all of it)
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -21,20 +31,9 @@ namespace hyp {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kStatsBlocks = 512;  // partial rows per reduction: keeps the combine pass short
-constexpr int kFinCh = 8;          // finalize block: 8 channels x 32 partial-row groups
-constexpr int kFinGr = 32;
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-struct BwdFin {  // backward finalize inputs / outputs (bn_bwd_finalize_k's arguments)
-  const float* weight;
-  const float* mean;
-  const float* invstd;
-  int training;
-  float* dweight;
-  float* dbias;
-};
+constexpr int kStatsBlocks = 512;  // row blocks of the statistics kernels (= atomic adders per channel)
+constexpr int kFinCh = 256;        // channels per apply / dx block: one inline-finalized channel per thread
+constexpr int kApplyBlocks = 2048;
 
 struct BnGeom {
   int tpr;   // threads per row (each owns 8 channels)
@@ -44,20 +43,22 @@ struct BnGeom {
   int64_t rows_per_block;
 };
 
-bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g) {
+// max_tpr: channel-vectors per block row (the apply / dx kernels cap a block at kFinCh channels,
+// so their inline finalize is one channel per thread)
+bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g, int max_tpr = kBlock) {
   if (C % 8 != 0) return false;
   const int cv = C / 8;
-  if (cv <= kBlock) {
+  if (cv <= max_tpr) {
     g.tpr = cv;
     g.gy = 1;
   } else {
-    if (cv % kBlock != 0) return false;
-    g.tpr = kBlock;
-    g.gy = cv / kBlock;
+    if (cv % max_tpr != 0) return false;
+    g.tpr = max_tpr;
+    g.gy = cv / max_tpr;
   }
   g.rpi = kBlock / g.tpr;
-  // >= 4 row iterations per thread, and >= 16K elements per block so partial rows stay a tiny
-  // fraction of the data (the combine pass reads P*C partials)
+  // >= 4 row iterations per thread, and >= 16K elements per block so each block's atomics are a
+  // tiny fraction of its traffic
   int64_t min_rows = (int64_t)g.rpi * 4;
   const int64_t by_size = (16384 + C - 1) / C;
   if (max_blocks <= kStatsBlocks && by_size > min_rows) min_rows = by_size;
@@ -72,13 +73,131 @@ bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g) {
   return true;
 }
 
-// ---------------------------------------------------------------- forward stats
-template <typename T>
-__global__ __launch_bounds__(kBlock) void bn_stats_partial_k(const T* __restrict__ x, int64_t M, int C, int tpr,
-                                                             int rpi, int64_t rpb, float* __restrict__ psum,
-                                                             float* __restrict__ psq) {
+// Statistics / backward-reduce geometry: every row block adds one fp64 pair per channel, so the
+// atomic traffic is P x C x 16 bytes — keep it near 512 KB (P = 32768 / C row blocks, 16..512)
+// and get the parallelism from narrow 64-channel blocks instead (gy = C / 64; one 128-byte row
+// segment per block row).  At P = 512 for every C, layer3's C = 1024 reduce moved 8 MB of
+// atomics and ran 3.5-8 us slower than with plain partial-row stores.
+constexpr int64_t kAtomicBudget = 32768;
+
+bool stats_geom(int64_t M, int C, BnGeom& g) {
+  if (C % 8 != 0) return false;
+  const int cv = C / 8;
+  g.tpr = cv % 8 == 0 ? 8 : (cv <= kBlock ? cv : 0);
+  if (g.tpr == 0) return bn_geom(M, C, kStatsBlocks, g);
+  g.gy = cv / g.tpr;
+  g.rpi = kBlock / g.tpr;
+  int64_t P = kAtomicBudget / C;
+  P = P < 16 ? 16 : (P > kStatsBlocks ? kStatsBlocks : P);
+  const int64_t by_rows = (M + (int64_t)g.rpi * 4 - 1) / ((int64_t)g.rpi * 4);  // >= 4 row iterations
+  if (P > by_rows) P = by_rows;
+  if (P < 1) P = 1;
+  g.rows_per_block = (M + P - 1) / P;
+  g.P = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
+  return true;
+}
+
+// ---------------------------------------------------------------- inline finalize
+struct FwdFin {
+  const double* sums;  // [kStatSlots][2][C]: Σx, Σx²
+  const float* weight;
+  const float* bias;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;
+  float* save_invstd;
+  double invM;    // 1 / M
+  double unbias;  // M / (M - 1): the running variance is unbiased
+};
+
+// scale / shift of channel c (the arithmetic the backward's ReluMask repeats bit for bit: invstd
+// and mean rounded to float, scale = w*invstd, shift = b - mean*scale).  `writer`: also store
+// save_mean / save_invstd and update the running statistics.
+__device__ __forceinline__ void fwd_const1(const FwdFin& f, int C, int c, bool writer, float& sc, float& sh) {
+  double a = 0.0, b2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) {  // fixed order
+    a += f.sums[(int64_t)k * 2 * C + c];
+    b2 += f.sums[(int64_t)k * 2 * C + C + c];
+  }
+  const double mean = a * f.invM;
+  double var = b2 * f.invM - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float w = f.weight ? f.weight[c] : 1.f;
+  const float b = f.bias ? f.bias[c] : 0.f;
+  const float s = w * invstd;
+  sc = s;
+  sh = b - (float)mean * s;
+  if (writer) {
+    f.save_mean[c] = (float)mean;
+    f.save_invstd[c] = invstd;
+    if (f.running_mean != nullptr) {
+      f.running_mean[c] = (float)((1.0 - f.momentum) * f.running_mean[c] + f.momentum * mean);
+      f.running_var[c] = (float)((1.0 - f.momentum) * f.running_var[c] + f.momentum * var * f.unbias);
+    }
+  }
+}
+
+struct BwdFin {
+  const float* weight;
+  const float* mean;
+  const float* invstd;
+  int training;
+  float* dweight;
+  float* dbias;
+  const double* sums;  // [kStatSlots][2][C]: Σdz, Σdz·x (the reduce + dx path)
+  double invM;         // 1 / M
+};
+
+// dx = A·dz + B·x + C coefficients of channel c from a = Σdz, b = Σdz·x (fp64)
+__device__ __forceinline__ void bwd_coeffs(const BwdFin& f, int c, double a, double b, bool writer, float& A,
+                                           float& B, float& Cc) {
+  const double mu = f.mean[c], is = f.invstd[c];
+  const double sum_dz_xhat = is * (b - mu * a);
+  if (writer) {
+    if (f.dweight) f.dweight[c] = (float)sum_dz_xhat;
+    if (f.dbias) f.dbias[c] = (float)a;
+  }
+  const double g = f.weight ? f.weight[c] : 1.0;
+  const double Ad = g * is;
+  const double Bd = f.training ? -Ad * is * sum_dz_xhat * f.invM : 0.0;
+  const double Cd = f.training ? -Ad * a * f.invM - Bd * mu : 0.0;
+  A = (float)Ad;
+  B = (float)Bd;
+  Cc = (float)Cd;
+}
+
+// Block-level column sums of s/q (8 per thread) -> one atomic per channel per block
+__device__ __forceinline__ void block_atomic_sums(const float (&s)[8], const float (&q)[8], int tpr, int rpi, int C,
+                                                  int cbase, double* __restrict__ sums) {
   __shared__ float ls[kBlock * 8];
   __shared__ float lq[kBlock * 8];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ls[tid * 8 + j] = s[j];
+    lq[tid * 8 + j] = q[j];
+  }
+  __syncthreads();
+  const int nch = tpr * 8;
+  for (int ch = tid; ch < nch; ch += kBlock) {
+    float a = 0.f, b = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      a += ls[rr * nch + ch];
+      b += lq[rr * nch + ch];
+    }
+    double* slot = sums + (int64_t)(blockIdx.x % kStatSlots) * 2 * C;
+    unsafeAtomicAdd(slot + cbase + ch, (double)a);  // hardware global_atomic_add_f64 (no CAS loop)
+    unsafeAtomicAdd(slot + C + cbase + ch, (double)b);
+  }
+}
+
+// ---------------------------------------------------------------- forward stats
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_stats_k(const T* __restrict__ x, int64_t M, int C, int tpr, int rpi,
+                                                     int64_t rpb, double* __restrict__ sums) {
   const int tid = threadIdx.x;
   const int r = tid / tpr, c8 = tid - r * tpr;
   const int cbase = blockIdx.y * tpr * 8;
@@ -113,86 +232,7 @@ __global__ __launch_bounds__(kBlock) void bn_stats_partial_k(const T* __restrict
       }
     }
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ls[tid * 8 + j] = s[j];
-    lq[tid * 8 + j] = q[j];
-  }
-  __syncthreads();
-  const int nch = tpr * 8;
-  for (int ch = tid; ch < nch; ch += kBlock) {
-    float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < rpi; ++rr) {
-      a += ls[rr * nch + ch];
-      b += lq[rr * nch + ch];
-    }
-    psum[(int64_t)blockIdx.x * C + cbase + ch] = a;
-    psq[(int64_t)blockIdx.x * C + cbase + ch] = b;
-  }
-}
-
-// Sum partial rows p = threadIdx.y, +16, ... of column c with 8 independent loads in flight
-// (the loop is latency-bound; a rolled loop waits one L2 round trip per partial).
-__device__ __forceinline__ void combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int P,
-                                                 int C, int c, float& a, float& b) {
-  float sa[8], sb[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.f;
-  int p = threadIdx.y;
-  for (; p + kFinGr * 7 < P; p += kFinGr * 8) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      sa[i] += pa[(int64_t)(p + kFinGr * i) * C + c];
-      sb[i] += pb[(int64_t)(p + kFinGr * i) * C + c];
-    }
-  }
-  for (; p < P; p += kFinGr) {
-    sa[0] += pa[(int64_t)p * C + c];
-    sb[0] += pb[(int64_t)p * C + c];
-  }
-  a = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
-  b = ((sb[0] + sb[1]) + (sb[2] + sb[3])) + ((sb[4] + sb[5]) + (sb[6] + sb[7]));
-}
-
-// grid: ceil(C/8); block (8, 32)
-__global__ __launch_bounds__(256) void bn_stats_finalize_k(const float* __restrict__ psum, const float* __restrict__ psq,
-                                                            int P, int C, int64_t M, const float* __restrict__ weight,
-                                                            const float* __restrict__ bias, float* running_mean,
-                                                            float* running_var, float momentum, float eps,
-                                                            float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                                            float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ float red_s[kFinGr][kFinCh];
-  __shared__ float red_q[kFinGr][kFinCh];
-  const int c = blockIdx.x * kFinCh + threadIdx.x;
-  float a = 0.f, b = 0.f;
-  if (c < C) combine_partials(psum, psq, P, C, c, a, b);
-  red_s[threadIdx.y][threadIdx.x] = a;
-  red_q[threadIdx.y][threadIdx.x] = b;
-  __syncthreads();
-  if (threadIdx.y == 0 && c < C) {
-    double da = a, db = b;
-    for (int i = 1; i < kFinGr; ++i) {
-      da += red_s[i][threadIdx.x];
-      db += red_q[i][threadIdx.x];
-    }
-    const double a = da, b = db;
-    const double mean = a / (double)M;
-    double var = b / (double)M - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    save_mean[c] = (float)mean;
-    save_invstd[c] = invstd;
-    if (running_mean != nullptr) {
-      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
-    }
-    const float w = weight ? weight[c] : 1.f;
-    const float bb = bias ? bias[c] : 0.f;
-    const float sc = w * invstd;
-    scale[c] = sc;
-    shift[c] = bb - (float)mean * sc;
-  }
+  block_atomic_sums(s, q, tpr, rpi, C, cbase, sums);
 }
 
 // eval-mode constants from running stats
@@ -212,17 +252,29 @@ __global__ void bn_eval_consts_k(int C, const float* __restrict__ weight, const 
 }
 
 // ---------------------------------------------------------------- forward apply
-template <typename T, bool ACT, bool RES>
+// FIN: training — scale/shift finalized inline from the statistics sums; else read from arrays.
+template <typename T, bool ACT, bool RES, bool FIN>
 __global__ __launch_bounds__(kBlock) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
                                                      T* __restrict__ y, const float* __restrict__ scale,
-                                                     const float* __restrict__ shift, int64_t M, int C, int tpr,
-                                                     int rpi, int64_t rpb) {
+                                                     const float* __restrict__ shift, FwdFin fin, int64_t M, int C,
+                                                     int tpr, int rpi, int64_t rpb) {
+  __shared__ float kk[2][FIN ? kFinCh : 1];
   const int tid = threadIdx.x;
   const int r = tid / tpr, c8 = tid - r * tpr;
-  if (r >= rpi) return;
   const int c0 = blockIdx.y * tpr * 8 + c8 * 8;
   float sc[8], sh[8];
-  {
+  if (FIN) {  // finalize this block's <= kFinCh channels, one per thread (block x == 0 also writes)
+    const int nch = tpr * 8, cb = blockIdx.y * nch;
+    if (tid < nch) fwd_const1(fin, C, cb + tid, blockIdx.x == 0, kk[0][tid], kk[1][tid]);
+    __syncthreads();
+    if (r >= rpi) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = kk[0][c8 * 8 + j];
+      sh[j] = kk[1][c8 * 8 + j];
+    }
+  } else {
+    if (r >= rpi) return;
     const float4 a = reinterpret_cast<const float4*>(scale + c0)[0];
     const float4 b = reinterpret_cast<const float4*>(scale + c0)[1];
     const float4 d = reinterpret_cast<const float4*>(shift + c0)[0];
@@ -278,8 +330,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_k(const T* __restrict__ x, co
 
 // ---------------------------------------------------------------- backward
 // ReLU mask of the forward output.  MASKX: recomputed from x as x*scale + shift > 0 with the
-// forward's exact float scale/shift (scale = w*invstd, shift = b - mean*scale, the finalize
-// kernel's arithmetic), so the non-residual backward never reads y (one stream less).
+// forward's exact float scale/shift (fwd_const1's arithmetic), so the non-residual backward
+// never reads y (one stream less).
 template <typename T, bool ACT, bool MASKX>
 struct ReluMask {
   float sc[8], sh[8];
@@ -303,12 +355,10 @@ struct ReluMask {
 template <typename T, bool ACT, bool MASKX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ y, int64_t M, int C, int tpr, int rpi,
-                                                          int64_t rpb, float* __restrict__ pdz,
-                                                          float* __restrict__ pdzx, const float* __restrict__ w,
-                                                          const float* __restrict__ b, const float* __restrict__ mean,
+                                                          int64_t rpb, double* __restrict__ sums,
+                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          const float* __restrict__ mean,
                                                           const float* __restrict__ invstd) {
-  __shared__ float ls[kBlock * 8];
-  __shared__ float lq[kBlock * 8];
   const int tid = threadIdx.x;
   const int r = tid / tpr, c8 = tid - r * tpr;
   const int cbase = blockIdx.y * tpr * 8;
@@ -354,184 +404,43 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_k(const T* __restrict__ 
       }
     }
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ls[tid * 8 + j] = s[j];
-    lq[tid * 8 + j] = q[j];
-  }
-  __syncthreads();
-  const int nch = tpr * 8;
-  for (int ch = tid; ch < nch; ch += kBlock) {
-    float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < rpi; ++rr) {
-      a += ls[rr * nch + ch];
-      b += lq[rr * nch + ch];
-    }
-    pdz[(int64_t)blockIdx.x * C + cbase + ch] = a;
-    pdzx[(int64_t)blockIdx.x * C + cbase + ch] = b;
-  }
+  block_atomic_sums(s, q, tpr, rpi, C, cbase, sums);
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_k(const float* __restrict__ pdz, const float* __restrict__ pdzx,
-                                                          int P, int C, int64_t M, const float* __restrict__ weight,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd, int training,
-                                                          float* __restrict__ dweight, float* __restrict__ dbias,
-                                                          float* __restrict__ kA, float* __restrict__ kB,
-                                                          float* __restrict__ kC) {
-  __shared__ float red_s[kFinGr][kFinCh];
-  __shared__ float red_q[kFinGr][kFinCh];
-  const int c = blockIdx.x * kFinCh + threadIdx.x;
-  float a = 0.f, b = 0.f;
-  if (c < C) combine_partials(pdz, pdzx, P, C, c, a, b);
-  red_s[threadIdx.y][threadIdx.x] = a;
-  red_q[threadIdx.y][threadIdx.x] = b;
-  __syncthreads();
-  if (threadIdx.y == 0 && c < C) {
-    double da = a, db = b;
-    for (int i = 1; i < kFinGr; ++i) {
-      da += red_s[i][threadIdx.x];
-      db += red_q[i][threadIdx.x];
-    }
-    const double a = da, b = db;
-    const double mu = mean[c], is = invstd[c];
-    const double sum_dz_xhat = is * (b - mu * a);
-    if (dweight) dweight[c] = (float)sum_dz_xhat;
-    if (dbias) dbias[c] = (float)a;
-    const double g = weight ? weight[c] : 1.0;
-    const double A = g * is;
-    if (training) {
-      const double Bc = -A * is * sum_dz_xhat / (double)M;
-      const double Cc = -A * a / (double)M - Bc * mu;
-      kA[c] = (float)A;
-      kB[c] = (float)Bc;
-      kC[c] = (float)Cc;
-    } else {
-      kA[c] = (float)A;
-      kB[c] = 0.f;
-      kC[c] = 0.f;
-    }
-  }
-}
-
-// ---------------------------------------------------------------- wide finalize
-// The conv epilogue (forward) and bn_bwd_reduce_k (backward) leave P partial rows [P, C] — up to
-// 784 for ResNet-50 layer1.  The finalize kernels above give each of C/8 blocks P/32 scalar loads
-// per thread, issued 8 at a time: three or four dependent memory round trips, a 5-7 us
-// latency-bound launch (8 blocks at C = 64; 75 such launches per ResNet-50 step).  A ticketed
-// two-level variant (last arriver combines) measured 10-14 us: the agent-scope release/acquire
-// fences and the winner's serial second pass cost more than they save (MI355X_MICROARCH.md
-// "splitk-seam").  Here one 1024-thread block owns 16 channels (4 float4 lanes) x 256 row lanes:
-// every partial is read by ONE round of independent 16-byte loads (<= 4 per thread for P <= 1024),
-// then a fixed-order LDS tree over the 256 row lanes (deterministic) and the fp64 finalize.
-struct Fin2Fwd {  // forward: statistics -> mean / invstd / running stats / scale / shift
-  const float* weight;
-  const float* bias;
-  float* running_mean;
-  float* running_var;
-  float momentum, eps;
-  float* save_mean;
-  float* save_invstd;
-  float* scale;
-  float* shift;
-};
-
-constexpr int kWideRows = 256;  // row lanes per block
-constexpr int kWideUnroll = 4;  // partial rows per thread per round
-
-template <bool BWD>
-__global__ __launch_bounds__(1024) void bn_fin_wide_k(const float* __restrict__ pa, const float* __restrict__ pb,
-                                                       int P, int C, int64_t M, Fin2Fwd ff, BwdFin bf,
-                                                       float* __restrict__ kA, float* __restrict__ kB,
-                                                       float* __restrict__ kC) {
-  __shared__ f32x4 red[2][kWideRows][4];
-  const int tid = threadIdx.x, q = tid & 3, ry = tid >> 2;
-  const int c = blockIdx.x * 16 + q * 4;
-  f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = sa;
-  for (int r0 = ry; r0 < P; r0 += kWideRows * kWideUnroll) {
-    f32x4 va[kWideUnroll], vb[kWideUnroll];
-#pragma unroll
-    for (int u = 0; u < kWideUnroll; ++u) {  // all loads of the round in flight before any add
-      const int r = r0 + u * kWideRows;
-      const bool ok = r < P;
-      va[u] = ok ? *reinterpret_cast<const f32x4*>(pa + (int64_t)r * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-      vb[u] = ok ? *reinterpret_cast<const f32x4*>(pb + (int64_t)r * C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int u = 0; u < kWideUnroll; ++u) {
-      sa += va[u];
-      sb += vb[u];
-    }
-  }
-  red[0][ry][q] = sa;
-  red[1][ry][q] = sb;
-  __syncthreads();
-  for (int h = kWideRows / 2; h >= 1; h >>= 1) {  // fixed pairing: deterministic
-    if (ry < h) {
-      red[0][ry][q] += red[0][ry + h][q];
-      red[1][ry][q] += red[1][ry + h][q];
-    }
-    __syncthreads();
-  }
-  if (tid < 16) {
-    const int ch = blockIdx.x * 16 + tid;
-    if (ch < C) {
-      const double a = red[0][0][tid >> 2][tid & 3], b = red[1][0][tid >> 2][tid & 3];
-      if (!BWD) {
-        const double mean = a / (double)M;
-        double var = b / (double)M - mean * mean;
-        if (var < 0.0) var = 0.0;
-        const float invstd = (float)(1.0 / sqrt(var + (double)ff.eps));
-        ff.save_mean[ch] = (float)mean;
-        ff.save_invstd[ch] = invstd;
-        if (ff.running_mean != nullptr) {
-          const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-          ff.running_mean[ch] = (float)((1.0 - ff.momentum) * ff.running_mean[ch] + ff.momentum * mean);
-          ff.running_var[ch] = (float)((1.0 - ff.momentum) * ff.running_var[ch] + ff.momentum * unbiased);
-        }
-        const float w = ff.weight ? ff.weight[ch] : 1.f;
-        const float bb = ff.bias ? ff.bias[ch] : 0.f;
-        const float sc = w * invstd;
-        ff.scale[ch] = sc;
-        ff.shift[ch] = bb - (float)mean * sc;
-      } else {
-        const double mu = bf.mean[ch], is = bf.invstd[ch];
-        const double sum_dz_xhat = is * (b - mu * a);
-        if (bf.dweight) bf.dweight[ch] = (float)sum_dz_xhat;
-        if (bf.dbias) bf.dbias[ch] = (float)a;
-        const double gw = bf.weight ? bf.weight[ch] : 1.0;
-        const double A = gw * is;
-        const double Bc = bf.training ? -A * is * sum_dz_xhat / (double)M : 0.0;
-        const double Cc = bf.training ? -A * a / (double)M - Bc * mu : 0.0;
-        kA[ch] = (float)A;
-        kB[ch] = (float)Bc;
-        kC[ch] = (float)Cc;
-      }
-    }
-  }
-}
-
+// dx = A·dz + B·x + C with the coefficients finalized inline from the Σdz, Σdz·x sums (block 0
+// writes dγ, dβ).  Without ACT, dy is already dz (masked — e.g. by the dgrad epilogue that
+// produced it), and the residual gradient IS dy: RES only matters for the masking variants.
 template <typename T, bool ACT, bool RES, bool MASKX>
 __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                       const T* __restrict__ y, T* __restrict__ dx,
-                                                      T* __restrict__ dres, const float* __restrict__ kA,
-                                                      const float* __restrict__ kB, const float* __restrict__ kC,
-                                                      int64_t M, int C, int tpr, int rpi, int64_t rpb,
-                                                      const float* __restrict__ w, const float* __restrict__ b,
-                                                      const float* __restrict__ mean,
-                                                      const float* __restrict__ invstd) {
+                                                      T* __restrict__ dres, BwdFin fin, int64_t M, int C, int tpr,
+                                                      int rpi, int64_t rpb, const float* __restrict__ bn_b) {
+  __shared__ float kk[3][kFinCh];
   const int tid = threadIdx.x;
   const int r = tid / tpr, c8 = tid - r * tpr;
+  {  // this block's <= kFinCh channels, one per thread (block x == 0 also writes dγ, dβ)
+    const int nch = tpr * 8, c = blockIdx.y * nch + tid;
+    if (tid < nch) {
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int k = 0; k < kStatSlots; ++k) {  // fixed order
+        a += fin.sums[(int64_t)k * 2 * C + c];
+        b += fin.sums[(int64_t)k * 2 * C + C + c];
+      }
+      bwd_coeffs(fin, c, a, b, blockIdx.x == 0, kk[0][tid], kk[1][tid], kk[2][tid]);
+    }
+  }
+  __syncthreads();
   if (r >= rpi) return;
   const int c0 = blockIdx.y * tpr * 8 + c8 * 8;
   ReluMask<T, ACT, MASKX> mk;
-  mk.init(w, b, mean, invstd, c0);
+  mk.init(fin.weight, bn_b, fin.mean, fin.invstd, c0);
   float A[8], B[8], Cc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    A[j] = kA[c0 + j];
-    B[j] = kB[c0 + j];
-    Cc[j] = kC[c0 + j];
+    A[j] = kk[0][c8 * 8 + j];
+    B[j] = kk[1][c8 * 8 + j];
+    Cc[j] = kk[2][c8 * 8 + j];
   }
   const int64_t row0 = (int64_t)blockIdx.x * rpb;
   const int64_t row1 = min(M, row0 + rpb);
@@ -553,111 +462,12 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, 
   }
 }
 
-// ---------------------------------------------------------------- small-M fused paths
-// Below ~8K rows (ResNet-50 layer3/layer4 at batch 32: M = 6272 / 1568) every BN kernel is
-// launch/latency-bound (~4-5 us each on MI355X whatever its size), so the separate finalize
-// launches are folded away:
-//  * forward: each apply block re-derives scale/shift for ITS 64 channels from the P partial rows
-//    (P <= 128, L2-resident) — the same double-precision finalize arithmetic, blockIdx.y == 0
-//    also writes save_mean / save_invstd / running stats — then applies;
-//  * backward (M <= 2048: layer4): one block owns 8 channels over ALL M rows, register-resident:
-//    Σdz, Σdz·x, in-block finalize, dx — reduce + finalize + dx in one launch.
-int g_bn_small = 1;  // small-M fused paths on (bn_set_small_paths: A/B and tests)
-constexpr int kSmallFinP = 128;
-constexpr int64_t kSmallBwdM = 8192;
-
-struct StatsFin {  // forward finalize inputs / outputs (bn_stats_finalize_k's arguments)
-  const float* weight;
-  const float* bias;
-  float* running_mean;
-  float* running_var;
-  float momentum, eps;
-  float* save_mean;
-  float* save_invstd;
-};
-
-template <typename T, bool ACT, bool RES>
-__global__ __launch_bounds__(kBlock) void bn_fin_apply_k(const T* __restrict__ x, const T* __restrict__ res,
-                                                         T* __restrict__ y, const float* __restrict__ psum,
-                                                         const float* __restrict__ psq, int P, int64_t M, int C,
-                                                         int64_t rpb, StatsFin fin) {
-  __shared__ double red[2][32][64];
-  __shared__ float s_sc[64], s_sh[64];
-  const int tid = threadIdx.x, cx = tid & 7, ry = tid >> 3;
-  const int cb = blockIdx.x * 64, c0 = cb + cx * 8;
-  // ---- finalize this block's 64 channels (fixed summation order: identical in every block)
-  float a[8], b[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
-  for (int p = ry; p < P; p += 32) {
-    const float4* ps = reinterpret_cast<const float4*>(psum + (int64_t)p * C + c0);
-    const float4* pq = reinterpret_cast<const float4*>(psq + (int64_t)p * C + c0);
-    const float4 s0 = ps[0], s1 = ps[1], q0 = pq[0], q1 = pq[1];
-    a[0] += s0.x; a[1] += s0.y; a[2] += s0.z; a[3] += s0.w; a[4] += s1.x; a[5] += s1.y; a[6] += s1.z; a[7] += s1.w;
-    b[0] += q0.x; b[1] += q0.y; b[2] += q0.z; b[3] += q0.w; b[4] += q1.x; b[5] += q1.y; b[6] += q1.z; b[7] += q1.w;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    red[0][ry][cx * 8 + j] = a[j];
-    red[1][ry][cx * 8 + j] = b[j];
-  }
-  __syncthreads();
-  if (tid < 64) {
-    double sa = 0.0, sb = 0.0;
-    for (int i = 0; i < 32; ++i) {
-      sa += red[0][i][tid];
-      sb += red[1][i][tid];
-    }
-    const int c = cb + tid;
-    const double mean = sa / (double)M;
-    double var = sb / (double)M - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)fin.eps));
-    const float w = fin.weight ? fin.weight[c] : 1.f;
-    const float bb = fin.bias ? fin.bias[c] : 0.f;
-    const float sc = w * invstd;
-    s_sc[tid] = sc;
-    s_sh[tid] = bb - (float)mean * sc;
-    if (blockIdx.y == 0) {
-      fin.save_mean[c] = (float)mean;
-      fin.save_invstd[c] = invstd;
-      if (fin.running_mean != nullptr) {
-        const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-        fin.running_mean[c] = (float)((1.0 - fin.momentum) * fin.running_mean[c] + fin.momentum * mean);
-        fin.running_var[c] = (float)((1.0 - fin.momentum) * fin.running_var[c] + fin.momentum * unbiased);
-      }
-    }
-  }
-  __syncthreads();
-  float sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = s_sc[cx * 8 + j];
-    sh[j] = s_sh[cx * 8 + j];
-  }
-  // ---- apply rows [y*rpb, +rpb)
-  const int64_t row1 = min(M, (int64_t)(blockIdx.y + 1) * rpb);
-  for (int64_t row = (int64_t)blockIdx.y * rpb + ry; row < row1; row += 32) {
-    const int64_t off = row * C + c0;
-    float v[8], rr[8];
-    Vec8<T>::load(x + off, v);
-    if (RES) Vec8<T>::load(res + off, rr);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = fmaf(v[j], sc[j], sh[j]);
-      if (RES) t += rr[j];
-      if (ACT) t = fmaxf(t, 0.f);
-      v[j] = t;
-    }
-    Vec8<T>::store(y + off, v);
-  }
-}
-
-// grid C/8, block 256: 8 channels (one 16-byte vector per row) x all M <= 2048 rows.  Every
-// thread loads its <= 8 rows of dy / x (/ y) ONCE, in one burst (all loads in flight), keeps
-// them packed in registers across the block reduction and the in-block finalize, and writes
-// dx from them: one memory round trip per tensor (a row loop re-reading the data was
-// latency-bound: 47-100 us at M = 6272).
+// ---------------------------------------------------------------- small-M backward
+// Below ~2K rows (ResNet-50 layer4 at batch 32: M = 1568) the reduce + dx pair is latency-bound,
+// so one block owns 8 channels over ALL M rows: grid C/8, block 256.  Every thread loads its
+// <= 8 rows of dy / x (/ y) ONCE, in one burst (all loads in flight), keeps them packed in
+// registers across the block reduction and the in-block finalize, and writes dx from them: one
+// memory round trip per tensor, no atomics, deterministic.
 constexpr int kBwdRows = 8;
 
 template <typename T>
@@ -732,21 +542,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_small_k(const T* __restrict__ dy, c
     ksum[which][j] = acc;
   }
   __syncthreads();
-  if (tid < 8) {
-    const int c = c0 + tid;
-    const double a = ksum[0][tid], b = ksum[1][tid];
-    const double mu = fin.mean[c], is = fin.invstd[c];
-    const double sum_dz_xhat = is * (b - mu * a);
-    if (fin.dweight) fin.dweight[c] = (float)sum_dz_xhat;
-    if (fin.dbias) fin.dbias[c] = (float)a;
-    const double g = fin.weight ? fin.weight[c] : 1.0;
-    const double A = g * is;
-    const double Bc = fin.training ? -A * is * sum_dz_xhat / (double)M : 0.0;
-    const double Cc = fin.training ? -A * a / (double)M - Bc * mu : 0.0;
-    kk[0][tid] = (float)A;
-    kk[1][tid] = (float)Bc;
-    kk[2][tid] = (float)Cc;
-  }
+  if (tid < 8) bwd_coeffs(fin, c0 + tid, ksum[0][tid], ksum[1][tid], true, kk[0][tid], kk[1][tid], kk[2][tid]);
   __syncthreads();
   float A[8], B[8], Cc[8];
 #pragma unroll
@@ -776,52 +572,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_small_k(const T* __restrict__ dy, c
   }
 }
 
-int g_fin2 = 1;  // wide finalize on (bn_set_fin2: A/B against the one-level kernels)
-
-// Wide finalize launch (false: not applicable — C % 16, or disabled)
-template <bool BWD>
-bool launch_fin_wide(const float* pa, const float* pb, int P, int C, int64_t M, const Fin2Fwd& ff, const BwdFin& bf,
-                     float* kA, float* kB, float* kC, hipStream_t stream) {
-  if (!g_fin2 || C % 16 != 0) return false;
-  hipLaunchKernelGGL((bn_fin_wide_k<BWD>), dim3(C / 16), dim3(1024), 0, stream, pa, pb, P, C, M, ff, bf, kA, kB, kC);
-  return true;
-}
-
-// small-M forward: finalize folded into the apply (returns false when the shape is not covered)
-bool launch_fin_apply(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* psum,
-                      const float* psq, int P, const float* weight, const float* bias, float* running_mean,
-                      float* running_var, float momentum, float eps, int act, float* save_mean, float* save_invstd,
-                      hipStream_t stream) {
-  if (g_bn_small == 0 || P > kSmallFinP || M > 2 * kSmallBwdM || C % 64 != 0 || (dtype != kBF16 && dtype != kF16))
-    return false;
-  const int groups = C / 64;
-  int64_t R = (M + 127) / 128;  // >= 4 rows per thread-lane (32 lanes)
-  const int64_t cap = 512 / groups > 0 ? 512 / groups : 1;
-  if (R > cap) R = cap;
-  if (R < 1) R = 1;
-  const int64_t rpb = (M + R - 1) / R;
-  R = (M + rpb - 1) / rpb;
-  const StatsFin fin{weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd};
-  const dim3 grid(groups, (unsigned)R);
-  HYP_DISPATCH_FLOAT(dtype, T, {
-    const T* xt = static_cast<const T*>(x);
-    const T* rt = static_cast<const T*>(res);
-    T* yt = static_cast<T*>(y);
-    if (act && res)
-      hipLaunchKernelGGL((bn_fin_apply_k<T, true, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P, M,
-                         C, rpb, fin);
-    else if (act)
-      hipLaunchKernelGGL((bn_fin_apply_k<T, true, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P, M,
-                         C, rpb, fin);
-    else if (res)
-      hipLaunchKernelGGL((bn_fin_apply_k<T, false, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P, M,
-                         C, rpb, fin);
-    else
-      hipLaunchKernelGGL((bn_fin_apply_k<T, false, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, psum, psq, P,
-                         M, C, rpb, fin);
-  });
-  return true;
-}
+int g_bn_small = 1;  // small-M one-launch backward on (bn_set_small_paths: A/B and tests)
 
 // small-M backward: reduce + finalize + dx in one launch (false when not covered)
 bool launch_bwd_small(int dtype, bool maskx, bool act, const void* dy, const void* x, const void* y, void* dx,
@@ -830,7 +581,7 @@ bool launch_bwd_small(int dtype, bool maskx, bool act, const void* dy, const voi
     return false;
   const dim3 grid(C / 8);
   // 256 threads x 8 register-resident rows (M <= 2048: layer4).  Wider blocks for layer3's 6272
-  // rows (512 x 13, 1024 x 8) spill VGPRs: that case keeps the 3-kernel path.
+  // rows (512 x 13, 1024 x 8) spill VGPRs: that case keeps the 2-kernel path.
 #define HYP_BN_SMALL(ACTV, RESV, MX)                                                                               \
   hipLaunchKernelGGL((bn_bwd_small_k<T, ACTV, RESV, MX, kBlock, kBwdRows>), grid, dim3(kBlock), 0, stream, dyt, xt, \
                      yt, dxt, drt, M, C, fin, bias)
@@ -861,69 +612,83 @@ bool launch_bwd_small(int dtype, bool maskx, bool act, const void* dy, const voi
   return true;
 }
 
+template <typename T, bool FIN>
+void launch_apply(bool act, const void* res, dim3 grid, hipStream_t stream, const T* xt, T* yt, const float* scale,
+                  const float* shift, const FwdFin& fin, int64_t M, int C, const BnGeom& ga) {
+  const T* rt = static_cast<const T*>(res);
+#define HYP_BN_APPLY(ACTV, RESV)                                                                                  \
+  hipLaunchKernelGGL((bn_apply_k<T, ACTV, RESV, FIN>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, fin, \
+                     M, C, ga.tpr, ga.rpi, ga.rows_per_block)
+  if (act && res)
+    HYP_BN_APPLY(true, true);
+  else if (act)
+    HYP_BN_APPLY(true, false);
+  else if (res)
+    HYP_BN_APPLY(false, true);
+  else
+    HYP_BN_APPLY(false, false);
+#undef HYP_BN_APPLY
+}
+
 }  // namespace
 
 // ======================================================================== host launchers
 void bn_set_small_paths(int on) { g_bn_small = on ? 1 : 0; }
 
-hipError_t bn_workspace_rows(int64_t M, int C, int* P_out) {
-  BnGeom g;
-  if (!bn_geom(M, C, kStatsBlocks, g)) return hipErrorInvalidValue;
-  *P_out = g.P;
-  return hipSuccess;
+hipError_t bn_stats(int dtype, const void* x, int64_t M, int C, double* sums, hipStream_t stream) {
+  BnGeom gs;
+  if (!stats_geom(M, C, gs)) return hipErrorInvalidValue;
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    hipLaunchKernelGGL(bn_stats_k<T>, dim3(gs.P, gs.gy), dim3(kBlock), 0, stream, static_cast<const T*>(x), M, C,
+                       gs.tpr, gs.rpi, gs.rows_per_block, sums);
+  });
+  return hipGetLastError();
 }
-
-void bn_set_fin2(int on) { g_fin2 = on ? 1 : 0; }
 
 hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_t M, int C, const float* weight,
                       const float* bias, float* running_mean, float* running_var, float momentum, float eps,
-                      int training, int act, float* psum, float* psq, float* save_mean, float* save_invstd,
-                      float* scale, float* shift, hipStream_t stream) {
-  BnGeom gs, ga;
-  if (!bn_geom(M, C, kStatsBlocks, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+                      int training, int act, double* sums, float* save_mean, float* save_invstd, float* scale,
+                      float* shift, hipStream_t stream) {
+  if (training) {
+    const hipError_t e = bn_stats(dtype, x, M, C, sums, stream);
+    if (e != hipSuccess) return e;
+    return bn_forward_from_sums(dtype, x, res, y, M, C, weight, bias, running_mean, running_var, momentum, eps, act,
+                                sums, save_mean, save_invstd, stream);
+  }
+  BnGeom ga;
+  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_eval_consts_k, dim3((C + 255) / 256), dim3(256), 0, stream, C, weight, bias, running_mean,
+                     running_var, eps, save_mean, save_invstd, scale, shift);
   HYP_DISPATCH_FLOAT(dtype, T, {
-    const T* xt = static_cast<const T*>(x);
-    if (training) {
-      hipLaunchKernelGGL(bn_stats_partial_k<T>, dim3(gs.P, gs.gy), dim3(kBlock), 0, stream, xt, M, C, gs.tpr, gs.rpi,
-                         gs.rows_per_block, psum, psq);
-      if (launch_fin_apply(dtype, x, res, y, M, C, psum, psq, gs.P, weight, bias, running_mean, running_var, momentum,
-                           eps, act, save_mean, save_invstd, stream))
-        return hipGetLastError();
-      const Fin2Fwd ff{weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift};
-      if (!launch_fin_wide<false>(psum, psq, gs.P, C, M, ff, BwdFin{}, nullptr, nullptr, nullptr, stream))
-        hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum,
-                           psq, gs.P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean,
-                           save_invstd, scale, shift);
-    } else {
-      hipLaunchKernelGGL(bn_eval_consts_k, dim3((C + 255) / 256), dim3(256), 0, stream, C, weight, bias, running_mean,
-                         running_var, eps, save_mean, save_invstd, scale, shift);
-    }
-    const dim3 grid(ga.P, ga.gy);
-    const T* rt = static_cast<const T*>(res);
-    T* yt = static_cast<T*>(y);
-    if (act && res)
-      hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
-    else if (act)
-      hipLaunchKernelGGL((bn_apply_k<T, true, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
-    else if (res)
-      hipLaunchKernelGGL((bn_apply_k<T, false, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
-    else
-      hipLaunchKernelGGL((bn_apply_k<T, false, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
+    launch_apply<T, false>(act != 0, res, dim3(ga.P, ga.gy), stream, static_cast<const T*>(x), static_cast<T*>(y),
+                           scale, shift, FwdFin{}, M, C, ga);
+  });
+  return hipGetLastError();
+}
+
+// Training-mode BN forward whose per-channel sums were produced elsewhere (the conv epilogue of
+// conv_igemm.hip, the split-K reduce, or bn_stats): one apply launch, finalize inline.
+hipError_t bn_forward_from_sums(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                                const float* weight, const float* bias, float* running_mean, float* running_var,
+                                float momentum, float eps, int act, const double* sums, float* save_mean,
+                                float* save_invstd, hipStream_t stream) {
+  BnGeom ga;
+  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  const FwdFin fin{sums,        weight,     bias, running_mean, running_var, momentum, eps, save_mean,
+                   save_invstd, 1.0 / (double)M, M > 1 ? (double)M / (double)(M - 1) : 1.0};
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    launch_apply<T, true>(act != 0, res, dim3(ga.P, ga.gy), stream, static_cast<const T*>(x), static_cast<T*>(y),
+                          nullptr, nullptr, fin, M, C, ga);
   });
   return hipGetLastError();
 }
 
 template <typename T>
 void launch_bn_dx(bool maskx, bool act, bool res, dim3 grid, hipStream_t stream, const T* dy, const T* x, const T* y,
-                  T* dx, T* dres, const float* kA, const float* kB, const float* kC, int64_t M, int C,
-                  const BnGeom& ga, const float* w, const float* b, const float* mean, const float* invstd) {
-#define HYP_BN_DX(ACTV, RESV, MX)                                                                                 \
-  hipLaunchKernelGGL((bn_bwd_dx_k<T, ACTV, RESV, MX>), grid, dim3(kBlock), 0, stream, dy, x, y, dx, dres, kA, kB, \
-                     kC, M, C, ga.tpr, ga.rpi, ga.rows_per_block, w, b, mean, invstd)
+                  T* dx, T* dres, const BwdFin& fin, int64_t M, int C, const BnGeom& ga, const float* b) {
+#define HYP_BN_DX(ACTV, RESV, MX)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_dx_k<T, ACTV, RESV, MX>), grid, dim3(kBlock), 0, stream, dy, x, y, dx, dres, fin, M, C, \
+                     ga.tpr, ga.rpi, ga.rows_per_block, b)
   if (maskx)
     HYP_BN_DX(true, false, true);
   else if (act && res)
@@ -939,17 +704,15 @@ void launch_bn_dx(bool maskx, bool act, bool res, dim3 grid, hipStream_t stream,
 
 hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, void* dx, void* dres, int64_t M, int C,
                        const float* weight, const float* bias, const float* save_mean, const float* save_invstd,
-                       int training, int act, float* pdz, float* pdzx, float* dweight, float* dbias, float* kA,
-                       float* kB, float* kC, hipStream_t stream) {
+                       int training, int act, double* sums, float* dweight, float* dbias, hipStream_t stream) {
   BnGeom gs, ga;
-  if (!bn_geom(M, C, kStatsBlocks, gs) || !bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
+  if (!stats_geom(M, C, gs) || !bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
   // act with no forward output given: recompute the ReLU mask from x (training stats only: the
   // eval-mode constants are running stats, which the mask recomputation below does not model)
   const bool maskx = act && y == nullptr;
   if (maskx && (!training || dres != nullptr)) return hipErrorInvalidValue;
-  if (launch_bwd_small(dtype, maskx, act != 0, dy, x, y, dx, dres, M, C,
-                       BwdFin{weight, save_mean, save_invstd, training, dweight, dbias}, bias, stream))
-    return hipGetLastError();
+  const BwdFin fin{weight, save_mean, save_invstd, training, dweight, dbias, sums, 1.0 / (double)M};
+  if (launch_bwd_small(dtype, maskx, act != 0, dy, x, y, dx, dres, M, C, fin, bias, stream)) return hipGetLastError();
   HYP_DISPATCH_FLOAT(dtype, T, {
     const T* dyt = static_cast<const T*>(dy);
     const T* xt = static_cast<const T*>(x);
@@ -957,62 +720,32 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
     const dim3 grs(gs.P, gs.gy);
     if (maskx)
       hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, true>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
-                         gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
+                         gs.rpi, gs.rows_per_block, sums, weight, bias, save_mean, save_invstd);
     else if (act)
       hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
-                         gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
+                         gs.rpi, gs.rows_per_block, sums, weight, bias, save_mean, save_invstd);
     else
       hipLaunchKernelGGL((bn_bwd_reduce_k<T, false, false>), grs, dim3(kBlock), 0, stream, dyt, xt, yt, M, C, gs.tpr,
-                         gs.rpi, gs.rows_per_block, pdz, pdzx, weight, bias, save_mean, save_invstd);
-    const BwdFin bf{weight, save_mean, save_invstd, training, dweight, dbias};
-    if (!launch_fin_wide<true>(pdz, pdzx, gs.P, C, M, Fin2Fwd{}, bf, kA, kB, kC, stream))
-      hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, pdz,
-                         pdzx, gs.P, C, M, weight, save_mean, save_invstd, training, dweight, dbias, kA, kB, kC);
+                         gs.rpi, gs.rows_per_block, sums, weight, bias, save_mean, save_invstd);
     launch_bn_dx<T>(maskx, act, dres != nullptr, dim3(ga.P, ga.gy), stream, dyt, xt, yt, static_cast<T*>(dx),
-                    static_cast<T*>(dres), kA, kB, kC, M, C, ga, weight, bias, save_mean, save_invstd);
+                    static_cast<T*>(dres), fin, M, C, ga, bias);
   });
   return hipGetLastError();
 }
 
-}  // namespace hyp
-
-namespace hyp {
-// Training-mode BN forward whose per-channel partial sums were produced elsewhere (the conv
-// epilogue of conv_igemm.hip: one partial row per M-tile) — finalize + apply only, no statistics
-// pass over x.
-hipError_t bn_forward_from_partials(int dtype, const void* x, const void* res, void* y, int64_t M, int C,
-                                    const float* weight, const float* bias, float* running_mean, float* running_var,
-                                    float momentum, float eps, int act, const float* psum, const float* psq, int P,
-                                    float* save_mean, float* save_invstd, float* scale, float* shift,
-                                    hipStream_t stream) {
+// dy is already dz (masked by its producer, e.g. the dgrad epilogue) and the Σdz, Σdz·x sums are
+// complete: only the dx pass remains (the residual gradient is dz itself).
+hipError_t bn_backward_dx(int dtype, const void* dz, const void* x, void* dx, int64_t M, int C, const float* weight,
+                          const float* save_mean, const float* save_invstd, int training, const double* sums,
+                          float* dweight, float* dbias, hipStream_t stream) {
   BnGeom ga;
-  if (!bn_geom(M, C, 2048, ga)) return hipErrorInvalidValue;
-  if (launch_fin_apply(dtype, x, res, y, M, C, psum, psq, P, weight, bias, running_mean, running_var, momentum, eps,
-                       act, save_mean, save_invstd, stream))
-    return hipGetLastError();
-  const Fin2Fwd ff{weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift};
-  if (!launch_fin_wide<false>(psum, psq, P, C, M, ff, BwdFin{}, nullptr, nullptr, nullptr, stream))
-    hipLaunchKernelGGL(bn_stats_finalize_k, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh, kFinGr), 0, stream, psum,
-                       psq, P, C, M, weight, bias, running_mean, running_var, momentum, eps, save_mean, save_invstd,
-                       scale, shift);
+  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  const BwdFin fin{weight, save_mean, save_invstd, training, dweight, dbias, sums, 1.0 / (double)M};
   HYP_DISPATCH_FLOAT(dtype, T, {
-    const T* xt = static_cast<const T*>(x);
-    const T* rt = static_cast<const T*>(res);
-    T* yt = static_cast<T*>(y);
-    const dim3 grid(ga.P, ga.gy);
-    if (act && res)
-      hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
-    else if (act)
-      hipLaunchKernelGGL((bn_apply_k<T, true, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
-    else if (res)
-      hipLaunchKernelGGL((bn_apply_k<T, false, true>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
-    else
-      hipLaunchKernelGGL((bn_apply_k<T, false, false>), grid, dim3(kBlock), 0, stream, xt, rt, yt, scale, shift, M, C,
-                         ga.tpr, ga.rpi, ga.rows_per_block);
+    launch_bn_dx<T>(false, false, false, dim3(ga.P, ga.gy), stream, static_cast<const T*>(dz),
+                    static_cast<const T*>(x), nullptr, static_cast<T*>(dx), nullptr, fin, M, C, ga, nullptr);
   });
   return hipGetLastError();
 }
+
 }  // namespace hyp

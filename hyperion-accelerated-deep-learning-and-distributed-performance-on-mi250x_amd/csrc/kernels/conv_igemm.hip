@@ -17,8 +17,8 @@
 // Tiles BM x BN x 64 (BM, BN ∈ {64, 128}), 4 waves as 2 x 2, v_mfma_f32_16x16x32_{bf16,f16},
 // double-buffered LDS with the (row >> 1) & 7 chunk swizzle of gemm_mfma.hip, XCD-aware tile
 // order.  Epilogue: bf16/f16 store + (optional) per-channel Σy, Σy² over the tile's rows of the
-// ROUNDED outputs, written as one partial row per M-tile — exactly the partial layout the BN
-// finalize kernel (bn_act.hip) consumes, so BN's separate statistics pass over y disappears.
+// ROUNDED outputs, added atomically into the [2][K] sums the BN apply finalizes inline
+// (bn_act.hip), so BN's separate statistics pass over y and its finalize launch disappear.
 // Requirements: C % 64 == 0 (every ResNet conv but the 3-channel stem), 16-byte aligned tensors.
 #include "hyp_common.h"
 #include "hyp_kernels.h"
@@ -63,8 +63,8 @@ struct ConvArgs {
   const uint16_t* w;     // [K, R, S, C]
   uint16_t* out;         // [N, P, Q, K]
   const uint16_t* zero;  // >= 1 KiB of zeros
-  float* psum;           // [Mtiles, K] or null
-  float* psq;
+  double* psum;          // Σy accumulator [kStatSlots][2][K] (fp64, zeroed by the caller) or null
+  double* psq;           // psum + K: Σy²
   int N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw;
   int M;                 // N*P*Q
   int group;             // M-tiles per tile-order group (see conv_fwd_group)
@@ -276,6 +276,16 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
   __syncthreads();
+  // one no-return f64 atomic per channel per tile, issued BEFORE the tile's stores so their
+  // ~1 us memory-side latency overlaps the store phase instead of extending the workgroup's drain
+  if (STATS && tid < BN) {
+    const int k = n0 + tid;
+    if (k < a.K) {
+      const int64_t slot = (int64_t)(tm % kStatSlots) * 2 * a.K;
+      unsafeAtomicAdd(a.psum + slot + k, (double)(red[0 * BN + tid] + red[2 * BN + tid]));
+      unsafeAtomicAdd(a.psq + slot + k, (double)(red[1 * BN + tid] + red[3 * BN + tid]));
+    }
+  }
   constexpr int kChunksPerRow = BN / 8;
 #pragma unroll
   for (int it = 0; it < BM * kChunksPerRow / kThreads; ++it) {
@@ -294,13 +304,6 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
         Vec8<T>::store(reinterpret_cast<T*>(&v), o);
       }
       *reinterpret_cast<uint4*>(a.out + (int64_t)m * a.K + k) = v;
-    }
-  }
-  if (STATS && tid < BN) {
-    const int k = n0 + tid;
-    if (k < a.K) {
-      a.psum[(int64_t)tm * a.K + k] = red[0 * BN + tid] + red[2 * BN + tid];
-      a.psq[(int64_t)tm * a.K + k] = red[1 * BN + tid] + red[3 * BN + tid];
     }
   }
 }
@@ -374,7 +377,7 @@ int conv_fwd_splits(int M, int K, int nk, int bm, int bn) {
   return max(1, sp);
 }
 
-hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, float* psum, float* psq,
+hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
                     const SplitkEpilogue* ep, const void* addend) {
@@ -407,7 +410,7 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
       else e = launch<f16_t, 64, 64>(a, false, dgrad, st);
     }
     if (e != hipSuccess) return e;
-    if (psum != nullptr) {  // BN statistics from the reduce (rows of kStatRows)
+    if (psum != nullptr) {  // BN statistics from the reduce (atomics per kStatRows-row block)
       if (alpha != 1.f || (ep != nullptr && ep->U != nullptr)) return hipErrorInvalidValue;
       return splitk_reduce_stats(dtype, part, out, a.M, K, a.splits, psum, psq, st);
     }

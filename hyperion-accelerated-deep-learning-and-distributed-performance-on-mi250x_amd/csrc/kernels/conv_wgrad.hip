@@ -258,19 +258,19 @@ hipError_t reduce_launch(const float* part, T* out, int64_t n, int splits, float
 namespace {
 // Split-K reduce of a convolution's [splits, M, K] fp32 partials with the BN-statistics epilogue
 // of conv_fwd_k: out = Σ_s part[s] rounded to T, and per-channel Σy, Σy² of the ROUNDED outputs
-// over kStatRows-row blocks -> psum/psq [ceil(M / kStatRows), K] (the partial layout the BN
-// finalize consumes).  Used when a forward conv has too few output tiles to fill 256 CUs
+// over kStatRows-row blocks, added atomically into psum[K] / psq[K] (the sums the BN apply
+// finalizes inline).  Used when a forward conv has too few output tiles to fill 256 CUs
 // (ResNet-50 layer3/4: 200-392 tiles, 55 us at 0.8 workgroups per CU).  Block = 64 column quads
-// (256 channels, 16-byte loads) x 4 row lanes; fixed summation order (deterministic).
+// (256 channels, 16-byte loads) x 4 row lanes.
 template <typename T>
 __global__ __launch_bounds__(256) void splitk_reduce_stats_k(const float* __restrict__ part, T* __restrict__ out,
-                                                             int M, int K, int splits, float* __restrict__ psum,
-                                                             float* __restrict__ psq) {
+                                                             int M, int K, int splits, int rows,
+                                                             double* __restrict__ psum, double* __restrict__ psq) {
   __shared__ float red[2][4][256];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.y * 256 + tx * 4;
-  const int r0 = blockIdx.x * kStatRows;
-  const int r1 = min(M, r0 + kStatRows);
+  const int r0 = blockIdx.x * rows;
+  const int r1 = min(M, r0 + rows);
   const int64_t slab = (int64_t)M * K;
   f32x4 cs = {0.f, 0.f, 0.f, 0.f}, cq = cs;
   if (c < K) {
@@ -300,27 +300,31 @@ __global__ __launch_bounds__(256) void splitk_reduce_stats_k(const float* __rest
     red[1][ty][tx * 4 + e] = cq[e];
   }
   __syncthreads();
-  if (ty == 0 && c < K) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int j = tx * 4 + e;
-      psum[(int64_t)blockIdx.x * K + c + e] = (red[0][0][j] + red[0][1][j]) + (red[0][2][j] + red[0][3][j]);
-      psq[(int64_t)blockIdx.x * K + c + e] = (red[1][0][j] + red[1][1][j]) + (red[1][2][j] + red[1][3][j]);
+  // one atomic per channel per block: 64 consecutive channels per wave instruction (256-byte runs)
+  if (threadIdx.x < 256) {
+    const int j = threadIdx.x, ch = blockIdx.y * 256 + j;
+    if (ch < K) {
+      const int64_t slot = (int64_t)(blockIdx.x % kStatSlots) * 2 * K;
+      unsafeAtomicAdd(psum + slot + ch, (double)((red[0][0][j] + red[0][1][j]) + (red[0][2][j] + red[0][3][j])));
+      unsafeAtomicAdd(psq + slot + ch, (double)((red[1][0][j] + red[1][1][j]) + (red[1][2][j] + red[1][3][j])));
     }
   }
 }
 }  // namespace
 
-hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, float* psum,
-                               float* psq, hipStream_t st) {
+hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, double* psum,
+                               double* psq, hipStream_t st) {
   if (K % 4 != 0 || splits < 1 || M < 1) return hipErrorInvalidValue;
-  const dim3 grid((M + kStatRows - 1) / kStatRows, (K + 255) / 256);
+  // kStatRows-row blocks (fewer atomic adders per channel) unless that leaves < 512 blocks
+  const int cb = (K + 255) / 256;
+  const int rows = (int64_t)((M + kStatRows - 1) / kStatRows) * cb >= 512 ? kStatRows : 16;
+  const dim3 grid((M + rows - 1) / rows, cb);
   if (dtype == kBF16)
     hipLaunchKernelGGL(splitk_reduce_stats_k<bf16_t>, grid, dim3(256), 0, st, part, static_cast<bf16_t*>(out), M, K,
-                       splits, psum, psq);
+                       splits, rows, psum, psq);
   else if (dtype == kF16)
     hipLaunchKernelGGL(splitk_reduce_stats_k<f16_t>, grid, dim3(256), 0, st, part, static_cast<f16_t*>(out), M, K,
-                       splits, psum, psq);
+                       splits, rows, psum, psq);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -18,6 +18,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from ..ops import _native
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 
 from ..ops.batchnorm import BatchNormAct2d
@@ -135,17 +136,22 @@ class ResNet(nn.Module):
         x = self.layer3(x)
         return self.layer4(x)
 
+    # Each forward (or graph stage) opens one zero_scope: every BN statistics accumulator of the
+    # pass is a slice of one buffer zeroed by a single fill (ops/_native.py ZeroArena).
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.forward_features(x)
-        x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        with _native.zero_scope(self, "forward", x.device):
+            x = self.forward_features(x)
+            x = torch.flatten(self.avgpool(x), 1)
+            return self.fc(x)
 
     def _bottom(self, x: torch.Tensor) -> torch.Tensor:
-        return self.layer1(self.maxpool(conv_bn_act(self.conv1, self.bn1, x)))
+        with _native.zero_scope(self, "bottom", x.device):
+            return self.layer1(self.maxpool(conv_bn_act(self.conv1, self.bn1, x)))
 
     def _top(self, h: torch.Tensor) -> torch.Tensor:
-        x = self.layer4(self.layer3(self.layer2(h)))
-        return self.fc(torch.flatten(self.avgpool(x), 1))
+        with _native.zero_scope(self, "top", h.device):
+            x = self.layer4(self.layer3(self.layer2(h)))
+            return self.fc(torch.flatten(self.avgpool(x), 1))
 
     def graph_stages(self):
         """``forward(x) == top(bottom(x))``, cut after layer1: 99% of the gradient bytes (layer2-4,

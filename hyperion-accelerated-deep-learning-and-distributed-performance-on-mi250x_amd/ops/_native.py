@@ -21,6 +21,7 @@ _ERR: Optional[BaseException] = None
 _TRIED = False
 
 DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+STAT_SLOTS = 8  # hyp::kStatSlots: BN statistics sums are [STAT_SLOTS, 2, C] fp64 (csrc/hyp_kernels.h)
 
 
 def _load():
@@ -100,3 +101,68 @@ def reset_counters() -> None:
 def loaded_path() -> Optional[str]:
     m = _load()
     return getattr(m, "__file__", None) if m is not None else None
+
+
+class ZeroArena:
+    """Pre-zeroed fp64 workspace for the kernels' atomic accumulators (BN statistics sums).
+
+    The BN kernels ADD per-channel sums into [2, C] fp64 buffers with f64 atomics, so every
+    buffer must be zero before its producer runs.  A fresh ``torch.zeros`` per BN layer would be one
+    fill launch each (~100 per ResNet-50 step); instead a model opens ``zero_scope`` around its
+    forward and every BN call takes a slice of ONE buffer zeroed by a single fill (the forward's
+    and, reserved at forward time, the backward's sums).  The first call under a key learns the
+    size; later calls preallocate it.  Without an open scope (or past the learnt size), ``take``
+    returns a fresh zeroed tensor — always correct, just one fill more.  Slices keep the buffer
+    alive, so a later scope never recycles memory an unfinished backward still reads.
+    """
+
+    ALIGN = 32  # doubles (256 B): every slice starts on its own 256-byte run
+
+    def __init__(self, buf: Optional[torch.Tensor]):
+        self.buf = buf
+        self.off = 0
+        self.used = 0
+
+    def take(self, n: int, device) -> torch.Tensor:
+        need = -(-n // self.ALIGN) * self.ALIGN
+        self.used += need
+        if self.buf is not None and self.buf.device == torch.device(device) and self.off + need <= self.buf.numel():
+            t = self.buf[self.off:self.off + n]
+            self.off += need
+            return t
+        return torch.zeros(n, device=device, dtype=torch.float64)
+
+
+_ARENAS: list = []
+
+
+class zero_scope:
+    """``with zero_scope(owner, key, device):`` — one zero-fill for every accumulator taken inside
+    (nested scopes reuse the outermost).  ``owner`` keeps the learnt size per ``key``."""
+
+    def __init__(self, owner, key: str, device):
+        self.owner, self.key, self.device = owner, key, torch.device(device)
+        self.arena = None
+
+    def __enter__(self):
+        if _ARENAS or self.device.type != "cuda":
+            return self
+        sizes = self.owner.__dict__.setdefault("_zero_arena_sizes", {})
+        n = sizes.get(self.key, 0)
+        self.arena = ZeroArena(torch.zeros(n, device=self.device, dtype=torch.float64) if n else None)
+        _ARENAS.append(self.arena)
+        return self
+
+    def __exit__(self, *exc):
+        if self.arena is not None:
+            _ARENAS.pop()
+            sizes = self.owner.__dict__["_zero_arena_sizes"]
+            sizes[self.key] = max(sizes.get(self.key, 0), self.arena.used)
+        return False
+
+
+def zeroed(n: int, device) -> torch.Tensor:
+    """A zeroed fp64 [n] accumulator: a slice of the open ``zero_scope`` arena, else fresh."""
+    if _ARENAS:
+        return _ARENAS[-1].take(n, device)
+    return torch.zeros(n, device=device, dtype=torch.float64)

@@ -7,9 +7,9 @@ relu`` as three or four separate kernels (MIOpen BN, elementwise add, ReLU) per 
 ``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` subclass (same parameters, buffers and
 state-dict keys) whose forward takes an optional ``residual`` and applies ReLU when
 ``act=True``.  On GPU with channels-last activations it runs the gfx950 kernels in
-``csrc/kernels/bn_act.hip``: one stats pass + one apply pass forward (residual + ReLU folded into
-the apply), one reduce pass + one dx pass backward (ReLU mask from the saved output, residual
-gradient written by the same pass).  Elsewhere it runs the PyTorch reference composition, which
+``csrc/kernels/bn_act.hip``: one stats pass (atomic per-channel sums) + one apply pass forward
+that finalizes inline (residual + ReLU folded into the apply), one reduce pass + one dx pass
+backward (ReLU mask from the saved output, residual gradient written by the same pass).  Elsewhere it runs the PyTorch reference composition, which
 is also the test oracle.
 """
 from __future__ import annotations
@@ -66,7 +66,10 @@ class _BNActFn(torch.autograd.Function):
             residual = residual.to(x.dtype)
         if residual is not None and x.dim() == 4 and not residual.is_contiguous(memory_format=torch.channels_last):
             residual = residual.contiguous(memory_format=torch.channels_last)
-        y, mean, invstd = C.bn_fwd(x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act)
+        sums = _native.zeroed(_native.STAT_SLOTS * 2 * x.shape[1], x.device) if training else None
+        ctx.bsums = _native.zeroed(_native.STAT_SLOTS * 2 * x.shape[1], x.device)  # the backward's Σdz, Σdz·x (same fill)
+        y, mean, invstd = C.bn_fwd(x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act,
+                                   sums=sums)
         ctx.act = act
         ctx.training = training
         ctx.has_res = residual is not None
@@ -80,8 +83,9 @@ class _BNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, weight, bias, mean, invstd = ctx.saved_tensors
         need_res = ctx.has_res and ctx.needs_input_grad[1]
+        bsums, ctx.bsums = ctx.bsums, None  # a second backward (retain_graph) takes fresh zeros
         dx, dres, dw, db = _native.native().bn_bwd(
-            dy, x, y, weight, bias, mean, invstd, ctx.training, ctx.act, need_res
+            dy, x, y, weight, bias, mean, invstd, ctx.training, ctx.act, need_res, sums=bsums
         )
         return (
             dx if ctx.needs_input_grad[0] else None,

@@ -7,10 +7,10 @@ SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
 
 ``conv_bn_act(conv, bn, x, residual)`` (training mode, bf16/f16 channels-last):
 
-* forward  — ``csrc/kernels/conv_igemm.hip`` computes the convolution on MFMA AND the per-channel
-  Σy, Σy² of its (rounded) outputs in the epilogue; BN then only finalizes the statistics and runs
-  one apply pass with the residual add and ReLU folded in (``bn_act.hip``).  The separate BN
-  statistics read of the conv output is gone.
+* forward  — ``csrc/kernels/conv_igemm.hip`` computes the convolution on MFMA AND adds the
+  per-channel Σy, Σy² of its (rounded) outputs into a zeroed accumulator in the epilogue (float
+  atomics); BN then runs ONE apply launch that finalizes the statistics inline, with the residual
+  add and ReLU folded in (``bn_act.hip``).  No separate statistics read, no finalize launch.
 * backward — the fused BN/ReLU/residual backward (``bn_act.hip``) produces dconv; the data
   gradient of a stride-1 convolution is the same implicit-GEMM kernel in DGRAD mode (the forward
   filter read flipped and channel-transposed through ds_read_b64_tr_b16, no filter copy); weight
@@ -166,10 +166,16 @@ class _ConvBNActFn(torch.autograd.Function):
     def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out,
                 branch, bidx):
         C = _native.native()
-        yc, psum, psq = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True)
+        # BN statistics: the conv epilogue ADDS Σy, Σy² into a zeroed [2, K] slice of the forward's
+        # arena; the apply finalizes inline.  The backward's Σdz, Σdz·x slice is reserved now so
+        # it shares the same single zero-fill.
+        K = w.shape[0]
+        sums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
+        ctx.bsums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
+        yc, _, _ = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True, sums=sums)
         if residual is not None:
             residual = residual.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        out, mean, invstd = C.bn_fwd_partials(yc, residual, psum, psq, bn_w, bn_b, rm, rv, momentum, eps, act)
+        out, mean, invstd = C.bn_fwd_sums(yc, residual, sums, bn_w, bn_b, rm, rv, momentum, eps, act)
         # without a residual the backward recomputes the ReLU mask from yc (no need to keep `out`)
         ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
@@ -182,7 +188,9 @@ class _ConvBNActFn(torch.autograd.Function):
         stride, padding, act, has_res = ctx.cfg
         link_in, link_out, branch, bidx = ctx.links
         need_res = has_res and ctx.needs_input_grad[6]
-        dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res)
+        bsums, ctx.bsums = ctx.bsums, None  # a second backward (retain_graph) takes fresh zeros
+        dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res,
+                                                      sums=bsums)
         if need_res and link_out is not None and link_out.armed and _will_run(link_out.first_node):
             link_out.dres, dres = dres, None  # added by the block's first conv dgrad instead
         add = None

@@ -37,12 +37,13 @@ small = torch.zeros(8, device=dev)
 print("fill8          us/kernel", round(graph_time(lambda: small.fill_(1.0)), 2))
 x = torch.randn(32, 64, 56, 56, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
 w = (torch.randn(64, 64, 1, 1, device=dev) * 0.1).bfloat16().contiguous(memory_format=torch.channels_last)
-y, psum, psq = C_.conv_fwd(x, w, 1, 1, 0, 0, True)
+sums = torch.zeros(8, 2, w.shape[0], device="cuda", dtype=torch.float64)
+y, psum, psq = C_.conv_fwd(x, w, 1, 1, 0, 0, True, sums=sums)
 bw, bb = torch.ones(64, device=dev), torch.zeros(64, device=dev)
 rm, rv = torch.zeros(64, device=dev), torch.ones(64, device=dev)
-print("partials", tuple(psum.shape))
+print("sums", tuple(sums.shape))
 print("conv1x1+stats   us/kernel", round(graph_time(lambda: C_.conv_fwd(x, w, 1, 1, 0, 0, True), n=20), 2))
-print("bn_fwd_partials us/call  ", round(graph_time(lambda: C_.bn_fwd_partials(y, None, psum, psq, bw, bb, rm, rv, 0.1, 1e-5, True), n=50), 2))
+print("bn_fwd_sums us/call      ", round(graph_time(lambda: C_.bn_fwd_sums(y, None, sums, bw, bb, rm, rv, 0.1, 1e-5, True), n=50), 2))
 big = torch.empty(51 * 2**20 // 4, device=dev)
 print("fill51MB        us/kernel", round(graph_time(lambda: big.fill_(1.0), n=20), 2))
 print("fill51MB+fill8  us/pair  ", round(graph_time(lambda: (big.fill_(1.0), small.fill_(2.0)), n=20), 2))

@@ -31,8 +31,8 @@ def test_conv_fwd_and_stats_match_fp32(shape, dtype):
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
     yr = y.float()
-    torch.testing.assert_close(psum.sum(0), yr.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
-    torch.testing.assert_close(psq.sum(0), (yr * yr).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(psum.sum(0).float(), yr.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(psq.sum(0).float(), (yr * yr).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("shape", SHAPES[:5])
@@ -157,8 +157,8 @@ def test_conv_splitk_fwd_stats_and_dgrad(shape, splits):
     ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
     yr = y.float()
-    torch.testing.assert_close(psum.sum(0), yr.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
-    torch.testing.assert_close(psq.sum(0), (yr * yr).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(psum.sum(0).float(), yr.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(psq.sum(0).float(), (yr * yr).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
     if K % 64 == 0:
         dy = torch.randn(N, K, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         dx = _native.native().conv_dgrad(dy, w, p, p, splits=splits)
