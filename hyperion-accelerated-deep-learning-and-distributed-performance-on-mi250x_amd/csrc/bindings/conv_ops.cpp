@@ -61,10 +61,61 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   return {y, acc.select(1, 0), acc.select(1, 1)};  // [kStatSlots, K] each: .sum(0) = per-channel totals
 }
 
+// Eval-mode conv -> BN -> (+ residual) -> (ReLU) in one launch: y = act(conv(x, w) * scale[k] +
+// shift[k] (+ residual)), scale / shift the BN's running-stat affine (fp32 [K]).
+at::Tensor conv_fwd_affine(const at::Tensor& x, const at::Tensor& w, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                           const at::Tensor& scale, const at::Tensor& shift, const c10::optional<at::Tensor>& residual,
+                           bool act) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_fwd_affine: channels-last 4D input and weight");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "conv_fwd_affine: bf16/f16 input and weight of one dtype");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int K = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(1) == C && hyp::conv_fwd_supported(C, K), "conv_fwd_affine: needs C % 64 == 0, K % 8 == 0");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == K &&
+                  shift.numel() == K && scale.is_contiguous() && shift.is_contiguous(),
+              "conv_fwd_affine: fp32 [K] scale / shift");
+  const int P = (H + 2 * ph - R) / sh + 1, Q = (W + 2 * pw - S) / sw + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "conv_fwd_affine: empty output");
+  const at::DeviceGuard guard(x.device());
+  auto y = at::empty({N, K, P, Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res)
+    TORCH_CHECK(residual->sizes() == y.sizes() && residual->scalar_type() == y.scalar_type() &&
+                    residual->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_fwd_affine: residual must match the output (shape, dtype, channels-last)");
+  const int M = N * P * Q;
+  int bm = 128, bn = 128;
+  hyp::conv_fwd_tile(M, K, &bm, &bn);
+  const int splits = plan_splits(M, K, R * S * (C / 64), bm, bn, -1);
+  at::Tensor slabs;
+  if (splits > 1) slabs = at::empty({splits, M, K}, x.options().dtype(at::kFloat));
+  hyp::SplitkEpilogue ep;
+  ep.N = K;
+  ep.scale = scale.data_ptr<float>();
+  ep.shift = shift.data_ptr<float>();
+  ep.residual = has_res ? residual->data_ptr() : nullptr;
+  ep.act = act ? 1 : 0;
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
+                              nullptr, nullptr, N, H, W, C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn,
+                              0, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f, &ep));
+  return y;
+}
+
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
 // filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
+// bn_mode >= 0: BN-backward epilogue for the BN layer whose OUTPUT is dx's tensor (hyp::BnBwdEpilogue):
+// bn_x its input [N,C,H,W], bn_y its output (mode 2), bn_w/bn_b/bn_mean/bn_invstd (mode 1), bn_sums
+// a zeroed fp64 [kStatSlots*2*C] accumulator; the result is then dz = dx · mask.
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
-                      int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend) {
+                      int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend,
+                      const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_y,
+                      const c10::optional<at::Tensor>& bn_w, const c10::optional<at::Tensor>& bn_b,
+                      const c10::optional<at::Tensor>& bn_mean, const c10::optional<at::Tensor>& bn_invstd,
+                      int64_t bn_mode, const c10::optional<at::Tensor>& bn_sums) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -84,6 +135,13 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   int bm = 128, bn = 128;
   hyp::conv_fwd_tile(N * H * W, C, &bm, &bn);
+  if (bn_mode >= 0) {
+    // BN-backward epilogue: its store phase (x / y reads, masked stores, column sums) is memory
+    // bound — 64-wide tiles keep 3-4 workgroups per CU on it (128x128: 264 VGPRs, one; 3x slower
+    // on layer1, scripts/bnb_tiles.py); 64 rows for 1x1 (one MFMA k-step), 128 for 3x3
+    bn = 64;
+    bm = R * S == 1 ? 64 : 128;
+  }
   if (bm_req > 0) bm = (int)bm_req;
   if (bn_req > 0) bn = (int)bn_req;
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
@@ -96,11 +154,39 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
     TORCH_CHECK(addend->sizes() == dx.sizes() && addend->scalar_type() == dx.scalar_type() &&
                     addend->is_contiguous(at::MemoryFormat::ChannelsLast) && addend->device() == dx.device(),
                 "conv_dgrad: addend must match dx (shape, dtype, channels-last)");
+  hyp::BnBwdEpilogue bnb;
+  const bool fuse_bn = bn_mode >= 0;
+  if (fuse_bn) {
+    TORCH_CHECK(bn_mode <= 2 && bn_x.has_value() && bn_x->defined() && bn_sums.has_value() && bn_sums->defined(),
+                "conv_dgrad: BN epilogue needs bn_x and bn_sums");
+    TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_x->scalar_type() == dx.scalar_type() &&
+                    bn_x->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_dgrad: bn_x must match dx (shape, dtype, channels-last)");
+    TORCH_CHECK(bn_sums->scalar_type() == at::kDouble && bn_sums->is_contiguous() &&
+                    bn_sums->numel() == 2 * C * hyp::kStatSlots,
+                "conv_dgrad: bn_sums must be a zeroed fp64 [kStatSlots * 2 * C] tensor");
+    if (bn_mode == 2)
+      TORCH_CHECK(bn_y.has_value() && bn_y->defined() && bn_y->sizes() == dx.sizes() &&
+                      bn_y->scalar_type() == dx.scalar_type() && bn_y->is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "conv_dgrad: bn_y must match dx");
+    if (bn_mode == 1)
+      TORCH_CHECK(bn_mean.has_value() && bn_invstd.has_value() && bn_mean->numel() == C && bn_invstd->numel() == C,
+                  "conv_dgrad: mode 1 needs bn_mean / bn_invstd");
+    bnb.x = bn_x->data_ptr();
+    bnb.y = bn_mode == 2 ? bn_y->data_ptr() : nullptr;
+    bnb.w = ptr_or_null<float>(bn_w);
+    bnb.b = ptr_or_null<float>(bn_b);
+    bnb.mean = ptr_or_null<float>(bn_mean);
+    bnb.invstd = ptr_or_null<float>(bn_invstd);
+    bnb.mode = (int)bn_mode;
+    bnb.sums = bn_sums->data_ptr<double>();
+  }
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                               zero_page(dy.device()).data_ptr(), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
                               dph, dpw, bm, bn, 1, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr,
-                              cur_stream(), 1.f, nullptr, (add && splits == 1) ? addend->data_ptr() : nullptr));
-  if (add && splits > 1) dx.add_(*addend);  // the split-K reduce has no addend input
+                              cur_stream(), 1.f, nullptr, (add && (splits == 1 || fuse_bn)) ? addend->data_ptr() : nullptr,
+                              fuse_bn ? &bnb : nullptr));
+  if (add && splits > 1 && !fuse_bn) dx.add_(*addend);  // the plain split-K reduce has no addend input
   return dx;
 }
 
@@ -349,6 +435,10 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
         pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1, pybind11::arg("splits") = -1,
         pybind11::arg("sums") = pybind11::none());
+  m.def("conv_fwd_affine", &conv_fwd_affine, "eval conv + folded BN affine (+ residual) (+ ReLU), one launch",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
+        pybind11::arg("pw"), pybind11::arg("scale"), pybind11::arg("shift"),
+        pybind11::arg("residual") = pybind11::none(), pybind11::arg("act") = false);
   m.def("conv_set_stages", [](int64_t fwd, int64_t wgrad) {
     hyp::conv_set_stages((int)fwd);
     hyp::conv_wgrad_set_stages((int)wgrad);
@@ -370,7 +460,11 @@ void register_conv_ops(pybind11::module& m) {
   m.def("global_avgpool_bwd", &global_avgpool_bwd, "NHWC global average pool backward");
   m.def("conv_dgrad", &conv_dgrad, "stride-1 conv data gradient on MFMA (filter read flipped/transposed)",
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
-        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("addend") = pybind11::none());
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("addend") = pybind11::none(),
+        pybind11::arg("bn_x") = pybind11::none(), pybind11::arg("bn_y") = pybind11::none(),
+        pybind11::arg("bn_w") = pybind11::none(), pybind11::arg("bn_b") = pybind11::none(),
+        pybind11::arg("bn_mean") = pybind11::none(), pybind11::arg("bn_invstd") = pybind11::none(),
+        pybind11::arg("bn_mode") = -1, pybind11::arg("bn_sums") = pybind11::none());
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

@@ -71,6 +71,29 @@ std::vector<at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& x, const 
   return {dx, dres, dwb[0], dwb[1]};
 }
 
+// BN backward dx pass only: dz (already masked, e.g. by the dgrad BN epilogue) and its complete
+// Σdz, Σdz·x sums -> (dx, dweight, dbias); the residual gradient is dz itself.
+std::vector<at::Tensor> bn_bwd_dx(const at::Tensor& dz, const at::Tensor& x, const c10::optional<at::Tensor>& weight,
+                                  const at::Tensor& save_mean, const at::Tensor& save_invstd, bool training,
+                                  const at::Tensor& sums) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(dz.sizes() == x.sizes() && dz.scalar_type() == x.scalar_type() && is_rows_by_channels(dz) &&
+                  is_rows_by_channels(x),
+              "bn_bwd_dx: dz and x of one shape / dtype, channels-last");
+  TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.is_contiguous() && sums.numel() == 2 * C * hyp::kStatSlots,
+              "bn_bwd_dx: sums must be an fp64 [kStatSlots * 2 * C] tensor");
+  const at::DeviceGuard guard(x.device());
+  auto dx = at::empty_like(x);
+  auto dwb = at::empty({2, C}, x.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::bn_backward_dx(dtype_code(x), dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C,
+                                    ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
+                                    save_invstd.data_ptr<float>(), training ? 1 : 0, sums.data_ptr<double>(),
+                                    dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, cur_stream()));
+  return {dx, dwb[0], dwb[1]};
+}
+
 // ---- column sums (bias gradients) ---------------------------------------------------------------
 // x: [..., N] contiguous -> Σ over all leading dims, [N] in out_dtype (default x's dtype)
 at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dtype) {
@@ -153,6 +176,7 @@ void register_norm_ops(pybind11::module& m) {
         pybind11::arg("y"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("save_mean"),
         pybind11::arg("save_invstd"), pybind11::arg("training"), pybind11::arg("act"), pybind11::arg("has_res"),
         pybind11::arg("sums") = pybind11::none());
+  m.def("bn_bwd_dx", &bn_bwd_dx, "BN backward dx pass from a pre-masked dz and its complete sums");
   m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());

@@ -139,10 +139,26 @@ void conv_fwd_tile(int M, int K, int* bm, int* bn);
 // addend (optional, splits == 1, no stats): out [M, K] += addend after rounding (fused residual grad).
 // dgrad != 0: stride-1 data gradient; "in" is dY [N,H,W,C], "w" the ORIGINAL filter [C][R][S][K]
 // (read flipped and transposed in-kernel), (ph, pw) the dgrad padding R-1-p.
+// bnb (dgrad only): the BatchNorm-backward epilogue above (any split count).
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
-                    const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr);
+                    const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr,
+                    const struct BnBwdEpilogue* bnb = nullptr);
+// Optional BatchNorm-backward epilogue of a stride-1 data gradient dX whose tensor is the output of a
+// fused BN(+residual)(+ReLU) layer: the stored value becomes dz = dX·mask (the BN input's upstream
+// gradient), and Σdz, Σdz·x per channel are added into `sums` — bn_backward_dx then needs no reduce
+// pass (ops/conv.py BNGradLink).
+struct BnBwdEpilogue {
+  const void* x = nullptr;  // [M, K] the BN layer's input (its conv output)
+  const void* y = nullptr;  // [M, K] the BN layer's output (mode 2 mask source)
+  const float* w = nullptr;  // mode 1 mask: x * (w*invstd) + (b - mean*w*invstd) > 0
+  const float* b = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  int mode = 0;              // 0: no mask (no ReLU); 1: ReLU mask recomputed from x; 2: mask y > 0
+  double* sums = nullptr;    // [kStatSlots][2][K] Σdz, Σdz·x (zeroed)
+};
 // Optional rank-r epilogue of a split-K reduce over an [M, N] output:
 //   out[m, n] += beta * (mask ? mask[m, n] : 1) * sum_j U[m, j] * V[j * sv_j + n * sv_n]
 // (U, V, mask in the output dtype).  U == nullptr: no epilogue.
@@ -153,6 +169,12 @@ struct SplitkEpilogue {
   int64_t sv_j = 0, sv_n = 0;
   int N = 0, r = 0;
   float beta = 1.f;
+  // per-column affine (+ residual) (+ ReLU) — the eval-mode BatchNorm folded into the epilogue:
+  // out[m, n] = act(round(acc) * scale[n] + shift[n] (+ residual[m, n]))   (no rank-r term)
+  const float* scale = nullptr;
+  const float* shift = nullptr;
+  const void* residual = nullptr;
+  int act = 0;
 };
 // out (T) = alpha * sum over `splits` fp32 partial slabs of n elements (fixed order; n % 4 == 0)
 // [+ the rank-r epilogue]
@@ -163,6 +185,10 @@ hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int
 constexpr int kStatRows = 64;  // (16 when that leaves < 512 blocks)
 hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, int K, int splits, double* psum,
                                double* psq, hipStream_t st);
+// Split-K reduce of a data gradient [splits, M, K] (+ addend [M, K] in T) with the BN-backward
+// epilogue: out = dz = round(round(Σ part) + addend) · mask, Σdz, Σdz·x into bnb.sums.
+hipError_t splitk_reduce_bnb(int dtype, const float* part, void* out, const void* addend, int M, int K, int splits,
+                             const BnBwdEpilogue& bnb, hipStream_t st);
 // Split-K plan for a convolution (forward or stride-1 dgrad) whose bm x bn tiling leaves fewer than
 // ~2 workgroups per CU: returns splits >= 1 over the nk = R*S*C/64 reduction steps.
 int conv_fwd_splits(int M, int K, int nk, int bm, int bn);

@@ -446,19 +446,37 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_k(const T* __restrict__ dy, 
   const int64_t row1 = min(M, row0 + rpb);
   const int64_t step = (int64_t)rpi * C;
   int64_t off = (row0 + r) * C + c0;
-  for (int64_t row = row0 + r; row < row1; row += rpi, off += step) {
+  int64_t row = row0 + r;
+  auto one = [&](const float (&gi)[8], const float (&xi)[8], const float (&yi)[8], int64_t o) {
+    float g[8], xo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = mk.keep(xi, yi, j) ? gi[j] : 0.f;
+      g[j] = d;
+      xo[j] = fmaf(A[j], d, fmaf(B[j], xi[j], Cc[j]));
+    }
+    Vec8<T>::store(dx + o, xo);
+    if (RES) Vec8<T>::store(dres + o, g);
+  };
+  for (; row + rpi < row1; row += 2 * rpi, off += 2 * step) {  // two rows' loads in flight
+    float g0[8], x0[8], y0[8], g1[8], x1[8], y1[8];
+    Vec8<T>::load(dy + off, g0);
+    Vec8<T>::load(dy + off + step, g1);
+    Vec8<T>::load(x + off, x0);
+    Vec8<T>::load(x + off + step, x1);
+    if (ACT && !MASKX) {
+      Vec8<T>::load(y + off, y0);
+      Vec8<T>::load(y + off + step, y1);
+    }
+    one(g0, x0, y0, off);
+    one(g1, x1, y1, off + step);
+  }
+  if (row < row1) {
     float g[8], xv[8], yv[8];
     Vec8<T>::load(dy + off, g);
     Vec8<T>::load(x + off, xv);
     if (ACT && !MASKX) Vec8<T>::load(y + off, yv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d = mk.keep(xv, yv, j) ? g[j] : 0.f;
-      g[j] = d;
-      xv[j] = fmaf(A[j], d, fmaf(B[j], xv[j], Cc[j]));
-    }
-    Vec8<T>::store(dx + off, xv);
-    if (RES) Vec8<T>::store(dres + off, g);
+    one(g, xv, yv, off);
   }
 }
 

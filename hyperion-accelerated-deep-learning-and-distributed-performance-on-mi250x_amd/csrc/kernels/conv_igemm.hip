@@ -70,7 +70,11 @@ struct ConvArgs {
   int group;             // M-tiles per tile-order group (see conv_fwd_group)
   int splits, steps_per_split;  // split-K over the reduction (splits > 1: fp32 partials, no STATS)
   float* part;                  // [splits, M, K] fp32 when splits > 1
-  const uint16_t* addend;       // optional [M, K] tensor added to the rounded output (no STATS, no split)
+  const uint16_t* addend;       // optional [M, K] tensor added to the rounded output (no split)
+  BnBwdEpilogue bnb;            // STATS && DGRAD: the BatchNorm-backward epilogue
+  const float* aff_scale;       // !STATS: out = act(round(acc) * scale[k] + shift[k] (+ addend)) (eval BN)
+  const float* aff_shift;
+  int aff_act;
 };
 
 // DGRAD = false: W is [K, R, S, C] (reduction contiguous; B tiles are row slices, read row-wise).
@@ -176,6 +180,32 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   };
 
+  // per-channel epilogue constants of this thread's store column (the eval-BN affine or the
+  // BN-backward ReLU-mask scale/shift), loaded before the main loop so the epilogue never waits
+  // on them (loaded there, they cost a full memory round trip per tile)
+  float asc[8], ash[8];
+  {
+    constexpr int kCpr = BN / 8;
+    const int my_k = n0 + (tid % kCpr) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asc[e] = ash[e] = 0.f;
+    if (!STATS && a.aff_scale != nullptr && my_k < a.K) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        asc[e] = a.aff_scale[my_k + e];
+        ash[e] = a.aff_shift[my_k + e];
+      }
+    }
+    if (STATS && DGRAD && a.bnb.mode == 1 && my_k < a.K) {  // ReluMask<MASKX> arithmetic of bn_act.hip
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sc = (a.bnb.w ? a.bnb.w[my_k + e] : 1.f) * a.bnb.invstd[my_k + e];
+        asc[e] = sc;
+        ash[e] = (a.bnb.b ? a.bnb.b[my_k + e] : 0.f) - a.bnb.mean[my_k + e] * sc;
+      }
+    }
+  }
+
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -230,9 +260,32 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   }
 
   // ---- epilogue.  acc[i][j][e] is out[m0 + wm*BM/2 + i*16 + c4*4 + e][n0 + wn*BN/2 + j*16 + r16].
+  // STATS && !DGRAD: forward BN statistics; STATS && DGRAD: the BN-backward epilogue (a.bnb).
+  constexpr bool FSTATS = STATS && !DGRAD, BNB = STATS && DGRAD;
   // Values are rounded to T once; the BN statistics use the rounded values (what BN will read),
   // and the tile is transposed through LDS so the global stores are whole 16-byte row chunks
   // (a raw accumulator store would be 2-byte scattered writes).
+  // Epilogue operand prefetch: the addend / BN-backward x, y chunks this thread will store,
+  // issued BEFORE the LDS transpose so their memory latency overlaps it (loaded inside the store
+  // loop, every iteration waited a full round trip: +18 us on a layer1 dgrad with the BN epilogue)
+  constexpr int kChunksPerRow = BN / 8;
+  constexpr int kIt = BM * kChunksPerRow / kThreads;
+  uint4 pd[kIt], px[kIt], py[kIt];
+  const bool has_add = !FSTATS && a.addend != nullptr;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int idx = it * kThreads + tid;
+    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
+    const int m = m0 + lr, k = n0 + ch * 8;
+    const bool ok = m < a.M && k < a.K;
+    const int64_t off = (int64_t)m * a.K + k;
+    pd[it] = px[it] = py[it] = uint4{0u, 0u, 0u, 0u};
+    if (has_add && ok) pd[it] = *reinterpret_cast<const uint4*>(a.addend + off);
+    if (BNB && ok) {
+      px[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.x) + off);
+      if (a.bnb.mode == 2) py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
+    }
+  }
   constexpr int kLd = BN + 8;  // padded LDS row (elements)
   uint16_t* tile = smem;       // [BM][kLd] of T (the K loop ended with a barrier: smem is free)
   float* red = reinterpret_cast<float*>(smem + BM * kLd);  // [2 (wm)][2 (sum, sq)][BN]
@@ -250,14 +303,14 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
         const int lc = wn * (BN / 2) + j * 16 + r16;
         const float v = rnd<T>(acc[i][j][e]);
         st1<T>(reinterpret_cast<T*>(tile) + lr * kLd + lc, v);
-        if (STATS && row_ok) {
+        if (FSTATS && row_ok) {
           csum[j] += v;
           csq[j] += v * v;
         }
       }
     }
   }
-  if (STATS) {
+  if (FSTATS) {
     // reduce over the 4 row groups of the wave (lanes l, l^16, l^32, l^48 share a column)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -278,7 +331,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   __syncthreads();
   // one no-return f64 atomic per channel per tile, issued BEFORE the tile's stores so their
   // ~1 us memory-side latency overlaps the store phase instead of extending the workgroup's drain
-  if (STATS && tid < BN) {
+  if (FSTATS && tid < BN) {
     const int k = n0 + tid;
     if (k < a.K) {
       const int64_t slot = (int64_t)(tm % kStatSlots) * 2 * a.K;
@@ -286,7 +339,12 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       unsafeAtomicAdd(a.psq + slot + k, (double)(red[1 * BN + tid] + red[3 * BN + tid]));
     }
   }
-  constexpr int kChunksPerRow = BN / 8;
+  // BNB: every thread keeps ONE 8-channel chunk column (kThreads % kChunksPerRow == 0) across its rows
+  float bs[8], bq[8];
+  if (BNB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs[e] = bq[e] = 0.f;
+  }
 #pragma unroll
   for (int it = 0; it < BM * kChunksPerRow / kThreads; ++it) {
     const int idx = it * kThreads + tid;
@@ -294,16 +352,83 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     const int m = m0 + lr, k = n0 + ch * 8;
     if (m < a.M && k < a.K) {
       uint4 v = *reinterpret_cast<const uint4*>(tile + lr * kLd + ch * 8);
-      if (!STATS && a.addend != nullptr) {
-        // out = round(round(acc) + addend): the same two roundings as a separate T add kernel
-        float o[8], d[8];
+      if (BNB) {
+        // dz = round(round(acc) + addend) * mask; Σdz, Σdz·x over the stored (rounded) values
+        float o[8], xv[8], yv[8];
         Vec8<T>::load(reinterpret_cast<const T*>(&v), o);
-        Vec8<T>::load(reinterpret_cast<const T*>(a.addend + (int64_t)m * a.K + k), d);
+        if (has_add) {
+          float d[8];
+          Vec8<T>::load(reinterpret_cast<const T*>(&pd[it]), d);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] += d[e];
+          for (int e = 0; e < 8; ++e) o[e] = rnd<T>(o[e] + d[e]);
+        }
+        Vec8<T>::load(reinterpret_cast<const T*>(&px[it]), xv);
+        Vec8<T>::load(reinterpret_cast<const T*>(&py[it]), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool keep = a.bnb.mode == 0 || (a.bnb.mode == 1 ? fmaf(xv[e], asc[e], ash[e]) > 0.f : yv[e] > 0.f);
+          o[e] = keep ? o[e] : 0.f;
+          bs[e] += o[e];
+          bq[e] += o[e] * xv[e];
+        }
+        Vec8<T>::store(reinterpret_cast<T*>(&v), o);
+      } else if (!STATS && (has_add || a.aff_scale != nullptr)) {
+        // out = round(round(acc) + addend): the same two roundings as a separate T add kernel;
+        // eval BN: out = round(act(round(acc) * scale + shift (+ addend))), the conv -> BN(eval)
+        // (-> + residual) (-> ReLU) composition in one store
+        float o[8];
+        Vec8<T>::load(reinterpret_cast<const T*>(&v), o);
+        if (a.aff_scale != nullptr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = fmaf(o[e], asc[e], ash[e]);
+        }
+        if (has_add) {
+          float d[8];
+          Vec8<T>::load(reinterpret_cast<const T*>(&pd[it]), d);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += d[e];
+        }
+        if (a.aff_act) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = fmaxf(o[e], 0.f);
+        }
         Vec8<T>::store(reinterpret_cast<T*>(&v), o);
       }
       *reinterpret_cast<uint4*>(a.out + (int64_t)m * a.K + k) = v;
+    }
+  }
+  if (BNB) {
+    // column sums: the lanes of a wave that share a chunk column (lane % kChunksPerRow) by xor
+    // shuffles, then the 4 waves through LDS in fixed order
+    static_assert(64 % kChunksPerRow == 0, "chunk columns repeat within a wave");
+#pragma unroll
+    for (int o = kChunksPerRow; o < 64; o <<= 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bs[e] += __shfl_xor(bs[e], o, 64);
+        bq[e] += __shfl_xor(bq[e], o, 64);
+      }
+    }
+    float* wred = reinterpret_cast<float*>(smem + BM * kLd);  // [4 waves][kChunksPerRow][16]
+    if (lane < kChunksPerRow) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        wred[(wave * kChunksPerRow + lane) * 16 + e] = bs[e];
+        wred[(wave * kChunksPerRow + lane) * 16 + 8 + e] = bq[e];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.K) {
+      const int chn = tid >> 3, e = tid & 7;
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        sa += wred[(w * kChunksPerRow + chn) * 16 + e];
+        sb += wred[(w * kChunksPerRow + chn) * 16 + 8 + e];
+      }
+      double* slot = a.bnb.sums + (int64_t)(tm % kStatSlots) * 2 * a.K;
+      unsafeAtomicAdd(slot + n0 + tid, (double)sa);
+      unsafeAtomicAdd(slot + a.K + n0 + tid, (double)sb);
     }
   }
 }
@@ -311,7 +436,9 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 template <typename T, int BM, int BN, int NB>
 hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.K + BN - 1) / BN) * a.splits;
-  if (dgrad)
+  if (dgrad && stats)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
+  else if (dgrad)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   else if (stats)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, false, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
@@ -380,13 +507,20 @@ int conv_fwd_splits(int M, int K, int nk, int bm, int bn) {
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
-                    const SplitkEpilogue* ep, const void* addend) {
+                    const SplitkEpilogue* ep, const void* addend, const BnBwdEpilogue* bnb) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
   if (splits > 1 && part == nullptr) return hipErrorInvalidValue;
-  if (addend != nullptr && (splits > 1 || psum != nullptr)) return hipErrorInvalidValue;
+  if (addend != nullptr && ((splits > 1 && bnb == nullptr) || psum != nullptr)) return hipErrorInvalidValue;
+  if (bnb != nullptr && (!dgrad || bnb->sums == nullptr || bnb->x == nullptr || (bnb->mode == 2 && bnb->y == nullptr) ||
+                         (bnb->mode == 1 && (bnb->mean == nullptr || bnb->invstd == nullptr)) || alpha != 1.f ||
+                         (ep != nullptr && ep->U != nullptr)))
+    return hipErrorInvalidValue;
   // alpha / the rank-r epilogue live in the split-K reduce
   if ((alpha != 1.f || (ep != nullptr && ep->U != nullptr)) && splits < 2) return hipErrorInvalidValue;
+  const bool aff = ep != nullptr && ep->scale != nullptr;
+  if (aff && (ep->shift == nullptr || ep->U != nullptr || dgrad || psum != nullptr || addend != nullptr || alpha != 1.f))
+    return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
   if (M64 <= 0 || M64 > INT32_MAX) return hipErrorInvalidValue;
   ConvArgs a{static_cast<const uint16_t*>(in), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out),
@@ -398,6 +532,11 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   a.splits = (nk + a.steps_per_split - 1) / a.steps_per_split;  // no empty splits
   a.part = part;
   a.addend = static_cast<const uint16_t*>(addend);
+  if (bnb != nullptr) a.bnb = *bnb;
+  a.aff_scale = aff ? ep->scale : nullptr;
+  a.aff_shift = aff ? ep->shift : nullptr;
+  a.aff_act = aff ? ep->act : 0;
+  if (aff && a.splits == 1) a.addend = static_cast<const uint16_t*>(ep->residual);
   if (a.splits > 1) {
     hipError_t e;
     if (dtype == kBF16) {
@@ -410,13 +549,14 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
       else e = launch<f16_t, 64, 64>(a, false, dgrad, st);
     }
     if (e != hipSuccess) return e;
+    if (bnb != nullptr) return splitk_reduce_bnb(dtype, part, out, addend, a.M, K, a.splits, *bnb, st);
     if (psum != nullptr) {  // BN statistics from the reduce (atomics per kStatRows-row block)
       if (alpha != 1.f || (ep != nullptr && ep->U != nullptr)) return hipErrorInvalidValue;
       return splitk_reduce_stats(dtype, part, out, a.M, K, a.splits, psum, psq, st);
     }
     return splitk_reduce(dtype, part, out, (int64_t)a.M * K, a.splits, st, alpha, ep);
   }
-  const bool stats = psum != nullptr && psq != nullptr;
+  const bool stats = (psum != nullptr && psq != nullptr) || bnb != nullptr;
   if (dtype == kBF16) {
     if (bm == 128 && bn == 128) return launch<bf16_t, 128, 128>(a, stats, dgrad, st);
     if (bm == 128 && bn == 64) return launch<bf16_t, 128, 64>(a, stats, dgrad, st);

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
 // on 256 CUs) and 4 independent accumulators, so 4 slab loads are in flight per thread.
 constexpr int kRedThreads = 64;
 
-template <typename T, bool LOWRANK>
+template <typename T, bool LOWRANK, bool AFF>
 __global__ __launch_bounds__(kRedThreads) void splitk_reduce_k(const float* __restrict__ part, T* __restrict__ out,
                                                                int64_t n, int splits, float alpha, SplitkEpilogue ep) {
   const int64_t i4 = ((int64_t)blockIdx.x * kRedThreads + threadIdx.x) * 4;
@@ -236,6 +236,16 @@ __global__ __launch_bounds__(kRedThreads) void splitk_reduce_k(const float* __re
     }
     acc += ep.beta * lr;
   }
+  if (AFF) {  // eval BN folded in: act(round(acc) * scale + shift (+ residual)), N % 4 == 0
+    const int64_t n0 = i4 % ep.N;
+    const T* res = static_cast<const T*>(ep.residual);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = fmaf(rnd<T>(acc[e]), ep.scale[n0 + e], ep.shift[n0 + e]);
+      if (res != nullptr) v += ld1<T>(res + i4 + e);
+      acc[e] = ep.act ? fmaxf(v, 0.f) : v;
+    }
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) st1<T>(out + i4 + e, acc[e]);
 }
@@ -245,11 +255,14 @@ hipError_t reduce_launch(const float* part, T* out, int64_t n, int splits, float
                          hipStream_t st) {
   const int blocks = (int)((n / 4 + kRedThreads - 1) / kRedThreads);
   if (ep != nullptr && ep->U != nullptr)
-    hipLaunchKernelGGL((splitk_reduce_k<T, true>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n, splits, alpha,
-                       *ep);
+    hipLaunchKernelGGL((splitk_reduce_k<T, true, false>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n, splits,
+                       alpha, *ep);
+  else if (ep != nullptr && ep->scale != nullptr)
+    hipLaunchKernelGGL((splitk_reduce_k<T, false, true>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n, splits,
+                       alpha, *ep);
   else
-    hipLaunchKernelGGL((splitk_reduce_k<T, false>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n, splits,
-                       alpha, SplitkEpilogue{});
+    hipLaunchKernelGGL((splitk_reduce_k<T, false, false>), dim3(blocks), dim3(kRedThreads), 0, st, part, out, n,
+                       splits, alpha, SplitkEpilogue{});
   return hipGetLastError();
 }
 
@@ -330,10 +343,105 @@ hipError_t splitk_reduce_stats(int dtype, const float* part, void* out, int M, i
   return hipGetLastError();
 }
 
+namespace {
+// Split-K reduce of a stride-1 data gradient with the BN-backward epilogue (conv_igemm.hip's BNB
+// epilogue for the split case): out = dz = round(round(Σ_s part[s]) + addend) · mask and Σdz,
+// Σdz·x per channel into slot blockIdx.x % kStatSlots of bnb.sums.  Same block shape as
+// splitk_reduce_stats_k (64 column quads x 4 row lanes, `rows` rows per block).
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_bnb_k(const float* __restrict__ part, T* __restrict__ out,
+                                                           const T* __restrict__ addend, int M, int K, int splits,
+                                                           int rows, BnBwdEpilogue bnb) {
+  __shared__ float red[2][4][256];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.y * 256 + tx * 4;
+  const int r0 = blockIdx.x * rows;
+  const int r1 = min(M, r0 + rows);
+  const int64_t slab = (int64_t)M * K;
+  const T* xb = static_cast<const T*>(bnb.x);
+  const T* yb = static_cast<const T*>(bnb.y);
+  float msc[4] = {0.f, 0.f, 0.f, 0.f}, msh[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bnb.mode == 1 && c < K) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sc = (bnb.w ? bnb.w[c + e] : 1.f) * bnb.invstd[c + e];
+      msc[e] = sc;
+      msh[e] = (bnb.b ? bnb.b[c + e] : 0.f) - bnb.mean[c + e] * sc;
+    }
+  }
+  f32x4 cs = {0.f, 0.f, 0.f, 0.f}, cq = cs;
+  if (c < K) {
+    for (int r = r0 + ty; r < r1; r += 4) {
+      const int64_t off = (int64_t)r * K + c;
+      const float* src = part + off;
+      f32x4 a0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src)), a1 = {0.f, 0.f, 0.f, 0.f};
+      int s = 1;
+      for (; s + 1 < splits; s += 2) {
+        a0 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (int64_t)s * slab));
+        a1 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (int64_t)(s + 1) * slab));
+      }
+      if (s < splits) a0 += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + (int64_t)s * slab));
+      const f32x4 acc = a0 + a1;
+      // 4 channels = one 8-byte run of each 2-byte operand
+      const uint2 rx = *reinterpret_cast<const uint2*>(xb + off);
+      const uint2 ry = bnb.mode == 2 ? *reinterpret_cast<const uint2*>(yb + off) : uint2{0u, 0u};
+      const uint2 rd = addend != nullptr ? *reinterpret_cast<const uint2*>(addend + off) : uint2{0u, 0u};
+      const T* hx = reinterpret_cast<const T*>(&rx);
+      const T* hy = reinterpret_cast<const T*>(&ry);
+      const T* hd = reinterpret_cast<const T*>(&rd);
+      T ov[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = rnd<T>(acc[e]);
+        if (addend != nullptr) v = rnd<T>(v + ld1<T>(hd + e));
+        const float xv = ld1<T>(hx + e);
+        const bool keep = bnb.mode == 0 || (bnb.mode == 1 ? fmaf(xv, msc[e], msh[e]) > 0.f : ld1<T>(hy + e) > 0.f);
+        v = keep ? v : 0.f;
+        st1<T>(ov + e, v);
+        cs[e] += v;
+        cq[e] += v * xv;
+      }
+      *reinterpret_cast<uint2*>(out + off) = *reinterpret_cast<const uint2*>(ov);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][ty][tx * 4 + e] = cs[e];
+    red[1][ty][tx * 4 + e] = cq[e];
+  }
+  __syncthreads();
+  const int j = threadIdx.x, ch = blockIdx.y * 256 + j;
+  if (ch < K) {
+    double* slot = bnb.sums + (int64_t)(blockIdx.x % kStatSlots) * 2 * K;
+    unsafeAtomicAdd(slot + ch, (double)((red[0][0][j] + red[0][1][j]) + (red[0][2][j] + red[0][3][j])));
+    unsafeAtomicAdd(slot + K + ch, (double)((red[1][0][j] + red[1][1][j]) + (red[1][2][j] + red[1][3][j])));
+  }
+}
+}  // namespace
+
+hipError_t splitk_reduce_bnb(int dtype, const float* part, void* out, const void* addend, int M, int K, int splits,
+                             const BnBwdEpilogue& bnb, hipStream_t st) {
+  if (K % 4 != 0 || splits < 1 || M < 1) return hipErrorInvalidValue;
+  const int cb = (K + 255) / 256;
+  const int rows = (int64_t)((M + kStatRows - 1) / kStatRows) * cb >= 512 ? kStatRows : 16;
+  const dim3 grid((M + rows - 1) / rows, cb);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(splitk_reduce_bnb_k<bf16_t>, grid, dim3(256), 0, st, part, static_cast<bf16_t*>(out),
+                       static_cast<const bf16_t*>(addend), M, K, splits, rows, bnb);
+  else if (dtype == kF16)
+    hipLaunchKernelGGL(splitk_reduce_bnb_k<f16_t>, grid, dim3(256), 0, st, part, static_cast<f16_t*>(out),
+                       static_cast<const f16_t*>(addend), M, K, splits, rows, bnb);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t splitk_reduce(int dtype, const float* part, void* out, int64_t n, int splits, hipStream_t st, float alpha,
                          const SplitkEpilogue* ep) {
   if (n % 4 != 0 || splits < 1) return hipErrorInvalidValue;
   if (ep != nullptr && ep->U != nullptr && (ep->N % 4 != 0 || ep->r < 8 || ep->r % 8 != 0 || n % ep->N != 0))
+    return hipErrorInvalidValue;
+  if (ep != nullptr && ep->scale != nullptr && (ep->N % 4 != 0 || n % ep->N != 0 || ep->shift == nullptr))
     return hipErrorInvalidValue;
   if (dtype == kBF16) return reduce_launch<bf16_t>(part, static_cast<bf16_t*>(out), n, splits, alpha, ep, st);
   if (dtype == kF16) return reduce_launch<f16_t>(part, static_cast<f16_t*>(out), n, splits, alpha, ep, st);

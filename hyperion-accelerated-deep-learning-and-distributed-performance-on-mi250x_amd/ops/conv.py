@@ -23,6 +23,7 @@ eval mode) falls back to ``bn(conv(x), residual)`` — the same math.
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Optional
 
@@ -33,8 +34,8 @@ from . import _native
 from . import streams as _streams
 
 
-def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
-    w = conv.weight
+def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d, w: Optional[torch.Tensor] = None) -> bool:
+    w = conv.weight if w is None else w
     return (
         x.is_cuda
         and x.dim() == 4
@@ -51,9 +52,44 @@ def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     )
 
 
+FUSE_BN_BACKWARD = True  # dgrad epilogue computes the producing BN layer's backward reduce (A/B switch)
+# Producer kinds that take the epilogue (mode 0: BN without ReLU, 1: BN+ReLU, 2: BN+residual+ReLU).
+# Mode 2 saves a 3-tensor reduce pass, the dx pass's y read and its dres write; modes 0/1 save only
+# a 2-tensor reduce, about what the epilogue's extra x read costs the dgrad's store phase
+# (scripts/bnb_tiles.py).  ResNet-50 bench on MI355X (scripts/gpu_ab_bnb.sh): none 5.73 ms,
+# {2} 5.60, {1,2} 5.58, {0,1,2} 5.60.
+FUSE_BN_MODES = {int(m) for m in os.environ.get("HYPERION_BNB_MODES", "1,2").split(",") if m.strip()}
+
+
+class BNGradLink:
+    """Hands the BatchNorm-backward reduction of a fused conv→BN(→+res)(→ReLU) layer (the
+    PRODUCER) to the data gradient of the conv that consumes its output.
+
+    The consumer's stride-1 dgrad kernel (``conv_igemm.hip`` BNB epilogue) then stores
+    dz = dX·ReLU-mask instead of dX and adds Σdz, Σdz·x into the producer's zeroed sums, so the
+    producer's backward is ONE dx pass (``bn_bwd_dx``) instead of a reduce pass + a dx pass, and
+    its residual gradient is dz itself (no extra write).  Masking is idempotent, so handing dz to
+    autograd is safe; the producer takes the fast path only when the gradient it receives IS that
+    dz object (any other contribution summed by autograd, or an epilogue that never ran, sends it
+    down the full path with fresh sums).  Each backward consumes the link once (``used``): a
+    second backward over a retained graph takes the full path."""
+
+    # no reference to the producer's OUTPUT here (it would be a ctx -> output -> grad_fn cycle):
+    # the mode-2 mask source is the consumer's own saved input, which is that output
+    __slots__ = ("yc", "bn_w", "bn_b", "mean", "invstd", "mode", "sums", "dz", "used")
+
+    def __init__(self, yc, bn_w, bn_b, mean, invstd, mode, sums):
+        self.yc, self.bn_w, self.bn_b = yc, bn_w, bn_b
+        self.mean, self.invstd, self.mode, self.sums = mean, invstd, mode, sums
+        self.dz = None
+        self.used = False
+
+
 def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
-           addend: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dX (+ addend: the identity-shortcut gradient of a residual block, fused into the store)."""
+           addend: Optional[torch.Tensor] = None, bn: Optional[BNGradLink] = None) -> torch.Tensor:
+    """dX (+ addend: the identity-shortcut gradient of a residual block, fused into the store).
+    ``bn``: the producing BN layer's link — when the native kernel runs, it returns dz = dX·mask
+    with the BN reduce done (``bn.dz`` is set)."""
     R, S = w.shape[2], w.shape[3]
     if (tuple(stride) == (1, 1) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0 and padding[0] <= R - 1
             and padding[1] <= S - 1 and _native.use_native(dy, op="dgrad")):
@@ -63,6 +99,14 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
         _native.count("dgrad")
+        if bn is not None and not bn.used and bn.yc.dtype == dy.dtype:
+            bn.used = True
+            _native.count("dgrad_bn_fused")
+            bn.dz = _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend, bn_x=bn.yc,
+                                                bn_y=x if bn.mode == 2 else None, bn_w=bn.bn_w, bn_b=bn.bn_b,
+                                                bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,
+                                                bn_sums=bn.sums)
+            return bn.dz
         return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend)
     if (R == 1 and S == 1 and tuple(padding) == (0, 0) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0
             and _native.use_native(dy, op="dgrad")):
@@ -164,7 +208,7 @@ def _will_run(ref) -> bool:
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out,
-                branch, bidx):
+                branch, bidx, prod):
         C = _native.native()
         # BN statistics: the conv epilogue ADDS Σy, Σy² into a zeroed [2, K] slice of the forward's
         # arena; the apply finalizes inline.  The backward's Σdz, Σdz·x slice is reserved now so
@@ -180,6 +224,11 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
         ctx.links = (link_in, link_out, branch, bidx)
+        ctx.prod = prod  # the BNGradLink of the fused layer that produced x (or None)
+        # this layer's own link for the conv that will consume `out` (reached as out.grad_fn.bnlink)
+        mode = (2 if residual is not None else 1) if act else 0
+        ctx.bnlink = (BNGradLink(yc, bn_w, bn_b, mean, invstd, mode, ctx.bsums)
+                      if FUSE_BN_BACKWARD and mode in FUSE_BN_MODES else None)
         return out
 
     @staticmethod
@@ -189,8 +238,18 @@ class _ConvBNActFn(torch.autograd.Function):
         link_in, link_out, branch, bidx = ctx.links
         need_res = has_res and ctx.needs_input_grad[6]
         bsums, ctx.bsums = ctx.bsums, None  # a second backward (retain_graph) takes fresh zeros
-        dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act, need_res,
-                                                      sums=bsums)
+        own = ctx.bnlink
+        if own is not None and own.dz is not None and dout is own.dz:
+            # the consumer's dgrad epilogue already masked dout and summed Σdz, Σdz·x: dx pass only
+            dyc, dbw, dbb = _native.native().bn_bwd_dx(dout, yc, bn_w, mean, invstd, True, own.sums)
+            dres = dout if need_res else None
+        else:
+            if own is not None and own.used:
+                bsums = None  # the epilogue ran into these sums, but its dz is not all of dout
+            dyc, dres, dbw, dbb = _native.native().bn_bwd(dout, yc, out, bn_w, bn_b, mean, invstd, True, act,
+                                                          need_res, sums=bsums)
+        if own is not None:
+            own.dz, own.used = None, True  # consumed: a retained-graph second backward takes the full path
         if need_res and link_out is not None and link_out.armed and _will_run(link_out.first_node):
             link_out.dres, dres = dres, None  # added by the block's first conv dgrad instead
         add = None
@@ -201,6 +260,7 @@ class _ConvBNActFn(torch.autograd.Function):
             # off the critical path: forked BEFORE the data gradient, so the two overlap
             dw = _streams.run_on_side(lambda: _wgrad(dyc, x, w, stride, padding), [dyc, x], dyc.device)
         dx = None
+        prod = ctx.prod
         if ctx.needs_input_grad[0]:
             if branch is not None and branch.users == 2 and _will_run(branch.nodes[1 - bidx]):
                 pend, branch.pending = branch.pending, None
@@ -208,15 +268,80 @@ class _ConvBNActFn(torch.autograd.Function):
                     pend = None  # our own dX from an abandoned pass (its partner never ran): stale
                 if pend is None:  # first of the block input's two consumers: park dX for the second
                     branch.pending = (bidx, _dgrad(dyc, x, w, stride, padding, addend=add))
-                else:
+                else:  # the second computes the whole gradient of x: it can run the BN epilogue
                     other = pend[1]
-                    dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add)
+                    dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add, bn=prod)
             else:
-                dx = _dgrad(dyc, x, w, stride, padding, addend=add)
+                # the whole gradient of x unless another op consumes x outside our links (then the
+                # producer sees a summed gradient and takes its full path)
+                dx = _dgrad(dyc, x, w, stride, padding, addend=add, bn=prod)
         if dw is None and ctx.needs_input_grad[1]:
             dw = _wgrad(dyc, x, w, stride, padding)
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
-                dres, None, None, None, None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None, None, None, None)
+
+
+def _eval_affine(bn: nn.Module, device):
+    """Eval-mode BN as a per-channel affine (scale = γ/sqrt(running_var + eps), shift = β -
+    running_mean·scale, fp32), cached on the module until its statistics or parameters change."""
+    ts = (bn.running_mean, bn.running_var, bn.weight, bn.bias)
+    key = tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)
+    cache = bn.__dict__.get("_hyp_eval_affine")
+    if cache is not None and cache[0] == key:
+        return cache[1], cache[2]
+    with torch.no_grad():
+        inv = torch.rsqrt(bn.running_var.float() + bn.eps)
+        sc = inv * bn.weight.float() if bn.weight is not None else inv
+        sh = -bn.running_mean.float() * sc
+        if bn.bias is not None:
+            sh = sh + bn.bias.float()
+        sc, sh = sc.contiguous(), sh.contiguous()
+    bn.__dict__["_hyp_eval_affine"] = (key, sc, sh)
+    return sc, sh
+
+
+def _inference_weight(conv: nn.Conv2d, dt: torch.dtype) -> torch.Tensor:
+    """The conv weight in ``dt`` for a no-grad forward, cast once and cached (autocast would re-cast
+    the fp32 weight on every call)."""
+    w = conv.weight
+    if w.dtype == dt:
+        return w
+    key = (dt, w.data_ptr(), w._version)
+    cache = conv.__dict__.get("_hyp_cast")
+    if cache is None or cache[0] != key:
+        with torch.no_grad():
+            cache = (key, w.to(dt).contiguous(memory_format=torch.channels_last))
+        conv.__dict__["_hyp_cast"] = cache
+    return cache[1]
+
+
+def _conv_bn_eval(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor,
+                  residual: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Inference: conv → BN(running stats) → (+ residual) → (ReLU) as ONE launch — the BN folded into
+    the conv kernel's epilogue as a per-channel affine (``conv_fwd_affine``; the split-K reduce
+    carries the same epilogue).  None when outside the kernel's envelope."""
+    if bn.training or not bn.track_running_stats or bn.running_mean is None:
+        return None
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x, conv.weight, bn.weight,
+                                                                                      bn.bias, residual)):
+        return None  # eval-mode training (frozen BN): the autograd path below
+    if not (x.is_cuda and _native.use_native(x, op="conv") and _native.use_native(x, op="bn")):
+        return None
+    dt = x.dtype
+    if torch.is_autocast_enabled(x.device.type):
+        dt = torch.get_autocast_dtype(x.device.type)
+    if dt not in (torch.bfloat16, torch.float16):
+        return None
+    xc = x.to(dt) if x.dtype != dt else x
+    w = _inference_weight(conv, dt)
+    if not _native_conv_ok(xc, conv, w):
+        return None
+    if residual is not None:
+        residual = residual.to(dt).contiguous(memory_format=torch.channels_last)
+    sc, sh = _eval_affine(bn, x.device)
+    _native.count("conv_bn_eval")
+    return _native.native().conv_fwd_affine(xc, w, conv.stride[0], conv.stride[1], conv.padding[0], conv.padding[1],
+                                            sc, sh, residual, bool(bn.act))
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
@@ -227,6 +352,27 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
     conv (``x is link.src``) and to its LAST (``residual is link.src``) to fuse the shortcut
     gradient into the first conv's data gradient.  ``branch``: a ``BranchSumLink`` on the block
     input, passed to the downsample conv and the first conv (sums their data gradients in-kernel)."""
+    if not bn.training:
+        out = _conv_bn_eval(conv, bn, x, residual)
+        if out is not None:
+            return out
+    w = conv.weight
+    if x.is_cuda and torch.is_autocast_enabled(x.device.type):
+        # autocast (the reference's fp16 / bf16 AMP trainers): run the fused kernels on the autocast
+        # dtype like torch's conv would — x and the fp32 master weight cast once per call (the cast
+        # is differentiable: dW flows back to the fp32 weight), BN parameters stay fp32
+        dt = torch.get_autocast_dtype(x.device.type)
+        if dt in (torch.bfloat16, torch.float16):
+            if x.dtype != dt:
+                x = x.to(dt)
+                if residual is None and link is not None:
+                    link = None  # the link tracks the caller's tensor, not this cast copy
+                if branch is not None:
+                    branch = None
+            if w.dtype != dt:
+                w = w.to(dt)
+            if residual is not None and residual.dtype != dt:
+                residual = residual.to(dt)
     use = (
         bn.training
         and bn.track_running_stats
@@ -234,7 +380,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
         and bn.affine
         and _native.use_native(x, op="conv")
         and _native.use_native(x, op="bn")
-        and _native_conv_ok(x, conv)
+        and _native_conv_ok(x, conv, w)
     )
     if not use:
         _native.count("conv_bn_act_fallback")
@@ -255,9 +401,11 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
             branch.users += 1
         else:
             branch = None
-    out = _ConvBNActFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
+    # x produced by another fused layer: its BN backward reduce can ride on our dgrad epilogue
+    prod = getattr(x.grad_fn, "bnlink", None) if (FUSE_BN_BACKWARD and x.grad_fn is not None) else None
+    out = _ConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
                              tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
-                             link_in, link_out, branch, bidx)
+                             link_in, link_out, branch, bidx, prod)
     if branch is not None:
         branch.nodes[bidx] = weakref.ref(out.grad_fn)
     if link_in is not None:

@@ -90,9 +90,17 @@ class _LinearFn(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear`` with the weight-streaming kernels on gfx950 (same math, same grads)."""
-    if not (x.is_cuda and _native.use_native(x, op="linear")) or torch.is_autocast_enabled(x.device.type):
+    """``F.linear`` with the weight-streaming kernels on gfx950 (same math, same grads).  Under
+    autocast, x and w are cast to the autocast dtype first (differentiable casts, like torch's own
+    autocast of ``F.linear``), so the native kernels serve the AMP trainers too."""
+    if not (x.is_cuda and _native.use_native(x, op="linear")):
         return F.linear(x, w, b)
+    if torch.is_autocast_enabled(x.device.type):
+        dt = torch.get_autocast_dtype(x.device.type)
+        if dt not in (torch.bfloat16, torch.float16):
+            return F.linear(x, w, b)
+        with torch.autocast(x.device.type, enabled=False):
+            return _LinearFn.apply(x.to(dt), w.to(dt), b)
     return _LinearFn.apply(x, w, b)
 
 

@@ -203,6 +203,7 @@ def test_shortcut_grad_fusion_matches_autograd_add(block):
 
     def run(fuse):
         hconv.FUSE_SHORTCUT_GRAD = fuse
+        hconv.FUSE_BN_BACKWARD = False  # bitwise A/B of the shortcut fusion alone (see test_bn_backward_fusion)
         try:
             for p in m.parameters():
                 p.grad = None
@@ -211,6 +212,7 @@ def test_shortcut_grad_fusion_matches_autograd_add(block):
             return [x.grad.clone()] + [p.grad.clone() for p in m.parameters()]
         finally:
             hconv.FUSE_SHORTCUT_GRAD = True
+            hconv.FUSE_BN_BACKWARD = True
 
     a, b = run(False), run(True)
     for u, v in zip(a, b):
@@ -285,6 +287,7 @@ def test_downsample_branch_grad_fusion_matches_autograd_add(block):
 
     def run(fuse):
         hconv.FUSE_SHORTCUT_GRAD = fuse
+        hconv.FUSE_BN_BACKWARD = False  # bitwise A/B of the shortcut fusion alone (see test_bn_backward_fusion)
         try:
             for p in m.parameters():
                 p.grad = None
@@ -293,6 +296,7 @@ def test_downsample_branch_grad_fusion_matches_autograd_add(block):
             return [x.grad.clone()] + [p.grad.clone() for p in m.parameters()]
         finally:
             hconv.FUSE_SHORTCUT_GRAD = True
+            hconv.FUSE_BN_BACKWARD = True
 
     # the strided 3x3 conv's data gradient is MIOpen's: pin its deterministic algorithm
     det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
@@ -333,6 +337,7 @@ def test_partial_backward_with_gradient_links(block):
 
     def run(fuse, partial):
         hconv.FUSE_SHORTCUT_GRAD = fuse
+        hconv.FUSE_BN_BACKWARD = False  # bitwise A/B of the shortcut fusion alone (see test_bn_backward_fusion)
         try:
             x = x0.clone().requires_grad_(True)
             out = m(x)
@@ -341,6 +346,7 @@ def test_partial_backward_with_gradient_links(block):
             return torch.autograd.grad(out, [x], gy)[0]
         finally:
             hconv.FUSE_SHORTCUT_GRAD = True
+            hconv.FUSE_BN_BACKWARD = True
 
     det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
@@ -350,3 +356,173 @@ def test_partial_backward_with_gradient_links(block):
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
     assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("arch", ["resnet50", "resnet18"])
+def test_bn_backward_fusion_matches_unfused(arch, monkeypatch):
+    """The BN-backward reduce computed in the consuming conv's dgrad epilogue (BNGradLink: dz =
+    dX·mask, Σdz, Σdz·x into the producer's sums) vs the separate reduce pass: both bf16 paths
+    are as close to an fp32 reference of the same network (torch ops, same weights) as each other,
+    and the fused path actually ran (dispatch counter)."""
+    import copy
+
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import resnet18, resnet50
+    from hyperion.ops import _native
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    m32 = (resnet50 if arch == "resnet50" else resnet18)(num_classes=16).cuda().to(memory_format=torch.channels_last)
+    m = copy.deepcopy(m32)
+    cast_for_compute(m, torch.bfloat16)
+    x0 = torch.randn(4, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(4, 16, device="cuda").bfloat16()
+
+    modes = hconv.FUSE_BN_MODES
+    hconv.FUSE_BN_MODES = {0, 1, 2}  # every producer kind
+
+    def run(fuse):
+        hconv.FUSE_BN_BACKWARD = fuse
+        try:
+            for p in m.parameters():
+                p.grad = None
+            _native.reset_counters()
+            x = x0.clone().requires_grad_(True)
+            m(x).backward(gy)
+            torch.cuda.synchronize()
+            return [x.grad.float().clone()] + [p.grad.float().clone() for p in m.parameters()], _native.counters()
+        finally:
+            hconv.FUSE_BN_BACKWARD = True
+
+    try:
+        a, ca = run(False)
+        b, cb = run(True)
+    finally:
+        hconv.FUSE_BN_MODES = modes
+    assert ca.get("dgrad_bn_fused", 0) == 0
+    assert cb.get("dgrad_bn_fused", 0) >= (20 if arch == "resnet50" else 5), cb
+    monkeypatch.setenv("HYPERION_KERNELS", "torch")
+    xr = x0.float().requires_grad_(True)
+    m32(xr).backward(gy.float())
+    ref = [xr.grad] + [p.grad for p in m32.parameters()]
+
+    def rel(u, r):
+        return ((u - r).norm() / (r.norm() + 1e-12)).item()
+
+    ea = [rel(u, r) for u, r in zip(a, ref)]
+    eb = [rel(v, r) for v, r in zip(b, ref)]
+    ma, mb = sorted(ea)[len(ea) // 2], sorted(eb)[len(eb) // 2]
+    print(f"vs fp32: unfused median {ma:.2e} max {max(ea):.2e}; fused median {mb:.2e} max {max(eb):.2e}")
+    assert mb <= 1.25 * ma + 1e-3, (ma, mb)
+    assert max(eb) <= 1.5 * max(ea) + 1e-2, (max(ea), max(eb))
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_autocast_resnet18_runs_native_kernels(dt, monkeypatch):
+    """The reference AMP trainers (C19 / C23 / C24) run under torch.autocast with fp32 weights:
+    conv_bn_act casts x / W to the autocast dtype and takes the fused kernels (dispatch counters),
+    and its gradients are as close to the fp32 network's as torch's own autocast path is.  (A
+    random-init ResNet at CIFAR size is chaotic in its backward — bf16/fp16 round-off alone moves
+    the stem gradients ~40% off fp32 for torch AND native — so the check is relative to torch.)"""
+    import copy
+
+    from hyperion.models.resnet import resnet18
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    m32 = copy.deepcopy(m)
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+
+    def run(model, amp):
+        for p in model.parameters():
+            p.grad = None
+        with torch.autocast("cuda", dtype=dt, enabled=amp):
+            loss = torch.nn.functional.cross_entropy(model(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.detach().float(), [p.grad.float().clone() for p in model.parameters()]
+
+    _native.reset_counters()
+    l1, g1 = run(m, True)
+    cnt = _native.counters()
+    assert cnt.get("conv_bn_act", 0) >= 18 and cnt.get("wgrad", 0) >= 18, cnt
+    monkeypatch.setenv("HYPERION_KERNELS", "torch")
+    l2, g2 = run(m, True)
+    l3, g3 = run(m32, False)
+
+    def rel(u, r):
+        return ((u - r).norm() / (r.norm() + 1e-12)).item()
+
+    en = sorted(rel(a, r) for a, r in zip(g1, g3))
+    et = sorted(rel(b, r) for b, r in zip(g2, g3))
+    print(f"vs fp32: native median {en[len(en) // 2]:.2e}, torch autocast median {et[len(et) // 2]:.2e}")
+    torch.testing.assert_close(l1, l3, rtol=2e-2, atol=2e-2)
+    assert en[len(en) // 2] <= 1.25 * et[len(et) // 2] + 1e-3
+    assert rel(g1[-2], g3[-2]) < 5e-2  # fc.weight: before the chaotic depth
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 16, 16, 64, 3, 1, 1), (8, 128, 8, 8, 256, 1, 1, 0), (32, 512, 1, 1, 512, 3, 1, 1),
+                                   (4, 256, 14, 14, 512, 1, 2, 0), (32, 256, 2, 2, 256, 3, 1, 1)])
+@pytest.mark.parametrize("act,use_res", [(True, False), (True, True), (False, False)])
+def test_conv_bn_eval_fused_matches_composition(shape, act, use_res):
+    """Eval-mode conv -> BN(running stats) -> (+res) -> (ReLU) in one launch (BN folded into the
+    conv epilogue, split-K reduce included) == the fp32 composition to bf16 rounding."""
+    from hyperion.ops import _native
+    from hyperion.ops.batchnorm import BatchNormAct2d
+    from hyperion.ops.conv import conv_bn_act
+
+    N, C, H, W, K, R, s, p = shape
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(C, K, R, stride=s, padding=p, bias=False).cuda()
+    bn = BatchNormAct2d(K, act=act).cuda()
+    with torch.no_grad():
+        bn.running_mean.normal_(0, 0.3)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.2)
+    conv = conv.to(torch.bfloat16).to(memory_format=torch.channels_last)
+    bn.eval()
+    x = torch.randn(N, C, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    P = (H + 2 * p - R) // s + 1
+    res = (torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+           if use_res else None)
+    _native.reset_counters()
+    with torch.no_grad():
+        got = conv_bn_act(conv, bn, x, residual=res)
+    assert _native.counters().get("conv_bn_eval", 0) == 1
+    with torch.no_grad():
+        yr = torch.nn.functional.conv2d(x.float(), conv.weight.float(), stride=s, padding=p)
+        yr = (yr - bn.running_mean.view(1, -1, 1, 1)) * torch.rsqrt(bn.running_var.view(1, -1, 1, 1) + bn.eps)
+        yr = yr * bn.weight.view(1, -1, 1, 1) + bn.bias.view(1, -1, 1, 1)
+        if use_res:
+            yr = yr + res.float()
+        if act:
+            yr = torch.relu(yr)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(got.float(), yr, atol=3e-2, rtol=3e-2)
+
+
+def test_resnet18_inference_fused_path():
+    """ResNet-18 CIFAR inference (the C32 fusion benchmark's config: eval, no_grad, bf16 autocast,
+    fp32 weights): every 64-channel-aligned conv+BN(+res)(+ReLU) is one fused launch, and the
+    logits match PyTorch's eager path."""
+    from hyperion.models.resnet import resnet18
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last).eval()
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    _native.reset_counters()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        got = m(x).float()
+    assert _native.counters().get("conv_bn_eval", 0) >= 18, _native.counters()
+    import os
+    os.environ["HYPERION_KERNELS"] = "torch"
+    try:
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            ref = m(x).float()
+    finally:
+        os.environ.pop("HYPERION_KERNELS")
+    torch.testing.assert_close(got, ref, atol=5e-2, rtol=5e-2)
