@@ -136,3 +136,86 @@ def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmu
             "trainable_params": trainable_parameters(m), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
 
+
+
+def _ensure_pg() -> None:
+    """A world-1 RCCL process group when none is up (FSDP's collectives need one; under
+    ``torch.distributed.run`` the launcher's group is used as is)."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return
+    if "MASTER_PORT" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", rank=int(os.environ.get("RANK", 0)), world_size=int(os.environ.get("WORLD_SIZE", 1)),
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+
+
+def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps: int = 10, warmup: int = 3) -> Dict:
+    """One FSDP FULL_SHARD training step exactly as the FSDP trainers run it (C25 / BASELINE config
+    4 / C26): Hyperion's FSDP over the native RCCL communicator, bf16 mixed precision (param /
+    reduce / buffer), FusedAdamW, global-norm clip 1.0.  ``model``: ``lm256`` (size-based wrap,
+    100k params), ``gpt2_small`` (one unit per transformer layer), ``llama7b_lora`` (LoRA r16,
+    one unit per decoder layer, frozen base weights sharded too).  World size = the launcher's
+    (1 on a single GPU: the gathers / reduce-scatters are then identity collectives, but every
+    flat-buffer pack, cast and hook runs)."""
+    import torch.distributed as dist
+
+    from ..data.synthetic import SyntheticWikiText2
+    from ..ops.optim import FusedAdam
+    from ..parallel.fsdp import FSDP, MixedPrecision, size_based_auto_wrap_policy, transformer_auto_wrap_policy
+
+    _ensure_pg()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.manual_seed(0)
+    bf = torch.bfloat16
+    if model == "llama7b_lora":
+        from ..models.llama import LlamaConfig, LlamaDecoderLayer, LlamaForCausalLM
+        from ..models.lora import apply_lora
+
+        cfg = LlamaConfig.llama2_7b()
+        with torch.device(dev):
+            base = LlamaForCausalLM(cfg).to(bf)
+        apply_lora(base)
+        policy = transformer_auto_wrap_policy({LlamaDecoderLayer})
+        vocab = cfg.vocab_size
+    else:
+        from ..models.simple_lm import GPT2_PAD, gpt2_small_lm, simple_lm_256
+        from ..models.transformer import TransformerEncoderLayer
+
+        base = simple_lm_256() if model == "lm256" else gpt2_small_lm()
+        policy = (size_based_auto_wrap_policy(100_000) if model == "lm256"
+                  else transformer_auto_wrap_policy({TransformerEncoderLayer}))
+        vocab = 50257
+    m = FSDP(base, auto_wrap_policy=policy, device_id=dev, mixed_precision=MixedPrecision(bf, bf, bf))
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = FusedAdam(params, lr=1e-4, weight_decay=0.01, adamw=True)
+    ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=dist.get_rank())
+    ids = (ds.input_ids % vocab).to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        if model == "llama7b_lora":
+            loss = m(ids, labels=ids).loss
+        else:
+            with torch.autocast("cuda", dtype=bf):
+                loss = m.forward_loss(ids[:, :-1], ids[:, 1:], ignore_index=GPT2_PAD)
+        loss.backward()
+        m.clip_grad_norm_(1.0)
+        opt.step()
+        return loss.detach()
+
+    torch.cuda.reset_peak_memory_stats()
+    t = _timeit(step, steps, warmup)
+    world = dist.get_world_size()
+    tok = batch * (seq if model == "llama7b_lora" else seq - 1)
+    return {"model": model, "fsdp": True, "world": world, "batch_per_gpu": batch, "seq": seq, "ms_per_step": t * 1e3,
+            "samples_per_s": world * batch / t, "tokens_per_s": world * tok / t,
+            "trainable_params": sum(p.numel() for p in params), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}

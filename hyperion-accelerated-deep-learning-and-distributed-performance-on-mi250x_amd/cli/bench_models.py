@@ -15,7 +15,7 @@ import sys
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--out", default="results/benchmarks/models")
-    ap.add_argument("--only", default="baseline,scaling,lm,vit,llama,fusion")
+    ap.add_argument("--only", default="baseline,scaling,lm,vit,llama,fsdp,fusion")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args(argv)
     parts = set(a.only.split(","))
@@ -68,6 +68,13 @@ def main(argv=None) -> int:
         summary["llama7b_lora_bf16_eager"] = bench_llama_lora_step(graph=False)
         print(summary["llama7b_lora_bf16_graph"], summary["llama7b_lora_bf16_eager"], flush=True)
         dump()
+    if "fsdp" in parts:
+        from hyperion.bench.models import bench_fsdp_step
+
+        for name, kw in (("lm256", {}), ("gpt2_small", {"batch": 16}), ("llama7b_lora", {"batch": 1, "steps": 5})):
+            summary[f"fsdp_{name}_bf16"] = bench_fsdp_step(name, **kw)
+            print(summary[f"fsdp_{name}_bf16"], flush=True)
+            dump()
     if "fusion" in parts:
         from hyperion.bench.fusion import run_fusion_benchmark
 

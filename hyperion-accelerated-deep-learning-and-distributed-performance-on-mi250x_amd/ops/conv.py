@@ -406,8 +406,9 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
     out = _ConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
                              tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
                              link_in, link_out, branch, bidx, prod)
-    if branch is not None:
-        branch.nodes[bidx] = weakref.ref(out.grad_fn)
-    if link_in is not None:
-        link_in.first_node = weakref.ref(out.grad_fn)
+    if out.grad_fn is not None:  # (no graph under no_grad: nothing to link)
+        if branch is not None:
+            branch.nodes[bidx] = weakref.ref(out.grad_fn)
+        if link_in is not None:
+            link_in.first_node = weakref.ref(out.grad_fn)
     return out

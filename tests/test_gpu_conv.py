@@ -526,3 +526,17 @@ def test_resnet18_inference_fused_path():
     finally:
         os.environ.pop("HYPERION_KERNELS")
     torch.testing.assert_close(got, ref, atol=5e-2, rtol=5e-2)
+
+
+def test_resnet_training_mode_forward_under_no_grad():
+    """A train-mode forward with autograd off (e.g. a benchmark's no-grad timing pass) takes the
+    fused training kernels without building gradient links (regression: weakref to a None grad_fn)."""
+    from hyperion.models.resnet import resnet50
+    from hyperion.train.amp import cast_for_compute
+
+    m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    x = torch.randn(2, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = m(x)
+    assert torch.isfinite(y.float()).all()
