@@ -14,7 +14,7 @@ void check_bshd(const at::Tensor& t, const char* name) {
 }
 
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bool causal,
-                                 double scale, double p_drop, int64_t seed, const c10::optional<at::Tensor>& kpm,
+                                 double scale, double p_drop, const c10::optional<at::Tensor>& rng, const c10::optional<at::Tensor>& kpm,
                                  bool need_lse) {
   check_bshd(q, "q");
   check_bshd(k, "k");
@@ -44,14 +44,19 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal = causal ? 1 : 0;
   p.p_drop = (float)p_drop;
-  p.seed = (uint64_t)seed;
+  if (p_drop > 0) {
+    TORCH_CHECK(rng.has_value() && rng->defined(), "attention dropout needs an rng state (hyperion._C.rng_state)");
+    p.rng = unpack_rng(*rng);
+  } else {
+    p.rng = hyp::RngState{};
+  }
   HYP_CHECK_HIP(hyp::attention_forward(dt, p, cur_stream()));
   return {o, lse};
 }
 
 // grads are written into dq/dk/dv (any [B,S,H,D] strided views, e.g. slices of a packed dQKV)
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-              const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, double p_drop, int64_t seed,
+              const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, double p_drop, const c10::optional<at::Tensor>& rng,
               const c10::optional<at::Tensor>& kpm, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
   check_bshd(q, "q");
   check_bshd(k, "k");
@@ -92,7 +97,12 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.scale_log2 = (float)(scale * 1.4426950408889634);
   p.causal = causal ? 1 : 0;
   p.p_drop = (float)p_drop;
-  p.seed = (uint64_t)seed;
+  if (p_drop > 0) {
+    TORCH_CHECK(rng.has_value() && rng->defined(), "attention dropout needs an rng state (hyperion._C.rng_state)");
+    p.rng = unpack_rng(*rng);
+  } else {
+    p.rng = hyp::RngState{};
+  }
   HYP_CHECK_HIP(hyp::attention_backward(dt, p, cur_stream()));
 }
 

@@ -9,6 +9,9 @@
 
 namespace hypbind {
 
+// rng_ops.cpp: a CPU int64 [6] rng-state record -> the kernels' RngState
+hyp::RngState unpack_rng(const at::Tensor& t);
+
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 inline int dtype_code(const at::Tensor& t) {

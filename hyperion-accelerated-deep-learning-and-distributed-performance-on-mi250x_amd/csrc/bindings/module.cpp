@@ -13,4 +13,5 @@ PYBIND11_MODULE(_C, m) {
   hypbind::register_gemm_ops(m);
   hypbind::register_comm(m);
   hypbind::register_conv_ops(m);
+  hypbind::register_rng_ops(m);
 }

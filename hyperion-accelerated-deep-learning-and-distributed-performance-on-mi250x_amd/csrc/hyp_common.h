@@ -126,6 +126,37 @@ __device__ __forceinline__ float rnd<bf16_t>(float v) { return bf16_to_float(flo
 template <>
 __device__ __forceinline__ float rnd<f16_t>(float v) { return (float)(f16_t)v; }
 
+// ---- counter-based RNG (dropout) ----------------------------------------------------------
+// The (seed, offset) pair comes from torch's default generator (PhiloxCudaState) so streams
+// advance like torch's own dropout AND stay hipGraph-safe: under capture the kernel reads the
+// seed and the graph's extragraph offset from device memory at replay time (the bindings pass
+// whichever form the generator handed out).
+struct RngState {
+  uint64_t seed, offset;       // not captured
+  const int64_t* seed_ptr;     // captured: *seed_ptr, *offset_ptr + intra
+  const int64_t* offset_ptr;
+  uint64_t intra;
+  int captured;
+};
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// one 64-bit key per (seed, offset): element streams are rng_u32(key, element index)
+__device__ __forceinline__ uint64_t rng_key(const RngState& s) {
+  const uint64_t seed = s.captured ? (uint64_t)*s.seed_ptr : s.seed;
+  const uint64_t off = s.captured ? (uint64_t)*s.offset_ptr + s.intra : s.offset;
+  return splitmix64(seed ^ splitmix64(off));
+}
+
+__device__ __forceinline__ uint32_t rng_u32(uint64_t key, uint64_t ctr) {
+  return (uint32_t)(splitmix64(key + 0xD1B54A32D192ED03ull * (ctr + 1)) >> 32);
+}
+
 // ---- wave / block reductions ------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

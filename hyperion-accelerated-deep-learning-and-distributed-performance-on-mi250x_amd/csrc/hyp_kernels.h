@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hyp_common.h"
+
 namespace hyp {
 
 // ---- bn_act.hip ----------------------------------------------------------------------------
@@ -77,7 +79,7 @@ struct AttnParams {
   float scale_log2;      // softmax scale * log2(e)
   int causal;
   float p_drop;
-  uint64_t seed;
+  RngState rng;  // dropout stream (torch generator seed / offset; graph-safe)
 };
 struct AttnBwdParams {
   const void* q; const void* k; const void* v; const void* o; const void* dout;
@@ -90,7 +92,7 @@ struct AttnBwdParams {
   float scale, scale_log2;
   int causal;
   float p_drop;
-  uint64_t seed;
+  RngState rng;  // dropout stream (torch generator seed / offset; graph-safe)
 };
 bool attention_supported(int dtype, int D);
 hipError_t attention_forward(int dtype, const AttnParams& p, hipStream_t st);
@@ -234,3 +236,12 @@ hipError_t embedding_forward(int dtype, const int64_t* ids, const void* w, void*
 hipError_t embedding_backward(int dtype, const int64_t* ids, const void* dy, float* dw32, void* dw, int64_t n, int E,
                               int64_t V, int64_t pad_idx, hipStream_t st);
 }  // namespace hyp
+
+namespace hyp {
+// ---- dropout.hip -----------------------------------------------------------------------------
+// mode 0: out = keep ? x / (1 - p) : 0 (also the backward on dy with the same state); mode 1: out =
+// the scaled keep mask keep / (1 - p).  keep = rng_u32(rng_key(rs), element index) >= p·2^32.
+hipError_t dropout_apply(int dtype, int mode, const void* x, void* out, int64_t n, float p, const RngState& rs,
+                         hipStream_t st);
+}  // namespace hyp
+

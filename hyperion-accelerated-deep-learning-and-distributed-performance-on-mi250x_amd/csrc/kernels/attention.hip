@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(AttnParams p) {
   float m = -INFINITY, l = 0.f;
   const float inv_keep = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
   const uint32_t thr = (uint32_t)(p.p_drop * 4294967296.0);
+  const uint64_t seed = p.p_drop > 0.f ? rng_key(p.rng) : 0;  // graph-safe generator state
   const uint8_t* kpm = p.kpm ? p.kpm + (int64_t)b * p.S : nullptr;
 
   int kt_end = (p.S + KB - 1) / KB;
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(AttnParams p) {
         if (p.p_drop > 0.f) {
           const int key = k0 + 16 * t + 4 * h + r;
           const uint64_t idx = (((uint64_t)bh * p.S + qrow) * p.S) + key;
-          pd = hash_keep(p.seed, idx) >= thr ? e * inv_keep : 0.f;
+          pd = hash_keep(seed, idx) >= thr ? e * inv_keep : 0.f;
         }
         pr[t][r] = pd;
       }
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(AttnBwdParams p) {
   for (int n = 0; n < NN; ++n) dvt[n] = dkt[n] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float inv_keep = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
   const uint32_t thr = (uint32_t)(p.p_drop * 4294967296.0);
+  const uint64_t seed = p.p_drop > 0.f ? rng_key(p.rng) : 0;  // graph-safe generator state
   const bool key_masked = key >= p.S || (p.kpm && p.kpm[(int64_t)b * p.S + key] != 0);
 
   const int nq = (p.S + KB - 1) / KB;
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(AttnBwdParams p) {
         float pdv = pv;
         if (p.p_drop > 0.f) {
           const uint64_t idx = (((uint64_t)bh * p.S + qg) * p.S) + key;
-          const bool keep = hash_keep(p.seed, idx) >= thr;
+          const bool keep = hash_keep(seed, idx) >= thr;
           pdv = keep ? pv * inv_keep : 0.f;
           dpv = keep ? dpv * inv_keep : 0.f;
         }

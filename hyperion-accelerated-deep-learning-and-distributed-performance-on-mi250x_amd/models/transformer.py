@@ -32,6 +32,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.attention import attention_packed
+from ..ops.dropout import Dropout
 from ..ops.layernorm import LayerNorm
 from ..ops.linear import Linear, linear
 from ..ops.linear_act import LinearAct, linear_act
@@ -97,13 +98,13 @@ class TransformerEncoderLayer(nn.Module):
         self.self_attn = MultiheadSelfAttention(d_model, nhead, dropout=dropout, bias=bias)
         # modules called as modules (FSDP gathers a unit's shard in its forward pre-hook)
         self.linear1 = LinearAct(d_model, dim_feedforward, bias=bias, activation=activation)
-        self.dropout = nn.Dropout(dropout)
+        self.dropout = Dropout(dropout)
         self.linear2 = Linear(dim_feedforward, d_model, bias=bias)
         self.norm_first = norm_first
         self.norm1 = LayerNorm(d_model, eps=layer_norm_eps)
         self.norm2 = LayerNorm(d_model, eps=layer_norm_eps)
-        self.dropout1 = nn.Dropout(dropout)
-        self.dropout2 = nn.Dropout(dropout)
+        self.dropout1 = Dropout(dropout)
+        self.dropout2 = Dropout(dropout)
         self.activation = activation
 
     def _ff(self, x: torch.Tensor) -> torch.Tensor:

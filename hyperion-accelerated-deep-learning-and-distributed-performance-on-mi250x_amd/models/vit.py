@@ -27,6 +27,7 @@ import torch.nn as nn
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 from torch.utils.checkpoint import checkpoint
 
+from ..ops.dropout import Dropout
 from ..ops.layernorm import LayerNorm, layer_norm
 from ..ops.linear import Linear
 from ..ops.linear_act import LinearAct
@@ -38,8 +39,8 @@ class MLPBlock(nn.Sequential):
 
     def __init__(self, dim: int, hidden: int, dropout: float = 0.0):
         # [0] applies the GELU itself (bias + GELU with the GEMM); [1] stays for the torchvision layout
-        super().__init__(LinearAct(dim, hidden, activation="gelu"), nn.GELU(), nn.Dropout(dropout),
-                         Linear(hidden, dim), nn.Dropout(dropout))
+        super().__init__(LinearAct(dim, hidden, activation="gelu"), nn.GELU(), Dropout(dropout),
+                         Linear(hidden, dim), Dropout(dropout))
         for m in (self[0], self[3]):
             nn.init.xavier_uniform_(m.weight)
             nn.init.normal_(m.bias, std=1e-6)
@@ -55,7 +56,7 @@ class EncoderBlock(nn.Module):
         self.num_heads = num_heads
         self.ln_1 = LayerNorm(hidden_dim, eps=1e-6)
         self.self_attention = MultiheadSelfAttention(hidden_dim, num_heads, dropout=attention_dropout)
-        self.dropout = nn.Dropout(dropout)
+        self.dropout = Dropout(dropout)
         self.ln_2 = LayerNorm(hidden_dim, eps=1e-6)
         self.mlp = MLPBlock(hidden_dim, mlp_dim, dropout)
 
@@ -85,7 +86,7 @@ class Encoder(nn.Module):
                  dropout: float = 0.0, attention_dropout: float = 0.0, use_checkpoint: bool = False):
         super().__init__()
         self.pos_embedding = nn.Parameter(torch.empty(1, seq_length, hidden_dim).normal_(std=0.02))
-        self.dropout = nn.Dropout(dropout)
+        self.dropout = Dropout(dropout)
         self.layers = nn.ModuleDict(
             OrderedDict(
                 (f"encoder_layer_{i}", EncoderBlock(num_heads, hidden_dim, mlp_dim, dropout, attention_dropout))
@@ -144,12 +145,22 @@ class VisionTransformer(nn.Module):
         self.encoder.use_checkpoint = bool(v)
 
     def _process_input(self, x: torch.Tensor) -> torch.Tensor:
+        """Patch embedding.  A p x p / stride-p convolution over non-overlapping patches IS a GEMM:
+        patches [n·(h/p)·(w/p), c·p·p] (one permute copy, in the conv weight's (c, kh, kw) order)
+        times the flattened weight — the tokens come out already as [n, h/p·w/p, hidden], and the
+        backward is a plain weight-gradient GEMM.  (MIOpen has no fast bf16 NHWC solver for the
+        3-channel 16x16/16 conv: it ran its naive reference kernels, 11 ms forward + 7 ms wrw per
+        ViT-B/16 step on MI355X, profiles/r02/vit_b16_kernels.)"""
         n, c, h, w = x.shape
         if h != self.image_size or w != self.image_size:
             raise ValueError(f"expected {self.image_size}x{self.image_size} input, got {h}x{w}")
-        x = self.conv_proj(x)  # [n, hidden, h/p, w/p]
-        # channels-last conv output is already [n, h/p, w/p, hidden] in memory: flatten is free
-        return x.permute(0, 2, 3, 1).reshape(n, -1, self.hidden_dim)
+        p = self.patch_size
+        wt = self.conv_proj.weight
+        x = x.to(wt.dtype) if not torch.is_autocast_enabled(x.device.type) else x
+        patches = (x.reshape(n, c, h // p, p, w // p, p).permute(0, 2, 4, 1, 3, 5)
+                   .reshape(n * (h // p) * (w // p), c * p * p))
+        tok = torch.nn.functional.linear(patches, wt.reshape(wt.shape[0], -1), self.conv_proj.bias)
+        return tok.reshape(n, (h // p) * (w // p), self.hidden_dim)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self._process_input(x)

@@ -103,6 +103,13 @@ def loaded_path() -> Optional[str]:
     return getattr(m, "__file__", None) if m is not None else None
 
 
+def rng_state(device: torch.device, increment: int = 8) -> torch.Tensor:
+    """A graph-safe (seed, offset) record from torch's default generator for the counter-based
+    dropout kernels (advances the generator like one torch dropout call)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return native().rng_state(idx, increment)
+
+
 class ZeroArena:
     """Pre-zeroed fp64 workspace for the kernels' atomic accumulators (BN statistics sums).
 

@@ -8,11 +8,11 @@ of the packed tensor in one buffer (no slice-grad accumulation).
 Reference attention: ``nn.MultiheadAttention`` → SDPA math fallback (C14/C15/C5) and HF Llama
 SDPA with a causal mask (C26).  Dropout (p=0.1 in nn.TransformerEncoderLayer) is applied to the
 attention probabilities inside the kernel with a counter-based hash (seed, b, h, q, k), so the
-backward regenerates the same mask.  Note: a hipGraph replay reuses the captured seed.
+backward regenerates the same mask.  The seed / offset come from torch's default generator
+(``_native.rng_state``): every hipGraph replay draws a fresh mask, as torch's dropout does.
 """
 from __future__ import annotations
 
-import itertools
 import math
 from typing import Optional
 
@@ -21,11 +21,8 @@ import torch.nn.functional as F
 
 from . import _native
 
-_seed_counter = itertools.count()
-
-
-def _next_seed() -> int:
-    return (torch.initial_seed() * 1000003 + next(_seed_counter)) & 0x7FFFFFFFFFFFFFFF
+def _rng(t: torch.Tensor, p: float):
+    return _native.rng_state(t.device) if p > 0 else None
 
 
 def _native_ok(*ts: torch.Tensor) -> bool:
@@ -55,7 +52,7 @@ def attention_reference(q, k, v, causal=False, dropout_p=0.0, key_padding_mask=N
 class _AttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, dropout_p, kpm, scale):
-        seed = _next_seed() if dropout_p > 0 else 0
+        seed = _rng(q, dropout_p)
         o, lse = _native.native().attn_fwd(q, k, v, causal, scale, dropout_p, seed, kpm, True)
         ctx.save_for_backward(q, k, v, o, lse, kpm)
         ctx.cfg = (causal, dropout_p, seed, scale)
@@ -74,7 +71,7 @@ class _AttnPackedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, causal, dropout_p, kpm, scale):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        seed = _next_seed() if dropout_p > 0 else 0
+        seed = _rng(q, dropout_p)
         o, lse = _native.native().attn_fwd(q, k, v, causal, scale, dropout_p, seed, kpm, True)
         ctx.save_for_backward(qkv, o, lse, kpm)
         ctx.cfg = (causal, dropout_p, seed, scale)

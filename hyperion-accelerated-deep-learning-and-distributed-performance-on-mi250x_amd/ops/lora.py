@@ -11,8 +11,9 @@ with ``c·t Bᵀ`` fused into the base GEMM's reduce; in backward ``dt = c·dy B
 conv weight-gradient kernel at 1x1.  The math:
 
 * forward: base GEMM (``ops.linear``: split-K weight-streaming MFMA kernel), ``t = drop(x)Aᵀ``
-  ([N, r] — tiny), then ``y += c·t Bᵀ`` with c = s/(1-p) (the dropout rescale folded into the
-  GEMM's alpha) as an in-place rank-r update (``addmm_``: no second [N, out] tensor);
+  ([N, r] — tiny), then ``y += c·t Bᵀ`` as a rank-r update fused into the base GEMM's reduce;
+  on gfx950 drop(x) is the graph-safe counter-based kernel (``ops/dropout.py``: no stored mask,
+  regenerated in backward — torch's bernoulli masks took ~4.5 ms of the Llama LoRA step);
 * backward: ``dx = dy W + (c·dy B) A ∘ keep``, ``dA = (c·dy B)ᵀ drop(x)``, ``dB = c·dyᵀ t``; W
   never gets a gradient buffer.  The keep-mask is drawn in the activation dtype from the default
   device generator (one kernel; the step stays hipGraph-capturable) and ``drop(x)`` is kept for
@@ -29,7 +30,8 @@ from . import _native
 from .linear import SKINNY_MAX_M, linear_dgrad, linear_fwd
 
 def _keep_mask(x: torch.Tensor, p: float) -> torch.Tensor:
-    # drawn directly in the activation dtype (one kernel; 0/1 are exact in bf16/f16)
+    # drawn directly in the activation dtype (one kernel; 0/1 are exact in bf16/f16) — the
+    # reference path only; the native path regenerates the mask (ops/dropout.py)
     return torch.empty(x.shape, device=x.device, dtype=x.dtype).bernoulli_(1.0 - p)
 
 
@@ -47,11 +49,18 @@ class _LoRAFn(torch.autograd.Function):
         cdt = torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else x.dtype
         xc, wc = x.to(cdt), w.to(cdt)
         ac, bc = a.to(cdt).contiguous(), bm.to(cdt).contiguous()
-        c = scaling / (1.0 - p) if p > 0 else scaling  # dropout's 1/(1-p) folded into the rank-r GEMM
         x2 = xc.reshape(-1, xc.shape[-1]).contiguous()
-        keep = _keep_mask(x2, p) if p > 0 else None
-        xd = x2 * keep if p > 0 else x2
         native = _native_ok(x2, wc, ac, bc)
+        st = keep = None
+        if native and p > 0:
+            # graph-safe counter-based dropout: xd = x·keep/(1-p), the mask regenerated in backward
+            st = _native.rng_state(x2.device)
+            xd = _native.native().dropout(x2, p, st)
+            c = scaling
+        else:
+            c = scaling / (1.0 - p) if p > 0 else scaling  # dropout's 1/(1-p) folded into the rank-r GEMM
+            keep = _keep_mask(x2, p) if p > 0 else None
+            xd = x2 * keep if p > 0 else x2
         if native:
             C = _native.native()
             t = C.linear_nt(xd, ac)  # [N, r]: split-K over the input features
@@ -64,13 +73,13 @@ class _LoRAFn(torch.autograd.Function):
         if b is not None:
             y += b.to(cdt)
         ctx.save_for_backward(wc, ac, bc, t, xd, keep)
-        ctx.cfg = (c, p, x.dtype, a.dtype, bm.dtype, xc.shape, native)
+        ctx.cfg = (c, p, x.dtype, a.dtype, bm.dtype, xc.shape, native, st)
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         wc, ac, bc, t, xd, keep = ctx.saved_tensors
-        c, p, xdt, adt, bdt, xshape, native = ctx.cfg
+        c, p, xdt, adt, bdt, xshape, native, st = ctx.cfg
         dy2 = dy.reshape(-1, dy.shape[-1]).to(wc.dtype).contiguous()
         dx = dA = dB = None
         M, r = t.shape
@@ -78,8 +87,10 @@ class _LoRAFn(torch.autograd.Function):
             C = _native.native()
             dt = C.linear_nn(dy2, bc, alpha=c)  # grad of t: c · dy B  [N, r]
             if ctx.needs_input_grad[0]:
-                # dx = dy W + keep ∘ (dt A): the rank-r term fused into the base dgrad's reduce
-                dx = C.linear_nn(dy2, wc, U=dt, V=ac, v_nr=False, mask=keep).view(xshape).to(xdt)
+                # dx = dy W + (keep/(1-p)) ∘ (dt A): the rank-r term fused into the base dgrad's reduce,
+                # the scaled mask regenerated from the forward's rng state
+                mask = C.dropout(xd, p, st, mask=True) if st is not None else None
+                dx = C.linear_nn(dy2, wc, U=dt, V=ac, v_nr=False, mask=mask).view(xshape).to(xdt)
             if ctx.needs_input_grad[3]:  # dA = dtᵀ drop(x): the conv weight-gradient kernel at 1x1
                 dA = C.conv_wgrad(dt.view(M, r, 1, 1), xd.view(M, -1, 1, 1), 1, 1, 1, 1, 0, 0).view(r, -1).to(adt)
             if ctx.needs_input_grad[4]:  # dBᵀ = c · tᵀ dy

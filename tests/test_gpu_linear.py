@@ -99,12 +99,18 @@ def test_lora_dropout_native_matches_reference():
     p, s = 0.1, 2.0
     torch.cuda.manual_seed(11)
     y = lora_linear(x, w, None, a, bm, s, p)
+    # the native path draws its mask from the generator's (seed, offset) record: re-seed, take the
+    # same record, and materialize the scaled keep mask keep/(1-p) it regenerates in backward
+    from hyperion.ops import _native
+
     torch.cuda.manual_seed(11)
-    keep = torch.empty(128, 512, device="cuda", dtype=torch.bfloat16).bernoulli_(1 - p).view(2, 64, 512)
+    st = _native.rng_state(x.device)
+    keep = _native.native().dropout(x.detach().reshape(128, 512).contiguous(), p, st, mask=True).view(2, 64, 512)
+    assert abs((keep != 0).float().mean().item() - (1 - p)) < 0.02
     g = torch.randn_like(y)
     y.backward(g)
     xr, ar, br = (t.detach().float().requires_grad_(True) for t in (x, a, bm))
-    yr = lora_linear_reference(xr, w.float(), None, ar, br, s, mask=keep.float() / (1 - p))
+    yr = lora_linear_reference(xr, w.float(), None, ar, br, s, mask=keep.float())
     yr.backward(g.float())
     for u, v in ((y, yr), (x.grad, xr.grad), (a.grad, ar.grad), (bm.grad, br.grad)):
         assert (u.float() - v).norm() <= 2e-2 * v.norm() + 1e-3

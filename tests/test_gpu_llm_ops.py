@@ -143,3 +143,50 @@ def test_linear_act_matches_reference(act):
     assert (y.float() - yr).norm() <= 2e-2 * yr.norm()
     for a, r in ((x, xr), (w, wr), (b, br)):
         assert (a.grad.float() - r.grad).norm() <= 0.03 * r.grad.norm()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+def test_native_dropout_mask_stats_and_backward(dt):
+    """Counter-based dropout: keep rate 1-p, kept values scaled by 1/(1-p), the backward applies
+    exactly the forward's mask (regenerated, never stored), and consecutive calls draw new masks."""
+    from hyperion.ops import _native
+    from hyperion.ops.dropout import dropout
+
+    torch.manual_seed(0)
+    p = 0.1
+    x = (torch.rand(4096, 1000, device="cuda") + 0.5).to(dt).requires_grad_(True)
+    _native.reset_counters()
+    y = dropout(x, p, True)
+    assert _native.counters().get("dropout") == 1
+    keep = y != 0
+    assert abs(keep.float().mean().item() - (1 - p)) < 2e-3
+    torch.testing.assert_close(y[keep].float(), (x[keep].float() / (1 - p)).to(dt).float())
+    g = torch.randn_like(x)
+    y.backward(g)
+    torch.testing.assert_close(x.grad, (g.float() * keep.float() / (1 - p)).to(dt))
+    y2 = dropout(x.detach(), p, True)
+    assert ((y2 != 0) != keep).float().mean().item() > 0.1  # a fresh mask
+
+
+def test_native_dropout_fresh_mask_per_graph_replay():
+    """Under hipGraph capture the seed/offset are read from torch's generator state at replay time:
+    every replay draws a new mask (the old host-seed scheme replayed the captured one)."""
+    from hyperion.ops.dropout import dropout
+
+    x = torch.ones(1 << 16, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out.copy_(dropout(x, 0.5, True))
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out.copy_(dropout(x, 0.5, True))
+    g.replay()
+    torch.cuda.synchronize()
+    m1 = out.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(m1, out)
+    assert abs((out != 0).float().mean().item() - 0.5) < 0.02
