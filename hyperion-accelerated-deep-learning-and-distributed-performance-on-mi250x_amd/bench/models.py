@@ -64,8 +64,9 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
 
 
 def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool = True, steps: int = 20,
-                   warmup: int = 5) -> Dict:
-    """ViT-B/16 bf16 + activation checkpointing (BASELINE.json config 3), MSE/Adam like C6."""
+                   warmup: int = 5, graph: bool = False) -> Dict:
+    """ViT-B/16 bf16 + activation checkpointing (BASELINE.json config 3), MSE/Adam like C6.
+    ``graph``: the whole step captured once as a hipGraph and replayed."""
     from ..models.vit import vit_b_16
     from ..ops.optim import FusedAdam
     from ..train.amp import cast_for_compute
@@ -76,21 +77,26 @@ def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool
     dt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(precision)
     if dt is not None:
         cast_for_compute(m, dt)
-    opt = FusedAdam(m.parameters(), lr=1e-3)
+    opt = FusedAdam(m.parameters(), lr=1e-3, zero_grad_in_step=graph)
     x = torch.rand(batch, 3, 224, 224, device=dev).contiguous(memory_format=torch.channels_last)
     x = x.to(dt) if dt is not None else x
     y = torch.rand(batch, 1000, device=dev)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
+    def body():
+        opt.zero_grad(set_to_none=not graph)
         loss = torch.nn.functional.mse_loss(m(x).float(), y)
         loss.backward()
         opt.step()
+        return loss.detach()
 
+    from ..train.step import GraphedClosure
+
+    step = GraphedClosure(body, warmup=2, module=m) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
     return {"model": "vit_b_16", "batch": batch, "precision": precision, "checkpointing": checkpointing,
-            "ms_per_step": t * 1e3, "samples_per_s": batch / t, "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
+            "graph": graph, "ms_per_step": t * 1e3, "samples_per_s": batch / t,
+            "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
 
 def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmup: int = 3, lora: bool = True,

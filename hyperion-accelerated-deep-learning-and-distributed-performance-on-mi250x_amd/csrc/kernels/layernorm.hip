@@ -19,69 +19,116 @@ namespace {
 constexpr int kWavesPerBlock = 4;
 
 // Each lane handles VPL vectors of 8 elements: lane l, vector v covers [ (v*64 + l)*8, +8 ).
+// Latency structure (the kernels are HBM-bound only when enough loads are in flight): the affine
+// parameters are loaded ONCE per lane before the first row, and every wave walks `rpw` rows with
+// the NEXT row's 16-byte vectors already in flight while the current row is reduced and written
+// (register double buffering).  One row per wave with w/b fetched after the row statistics cost
+// three dependent memory round trips per row: 26 us for a [6304, 768] bf16 LN on MI355X.
+template <typename T, int VPL>
+struct RowRegs {
+  static constexpr int kQ = sizeof(T) / 2;  // 16-byte quads per 8-element vector (2-byte T: 1, fp32: 2)
+  uint4 v[VPL][kQ];
+  __device__ __forceinline__ void load(const T* base, int64_t row, int d, int lane) {
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      const int c = (k * 64 + lane) * 8;
+#pragma unroll
+      for (int q = 0; q < kQ; ++q)
+        v[k][q] = c < d ? reinterpret_cast<const uint4*>(base + row * d + c)[q] : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void unpack(int k, float (&o)[8]) const { Vec8<T>::load(reinterpret_cast<const T*>(&v[k][0]), o); }
+};
+
+template <int VPL>
+__device__ __forceinline__ void load_affine(const float* p, int d, int lane, float (&o)[VPL][8], float dflt) {
+#pragma unroll
+  for (int k = 0; k < VPL; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (p != nullptr && c < d) {
+      const float4 a = reinterpret_cast<const float4*>(p + c)[0];
+      const float4 b = reinterpret_cast<const float4*>(p + c)[1];
+      o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
+      o[k][4] = b.x; o[k][5] = b.y; o[k][6] = b.z; o[k][7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[k][j] = dflt;
+    }
+  }
+}
+
 template <typename T, int VPL, bool RMS, bool HAS_RES>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_fwd_k(const T* __restrict__ x, const T* __restrict__ r,
                                                                   T* __restrict__ s_out, T* __restrict__ y,
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ b, float* __restrict__ mean_out,
                                                                   float* __restrict__ rstd_out, int64_t rows, int d,
-                                                                  float eps) {
+                                                                  float eps, int rpw) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const T* xr = x + row * d;
-  float v[VPL][8];
-  float sum = 0.f;
+  const int64_t row0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * rpw;
+  if (row0 >= rows) return;
+  float wv[VPL][8], bv[VPL][8];
+  load_affine<VPL>(w, d, lane, wv, 1.f);
+  load_affine<VPL>(RMS ? nullptr : b, d, lane, bv, 0.f);
+  RowRegs<T, VPL> cx, cr, nx, nr;
+  cx.load(x, row0, d, lane);
+  if (HAS_RES) cr.load(r, row0, d, lane);
+  for (int i = 0; i < rpw; ++i) {
+    const int64_t row = row0 + i;
+    if (row >= rows) break;
+    const bool more = i + 1 < rpw && row + 1 < rows;
+    if (more) {  // the next row's vectors in flight during this row's work
+      nx.load(x, row + 1, d, lane);
+      if (HAS_RES) nr.load(r, row + 1, d, lane);
+    }
+    float v[VPL][8];
+    float sum = 0.f;
 #pragma unroll
-  for (int k = 0; k < VPL; ++k) {
-    const int c = (k * 64 + lane) * 8;
-    if (c < d) {
-      Vec8<T>::load(xr + c, v[k]);
-      if (HAS_RES) {
+    for (int k = 0; k < VPL; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      cx.unpack(k, v[k]);
+      if (HAS_RES && c < d) {
         float rv[8];
-        Vec8<T>::load(r + row * d + c, rv);
+        cr.unpack(k, rv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = rnd<T>(v[k][j] + rv[j]);  // stats of the stored stream
         Vec8<T>::store(s_out + row * d + c, v[k]);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sum += v[k][j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+      for (int j = 0; j < 8; ++j) sum += v[k][j];  // zero-filled past d
     }
-  }
-  float mean = 0.f;
-  if (!RMS) mean = wave_sum(sum) / d;
-  float sq = 0.f;
+    float mean = 0.f;
+    if (!RMS) mean = wave_sum(sum) / d;
+    float sq = 0.f;
 #pragma unroll
-  for (int k = 0; k < VPL; ++k) {
-    const int c = (k * 64 + lane) * 8;
-    if (c < d) {
+    for (int k = 0; k < VPL; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < d) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float t = v[k][j] - mean;
-        sq += t * t;
+        for (int j = 0; j < 8; ++j) {
+          const float t = v[k][j] - mean;
+          sq += t * t;
+        }
       }
     }
-  }
-  const float rstd = rsqrtf(wave_sum(sq) / d + eps);
-  if (lane == 0) {
-    if (mean_out) mean_out[row] = mean;
-    rstd_out[row] = rstd;
-  }
+    const float rstd = rsqrtf(wave_sum(sq) / d + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
 #pragma unroll
-  for (int k = 0; k < VPL; ++k) {
-    const int c = (k * 64 + lane) * 8;
-    if (c < d) {
-      float o[8];
+    for (int k = 0; k < VPL; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < d) {
+        float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float wj = w ? w[c + j] : 1.f;
-        const float bj = (b && !RMS) ? b[c + j] : 0.f;
-        o[j] = (v[k][j] - mean) * rstd * wj + bj;
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * wv[k][j] + bv[k][j];
+        Vec8<T>::store(y + row * d + c, o);
       }
-      Vec8<T>::store(y + row * d + c, o);
+    }
+    if (more) {
+      cx = nx;
+      if (HAS_RES) cr = nr;
     }
   }
 }
@@ -97,16 +144,29 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
                                                                   int64_t rows, int d, int rows_per_wave) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  float gw[VPL][8], gb[VPL][8];
+  float gw[VPL][8], gb[VPL][8], wv[VPL][8];
 #pragma unroll
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) gw[k][j] = gb[k][j] = 0.f;
+  load_affine<VPL>(w, d, lane, wv, 1.f);
 
   const int64_t row_begin = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * rows_per_wave;
+  RowRegs<T, VPL> cg, cxr, cd, ng, nxr, nd;
+  if (row_begin < rows) {
+    cg.load(dy, row_begin, d, lane);
+    cxr.load(xin, row_begin, d, lane);
+    if (HAS_DRES) cd.load(dres, row_begin, d, lane);
+  }
   for (int rr = 0; rr < rows_per_wave; ++rr) {
     const int64_t row = row_begin + rr;
     if (row >= rows) break;
+    const bool more = rr + 1 < rows_per_wave && row + 1 < rows;
+    if (more) {  // next row in flight
+      ng.load(dy, row + 1, d, lane);
+      nxr.load(xin, row + 1, d, lane);
+      if (HAS_DRES) nd.load(dres, row + 1, d, lane);
+    }
     const float mean = RMS ? 0.f : mean_in[row];
     const float rstd = rstd_in[row];
     float g[VPL][8], xh[VPL][8];
@@ -114,14 +174,14 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
       const int c = (k * 64 + lane) * 8;
+      cg.unpack(k, g[k]);
       if (c < d) {
         float xv[8];
-        Vec8<T>::load(dy + row * d + c, g[k]);
-        Vec8<T>::load(xin + row * d + c, xv);
+        cxr.unpack(k, xv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[k][j] = (xv[j] - mean) * rstd;
-          const float gwv = g[k][j] * (w ? w[c + j] : 1.f);
+          const float gwv = g[k][j] * wv[k][j];
           s1 += gwv;
           s2 += gwv * xh[k][j];
           gw[k][j] += g[k][j] * xh[k][j];
@@ -137,18 +197,20 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
       if (c < d) {
         float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float gwv = g[k][j] * (w ? w[c + j] : 1.f);
-          o[j] = rstd * (gwv - (RMS ? 0.f : s1) - xh[k][j] * s2);
-        }
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] * wv[k][j] - (RMS ? 0.f : s1) - xh[k][j] * s2);
         if (HAS_DRES) {
           float rv[8];
-          Vec8<T>::load(dres + row * d + c, rv);
+          cd.unpack(k, rv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
         Vec8<T>::store(dx + row * d + c, o);
       }
+    }
+    if (more) {
+      cg = ng;
+      cxr = nxr;
+      if (HAS_DRES) cd = nd;
     }
   }
   // block partials of dγ/dβ through LDS: [wave][d]
@@ -183,15 +245,19 @@ template <typename T, bool RMS>
 hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, const float* b, float* mean,
                            float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
   const int vpl = (d + 511) / 512;
-  const dim3 grid((unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
+  // rows per wave: 2+ once there are enough rows to keep ~2048 waves busy (the prefetch needs a next row)
+  int rpw = 1;
+  if (rows >= 4096) rpw = (int)((rows + 2047) / 2048 < 8 ? (rows + 2047) / 2048 : 8);
+  const int64_t waves = (rows + rpw - 1) / rpw;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
 #define HYP_LN_F(V)                                                                                          \
   case V:                                                                                                    \
     if (r)                                                                                                   \
       hipLaunchKernelGGL((ln_fwd_k<T, V, RMS, true>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, \
-                         d, eps);                                                                            \
+                         d, eps, rpw);                                                                       \
     else                                                                                                     \
       hipLaunchKernelGGL((ln_fwd_k<T, V, RMS, false>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, \
-                         d, eps);                                                                            \
+                         d, eps, rpw);                                                                       \
     break;
   switch (vpl) {
     HYP_LN_F(1)
@@ -247,13 +313,14 @@ bool layernorm_supported(int d) {
 }
 
 void layernorm_bwd_geom(int64_t rows, int* P, int* rows_per_wave) {
-  // enough waves to fill 256 CUs (>= min(rows, 1024) waves: a 128-token Llama step has only 128
-  // rows of 4096 — at 8 rows per wave that was 4 workgroups, 136 us per RMSNorm backward), but
-  // few partial rows for the column reduction (<= 2048 waves, >= 8 rows per wave when possible)
-  int64_t waves = (rows + 7) / 8;
-  const int64_t floor_waves = rows < 1024 ? rows : 1024;
+  // enough waves to fill 256 CUs (>= min(rows, 2048) waves: a 128-token Llama step has only 128
+  // rows of 4096 — at 8 rows per wave that was 4 workgroups, 136 us per RMSNorm backward), with
+  // ~4 rows per wave so the row prefetch has work to hide behind; the partial rows (<= 1024
+  // blocks) are combined by the wide colsum_combine (reduce.hip)
+  int64_t waves = (rows + 3) / 4;  // ~4 rows per wave (the next row prefetched while one is reduced)
+  const int64_t floor_waves = rows < 2048 ? rows : 2048;
   if (waves < floor_waves) waves = floor_waves;
-  if (waves > 2048) waves = 2048;
+  if (waves > 4096) waves = 4096;
   if (waves < 1) waves = 1;
   int rpw = (int)((rows + waves - 1) / waves);
   int64_t nwaves = (rows + rpw - 1) / rpw;

@@ -9,8 +9,8 @@
 //   strides over a slab of rows with 4 independent accumulators in flight; the block's 4 row
 //   groups combine through LDS into one fp32 partial row.  grid = (column slabs, P row slabs)
 //   with P chosen so the launch has ~2 workgroups per CU.
-// * colsum_final_k: out[c] = Σ_p part[p][c], 8 independent loads in flight per thread (the
-//   rolled loop of the first version waited one L2 round trip per partial row).
+// * colsum_final_k: out[c] = Σ_p part[p][c] with 16 row lanes x 8 independent 16-byte loads in
+//   flight per column quad (see the kernel).
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -61,21 +61,54 @@ __global__ __launch_bounds__(kThreads) void colsum_partial_k(const T* __restrict
   }
 }
 
+// out[c] = Σ_p part[p][c].  One block = 64 columns (16 float4 column quads) x 16 row lanes, every
+// lane with 8 independent 16-byte loads in flight: the P partial rows are read in ~P/128 memory
+// round trips instead of P/8 (a thread-per-column combine over P = 256 partials was 11.5 us — 1.3 ms
+// per ViT-B/16 step over its ~100 bias / LayerNorm-parameter gradients), then a fixed-order LDS
+// sum over the 16 lanes (deterministic).
+constexpr int kFinLanes = 16;
+
 template <typename O>
 __global__ __launch_bounds__(kThreads) void colsum_final_k(const float* __restrict__ part, int P, int N,
                                                            O* __restrict__ out) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
-  if (c >= N) return;
-  float s[8];
+  __shared__ float red[kFinLanes][64];
+  const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  const int c = blockIdx.x * 64 + tx * 4;
+  float4 s[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s[i] = 0.f;
-  int p = 0;
-  for (; p + 7 < P; p += 8) {
+  for (int i = 0; i < 8; ++i) s[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < N) {  // N % 4 == 0: a quad never straddles the edge
+    int p = ty;
+    for (; p + 7 * kFinLanes < P; p += 8 * kFinLanes) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] += part[(int64_t)(p + i) * N + c];
+      for (int i = 0; i < 8; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)(p + i * kFinLanes) * N + c);
+        s[i].x += v.x; s[i].y += v.y; s[i].z += v.z; s[i].w += v.w;
+      }
+    }
+    for (; p < P; p += kFinLanes) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)p * N + c);
+      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+    }
   }
-  for (; p < P; ++p) s[0] += part[(int64_t)p * N + c];
-  st1<O>(out + c, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    s[0].x += s[i].x; s[0].y += s[i].y; s[0].z += s[i].z; s[0].w += s[i].w;
+  }
+  red[ty][tx * 4 + 0] = s[0].x;
+  red[ty][tx * 4 + 1] = s[0].y;
+  red[ty][tx * 4 + 2] = s[0].z;
+  red[ty][tx * 4 + 3] = s[0].w;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int cc = blockIdx.x * 64 + threadIdx.x;
+    if (cc < N) {
+      float a = 0.f;
+#pragma unroll
+      for (int l = 0; l < kFinLanes; ++l) a += red[l][threadIdx.x];
+      st1<O>(out + cc, a);
+    }
+  }
 }
 
 }  // namespace
@@ -90,7 +123,8 @@ int colsum_partials(int64_t M, int N) {
 }
 
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st) {
-  const dim3 grid((N + kThreads - 1) / kThreads);
+  if (N % 4 != 0 || P < 1) return hipErrorInvalidValue;
+  const dim3 grid((N + 63) / 64);
   if (out_dtype == kF32)
     hipLaunchKernelGGL(colsum_final_k<float>, grid, dim3(kThreads), 0, st, part, P, N, static_cast<float*>(out));
   else if (out_dtype == kBF16)

@@ -10,6 +10,8 @@ from hyperion.bench import models as M  # noqa: E402
 which = sys.argv[1]
 if which == "vit":
     r = M.bench_vit_step(checkpointing=False, steps=5, warmup=3)
+elif which == "vitgraph":
+    r = M.bench_vit_step(checkpointing=False, steps=20, warmup=5, graph=True)
 elif which == "vitckpt":
     r = M.bench_vit_step(checkpointing=True, steps=5, warmup=3)
 elif which == "llama":
