@@ -112,6 +112,27 @@ at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dty
   return out;
 }
 
+// (dy, db): the activation backward (act "relu": z = the saved output; "gelu": z = the pre-activation)
+// with the bias gradient summed in the same pass
+std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z, int64_t act,
+                                       c10::optional<at::ScalarType> db_dtype) {
+  HYP_CHECK_CUDA_TENSOR(dh);
+  TORCH_CHECK(dh.is_contiguous() && z.is_contiguous() && dh.sizes() == z.sizes() && dh.scalar_type() == z.scalar_type(),
+              "act_bwd_colsum: dh / z contiguous, one shape and dtype");
+  TORCH_CHECK(dh.scalar_type() == at::kBFloat16 || dh.scalar_type() == at::kHalf, "act_bwd_colsum: bf16/f16");
+  const int64_t N = dh.size(-1), M = dh.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && M >= 1, "act_bwd_colsum: N % 8 == 0");
+  const at::DeviceGuard guard(dh.device());
+  auto dy = at::empty_like(dh);
+  const auto odt = db_dtype.value_or(dh.scalar_type());
+  auto db = at::empty({N}, dh.options().dtype(odt));
+  const int P = hyp::colsum_partials(M, (int)N);
+  auto part = at::empty({(int64_t)P * N}, dh.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::act_bwd_colsum(dtype_code(dh), (int)act, dh.data_ptr(), z.data_ptr(), dy.data_ptr(), M, (int)N,
+                                    db.data_ptr(), dtype_code(db), part.data_ptr<float>(), P, cur_stream()));
+  return {dy, db};
+}
+
 // ---- multi-tensor optimizer ------------------------------------------------------------------
 void adam_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t T, int64_t chunk,
              double lr, double b1, double b2, double eps, double wd, bool adamw, const c10::optional<at::Tensor>& lr_t,
@@ -180,6 +201,8 @@ void register_norm_ops(pybind11::module& m) {
   m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());
+  m.def("act_bwd_colsum", &act_bwd_colsum, "activation backward + bias gradient in one pass (act 1 relu, 2 gelu)",
+        pybind11::arg("dh"), pybind11::arg("z"), pybind11::arg("act"), pybind11::arg("db_dtype") = pybind11::none());
   m.def("unscale_mt", &unscale_mt, "multi-tensor unscale + non-finite check");
   m.def("sumsq_mt", &sumsq_mt, "multi-tensor sum of squares");
   m.def("clip_mt", &clip_mt, "multi-tensor clip by global norm (device scalar)");

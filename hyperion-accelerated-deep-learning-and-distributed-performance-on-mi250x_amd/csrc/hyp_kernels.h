@@ -212,6 +212,10 @@ int colsum_partials(int64_t M, int N);
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,
                       hipStream_t st);
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);
+// dy = dh·act'(z) (act 1: ReLU with z = output; 2: exact GELU with z = pre-activation) and its column
+// sums into db (out_dtype; null: skip) — the FFN activation backward + bias gradient.
+hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, void* dy, int64_t M, int N, void* db,
+                          int out_dtype, float* part, int P, hipStream_t st);
 }  // namespace hyp
 
 namespace hyp {

@@ -68,6 +68,70 @@ __global__ __launch_bounds__(kThreads) void colsum_partial_k(const T* __restrict
 // sum over the 16 lanes (deterministic).
 constexpr int kFinLanes = 16;
 
+// Activation backward + bias-gradient partials in one pass (the FFN's first linear): dy = dh·act'(z)
+// is written once and its column sums are accumulated from registers — autograd ran the
+// activation backward, then read dy again for the bias gradient (two kernels more per layer).
+// ACT 1: ReLU with z = the saved output h (dy = h > 0 ? dh : 0); ACT 2: exact-erf GELU with z =
+// the saved pre-activation.
+template <typename T, int ACT>
+__global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict__ dh, const T* __restrict__ z,
+                                                             T* __restrict__ dy, int64_t M, int N,
+                                                             int64_t rows_per_block, float* __restrict__ part) {
+  __shared__ float red[kRowGroups][kColThreads * 8];
+  const int ct = threadIdx.x % kColThreads, rg = threadIdx.x / kColThreads;
+  const int c0 = (blockIdx.y * kColThreads + ct) * 8;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float acc[2][8];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[u][j] = 0.f;
+  auto one = [&](int64_t r, float (&a)[8], const float (&g)[8], const float (&zz)[8]) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float d;
+      if (ACT == 1) {
+        d = zz[j] > 0.f ? g[j] : 0.f;
+      } else {
+        const float x = zz[j];
+        const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+        const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+        d = g[j] * (cdf + x * pdf);
+      }
+      o[j] = rnd<T>(d);  // the column sums see what is stored (the vendor bias grad reads dy)
+      a[j] += o[j];
+    }
+    Vec8<T>::store(dy + r * N + c0, o);
+  };
+  if (c0 < N) {
+    int64_t r = r0 + rg;
+    for (; r + kRowGroups < r1; r += 2 * kRowGroups) {  // two rows' loads in flight
+      float g0[8], z0[8], g1[8], z1[8];
+      Vec8<T>::load(dh + r * N + c0, g0);
+      Vec8<T>::load(z + r * N + c0, z0);
+      Vec8<T>::load(dh + (r + kRowGroups) * N + c0, g1);
+      Vec8<T>::load(z + (r + kRowGroups) * N + c0, z1);
+      one(r, acc[0], g0, z0);
+      one(r + kRowGroups, acc[1], g1, z1);
+    }
+    if (r < r1) {
+      float g0[8], z0[8];
+      Vec8<T>::load(dh + r * N + c0, g0);
+      Vec8<T>::load(z + r * N + c0, z0);
+      one(r, acc[0], g0, z0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][ct * 8 + j] = acc[0][j] + acc[1][j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < kColThreads * 8; i += kThreads) {
+    const int c = blockIdx.y * kColThreads * 8 + i;
+    if (c < N) part[(int64_t)blockIdx.x * N + c] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
 template <typename O>
 __global__ __launch_bounds__(kThreads) void colsum_final_k(const float* __restrict__ part, int P, int N,
                                                            O* __restrict__ out) {
@@ -155,6 +219,30 @@ hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return colsum_combine(part, P, N, out, out_dtype, st);
+}
+
+// dy = dh·act'(z) and db = Σ_rows dy (out_dtype) in two launches (act: 1 ReLU on the output, 2 GELU
+// on the pre-activation).  part: [P, N] fp32 workspace, P = colsum_partials(M, N).
+hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, void* dy, int64_t M, int N, void* db,
+                          int out_dtype, float* part, int P, hipStream_t st) {
+  if (N % 8 != 0 || M < 1 || P < 1 || (act != 1 && act != 2) || (dtype != kBF16 && dtype != kF16))
+    return hipErrorInvalidValue;
+  const int64_t rpb = (M + P - 1) / P;
+  const dim3 grid(P, (N + kColThreads * 8 - 1) / (kColThreads * 8));
+#define HYP_ACT_COLSUM(TT, A)                                                                                   \
+  hipLaunchKernelGGL((act_bwd_colsum_k<TT, A>), grid, dim3(kThreads), 0, st, static_cast<const TT*>(dh),        \
+                     static_cast<const TT*>(z), static_cast<TT*>(dy), M, N, rpb, part)
+  if (dtype == kBF16) {
+    if (act == 1) HYP_ACT_COLSUM(bf16_t, 1);
+    else HYP_ACT_COLSUM(bf16_t, 2);
+  } else {
+    if (act == 1) HYP_ACT_COLSUM(f16_t, 1);
+    else HYP_ACT_COLSUM(f16_t, 2);
+  }
+#undef HYP_ACT_COLSUM
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess || db == nullptr) return e;
+  return colsum_combine(part, P, N, db, out_dtype, st);
 }
 
 }  // namespace hyp

@@ -11,7 +11,8 @@ transposed in-kernel (ds_read_b64_tr_b16) — no ``w.t().contiguous()`` copy.
 ``linear(x, w, b)``: native forward when M <= ``SKINNY_MAX_M`` tokens and the shapes fit the
 kernel (in % 64, out % 8); native data gradient when out % 64 and in % 8; otherwise the vendor
 GEMM (bias in its epilogue).  The bias gradient is ``csrc/kernels/reduce.hip``'s column sum at
-any size; the weight gradient (only for trainable weights) is the vendor GEMM.
+any size; the weight gradient (only for trainable weights) is the split-K MFMA weight-gradient
+kernel when its output is small (``linear_wgrad``), else the vendor GEMM.
 """
 from __future__ import annotations
 
@@ -53,6 +54,26 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dy2 @ w
 
 
+# Weight gradients whose output is small (out x in <= WGRAD_NATIVE_MAX elements) run on the
+# split-K MFMA weight-gradient kernel (conv_wgrad.hip at 1x1): at these shapes it beats the vendor
+# TN GEMM, which under-fills the chip (MI355X, scripts/gemm_shapes.py: [6304x768]ᵀ[6304x768]
+# 28.7 vs 48.4 us; LM-256 FFN [4064x2048]ᵀ[4064x256] 22 vs 32 us; [4064x256]ᵀ[4064x2048] 19.7 vs
+# 32.8 us) and loses on larger ones (6304 x 768 -> 3072: 94 vs 68 us).
+WGRAD_NATIVE_MAX = int(os.environ.get("HYPERION_WGRAD_NATIVE_MAX", str(1 << 20)))
+
+
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """``dy2ᵀ @ x2`` (the weight gradient of ``linear_fwd``) in the operands' dtype."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    if (dy2.is_cuda and dy2.dtype == x2.dtype and dy2.dtype in (torch.bfloat16, torch.float16)
+            and N * K <= WGRAD_NATIVE_MAX and K % 64 == 0 and N % 8 == 0 and M < (1 << 22)
+            and dy2.is_contiguous() and x2.is_contiguous() and _native.use_native(dy2, op="wgrad")):
+        _native.count("linear_wgrad")
+        return _native.native().conv_wgrad(dy2.view(M, N, 1, 1), x2.view(M, K, 1, 1), 1, 1, 1, 1, 0, 0).view(N, K)
+    return dy2.t() @ x2
+
+
 def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """``dy2.sum(0)`` (a bias gradient) — ``csrc/kernels/reduce.hip`` column sums on gfx950 (autograd's
     generic reduction ran [6304, 768] bf16 at 0.4 TB/s in the ViT step)."""
@@ -84,7 +105,7 @@ class _LinearFn(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(w.dtype)
         dx = linear_dgrad(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = (dy2.t() @ x2).to(w.dtype) if ctx.needs_input_grad[1] else None
+        dw = linear_wgrad(dy2.contiguous(), x2.contiguous()).to(w.dtype) if ctx.needs_input_grad[1] else None
         db = bias_grad(dy2.contiguous(), ctx.bdt) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db
 

@@ -8,7 +8,10 @@ tensor — but it has no autograd formula.  ``linear_act`` wraps it:
 * ReLU: forward = one epilogue GEMM; backward masks with the saved OUTPUT (``h > 0`` ⇔ ``y > 0``),
   so the pre-activation is never stored;
 * GELU: backward needs the pre-activation, so the forward keeps ``y = x Wᵀ + b`` (bias epilogue)
-  and applies GELU once (the fused epilogue would force a GEMM recompute in backward).
+  and applies GELU once (the fused epilogue would force a GEMM recompute in backward);
+* backward: the activation backward and the bias gradient are ONE native pass
+  (``act_bwd_colsum``: dy written once, its column sums taken from registers), the weight
+  gradient on the MFMA split-K kernel when its output is small (``linear.linear_wgrad``).
 """
 from __future__ import annotations
 
@@ -17,7 +20,23 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from .linear import bias_grad
+from . import _native
+from .linear import bias_grad, linear_wgrad
+
+
+def _act_bwd(dh: torch.Tensor, z: torch.Tensor, act: str, bdt: torch.dtype, need_b: bool):
+    """(dy, db): the activation backward and, when needed, the bias gradient — one native pass
+    (``reduce.hip`` act_bwd_colsum) on gfx950, else autograd's ops."""
+    if (z.is_cuda and z.dtype in (torch.bfloat16, torch.float16) and z.shape[-1] % 8 == 0 and z.is_contiguous()
+            and _native.use_native(z, op="act_bwd")):
+        _native.count("act_bwd_colsum")
+        dy, db = _native.native().act_bwd_colsum(dh.contiguous(), z, 1 if act == "relu" else 2, bdt)
+        return dy, (db if need_b else None)
+    if act == "relu":
+        dy = torch.ops.aten.threshold_backward(dh, z, 0)
+    else:
+        dy = torch.ops.aten.gelu_backward(dh, z)
+    return dy, (bias_grad(dy, bdt) if need_b else None)
 
 
 def _cdt(x: torch.Tensor) -> torch.dtype:
@@ -40,10 +59,9 @@ class _LinearReLU(torch.autograd.Function):
     def backward(ctx, dh):
         x2, wc, h = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
-        dy = torch.ops.aten.threshold_backward(dh.reshape(h.shape).to(h.dtype), h, 0)
+        dy, db = _act_bwd(dh.reshape(h.shape).to(h.dtype), h, "relu", bdt, ctx.needs_input_grad[2])
         dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
-        dw = (dy.t() @ x2).to(wdt) if ctx.needs_input_grad[1] else None
-        db = bias_grad(dy, bdt) if ctx.needs_input_grad[2] else None
+        dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 
 
@@ -65,10 +83,9 @@ class _LinearGELU(torch.autograd.Function):
     def backward(ctx, dh):
         x2, wc, y = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
-        dy = torch.ops.aten.gelu_backward(dh.reshape(y.shape).to(y.dtype), y)
+        dy, db = _act_bwd(dh.reshape(y.shape).to(y.dtype), y, "gelu", bdt, ctx.needs_input_grad[2])
         dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
-        dw = (dy.t() @ x2).to(wdt) if ctx.needs_input_grad[1] else None
-        db = bias_grad(dy, bdt) if ctx.needs_input_grad[2] else None
+        dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 
 

@@ -143,3 +143,37 @@ def test_gelu_linear_act_grads_match_reference():
     yr.backward(g.float())
     for u, v in ((y, yr), (x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
         assert (u.float() - v).norm() <= 2e-2 * v.norm() + 1e-3
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+@pytest.mark.parametrize("shape", [(6304, 3072), (4064, 2048), (37, 264)])
+def test_act_bwd_colsum_matches_autograd(act, shape):
+    """Activation backward + bias-gradient column sums in one native pass == aten's
+    threshold/gelu backward followed by an fp64 column sum."""
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    M, N = shape
+    z = torch.randn(M, N, device="cuda").bfloat16()
+    dh = torch.randn(M, N, device="cuda").bfloat16()
+    dy, db = _native.native().act_bwd_colsum(dh, z, 1 if act == "relu" else 2, torch.float32)
+    ref = torch.ops.aten.threshold_backward(dh, z, 0) if act == "relu" else torch.ops.aten.gelu_backward(dh, z)
+    torch.testing.assert_close(dy.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(db, dy.double().sum(0).float(), atol=1e-2 * M ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(6304, 768, 768), (4064, 2048, 256), (4064, 256, 2048), (100, 64, 40)])
+def test_linear_wgrad_native_matches_mm(shape):
+    """Small-output weight gradients on the split-K MFMA kernel == dyᵀ·x (fp32 reference)."""
+    from hyperion.ops import _native
+    from hyperion.ops.linear import linear_wgrad
+
+    M, K, N = shape
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    _native.reset_counters()
+    dw = linear_wgrad(dy, x)
+    assert _native.counters().get("linear_wgrad", 0) == (1 if N % 8 == 0 and K % 64 == 0 else 0)
+    ref = dy.float().t() @ x.float()
+    assert (dw.float() - ref).norm() <= 5e-3 * ref.norm()
