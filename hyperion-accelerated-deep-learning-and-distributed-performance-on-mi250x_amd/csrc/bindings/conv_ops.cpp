@@ -105,6 +105,84 @@ at::Tensor conv_fwd_affine(const at::Tensor& x, const at::Tensor& w, int64_t sh,
   return y;
 }
 
+// ---- fused linear + cross-entropy (ops/cross_entropy.py) ----------------------------------------
+namespace {
+hyp::CeEpilogue ce_args(const c10::optional<at::Tensor>& bias, const at::Tensor& target, int64_t ignore, int64_t M,
+                        int64_t V, const at::Tensor& x) {
+  TORCH_CHECK(target.is_contiguous() && target.scalar_type() == at::kLong && target.numel() == M &&
+                  target.device() == x.device(),
+              "linear_ce: target must be a contiguous int64 [M] tensor on the input's device");
+  hyp::CeEpilogue ce;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == V,
+                "linear_ce: bias must be a contiguous fp32 [V] tensor");
+    ce.bias = bias->data_ptr<float>();
+  }
+  ce.target = target.data_ptr<int64_t>();
+  ce.ignore = ignore;
+  return ce;
+}
+
+void check_ce_operands(const at::Tensor& x, const at::Tensor& w) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous() && x.size(1) == w.size(1),
+              "linear_ce: contiguous x [M, E], w [V, E]");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "linear_ce: bf16/f16 x and w of one dtype");
+  TORCH_CHECK(x.size(1) % 64 == 0, "linear_ce: E % 64 == 0");
+}
+}  // namespace
+
+// Pass 1: (lse [M], loss_rows [M]) of z = x wᵀ (+ b) over all V classes without storing z.
+std::vector<at::Tensor> linear_ce_lse(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                                      const at::Tensor& target, int64_t ignore, int64_t bn) {
+  check_ce_operands(x, w);
+  const int64_t M = x.size(0), E = x.size(1), V = w.size(0);
+  TORCH_CHECK(M < INT32_MAX && V < INT32_MAX, "linear_ce: sizes");
+  const at::DeviceGuard guard(x.device());
+  hyp::CeEpilogue ce = ce_args(bias, target, ignore, M, V, x);
+  TORCH_CHECK(bn == 64 || bn == 128, "linear_ce_lse: bn 64 or 128");
+  const int kcols = (int)((V + 7) / 8 * 8);
+  const int tiles = (kcols + (int)bn - 1) / (int)bn;
+  auto fopt = x.options().dtype(at::kFloat);
+  auto part = at::empty({(int64_t)tiles * M * 2}, fopt);
+  auto zt = at::zeros({M}, fopt);
+  auto lse = at::empty({M}, fopt);
+  auto loss_rows = at::empty({M}, fopt);
+  ce.part = reinterpret_cast<float2*>(part.data_ptr<float>());
+  ce.zt = zt.data_ptr<float>();
+  HYP_CHECK_HIP(hyp::linear_ce(dtype_code(x), 1, x.data_ptr(), w.data_ptr(), nullptr, zero_page(x.device()).data_ptr(),
+                               (int)M, (int)E, kcols, (int)V, ce, cur_stream(), (int)bn));
+  HYP_CHECK_HIP(hyp::ce_lse_combine(ce.part, tiles, (int)M, ce.zt, ce.target, ignore, lse.data_ptr<float>(),
+                                    loss_rows.data_ptr<float>(), cur_stream()));
+  return {lse, loss_rows};
+}
+
+// Pass 2: dz [M, ceil8(n)] of classes [c0, c0 + n) (columns >= n are zero): the softmax gradient
+// (exp(z - lse) - onehot) * scale straight from the recomputed GEMM accumulators.
+at::Tensor linear_ce_grad(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                          const at::Tensor& target, int64_t ignore, const at::Tensor& lse, const at::Tensor& scale,
+                          int64_t c0, int64_t n, int64_t bn) {
+  check_ce_operands(x, w);
+  const int64_t M = x.size(0), E = x.size(1), V = w.size(0);
+  TORCH_CHECK(c0 >= 0 && n >= 1 && c0 + n <= V, "linear_ce_grad: class range");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == M && scale.scalar_type() == at::kFloat &&
+                  scale.numel() == 1 && lse.device() == x.device() && scale.device() == x.device(),
+              "linear_ce_grad: fp32 lse [M] and device scalar scale");
+  const at::DeviceGuard guard(x.device());
+  hyp::CeEpilogue ce = ce_args(bias, target, ignore, M, V, x);
+  ce.col_off = (int)c0;
+  ce.lse = lse.data_ptr<float>();
+  ce.scale = scale.data_ptr<float>();
+  const int kcols = (int)((n + 7) / 8 * 8);
+  auto dz = at::empty({M, kcols}, x.options());
+  const char* wrow = static_cast<const char*>(w.data_ptr()) + c0 * E * w.element_size();
+  TORCH_CHECK(bn == 64 || bn == 128, "linear_ce_grad: bn 64 or 128");
+  HYP_CHECK_HIP(hyp::linear_ce(dtype_code(x), 2, x.data_ptr(), wrow, dz.data_ptr(), zero_page(x.device()).data_ptr(),
+                               (int)M, (int)E, kcols, (int)n, ce, cur_stream(), (int)bn));
+  return dz;
+}
+
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
 // filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
 // bn_mode >= 0: BN-backward epilogue for the BN layer whose OUTPUT is dx's tensor (hyp::BnBwdEpilogue):
@@ -439,6 +517,12 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
         pybind11::arg("pw"), pybind11::arg("scale"), pybind11::arg("shift"),
         pybind11::arg("residual") = pybind11::none(), pybind11::arg("act") = false);
+  m.def("linear_ce_lse", &linear_ce_lse, "fused linear+CE pass 1: (lse, loss_rows), logits never stored",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("target"), pybind11::arg("ignore"),
+        pybind11::arg("bn") = 128);
+  m.def("linear_ce_grad", &linear_ce_grad, "fused linear+CE pass 2: softmax gradient of classes [c0, c0+n)",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"), pybind11::arg("target"), pybind11::arg("ignore"),
+        pybind11::arg("lse"), pybind11::arg("scale"), pybind11::arg("c0"), pybind11::arg("n"), pybind11::arg("bn") = 128);
   m.def("conv_set_stages", [](int64_t fwd, int64_t wgrad) {
     hyp::conv_set_stages((int)fwd);
     hyp::conv_wgrad_set_stages((int)wgrad);

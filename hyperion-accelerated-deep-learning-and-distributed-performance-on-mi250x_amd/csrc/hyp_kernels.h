@@ -147,6 +147,22 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
                     const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr,
                     const struct BnBwdEpilogue* bnb = nullptr);
+// Fused linear + cross-entropy epilogues of the implicit-GEMM kernel (linear_ce below).
+struct CeEpilogue {
+  const float* bias = nullptr;      // [V] fp32 or null, indexed by vocabulary index
+  const int64_t* target = nullptr;  // [M]
+  int64_t ignore = -100;
+  int col_off = 0;                  // vocabulary index of the chunk's first class
+  float2* part = nullptr;           // mode 1: [tiles_n][M] (row max, row Σexp)
+  float* zt = nullptr;              // mode 1: [M] target logit (written by the tile holding it)
+  const float* lse = nullptr;       // mode 2: [M]
+  const float* scale = nullptr;     // mode 2: device scalar (1 / non-ignored rows)
+};
+hipError_t linear_ce(int dtype, int mode, const void* x, const void* w, void* out, const void* zero, int M, int E,
+                     int kcols, int kvalid, const CeEpilogue& ce, hipStream_t st, int bn = 64);
+// lse[m] = log-sum-exp of the tiles' partials; loss_rows[m] = lse - zt (0 for ignored rows)
+hipError_t ce_lse_combine(const float2* part, int tiles, int M, const float* zt, const int64_t* target,
+                          int64_t ignore, float* lse, float* loss_rows, hipStream_t st);
 // Optional BatchNorm-backward epilogue of a stride-1 data gradient dX whose tensor is the output of a
 // fused BN(+residual)(+ReLU) layer: the stored value becomes dz = dX·mask (the BN input's upstream
 // gradient), and Σdz, Σdz·x per channel are added into `sums` — bn_backward_dx then needs no reduce

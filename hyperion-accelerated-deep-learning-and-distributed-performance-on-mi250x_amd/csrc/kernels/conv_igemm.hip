@@ -75,6 +75,8 @@ struct ConvArgs {
   const float* aff_scale;       // !STATS: out = act(round(acc) * scale[k] + shift[k] (+ addend)) (eval BN)
   const float* aff_shift;
   int aff_act;
+  int kvalid;                   // B rows that exist (< K only for a padded linear-CE vocabulary chunk)
+  CeEpilogue ce;                // EPI 1 / 2: fused linear + cross-entropy (see linear_ce)
 };
 
 // DGRAD = false: W is [K, R, S, C] (reduction contiguous; B tiles are row slices, read row-wise).
@@ -82,7 +84,9 @@ struct ConvArgs {
 //   the ORIGINAL filter [C_dgrad_in = a.C][R][S][K_dgrad_out = a.K]: a B tile is 64 reduction rows
 //   of W[c, R-1-r, S-1-s, n0 : n0+BN] (output channels contiguous), staged row-permuted
 //   (tr_row_to_k) and read transposed with ds_read_b64_tr_b16 — no flipped/transposed filter copy.
-template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB>
+// EPI 0: the stores above; 1: linear-CE log-sum-exp partials (no output tensor); 2: linear-CE
+// softmax gradient written in place of the logits (see linear_ce)
+template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, int EPI = 0>
 __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (wave tile BM/2 x BN/2)
   constexpr int IA = BM / 32, IB = BN / 32;  // glds instructions per wave per slice
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       const int row = (i * 4 + wave) * 8 + (lane >> 3);
       const int k = n0 + row;
       const int chunk = slot ^ swz(row);
-      b_src[i] = k < a.K ? a.w + (int64_t)k * ldw + chunk * 8 : nullptr;
+      b_src[i] = k < a.kvalid ? a.w + (int64_t)k * ldw + chunk * 8 : nullptr;
     } else {  // image [64 reduction rows][BN]: a wave instruction fills 1024 / (2 BN) rows
       constexpr int RB = 1024 / (2 * BN), CB = BN / 8;
       const int row = (i * 4 + wave) * RB + lane / CB;
@@ -240,6 +244,87 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
   __syncthreads();  // the epilogue reuses the ring
+
+  if (EPI != 0) {
+    // ---- fused linear + cross-entropy.  Class n0 + n of this tile is vocabulary index
+    // col_off + n; z = round(acc + bias) (the bf16 logit the unfused path would store).
+    // EPI 1: per-row (max, Σexp) over the tile's classes -> ce.part[tile_n][m], the target
+    //        logit -> ce.zt[m]; the logits are never written.
+    // EPI 2: acc <- (exp(z - lse[m]) - [class == target]) * scale (0 for ignored rows and padded
+    //        classes), then the regular store epilogue writes dz.
+    const CeEpilogue& ce = a.ce;
+    float bcol[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * (BN / 2) + j * 16 + r16;
+      bcol[j] = (ce.bias != nullptr && n < a.kvalid) ? ce.bias[a.ce.col_off + n] : 0.f;
+    }
+    const float gscale = EPI == 2 ? *ce.scale : 0.f;
+    float* ls = reinterpret_cast<float*>(smem);  // EPI 1: [2 (wn)][BM][2] (row max, row Σexp)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int lr = wm * (BM / 2) + i * 16 + c4 * 4 + e;
+        const int m = m0 + lr;
+        const int64_t tg = m < a.M ? ce.target[m] : ce.ignore;
+        if (EPI == 1) {
+          float v[FN], mx = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int n = n0 + wn * (BN / 2) + j * 16 + r16;
+            v[j] = -INFINITY;
+            if (n < a.kvalid) {
+              v[j] = rnd<T>(acc[i][j][e] + bcol[j]);
+              if (m < a.M && (int64_t)(ce.col_off + n) == tg) ce.zt[m] = v[j];
+            }
+            mx = fmaxf(mx, v[j]);
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));  // the row's 16 lanes
+          float sm = 0.f;
+          if (mx != -INFINITY) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) sm += __expf(v[j] - mx);  // exp(-inf) = 0 for padding
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+          if (r16 == 0) {
+            ls[(wn * BM + lr) * 2 + 0] = mx;
+            ls[(wn * BM + lr) * 2 + 1] = sm;
+          }
+        } else {
+          const float lse = m < a.M ? ce.lse[m] : 0.f;
+          const float sc = (m < a.M && tg != ce.ignore) ? gscale : 0.f;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int n = n0 + wn * (BN / 2) + j * 16 + r16;
+            float g = 0.f;
+            if (n < a.kvalid) {
+              const float z = rnd<T>(acc[i][j][e] + bcol[j]);
+              g = (__expf(z - lse) - ((int64_t)(ce.col_off + n) == tg ? 1.f : 0.f)) * sc;
+            }
+            acc[i][j][e] = g;
+          }
+        }
+      }
+    }
+    if (EPI == 1) {
+      __syncthreads();
+      for (int lr = tid; lr < BM; lr += kThreads) {
+        const int m = m0 + lr;
+        if (m < a.M) {
+          const float m0v = ls[lr * 2], s0 = ls[lr * 2 + 1];
+          const float m1v = ls[(BM + lr) * 2], s1 = ls[(BM + lr) * 2 + 1];
+          const float mx = fmaxf(m0v, m1v);
+          float sm = 0.f;
+          if (mx != -INFINITY) sm = s0 * __expf(m0v - mx) + s1 * __expf(m1v - mx);
+          ce.part[(int64_t)tn * a.M + m] = make_float2(mx, sm);
+        }
+      }
+      return;
+    }
+  }
 
   if (a.splits > 1) {  // split-K: raw fp32 partials (16 lanes = one 64-byte row segment per store)
     float* part = a.part + (int64_t)split * a.M * a.K;
@@ -526,6 +611,7 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   ConvArgs a{static_cast<const uint16_t*>(in), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out),
              static_cast<const uint16_t*>(zero), psum, psq, N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw, (int)M64};
   a.group = conv_fwd_group(a.M, K, R * S, bm, bn);
+  a.kvalid = K;
   const int nk = R * S * (C / kBK);
   splits = max(1, min(splits, nk));
   a.steps_per_split = (nk + splits - 1) / splits;
@@ -565,6 +651,50 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   if (bm == 128 && bn == 128) return launch<f16_t, 128, 128>(a, stats, dgrad, st);
   if (bm == 128 && bn == 64) return launch<f16_t, 128, 64>(a, stats, dgrad, st);
   return launch<f16_t, 64, 64>(a, stats, dgrad, st);
+}
+
+// Fused linear + cross-entropy GEMM passes (ops/cross_entropy.py): z = x[M, E] · w[classes]ᵀ (+ b)
+// on the MFMA implicit-GEMM kernel (R = S = 1), 128 x bn tiles, classes [col_off, col_off + kvalid)
+// of the vocabulary (w points at row col_off; kcols = kvalid rounded up to 8 for mode 2's store).
+//   mode 1: ce.part [ceil(kcols / bn), M] (row max, row Σexp) + ce.zt — the logits never stored;
+//   mode 2: out [M, kcols] = dz of those classes (the softmax gradient, ready for the dX / dW GEMMs).
+hipError_t linear_ce(int dtype, int mode, const void* x, const void* w, void* out, const void* zero, int M, int E,
+                     int kcols, int kvalid, const CeEpilogue& ce, hipStream_t st, int bn) {
+  if (E % kBK != 0 || kcols % 8 != 0 || kvalid > kcols || kvalid < 1 || M < 1 || (mode != 1 && mode != 2) ||
+      (dtype != kBF16 && dtype != kF16) || (bn != 64 && bn != 128))
+    return hipErrorInvalidValue;
+  if (mode == 1 && (ce.part == nullptr || ce.zt == nullptr)) return hipErrorInvalidValue;
+  if (mode == 2 && (out == nullptr || ce.lse == nullptr || ce.scale == nullptr)) return hipErrorInvalidValue;
+  ConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out),
+             static_cast<const uint16_t*>(zero), nullptr, nullptr, M, 1, 1, E, kcols, 1, 1, 1, 1, 1, 1, 0, 0, M};
+  constexpr int BM = 128;
+  a.group = conv_fwd_group(M, kcols, 1, BM, bn);
+  a.kvalid = kvalid;
+  a.splits = 1;
+  a.steps_per_split = E / kBK;
+  a.ce = ce;
+  const int tiles = ((M + BM - 1) / BM) * ((kcols + bn - 1) / bn);
+#define HYP_CE_LAUNCH(TT, BNV, MODE) \
+  hipLaunchKernelGGL((conv_fwd_k<TT, BM, BNV, false, false, 2, MODE>), dim3(tiles), dim3(kThreads), 0, st, a)
+  if (dtype == kBF16) {
+    if (bn == 128) {
+      if (mode == 1) HYP_CE_LAUNCH(bf16_t, 128, 1);
+      else HYP_CE_LAUNCH(bf16_t, 128, 2);
+    } else {
+      if (mode == 1) HYP_CE_LAUNCH(bf16_t, 64, 1);
+      else HYP_CE_LAUNCH(bf16_t, 64, 2);
+    }
+  } else {
+    if (bn == 128) {
+      if (mode == 1) HYP_CE_LAUNCH(f16_t, 128, 1);
+      else HYP_CE_LAUNCH(f16_t, 128, 2);
+    } else {
+      if (mode == 1) HYP_CE_LAUNCH(f16_t, 64, 1);
+      else HYP_CE_LAUNCH(f16_t, 64, 2);
+    }
+  }
+#undef HYP_CE_LAUNCH
+  return hipGetLastError();
 }
 
 }  // namespace hyp

@@ -153,4 +153,44 @@ hipError_t cross_entropy_fwd_bwd(int dtype, void* logits, int64_t rows, int V, i
   return hipGetLastError();
 }
 
+namespace {
+// One wave per row: merge the GEMM tiles' (max, Σexp) partials of the row (fixed order within a
+// lane, then a wave tree: deterministic) into lse and the per-row loss.
+__global__ __launch_bounds__(256) void ce_lse_combine_k(const float2* __restrict__ part, int tiles, int M,
+                                                        const float* __restrict__ zt,
+                                                        const int64_t* __restrict__ target, int64_t ignore,
+                                                        float* __restrict__ lse, float* __restrict__ loss_rows) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float mx = -INFINITY, sm = 0.f;
+  for (int t = lane; t < tiles; t += 64) {
+    const float2 p = part[(int64_t)t * M + m];
+    if (p.x == -INFINITY) continue;
+    if (p.x > mx) {
+      sm = sm * __expf(mx - p.x) + p.y;
+      mx = p.x;
+    } else {
+      sm += p.y * __expf(p.x - mx);
+    }
+  }
+  const float gmx = wave_max(mx);
+  float s = mx == -INFINITY ? 0.f : sm * __expf(mx - gmx);
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float l = gmx + __logf(s);
+    lse[m] = l;
+    loss_rows[m] = target[m] == ignore ? 0.f : l - zt[m];
+  }
+}
+}  // namespace
+
+hipError_t ce_lse_combine(const float2* part, int tiles, int M, const float* zt, const int64_t* target,
+                          int64_t ignore, float* lse, float* loss_rows, hipStream_t st) {
+  if (tiles < 1 || M < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_lse_combine_k, dim3((M + 3) / 4), dim3(256), 0, st, part, tiles, M, zt, target, ignore, lse,
+                     loss_rows);
+  return hipGetLastError();
+}
+
 }  // namespace hyp

@@ -5,18 +5,23 @@ every LM trainer (``02_development/distributed_utils.py:161,175-177``, ``core_fr
 243-262``, ``mixed_precision.ipynb:121-145``) — the logits GEMM dominates LM compute (≈105 GFLOP
 forward at 4064 tokens) and PyTorch materialises fp32 log-softmax and its gradient.
 
-Hyperion computes the loss AND all three gradients inside the forward:
+Hyperion computes the loss AND all three gradients inside the forward, without ever storing the
+[N, V] logits (gfx950, bf16/f16, E % 64 == 0):
 
-1. ``z = x @ Wᵀ + b`` (one hipBLASLt GEMM; bf16 under AMP);
-2. ``ce_fwd_bwd`` (``csrc/kernels/cross_entropy.hip``) turns ``z`` into ``dz = (softmax(z) −
-   onehot) / n_valid`` in place and emits per-row losses — two passes over the logits, the
-   second served from L2;
-3. ``dx = dz @ W``, ``dW = dzᵀ @ x``, ``db = Σ dz``.
+1. ``linear_ce_lse`` — the logits GEMM on the MFMA implicit-GEMM kernel with a log-sum-exp
+   epilogue (``conv_igemm.hip`` EPI 1): every 128 x 64 tile reduces its accumulators to per-row
+   (max, Σexp) partials and captures the target logit; a one-wave-per-row combine
+   (``cross_entropy.hip``) gives lse and the per-row losses.  No logits tensor exists;
+2. per vocabulary chunk (``chunk`` classes, default 8192): ``linear_ce_grad`` recomputes the
+   chunk's logits on the same kernel and its epilogue writes dz = (exp(z − lse) − onehot) /
+   n_valid straight from the accumulators (EPI 2); then ``dx += dz W_c`` and ``dW_c = dzᵀ x``
+   (vendor GEMMs) and ``db_c = Σ dz`` (column sums).  Peak extra memory is one [N, chunk] dz
+   block instead of the [N, V] logits (LM-256: 65 MB instead of 408 MB).
 
 Backward then only scales the saved gradients by the incoming scalar.  ``n_valid`` (non-ignored
-tokens) stays on the device, so the op has no host sync and is hipGraph-capturable.  With 288 GB
-of HBM per GPU the whole [N, V] logits block is processed at once unless it exceeds
-``max_logits_bytes`` (default 4 GiB), in which case rows are chunked and dW accumulates in fp32.
+tokens) stays on the device, so the op has no host sync and is hipGraph-capturable.  Elsewhere
+(CPU, fp32) the reference path materializes ``z`` (in row chunks above ``max_logits_bytes``) and
+runs ``ce_fwd_bwd`` / the PyTorch oracle on it.
 """
 from __future__ import annotations
 
@@ -27,7 +32,21 @@ import torch.nn.functional as F
 
 from . import _native
 
+import os
+
 DEFAULT_MAX_LOGITS_BYTES = 4 << 30
+# The fused path's dz block is at most CE_BLOCK_BYTES: the vocabulary is cut into the fewest equal
+# 64-class-aligned chunks that fit (LM-256, 4064 x 50257 bf16 = 408 MB of logits: 2 chunks; fewer,
+# larger chunks keep the dX / dW GEMMs efficient).  HYPERION_CE_CHUNK forces a class count.
+CE_BLOCK_BYTES = int(os.environ.get("HYPERION_CE_BLOCK_MB", "256")) << 20
+CE_CHUNK = int(os.environ.get("HYPERION_CE_CHUNK", "0"))
+
+
+def _ce_chunk(N: int, V: int, elt: int) -> int:
+    if CE_CHUNK > 0:
+        return CE_CHUNK
+    n = max(1, -(-N * V * elt // CE_BLOCK_BYTES))
+    return -(-(-(-V // n)) // 64) * 64
 
 
 def _compute_dtype(x: torch.Tensor, w: torch.Tensor) -> torch.dtype:
@@ -63,6 +82,8 @@ class _FusedLinearCE(torch.autograd.Function):
         n_valid = (t != ignore_index).sum().to(torch.float32).clamp_min(1.0)
         scale = (1.0 / n_valid).reshape(1)
         native = _native.use_native(x2, op="ce") and cdt in _native.DTYPE_CODE
+        if native and cdt in (torch.bfloat16, torch.float16) and x2.shape[1] % 64 == 0:
+            return _FusedLinearCE._fused(ctx, x, x2, w, bias, t, ignore_index, scale, n_valid, shape)
         rows = max(1, min(N, max_bytes // max(1, V * x2.element_size())))
         dx = torch.empty_like(x2)
         need_w = ctx.needs_input_grad[1]
@@ -94,6 +115,41 @@ class _FusedLinearCE(torch.autograd.Function):
         ctx.save_for_backward(dx.view(shape), dw if dw is not None else torch.empty(0),
                               db if db is not None else torch.empty(0))
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype, need_w, need_b)
+        return loss
+
+    @staticmethod
+    def _fused(ctx, x, x2, w, bias, t, ignore_index, scale, n_valid, shape):
+        """The no-logits path (module docstring): LSE pass, then per-chunk gradient passes."""
+        C = _native.native()
+        _native.count("linear_ce_fused")
+        x2 = x2.contiguous()
+        w = w.contiguous()
+        b32 = bias.float().contiguous() if bias is not None else None
+        t = t.contiguous()
+        N, V = x2.shape[0], w.shape[0]
+        lse, loss_rows = C.linear_ce_lse(x2, w, b32, t, int(ignore_index))
+        need_w = ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        dx32 = None
+        dw = torch.empty_like(w) if need_w else None
+        db = torch.empty(V, dtype=torch.float32, device=x2.device) if need_b else None
+        chunk = _ce_chunk(N, V, x2.element_size())
+        for c0 in range(0, V, chunk):
+            n = min(chunk, V - c0)
+            dz = C.linear_ce_grad(x2, w, b32, t, int(ignore_index), lse, scale, c0, n)  # [N, ceil8(n)]
+            dzv = dz[:, :n]
+            wc = w[c0:c0 + n]
+            # dX accumulates over the chunks in fp32 inside the GEMM (bf16 inputs, fp32 output)
+            dx32 = (torch.mm(dzv, wc, out_dtype=torch.float32) if dx32 is None
+                    else torch.addmm(dx32, dzv, wc, out_dtype=torch.float32))
+            if need_w:
+                torch.mm(dzv.t(), x2, out=dw[c0:c0 + n])
+            if need_b:
+                db[c0:c0 + n] = C.column_sum(dz, torch.float32)[:n]
+        loss = loss_rows.sum() * scale.reshape(())
+        ctx.save_for_backward(dx32.to(x2.dtype).view(shape), dw if dw is not None else torch.empty(0),
+                              db if db is not None else torch.empty(0))
+        ctx.meta = (x.dtype, w.dtype, None if bias is None else bias.dtype, need_w, need_b)
         return loss
 
     @staticmethod

@@ -34,6 +34,40 @@ def test_fused_linear_ce_matches_fp32_reference(dtype, V):
     torch.testing.assert_close(b.grad.float(), br.grad, **gt)
 
 
+@pytest.mark.parametrize("chunk", [8192, 1000])
+def test_fused_linear_ce_no_logits_path(chunk, monkeypatch):
+    """The bf16 path that never stores the [N, V] logits (LSE epilogue pass + per-chunk softmax-
+    gradient epilogue passes) runs, matches the fp32 reference, and its peak extra memory stays
+    well below the logits' size (LM-256 shape: 4064 tokens x 50257 classes, E = 256)."""
+    import hyperion.ops.cross_entropy as hce
+    from hyperion.ops import _native
+
+    monkeypatch.setattr(hce, "CE_CHUNK", chunk)
+    torch.manual_seed(0)
+    N, E, V, pad = 4064, 256, 50257, 50256
+    x = (torch.randn(N, E, device="cuda") * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(V, E, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    b = (torch.randn(V, device="cuda") * 0.1).requires_grad_(True)
+    t = torch.randint(0, V - 1, (N,), device="cuda")
+    t[::9] = pad
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    _native.reset_counters()
+    loss = hce.fused_linear_cross_entropy(x, w, b, t, ignore_index=pad)
+    loss.backward()
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    assert _native.counters().get("linear_ce_fused") == 1
+    assert peak < 0.6 * N * V * 2, peak  # the bf16 logits alone would be 408 MB
+    xr, wr, br = (a.detach().float().requires_grad_(True) for a in (x, w, b))
+    ref = F.cross_entropy(F.linear(xr, wr, br), t, ignore_index=pad)
+    ref.backward()
+    torch.testing.assert_close(loss.float(), ref, rtol=2e-2, atol=2e-2)
+    for got, want in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert (got.float() - want).norm() <= 3e-2 * want.norm() + 1e-6
+
+
 def test_fused_linear_ce_chunked_equals_unchunked():
     from hyperion.ops.cross_entropy import fused_linear_cross_entropy
 
