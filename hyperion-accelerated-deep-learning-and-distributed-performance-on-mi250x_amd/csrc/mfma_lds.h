@@ -95,6 +95,46 @@ __device__ __forceinline__ u16x8 frag_tr(const uint16_t* img, int r0, int cb, in
   return out;
 }
 
+// The same transposed fragment read with the image base in one VGPR and the row offset as the
+// instruction's immediate: the swizzle term of frag_tr depends only on (4g + q) for row offsets
+// that are multiples of 16, so a lane's byte offset (frag_tr_lane<W>) is fixed per column block
+// and every (k-step, half) variant is `base + imm` — no address VALU in the MFMA loop.
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_read_tr16_imm(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+  typedef short s16x4_t __attribute__((ext_vector_type(4)));
+  s16x4_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ unsigned frag_tr_lane(int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int row = 4 * g + q;
+  const int chunk = (cb >> 3) + (p >> 1);
+  return (unsigned)((row * W + ((chunk ^ swz_tr<W>(row)) << 3) + ((p & 1) << 2)) * 2);
+}
+
+// frag_tr<W>(img, R0, cb, lane) == frag_tr_at<W, R0>(lds_addr(img) + frag_tr_lane<W>(cb, lane))
+template <int W, int R0>
+__device__ __forceinline__ u16x8 frag_tr_at(unsigned base) {
+  static_assert(R0 % 16 == 0, "row offsets keep the swizzle phase");
+  const s16x4 v0 = ds_read_tr16_imm<R0 * W * 2>(base);
+  const s16x4 v1 = ds_read_tr16_imm<(R0 + 16) * W * 2>(base);
+  u16x8 out;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    out[e] = (uint16_t)v0[e];
+    out[4 + e] = (uint16_t)v1[e];
+  }
+  return out;
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their "don't wait" maxima).  gfx9 encoding:
 // vmcnt[3:0] in bits 3:0, vmcnt[5:4] in bits 15:14, expcnt in 6:4, lgkmcnt in 11:8.
 template <int N>

@@ -123,6 +123,35 @@ def test_conv_wgrad_matches_fp32(shape, dtype):
     assert err < 1e-2, f"rel err {err:.3e}"
 
 
+@pytest.mark.parametrize("cfg", [(64, 64, 1, 2), (64, 64, 7, 3), (128, 128, 3, 2), (128, 64, 5, 4),
+                                 (64, 128, 2, 2), (128, 128, 1, 3),
+                                 # | 32: 128-pixel stages (dense kernel), | 16: dense shapes on the general kernel
+                                 (64, 64, 3, 2 | 32), (128, 64, 2, 3 | 32), (128, 128, 5, 2 | 32), (64, 64, 2, 2 | 16)])
+@pytest.mark.parametrize("shape", [(3, 256, 9, 9, 128, 1, 1, 0),    # dense 1x1, M = 243 (tail stage)
+                                   (2, 128, 13, 13, 192, 3, 1, 1),  # gathered 3x3, K % 128 != 0
+                                   (5, 128, 11, 11, 128, 1, 2, 0)])  # strided 1x1, several images per stage
+def test_conv_wgrad_tiles_splits_stages(shape, cfg):
+    """Every tile / split / LDS-ring variant of conv_wgrad.hip (the automatic plan picks among
+    them) against the fp32 reference, on dense and gathered inputs with partial stages."""
+    from hyperion.ops import _native
+
+    C_ = _native.native()
+    N, C, H, W, K, R, s, p = shape
+    bm, bn, splits, nb = cfg
+    torch.manual_seed(0)
+    P = (H + 2 * p - R) // s + 1
+    x = torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, P, P, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float().cpu(), (K, C, R, R), dy.float().cpu(), stride=s, padding=p)
+    C_.conv_set_stages(0, nb)
+    try:
+        dw = C_.conv_wgrad(dy, x, R, R, s, s, p, p, bm, bn, splits)
+    finally:
+        C_.conv_set_stages(0, 0)
+    err = (dw.float().cpu() - ref).norm() / ref.norm()
+    assert err < 1e-2, f"rel err {err:.3e}"
+
+
 @pytest.mark.parametrize("shape", [s for s in WGRAD_SHAPES if s[6] == 1 and s[4] % 64 == 0])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_conv_dgrad_matches_fp32(shape, dtype):
