@@ -146,7 +146,7 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
   const at::DeviceGuard guard(xin.device());
   auto dx = at::empty_like(xin);
   int P = 1, rpw = 1;
-  hyp::layernorm_bwd_geom(rows, &P, &rpw);
+  hyp::layernorm_bwd_geom(rows, d, &P, &rpw);
   auto fopt = xin.options().dtype(at::kFloat);
   auto part = at::empty({2 * (int64_t)P * d}, fopt);
   at::Tensor dw, db;

@@ -59,7 +59,7 @@ hipError_t stream_op(int op, const float* a, const float* b, float* c, float s, 
 namespace hyp {
 // ---- layernorm.hip ---------------------------------------------------------------------------
 bool layernorm_supported(int d);
-void layernorm_bwd_geom(int64_t rows, int* P, int* rows_per_wave);
+void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave);
 hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
                              const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
                              hipStream_t st);

@@ -241,9 +241,219 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
   }
 }
 
+// ---- wide rows (2048 < d <= 4096: Llama-2-7B's 4096) ------------------------------------------
+// One 256-thread block per row (4 waves x 64 lanes x VW vectors of 8): at one row per wave the
+// backward's register image of a 4096-wide row (dy, x, dres, their prefetch, dγ/dβ and the affine:
+// ~1 KB per lane) spilled 788 B/lane to scratch — 40-47 us per [128, 4096] RMSNorm backward on
+// MI355X, 2.7 ms of a Llama-2-7B LoRA step.  Here a lane holds VW <= 2 vectors per tensor, the row
+// statistics are a wave shuffle + a 4-wave LDS combine, and dγ/dβ partials are per-thread columns
+// written straight to the block's partial row (no LDS transpose).
+constexpr int kWideThreads = 256;
+
+template <typename T, int VW>
+__device__ __forceinline__ void wide_load(const T* base, int64_t row, int d, int tid, float (&o)[VW][8]) {
+#pragma unroll
+  for (int k = 0; k < VW; ++k) {
+    const int c = (k * kWideThreads + tid) * 8;
+    if (c < d) {
+      Vec8<T>::load(base + row * d + c, o[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[k][j] = 0.f;
+    }
+  }
+}
+
+template <int VW>
+__device__ __forceinline__ void wide_affine(const float* p, int d, int tid, float (&o)[VW][8], float dflt) {
+#pragma unroll
+  for (int k = 0; k < VW; ++k) {
+    const int c = (k * kWideThreads + tid) * 8;
+    if (p != nullptr && c < d) {
+      const float4 a = reinterpret_cast<const float4*>(p + c)[0];
+      const float4 b = reinterpret_cast<const float4*>(p + c)[1];
+      o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
+      o[k][4] = b.x; o[k][5] = b.y; o[k][6] = b.z; o[k][7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[k][j] = dflt;
+    }
+  }
+}
+
+// two block sums at once (one LDS round): red holds 2 x 4 floats
+__device__ __forceinline__ float2 block_sum2(float a, float b, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  __syncthreads();  // the previous row's readers are done with red
+  if (lane == 0) {
+    red[wid] = a;
+    red[4 + wid] = b;
+  }
+  __syncthreads();
+  return make_float2((red[0] + red[1]) + (red[2] + red[3]), (red[4] + red[5]) + (red[6] + red[7]));
+}
+
+template <typename T, int VW, bool RMS, bool HAS_RES>
+__global__ __launch_bounds__(kWideThreads) void ln_fwd_wide_k(const T* __restrict__ x, const T* __restrict__ r,
+                                                              T* __restrict__ s_out, T* __restrict__ y,
+                                                              const float* __restrict__ w, const float* __restrict__ b,
+                                                              float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                              int64_t rows, int d, float eps, int rpb) {
+  __shared__ float red[8];
+  const int tid = threadIdx.x;
+  float wv[VW][8], bv[VW][8];
+  wide_affine<VW>(w, d, tid, wv, 1.f);
+  wide_affine<VW>(RMS ? nullptr : b, d, tid, bv, 0.f);
+  for (int i = 0; i < rpb; ++i) {
+    const int64_t row = (int64_t)blockIdx.x * rpb + i;
+    if (row >= rows) break;
+    float v[VW][8];
+    wide_load<T, VW>(x, row, d, tid, v);
+    if (HAS_RES) {
+      float rv[VW][8];
+      wide_load<T, VW>(r, row, d, tid, rv);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        const int c = (k * kWideThreads + tid) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = rnd<T>(v[k][j] + rv[k][j]);  // stats of the stored stream
+        if (c < d) Vec8<T>::store(s_out + row * d + c, v[k]);
+      }
+    }
+    // two passes like the narrow kernel: the mean, then Σ(x - mean)² (zero-filled lanes past d
+    // are excluded from the second)
+    float mean = 0.f;
+    if (!RMS) {
+      float s1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < VW; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s1 += v[k][j];
+      mean = block_sum2(s1, 0.f, red).x / d;
+    }
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < VW; ++k) {
+      if ((k * kWideThreads + tid) * 8 < d) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float tt = v[k][j] - mean;
+          s2 += tt * tt;
+        }
+      }
+    }
+    const float rstd = rsqrtf(block_sum2(s2, 0.f, red).x / d + eps);
+    if (tid == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+#pragma unroll
+    for (int k = 0; k < VW; ++k) {
+      const int c = (k * kWideThreads + tid) * 8;
+      if (c < d) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * wv[k][j] + bv[k][j];
+        Vec8<T>::store(y + row * d + c, o);
+      }
+    }
+  }
+}
+
+template <typename T, int VW, bool RMS, bool HAS_DRES>
+__global__ __launch_bounds__(kWideThreads) void ln_bwd_wide_k(const T* __restrict__ dy, const T* __restrict__ xin,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ mean_in,
+                                                              const float* __restrict__ rstd_in,
+                                                              const T* __restrict__ dres, T* __restrict__ dx,
+                                                              float* __restrict__ pdw, float* __restrict__ pdb,
+                                                              int64_t rows, int d, int rpb) {
+  __shared__ float red[8];
+  const int tid = threadIdx.x;
+  float gw[VW][8], gb[VW][8], wv[VW][8];
+#pragma unroll
+  for (int k = 0; k < VW; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gw[k][j] = gb[k][j] = 0.f;
+  wide_affine<VW>(w, d, tid, wv, 1.f);
+  for (int i = 0; i < rpb; ++i) {
+    const int64_t row = (int64_t)blockIdx.x * rpb + i;
+    if (row >= rows) break;
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float g[VW][8], xh[VW][8];
+    wide_load<T, VW>(dy, row, d, tid, g);
+    wide_load<T, VW>(xin, row, d, tid, xh);
+    float s1 = 0.f, s2 = 0.f;  // Σ g·w, Σ g·w·xhat
+#pragma unroll
+    for (int k = 0; k < VW; ++k) {
+      const int c = (k * kWideThreads + tid) * 8;
+      if (c < d) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[k][j] = (xh[k][j] - mean) * rstd;
+          const float gwv = g[k][j] * wv[k][j];
+          s1 += gwv;
+          s2 += gwv * xh[k][j];
+          gw[k][j] += g[k][j] * xh[k][j];
+          gb[k][j] += g[k][j];
+        }
+      }
+    }
+    const float2 t = block_sum2(s1, s2, red);
+    const float m1 = t.x / d, m2 = t.y / d;
+#pragma unroll
+    for (int k = 0; k < VW; ++k) {
+      const int c = (k * kWideThreads + tid) * 8;
+      if (c < d) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] * wv[k][j] - (RMS ? 0.f : m1) - xh[k][j] * m2);
+        if (HAS_DRES) {
+          float rv[8];
+          Vec8<T>::load(dres + row * d + c, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rv[j];
+        }
+        Vec8<T>::store(dx + row * d + c, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < VW; ++k) {
+    const int c = (k * kWideThreads + tid) * 8;
+    if (c < d) {
+      float4* pw = reinterpret_cast<float4*>(pdw + (int64_t)blockIdx.x * d + c);
+      pw[0] = make_float4(gw[k][0], gw[k][1], gw[k][2], gw[k][3]);
+      pw[1] = make_float4(gw[k][4], gw[k][5], gw[k][6], gw[k][7]);
+      if (pdb) {
+        float4* pb = reinterpret_cast<float4*>(pdb + (int64_t)blockIdx.x * d + c);
+        pb[0] = make_float4(gb[k][0], gb[k][1], gb[k][2], gb[k][3]);
+        pb[1] = make_float4(gb[k][4], gb[k][5], gb[k][6], gb[k][7]);
+      }
+    }
+  }
+}
+
+// rows per block of the wide kernels: >= 1 block per row up to 1024 blocks
+int wide_rows_per_block(int64_t rows) { return (int)((rows + 1023) / 1024); }
+
 template <typename T, bool RMS>
 hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, const float* b, float* mean,
                            float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
+  if (d > 2048) {
+    const int rpb = wide_rows_per_block(rows);
+    const dim3 grid((unsigned)((rows + rpb - 1) / rpb)), block(kWideThreads);
+    if (r)
+      hipLaunchKernelGGL((ln_fwd_wide_k<T, 2, RMS, true>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, d,
+                         eps, rpb);
+    else
+      hipLaunchKernelGGL((ln_fwd_wide_k<T, 2, RMS, false>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, d,
+                         eps, rpb);
+    return hipGetLastError();
+  }
   const int vpl = (d + 511) / 512;
   // rows per wave: 2+ once there are enough rows to keep ~2048 waves busy (the prefetch needs a next row)
   int rpw = 1;
@@ -276,6 +486,18 @@ template <typename T, bool RMS>
 hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const float* mean, const float* rstd,
                            const T* dres, T* dx, float* pdw, float* pdb, float* dw, float* db, int64_t rows, int d,
                            int P, int rows_per_wave, hipStream_t st) {
+  if (d > 2048) {  // P blocks of rows_per_wave rows (layernorm_bwd_geom)
+    if (dres)
+      hipLaunchKernelGGL((ln_bwd_wide_k<T, 2, RMS, true>), dim3(P), dim3(kWideThreads), 0, st, dy, xin, w, mean, rstd,
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave);
+    else
+      hipLaunchKernelGGL((ln_bwd_wide_k<T, 2, RMS, false>), dim3(P), dim3(kWideThreads), 0, st, dy, xin, w, mean, rstd,
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, kF32, st);
+    if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, kF32, st);
+    return e;
+  }
   const int vpl = (d + 511) / 512;
   const dim3 grid(P), block(64 * kWavesPerBlock);
   const size_t lds = 2 * kWavesPerBlock * d * sizeof(float);
@@ -308,11 +530,19 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
 
 bool layernorm_supported(int d) {
   if (d % 8 != 0 || d > 4096) return false;
+  if (d > 2048) return true;  // block-per-row kernels
   const int vpl = (d + 511) / 512;
   return vpl <= 4 || vpl == 8;
 }
 
-void layernorm_bwd_geom(int64_t rows, int* P, int* rows_per_wave) {
+void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave) {
+  if (d > 2048) {  // wide rows: one 256-thread block per row group (ln_bwd_wide_k)
+    const int rpb = wide_rows_per_block(rows);
+    *rows_per_wave = rpb;
+    *P = (int)((rows + rpb - 1) / rpb);
+    if (*P < 1) *P = 1;
+    return;
+  }
   // enough waves to fill 256 CUs (>= min(rows, 2048) waves: a 128-token Llama step has only 128
   // rows of 4096 — at 8 rows per wave that was 4 workgroups, 136 us per RMSNorm backward), with
   // ~4 rows per wave so the row prefetch has work to hide behind; the partial rows (<= 1024

@@ -63,5 +63,48 @@ def main():
     json.dump(rows, open("gpurun_out/gemm_shapes.json", "w"), indent=1)
 
 
+def skinny():
+    """Llama-2-7B LoRA step shapes (batch 1 x 128 tokens): weight-streaming GEMMs.  Four weight
+    copies are cycled inside the graph so each launch reads its weight from HBM (4 x 86 MB > the
+    256 MB Infinity Cache), as in the real step."""
+    rows = []
+    M = 128
+    for K, N in [(4096, 4096), (4096, 11008), (11008, 4096)]:
+        ws = [(torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16() for _ in range(4)]
+        x = torch.randn(M, K, device="cuda").bfloat16()
+        dy = torch.randn(M, N, device="cuda").bfloat16()
+        U = torch.randn(M, 16, device="cuda").bfloat16()
+        V = torch.randn(16, N, device="cuda").bfloat16()
+        it = {"i": 0}
+
+        def nxt():
+            it["i"] = (it["i"] + 1) % 4
+            return ws[it["i"]]
+
+        r = {"M": M, "K": K, "N": N, "floor_us": round(N * K * 2 / 6.0e6, 1)}
+        r["fwd_vendor"] = gtime(lambda: torch.nn.functional.linear(x, nxt()), n=8)
+        r["fwd_hyp"] = gtime(lambda: C_.linear_nt(x, nxt()), n=8)
+        r["fwd_hyp_lora"] = gtime(lambda: C_.linear_nt(x, nxt(), U=U, V=V), n=8)
+        r["fwd_vendor_lora"] = gtime(lambda: torch.addmm(torch.nn.functional.linear(x, nxt()), U, V), n=8)
+        r["dgrad_vendor"] = gtime(lambda: dy @ nxt(), n=8)
+        r["dgrad_hyp"] = gtime(lambda: C_.linear_nn(dy, nxt()), n=8)
+        for nb in (2, 3, 4):
+            C_.conv_set_stages(nb, 0)
+            for sp in (2, 4, 8, 16):
+                r[f"fwd_hyp_s{sp}_nb{nb}"] = gtime(lambda: C_.linear_nt(x, nxt(), splits=sp), n=8)
+                r[f"dgrad_hyp_s{sp}_nb{nb}"] = gtime(lambda: C_.linear_nn(dy, nxt(), splits=sp), n=8)
+            for bn in (64, 128):
+                r[f"fwd_hyp_bn{bn}_nb{nb}"] = gtime(lambda: C_.linear_nt(x, nxt(), bn=bn), n=8)
+        C_.conv_set_stages(0, 0)
+        r = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+    os.makedirs("gpurun_out", exist_ok=True)
+    json.dump(rows, open("gpurun_out/gemm_skinny.json", "w"), indent=1)
+
+
 if __name__ == "__main__":
-    main()
+    if "--skinny" in sys.argv:
+        skinny()
+    else:
+        main()

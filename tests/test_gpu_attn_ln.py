@@ -74,13 +74,14 @@ def test_attention_dropout_statistics_and_determinism():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("d", [256, 512, 768, 4096])
+@pytest.mark.parametrize("d", [256, 512, 768, 3072, 4096])
 @pytest.mark.parametrize("fused", [False, True])
 def test_layernorm(dtype, d, fused):
     from hyperion.ops.layernorm import _LNFn
 
     torch.manual_seed(0)
-    x = torch.randn(37, d, device="cuda", dtype=dtype)
+    # d > 2048 runs the block-per-row kernels; 2100 rows give them 3 rows per block and a partial last block
+    x = torch.randn(2100 if d == 3072 else 37, d, device="cuda", dtype=dtype)
     r = torch.randn_like(x) if fused else None
     w = torch.rand(d, device="cuda") + 0.5
     b = torch.randn(d, device="cuda")
