@@ -25,9 +25,115 @@ at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::S
   return c;
 }
 
+const at::Tensor& gemm_zero_page(const at::Device& dev) {
+  static at::Tensor z[16];
+  const int i = dev.index() < 0 ? 0 : dev.index();
+  if (!z[i].defined()) z[i] = at::zeros({256}, at::TensorOptions().device(dev).dtype(at::kByte));
+  return z[i];
+}
+
+// Operand view: a 2D tensor with unit stride in its last dim.  row form (tr = false): X[i, k] at
+// row i; tr form: X is [K, I] with X(i, k) = X[k, i].
+void check_operand(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) % 8 == 0 && t.stride(0) >= t.size(1),
+              "gemm: ", name, " must be 2D, unit stride in dim 1, row stride a multiple of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "gemm: ", name, " base must be 16-byte aligned");
+}
+
+// C = epi(alpha · A·Bᵀ) with A [M, K] (a_tr: [K, M]) and B [N, K] (b_tr: [K, N]).
+at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, c10::optional<at::ScalarType> out_dtype,
+                const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& aux,
+                const c10::optional<at::Tensor>& residual, double alpha, double beta,
+                const c10::optional<at::Tensor>& out, int64_t tile, int64_t splits) {
+  HYP_CHECK_CUDA_TENSOR(a);
+  check_operand(a, "a");
+  check_operand(b, "b");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf),
+              "gemm: bf16/f16 operands of one dtype");
+  const int64_t M = a_tr ? a.size(1) : a.size(0), K = a_tr ? a.size(0) : a.size(1);
+  const int64_t N = b_tr ? b.size(1) : b.size(0), Kb = b_tr ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm: reduction sizes differ (", K, " vs ", Kb, ")");
+  TORCH_CHECK(N % 4 == 0 && K % 8 == 0 && (!a_tr || M % 8 == 0) && (!b_tr || N % 8 == 0),
+              "gemm: needs N % 4 == 0, K % 8 == 0 (and M / N % 8 == 0 for transposed operands)");
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dims must fit int32");
+  const at::DeviceGuard guard(a.device());
+  at::Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 4 == 0,
+                "gemm: out must be [M, N] with unit column stride");
+    TORCH_CHECK(!out_dtype.has_value() || *out_dtype == c.scalar_type(), "gemm: out dtype mismatch");
+  } else {
+    TORCH_CHECK(beta == 0.0, "gemm: beta needs out");
+    c = at::empty({M, N}, a.options().dtype(out_dtype.has_value() ? *out_dtype : a.scalar_type()));
+  }
+  hyp::GemmTiledArgs g;
+  g.in_dtype = dtype_code(a);
+  g.out_dtype = dtype_code(c);
+  g.A = a.data_ptr();
+  g.B = b.data_ptr();
+  g.C = c.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = (int)a.stride(0);
+  g.ldb = (int)b.stride(0);
+  g.ldc = (int)c.stride(0);
+  g.a_tr = a_tr;
+  g.b_tr = b_tr;
+  g.act = (int)act;
+  TORCH_CHECK(act >= 0 && act <= 3, "gemm: act is 0 (none), 1 (relu), 2 (gelu), 3 (gelu tanh)");
+  g.alpha = (float)alpha;
+  g.beta = (float)beta;
+  g.tile = (int)tile;
+  g.splits = (int)splits;
+  g.zero = gemm_zero_page(a.device()).data_ptr();
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->dim() == 1 && bias->numel() == N && bias->is_contiguous(), "gemm: bias must be [N] contiguous");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm: bias must be 16-byte aligned");
+    g.bias = bias->data_ptr();
+    g.bias_dtype = dtype_code(*bias);
+  }
+  if (aux.has_value() && aux->defined()) {
+    TORCH_CHECK(act != 0 && aux->sizes() == c.sizes() && aux->strides() == c.strides() &&
+                    aux->scalar_type() == c.scalar_type(),
+                "gemm: aux (pre-activation) must match out and needs an activation");
+    g.aux = aux->data_ptr();
+  }
+  if (residual.has_value() && residual->defined()) {
+    const at::Tensor& r = *residual;
+    TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N && r.stride(1) == 1 && r.stride(0) % 4 == 0 &&
+                    r.scalar_type() == c.scalar_type(),
+                "gemm: residual must be [M, N], unit column stride, output dtype");
+    g.R = r.data_ptr();
+    g.ldr = (int)r.stride(0);
+  }
+  const int sp = hyp::gemm_tiled_splits(g);
+  at::Tensor part;
+  if (sp > 1) {
+    part = at::empty({(int64_t)sp * M * N}, a.options().dtype(at::kFloat));
+    g.part = part.data_ptr<float>();
+  }
+  HYP_CHECK_HIP(hyp::gemm_tiled(g, cur_stream()));
+  return c;
+}
+
+std::vector<int64_t> gemm_plan(int64_t M, int64_t N, int64_t K) {
+  int t, s;
+  hyp::gemm_tiled_plan((int)M, (int)N, (int)K, &t, &s);
+  return {t, s};
+}
+
 }  // namespace
 
 void register_gemm_ops(pybind11::module& m) {
+  m.def("gemm", &gemm, "C = epi(alpha A·Bᵀ): deep-pipelined MFMA GEMM, NT/NN/TN layouts, fused epilogue",
+        pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_tr") = false, pybind11::arg("b_tr") = false,
+        pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
+        pybind11::arg("act") = 0, pybind11::arg("aux") = pybind11::none(), pybind11::arg("residual") = pybind11::none(),
+        pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0, pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("tile") = -1, pybind11::arg("splits") = -1);
+  m.def("gemm_plan", &gemm_plan, "(tile, splits) the automatic plan picks for an M x N x K GEMM");
   m.def("gemm_nt", &gemm_nt, "C = alpha * A @ B.T on MFMA (bf16/f16 in)", pybind11::arg("a"), pybind11::arg("b"),
         pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("alpha") = 1.0, pybind11::arg("bk") = 64);
 }

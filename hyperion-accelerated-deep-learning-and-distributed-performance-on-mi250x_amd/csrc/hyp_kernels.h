@@ -127,6 +127,31 @@ namespace hyp {
 bool gemm_nt_supported(int M, int N, int K, int lda, int ldb, int bk);
 hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, void* C, int M, int N, int K, int lda,
                    int ldb, int ldc, float alpha, int bk, hipStream_t st);
+
+// ---- gemm_tiles.hip --------------------------------------------------------------------------
+// C[M,N] = epi(alpha Σ_k A(m,k) B(n,k)); A(m,k) at A + m*lda + k (a_tr = 0) or A + k*lda + m (a_tr = 1),
+// B likewise.  epi: + beta*C_old, + bias[n] (bias_dtype), aux = pre-activation, act (0 none, 1 relu,
+// 2 gelu-erf, 3 gelu-tanh), + R[m,n] (ldr), in out_dtype.  tile/splits < 0: automatic plan; split-K
+// needs part = fp32 [splits * M * N] (gemm_tiled_splits).  N % 4, K % 8, ld % 8; tr operands: M/N % 8.
+struct GemmTiledArgs {
+  int in_dtype = kBF16, out_dtype = kBF16, bias_dtype = kF32;
+  const void* A = nullptr;
+  const void* B = nullptr;
+  void* C = nullptr;
+  void* aux = nullptr;
+  const void* bias = nullptr;
+  const void* R = nullptr;
+  const void* zero = nullptr;
+  float* part = nullptr;
+  int M = 0, N = 0, K = 0, lda = 0, ldb = 0, ldc = 0, ldr = 0;
+  bool a_tr = false, b_tr = false;
+  int act = 0;
+  float alpha = 1.f, beta = 0.f;
+  int tile = -1, splits = -1;
+};
+void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits);
+int gemm_tiled_splits(const GemmTiledArgs& a);
+hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st);
 }  // namespace hyp
 
 namespace hyp {

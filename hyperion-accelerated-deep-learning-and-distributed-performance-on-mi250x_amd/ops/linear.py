@@ -10,9 +10,12 @@ transposed in-kernel (ds_read_b64_tr_b16) — no ``w.t().contiguous()`` copy.
 
 ``linear(x, w, b)``: native forward when M <= ``SKINNY_MAX_M`` tokens and the shapes fit the
 kernel (in % 64, out % 8); native data gradient when out % 64 and in % 8; otherwise the vendor
-GEMM (bias in its epilogue).  The bias gradient is ``csrc/kernels/reduce.hip``'s column sum at
-any size; the weight gradient (only for trainable weights) is the split-K MFMA weight-gradient
-kernel when its output is small (``linear_wgrad``), else the vendor GEMM.
+GEMM.  Above ``SKINNY_MAX_M`` tokens the three GEMMs go to the deep-pipelined tiled MFMA kernel
+(``ops.gemm``: bias fused in the forward epilogue, W read transposed in the data gradient, no
+copies) wherever it is at least as fast as the vendor GEMM for that shape.  The bias gradient is
+``csrc/kernels/reduce.hip``'s column sum at any size; the weight gradient (only for trainable
+weights) is the split-K MFMA weight-gradient kernel when its output is small (``linear_wgrad``),
+else the tiled kernel (or the vendor GEMM).
 """
 from __future__ import annotations
 
@@ -24,6 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from .gemm import mm_nn, mm_nt, mm_tn
 
 SKINNY_MAX_M = int(os.environ.get("HYPERION_SKINNY_MAX_M", "1024"))
 
@@ -44,14 +48,16 @@ def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x2 @ w.T`` for 2D ``x2`` (native when the shape fits, else the vendor GEMM)."""
     if x2.is_cuda and _fwd_ok(x2, w):
         return _native.native().linear_nt(x2.contiguous(), w)
-    return F.linear(x2, w)
+    y = mm_nt(x2, w) if x2.is_cuda else None
+    return y if y is not None else F.linear(x2, w)
 
 
 def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``dy2 @ w`` (the data gradient of ``linear_fwd``)."""
     if dy2.is_cuda and _bwd_ok(dy2, w):
         return _native.native().linear_nn(dy2.contiguous(), w)
-    return dy2 @ w
+    dx = mm_nn(dy2, w) if dy2.is_cuda else None
+    return dx if dx is not None else dy2 @ w
 
 
 # Weight gradients whose output is small (out x in <= WGRAD_NATIVE_MAX elements) run on the
@@ -59,7 +65,7 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # TN GEMM, which under-fills the chip (MI355X, scripts/gemm_shapes.py: [6304x768]ᵀ[6304x768]
 # 28.7 vs 48.4 us; LM-256 FFN [4064x2048]ᵀ[4064x256] 22 vs 32 us; [4064x256]ᵀ[4064x2048] 19.7 vs
 # 32.8 us) and loses on larger ones (6304 x 768 -> 3072: 94 vs 68 us).
-WGRAD_NATIVE_MAX = int(os.environ.get("HYPERION_WGRAD_NATIVE_MAX", str(1 << 20)))
+WGRAD_NATIVE_MAX = int(os.environ.get("HYPERION_WGRAD_NATIVE_MAX", str(1 << 18)))
 
 
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
@@ -71,7 +77,8 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
             and dy2.is_contiguous() and x2.is_contiguous() and _native.use_native(dy2, op="wgrad")):
         _native.count("linear_wgrad")
         return _native.native().conv_wgrad(dy2.view(M, N, 1, 1), x2.view(M, K, 1, 1), 1, 1, 1, 1, 0, 0).view(N, K)
-    return dy2.t() @ x2
+    dw = mm_tn(dy2, x2) if dy2.is_cuda else None
+    return dw if dw is not None else dy2.t() @ x2
 
 
 def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
@@ -88,8 +95,11 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
+        y = None
         if b is not None and not _fwd_ok(x2, w):
-            y = F.linear(x2, w, b.to(x2.dtype))  # bias in the vendor GEMM's epilogue
+            y = mm_nt(x2, w, bias=b) if x2.is_cuda else None  # bias in the tiled kernel's epilogue
+            if y is None:
+                y = F.linear(x2, w, b.to(x2.dtype))  # ... or the vendor GEMM's
         else:
             y = linear_fwd(x2, w)
             if b is not None:

@@ -1,4 +1,4 @@
-"""Linear + bias + activation with the activation in the GEMM epilogue (hipBLASLt).
+"""Linear + bias + activation with the activation in the GEMM epilogue (tiled MFMA kernel / hipBLASLt).
 
 Reference: every ``nn.TransformerEncoderLayer`` FFN runs ``linear1`` then ReLU/GELU as separate
 kernels (C14/C15/C5), and the ViT MLP likewise.  ``torch._addmm_activation`` asks hipBLASLt for the
@@ -7,8 +7,11 @@ tensor — but it has no autograd formula.  ``linear_act`` wraps it:
 
 * ReLU: forward = one epilogue GEMM; backward masks with the saved OUTPUT (``h > 0`` ⇔ ``y > 0``),
   so the pre-activation is never stored;
-* GELU: backward needs the pre-activation, so the forward keeps ``y = x Wᵀ + b`` (bias epilogue)
-  and applies GELU once (the fused epilogue would force a GEMM recompute in backward);
+* GELU: backward needs the pre-activation: the tiled MFMA kernel (``ops.gemm``) writes BOTH
+  ``z = x Wᵀ + b`` (aux output) and ``gelu(z)`` from one epilogue; on the vendor path the forward
+  keeps ``z`` (bias epilogue) and applies GELU as a second pass;
+* large-token GEMMs (forward, ``dy W``, ``dyᵀ x``) run on the tiled MFMA kernel where it beats the
+  vendor GEMM for the shape (``ops.gemm`` routing);
 * backward: the activation backward and the bias gradient are ONE native pass
   (``act_bwd_colsum``: dy written once, its column sums taken from registers), the weight
   gradient on the MFMA split-K kernel when its output is small (``linear.linear_wgrad``).
@@ -21,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native
+from .gemm import mm_nn, mm_nt
 from .linear import bias_grad, linear_wgrad
 
 
@@ -39,6 +43,11 @@ def _act_bwd(dh: torch.Tensor, z: torch.Tensor, act: str, bdt: torch.dtype, need
     return dy, (bias_grad(dy, bdt) if need_b else None)
 
 
+def _dgrad(dy: torch.Tensor, wc: torch.Tensor) -> torch.Tensor:
+    dx = mm_nn(dy, wc) if dy.is_cuda else None
+    return dx if dx is not None else dy @ wc
+
+
 def _cdt(x: torch.Tensor) -> torch.dtype:
     return torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else x.dtype
 
@@ -50,7 +59,9 @@ class _LinearReLU(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).to(dt)
         wc, bc = w.to(dt), b.to(dt)
-        h = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
+        h = mm_nt(x2, wc, bias=b, act="relu") if x2.is_cuda else None
+        if h is None:
+            h = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
         ctx.save_for_backward(x2, wc, h)
         ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
         return h.view(*shape[:-1], w.shape[0])
@@ -60,7 +71,7 @@ class _LinearReLU(torch.autograd.Function):
         x2, wc, h = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
         dy, db = _act_bwd(dh.reshape(h.shape).to(h.dtype), h, "relu", bdt, ctx.needs_input_grad[2])
-        dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(dy, wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 
@@ -74,17 +85,21 @@ class _LinearGELU(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).to(dt)
         wc, bc = w.to(dt), b.to(dt)
-        y = torch.addmm(bc, x2, wc.t())
+        y = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=dt) if x2.is_cuda else None
+        h = mm_nt(x2, wc, bias=b, act="gelu", aux=y) if x2.is_cuda else None
+        if h is None:
+            y = torch.addmm(bc, x2, wc.t())
+            h = F.gelu(y)
         ctx.save_for_backward(x2, wc, y)
         ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
-        return F.gelu(y).view(*shape[:-1], w.shape[0])
+        return h.view(*shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dh):
         x2, wc, y = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
         dy, db = _act_bwd(dh.reshape(y.shape).to(y.dtype), y, "gelu", bdt, ctx.needs_input_grad[2])
-        dx = (dy @ wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(dy, wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
         return dx, dw, db
 

@@ -18,8 +18,10 @@ elif which == "llama":
     r = M.bench_llama_lora_step(steps=3, warmup=2, graph=False)
 elif which == "llamagraph":
     r = M.bench_llama_lora_step(steps=5, warmup=3, graph=True)
+elif which == "lmgraph":
+    r = M.bench_lm_step(precision="bf16", graph=True, steps=20, warmup=5)
 elif which == "lm":
     r = M.bench_lm_step(precision="bf16", steps=5, warmup=3)
 else:
-    r = M.bench_lm_step(precision="bf16", graph=True, model="gpt2_small", batch=16, steps=5, warmup=3)
+    r = M.bench_lm_step(precision="bf16", graph=True, model="gpt2_small", batch=16, steps=10, warmup=3)
 print(json.dumps(r), flush=True)

@@ -1,0 +1,108 @@
+"""Deep-pipelined MFMA GEMM (gemm_tiles.hip) vs a plain fp32 PyTorch reference: NT / NN / TN
+operand layouts, every tile config, split-K, ragged M/N/K, and the fused epilogues (bias, ReLU,
+GELU with the pre-activation output, residual, alpha/beta accumulate)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from hyperion.ops import _native
+
+    return _native.native()
+
+
+def _rand(*shape, dtype=torch.bfloat16):
+    return (torch.rand(*shape, device="cuda") * 2 - 1).to(dtype)
+
+
+def _operands(M, N, K, a_tr, b_tr, dtype):
+    a = _rand(K, M, dtype=dtype) if a_tr else _rand(M, K, dtype=dtype)
+    b = _rand(K, N, dtype=dtype) if b_tr else _rand(N, K, dtype=dtype)
+    af = a.float().t() if a_tr else a.float()
+    bf = b.float().t() if b_tr else b.float()
+    return a, b, af @ bf.t()
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (392, 776, 200), (1000, 264, 1032)])
+def test_gemm_layouts_tiles_fp32_out(layout, tile, shape):
+    M, N, K = shape
+    a_tr, b_tr = layout[0] == "t", layout[1] == "n"
+    torch.manual_seed(0)
+    a, b, ref = _operands(M, N, K, a_tr, b_tr, torch.bfloat16)
+    c = _C().gemm(a, b, a_tr=a_tr, b_tr=b_tr, out_dtype=torch.float32, tile=tile, splits=1)
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+
+
+@pytest.mark.parametrize("splits", [2, 3, 7])
+@pytest.mark.parametrize("layout", ["nt", "tn"])
+def test_gemm_split_k(splits, layout):
+    M, N, K = 512, 384, 3072
+    a_tr, b_tr = layout[0] == "t", layout[1] == "n"
+    torch.manual_seed(1)
+    a, b, ref = _operands(M, N, K, a_tr, b_tr, torch.bfloat16)
+    c = _C().gemm(a, b, a_tr=a_tr, b_tr=b_tr, out_dtype=torch.float32, tile=2, splits=splits)
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+
+
+def test_gemm_fp16_and_identity():
+    # A = I with an asymmetric B catches a transposed C write (cdna guide §3)
+    n = 256
+    a = torch.eye(n, device="cuda", dtype=torch.float16)
+    b = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.float16)
+    for tile in (0, 1, 2):
+        c = _C().gemm(a, b, out_dtype=torch.float32, tile=tile, splits=1)
+        torch.testing.assert_close(c, b.float().t())
+
+
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_gemm_epilogue_bias_act_aux_residual(act):
+    M, N, K = 6304 // 8, 768, 768
+    torch.manual_seed(2)
+    x, w, ref = _operands(M, N, K, False, False, torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    res = _rand(M, N)
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if act else None
+    y = _C().gemm(x, w, bias=bias, act=act, aux=aux, residual=res)
+    z = (ref + bias).bfloat16().float()
+    if act == 1:
+        h = F.relu(z)
+    elif act == 2:
+        h = F.gelu(z)
+    elif act == 3:
+        h = F.gelu(z, approximate="tanh")
+    else:
+        h = ref + bias
+    want = h.bfloat16().float() + res.float()
+    torch.testing.assert_close(y.float(), want, rtol=2e-2, atol=2e-2)
+    if act:
+        torch.testing.assert_close(aux.float(), z, rtol=1e-2, atol=1e-2)
+
+
+def test_gemm_alpha_beta_accumulate_fp32():
+    # weight-gradient accumulation: out = alpha * A^T B + beta * out
+    M, N, K = 768, 3072, 4064
+    torch.manual_seed(3)
+    dy, x, ref = _operands(M, N, K, True, True, torch.bfloat16)
+    out = torch.randn(M, N, device="cuda")
+    want = 0.5 * ref + out
+    c = _C().gemm(dy, x, a_tr=True, b_tr=True, out=out, alpha=0.5, beta=1.0)
+    assert c.data_ptr() == out.data_ptr()
+    torch.testing.assert_close(out, want, rtol=1e-4, atol=2e-3 * K ** 0.5)
+
+
+def test_gemm_strided_operands_and_auto_plan():
+    # row-strided views (e.g. q/k/v column slices) and the automatic tile / split plan
+    torch.manual_seed(4)
+    big = _rand(1000, 2304)
+    x = big[:, 768:1536]
+    w = _rand(512, 768)
+    c = _C().gemm(x, w)
+    torch.testing.assert_close(c.float(), x.float() @ w.float().t(), rtol=2e-2, atol=5e-2)
+    for shape in [(6304, 768, 3072), (6304, 3072, 768), (768, 3072, 6304), (8192, 8192, 8192), (128, 4096, 4096)]:
+        t, s = _C().gemm_plan(*shape)
+        assert 0 <= t <= 2 and s >= 1

@@ -164,16 +164,24 @@ def test_act_bwd_colsum_matches_autograd(act, shape):
 
 @pytest.mark.parametrize("shape", [(6304, 768, 768), (4064, 2048, 256), (4064, 256, 2048), (100, 64, 40)])
 def test_linear_wgrad_native_matches_mm(shape):
-    """Small-output weight gradients on the split-K MFMA kernel == dyᵀ·x (fp32 reference)."""
-    from hyperion.ops import _native
-    from hyperion.ops.linear import linear_wgrad
+    """Weight gradients on the native kernels (split-K conv-wgrad kernel for small outputs, the
+    tiled MFMA GEMM above) == dyᵀ·x (fp32 reference)."""
+    from hyperion.ops import _native, gemm
+    from hyperion.ops.linear import WGRAD_NATIVE_MAX, linear_wgrad
 
     M, K, N = shape
     torch.manual_seed(0)
     x = torch.randn(M, K, device="cuda").bfloat16()
     dy = torch.randn(M, N, device="cuda").bfloat16()
     _native.reset_counters()
-    dw = linear_wgrad(dy, x)
-    assert _native.counters().get("linear_wgrad", 0) == (1 if N % 8 == 0 and K % 64 == 0 else 0)
+    gemm.set_mode("native")
+    try:
+        dw = linear_wgrad(dy, x)
+    finally:
+        gemm.set_mode("auto")
+    c = _native.counters()
+    small = N * K <= WGRAD_NATIVE_MAX and N % 8 == 0 and K % 64 == 0
+    assert c.get("linear_wgrad", 0) == int(small)
+    assert c.get("gemm_tn", 0) == int(not small and M % 8 == 0)
     ref = dy.float().t() @ x.float()
     assert (dw.float() - ref).norm() <= 5e-3 * ref.norm()
