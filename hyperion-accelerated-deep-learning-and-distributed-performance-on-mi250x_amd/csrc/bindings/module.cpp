@@ -3,9 +3,18 @@
 
 #include "bindings/registry.h"
 
-PYBIND11_MODULE(_C, m) {
+#ifndef HYP_MODULE_NAME
+#define HYP_MODULE_NAME _C
+#endif
+
+PYBIND11_MODULE(HYP_MODULE_NAME, m) {
   m.doc() = "Hyperion-MI355X native kernels (gfx950 HIP) and RCCL communicator";
   m.attr("arch") = "gfx950";
+#ifdef HYP_DEBUG
+  m.attr("debug_build") = true;
+#else
+  m.attr("debug_build") = false;
+#endif
   hypbind::register_norm_ops(m);
   hypbind::register_attn_ops(m);
   hypbind::register_loss_ops(m);

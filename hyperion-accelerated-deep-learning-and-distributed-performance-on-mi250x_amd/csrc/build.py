@@ -9,7 +9,11 @@ No setuptools/BuildExtension (that path hipifies sources); this drives ``hipcc``
   ``csrc/`` changes; the shared object lands next to the package ``__init__`` as ``_C.so`` so it
   travels with the repo snapshot to the GPU box.
 
-Usage: ``python -m hyperion.csrc.build [--force] [-j N]``.
+Usage: ``python -m hyperion.csrc.build [--force] [-j N] [--debug]``.
+
+``--debug`` builds ``_C_debug.so`` (objects under ``csrc/build_debug/``): ``-O1 -g``, ``HYP_DEBUG``
+device checks (``HYP_DASSERT``: staging addresses inside their operands, shape invariants) — the
+kernel bounds-check build of SURVEY §5.2, loaded instead of ``_C`` when ``HYPERION_DEBUG_BUILD=1``.
 """
 from __future__ import annotations
 
@@ -62,9 +66,9 @@ def _sources() -> List[str]:
     return srcs
 
 
-def _common_flags(inc, abi) -> List[str]:
+def _common_flags(inc, abi, debug: bool = False) -> List[str]:
     flags = [
-        "-O3",
+        "-O1" if debug else "-O3",
         "-std=c++17",
         "-fPIC",
         f"--offload-arch={ARCH}",
@@ -76,6 +80,8 @@ def _common_flags(inc, abi) -> List[str]:
         "-D__HIP_PLATFORM_AMD__=1",
         "-I" + CSRC,
     ]
+    if debug:
+        flags += ["-g", "-DHYP_DEBUG=1", "-DHYP_MODULE_NAME=_C_debug"]
     return flags
 
 
@@ -91,14 +97,16 @@ def _compile(src: str, obj: str, flags: List[str], torch_flags: List[str], verbo
     return obj
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool = False) -> str:
     inc, torch_lib, abi = _torch_paths()
+    BUILD = os.path.join(CSRC, "build_debug" if debug else "build")
+    OUT = os.path.join(PKG, "_C_debug.so" if debug else "_C.so")
     os.makedirs(BUILD, exist_ok=True)
-    flags = _common_flags(inc, abi)
+    flags = _common_flags(inc, abi, debug)
     py_inc = sysconfig.get_paths()["include"]
     torch_flags = [f"-I{p}" for p in inc] + [
         f"-I{py_inc}",
-        "-DTORCH_EXTENSION_NAME=_C",
+        "-DTORCH_EXTENSION_NAME=" + ("_C_debug" if debug else "_C"),
         "-DTORCH_API_INCLUDE_EXTENSION_H",
     ]
     hdr = _headers_digest()
@@ -157,8 +165,9 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="bounds-checked -O1 -g build -> _C_debug.so")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, debug=a.debug)
     print(out)
     return 0
 

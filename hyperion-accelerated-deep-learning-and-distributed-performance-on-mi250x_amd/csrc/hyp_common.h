@@ -7,6 +7,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Device-side checks of the debug build (python -m hyperion.csrc.build --debug -> _C_debug.so,
+// selected by HYPERION_DEBUG_BUILD=1): a failed check prints the kernel, block, lane and the
+// condition and the kernel carries on (no trap: a GPU trap can take the whole node down).  The
+// release build compiles them out.
+#ifdef HYP_DEBUG
+#define HYP_DASSERT(cond)                                                                                   \
+  do {                                                                                                     \
+    if (!(cond))                                                                                           \
+      printf("hyperion device check failed: %s:%d block %d thread %d: %s\n", __FILE__, __LINE__,           \
+             (int)blockIdx.x, (int)threadIdx.x, #cond);                                                    \
+  } while (0)
+#else
+#define HYP_DASSERT(cond) \
+  do {                    \
+  } while (0)
+#endif
+
 namespace hyp {
 
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };

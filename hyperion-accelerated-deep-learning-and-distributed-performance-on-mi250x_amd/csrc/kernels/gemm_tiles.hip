@@ -75,18 +75,20 @@ __device__ __forceinline__ unsigned row_lane(int ld, int lane) {
 
 template <int R, int NW, bool SAFE>
 __device__ __forceinline__ void row_issue(const uint16_t* g, int ld, int row0, int nrows, unsigned lp, int i, int k0,
-                                          int K, uint16_t* img, int wave, int lane, const uint16_t* zero) {
+                                          int K, uint16_t* img, int wave, int lane, const uint16_t* zero, int64_t ext) {
   static_assert(R / (16 * NW) >= 1 && R % (16 * NW) == 0, "row image rows per wave instruction");
   const int r0 = (i * NW + wave) * 16;
   uint16_t* dst = img + r0 * kBK;
   if constexpr (!SAFE) {
     asm volatile("" : "+v"(lp));  // keep the add per stage (no hoisted per-piece lane pointers)
     const char* base = reinterpret_cast<const char*>(g + (int64_t)(row0 + r0) * ld + k0);
+    HYP_DASSERT(reinterpret_cast<const uint16_t*>(base + lp) >= g && reinterpret_cast<const uint16_t*>(base + lp) + 8 <= g + ext);
     glds16(reinterpret_cast<const uint16_t*>(base + lp), dst);
   } else {
     const int chunk = (lane & 3) ^ ((lane >> 4) & 3);
     const int gr = min(row0 + r0 + (lane >> 2), nrows - 1);
     const int kk = k0 + chunk * 8;
+    HYP_DASSERT(kk >= K || (g + (int64_t)gr * ld + kk + 8 <= g + ext));
     glds16(kk < K ? g + (int64_t)gr * ld + kk : zero, dst);
   }
 }
@@ -105,19 +107,21 @@ __device__ __forceinline__ unsigned tr_lane_off(int ld, int wave, int lane) {
 
 template <int C, int NW, bool SAFE>
 __device__ __forceinline__ void tr_issue(const uint16_t* g, int ld, int col0, int ncols, unsigned lp, int i, int k0,
-                                         int K, uint16_t* img, int wave, int lane, const uint16_t* zero) {
+                                         int K, uint16_t* img, int wave, int lane, const uint16_t* zero, int64_t ext) {
   static_assert((C / 128) * 8 / NW >= 1 && ((C / 128) * 8) % NW == 0, "tr image instructions per wave");
   const int ins = i * NW + wave, blk = ins >> 3, rr = (ins & 7) * 4;
   uint16_t* dst = img + blk * (kBK * 128) + rr * 128;
   if constexpr (!SAFE) {
     asm volatile("" : "+v"(lp));
     const char* base = reinterpret_cast<const char*>(g + (int64_t)(k0 + tr_row_to_k(rr)) * ld + col0 + blk * 128);
+    HYP_DASSERT(reinterpret_cast<const uint16_t*>(base + lp) >= g && reinterpret_cast<const uint16_t*>(base + lp) + 8 <= g + ext);
     glds16(reinterpret_cast<const uint16_t*>(base + lp), dst);
   } else {
     const int rho = rr + (lane >> 4);
     const int chunk = (lane & 15) ^ swz_tr<128>(rho);
     const int k = k0 + tr_row_to_k(rho);
     const int c = min(col0 + blk * 128 + chunk * 8, ncols - 8);
+    HYP_DASSERT(k >= K || (g + (int64_t)k * ld + c + 8 <= g + ext));
     glds16(k < K ? g + (int64_t)k * ld + c : zero, dst);
   }
 }
@@ -253,6 +257,7 @@ struct GemmP {
   float* part;  // split-K slabs [splits][M][N] fp32 (null: epilogue in-kernel)
   Epi e;
   int M, N, K, lda, ldb, kper, splits;
+  int64_t a_ext, b_ext;  // operand extents in elements from their bases (debug-build bounds checks)
 };
 
 // SAFE = false: every piece on the fast path — needs M >= BM, N >= BN, K % 32 == 0 (the last tile
@@ -294,11 +299,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
     uint16_t* sb = sa + kA;
     const int k0 = kb + t * kBK;
     if (q < kLA) {
-      if constexpr (ATR) tr_issue<BM, NW, SAFE>(p.A, p.lda, m0, p.M, lpA, q, k0, ke, sa, wave, lane, p.zero);
-      else row_issue<BM, NW, SAFE>(p.A, p.lda, m0, p.M, lpA, q, k0, ke, sa, wave, lane, p.zero);
+      if constexpr (ATR) tr_issue<BM, NW, SAFE>(p.A, p.lda, m0, p.M, lpA, q, k0, ke, sa, wave, lane, p.zero, p.a_ext);
+      else row_issue<BM, NW, SAFE>(p.A, p.lda, m0, p.M, lpA, q, k0, ke, sa, wave, lane, p.zero, p.a_ext);
     } else {
-      if constexpr (BTR) tr_issue<BN, NW, SAFE>(p.B, p.ldb, n0, p.N, lpB, q - kLA, k0, ke, sb, wave, lane, p.zero);
-      else row_issue<BN, NW, SAFE>(p.B, p.ldb, n0, p.N, lpB, q - kLA, k0, ke, sb, wave, lane, p.zero);
+      if constexpr (BTR) tr_issue<BN, NW, SAFE>(p.B, p.ldb, n0, p.N, lpB, q - kLA, k0, ke, sb, wave, lane, p.zero, p.b_ext);
+      else row_issue<BN, NW, SAFE>(p.B, p.ldb, n0, p.N, lpB, q - kLA, k0, ke, sb, wave, lane, p.zero, p.b_ext);
     }
   };
   auto stage = [&](int t) {
@@ -551,6 +556,8 @@ hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st) {
   p.ldb = a.ldb;
   p.kper = per * kBK;
   p.splits = splits;
+  p.a_ext = a.a_tr ? (int64_t)(a.K - 1) * a.lda + a.M : (int64_t)(a.M - 1) * a.lda + a.K;
+  p.b_ext = a.b_tr ? (int64_t)(a.K - 1) * a.ldb + a.N : (int64_t)(a.N - 1) * a.ldb + a.K;
   const TileCfg& c = kTiles[tile];
   const int nwg = ((a.M + c.bm - 1) / c.bm) * ((a.N + c.bn - 1) / c.bn) * splits;
   hipError_t err;

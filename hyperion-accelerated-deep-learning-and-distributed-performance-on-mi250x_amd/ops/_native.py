@@ -7,6 +7,15 @@ Policy (so GPU runs can never silently measure a PyTorch fallback):
 * ``HYPERION_KERNELS=torch`` forces the PyTorch reference path everywhere (A/B benchmarking).
 * On CPU the kernels cannot run; ops use their PyTorch reference implementations, which are also
   the numerics oracles in ``tests/``.
+
+Kernel debugging (SURVEY §5.2 — the CUDA-sanitizer / launch-blocking role):
+
+* ``HYPERION_DEBUG_BUILD=1`` loads ``_C_debug.so`` (``python -m hyperion.csrc.build --debug``:
+  ``-O1 -g`` with the ``HYP_DASSERT`` device bounds checks) instead of ``_C.so``;
+* ``HYPERION_KERNEL_CHECK=1`` wraps every native entry point: outside graph capture each call is
+  followed by a device synchronize, so an asynchronous fault or launch error is reported AT the op
+  that caused it (``RuntimeError: hyperion kernel check: <op> ...``); ``HYPERION_KERNEL_CHECK=nan``
+  additionally scans the op's tensor outputs and names the first op that produced NaN/Inf.
 """
 from __future__ import annotations
 
@@ -29,12 +38,58 @@ def _load():
     if _TRIED:
         return _MOD
     _TRIED = True
+    name = "hyperion._C_debug" if os.environ.get("HYPERION_DEBUG_BUILD") == "1" else "hyperion._C"
     try:
-        _MOD = importlib.import_module("hyperion._C")
+        _MOD = importlib.import_module(name)
     except BaseException as e:  # noqa: BLE001 - report any load failure
         _ERR = e
         _MOD = None
+    mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
+    if _MOD is not None and mode:
+        _MOD = CheckedModule(_MOD, nan=mode == "nan")
     return _MOD
+
+
+class KernelCheckError(RuntimeError):
+    pass
+
+
+def _tensors(out):
+    if isinstance(out, torch.Tensor):
+        yield out
+    elif isinstance(out, (list, tuple)):
+        for o in out:
+            yield from _tensors(o)
+
+
+class CheckedModule:
+    """Proxy of the extension whose functions synchronize (and optionally NaN-scan) after each call."""
+
+    def __init__(self, mod, nan: bool = False):
+        self._mod, self._nan = mod, nan
+        self.__file__ = getattr(mod, "__file__", None)
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn):
+            return fn
+        nan = self._nan
+
+        def wrapped(*args, **kw):
+            out = fn(*args, **kw)
+            if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+                try:
+                    torch.cuda.synchronize()
+                except RuntimeError as e:  # the asynchronous fault surfaces here, named
+                    raise KernelCheckError(f"hyperion kernel check: {name} failed on the device: {e}") from e
+                if nan:
+                    for t in _tensors(out):
+                        if t.is_floating_point() and t.numel() and not torch.isfinite(t).all():
+                            raise KernelCheckError(f"hyperion kernel check: {name} produced NaN/Inf "
+                                                   f"(output {tuple(t.shape)} {t.dtype})")
+            return out
+
+        return wrapped
 
 
 def backend() -> str:

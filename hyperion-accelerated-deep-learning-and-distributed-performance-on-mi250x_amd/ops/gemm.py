@@ -50,9 +50,13 @@ def _ok(*ts: torch.Tensor) -> bool:
             and _native.use_native(t0, op="gemm"))
 
 
-def _time(fn, reps: int = 3) -> float:
+def _time(fn, reps: int = 5) -> float:
+    """Device time of one call: the calls are queued behind a spin kernel (torch.cuda._sleep) so the
+    events bracket GPU work only — host launch overhead (comparable to these 10-50 us GEMMs) must
+    not decide the choice, because the training step replays them from a hipGraph."""
     fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(2_000_000)  # ~1 ms of queue ahead of the timed calls
     s.record()
     for _ in range(reps):
         fn()

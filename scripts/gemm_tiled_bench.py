@@ -16,13 +16,25 @@ from hyperion.ops import _native  # noqa: E402
 
 
 def timeit(fn, iters=20, rounds=3):
+    """us per call from hipGraph replays of `iters` captured calls (no host launch overhead in the
+    number: the small shapes are 10-30 us, comparable to a Python-side launch)."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s0 = torch.cuda.Stream()
+    s0.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s0):
+        fn()
+        with torch.cuda.graph(g, stream=s0):
+            for _ in range(iters):
+                fn()
+    torch.cuda.current_stream().wait_stream(s0)
     best = []
     for _ in range(rounds):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        fn()
+        g.replay()
         s.record()
-        for _ in range(iters):
-            fn()
+        g.replay()
         e.record()
         torch.cuda.synchronize()
         best.append(s.elapsed_time(e) * 1e3 / iters)
@@ -47,6 +59,9 @@ def case(kind, M, N, K, sweep):
     plan = C.gemm_plan(M, N, K)
     res = {"kind": kind, "M": M, "N": N, "K": K, "plan": plan, "rel_err": err}
     res["vendor_us"] = timeit(ven)
+    if M <= 1024 and kind in ("fwd", "dgrad"):  # the split-K weight-streaming kernels (linear_nt / linear_nn)
+        sk = (lambda: C.linear_nt(a, b)) if kind == "fwd" else (lambda: C.linear_nn(a, b))
+        res["skinny_us"] = timeit(sk)
     res["hyp_us"] = timeit(lambda: C.gemm(a, b, a_tr=at, b_tr=bt))
     fl = 2.0 * M * N * K
     res["vendor_tf"] = fl / res["vendor_us"] / 1e6
@@ -77,6 +92,8 @@ def main():
             shapes += [("fwd", M, N, K), ("dgrad", M, K, N), ("wgrad", N, K, M)]
     for N, K in [(2048, 256), (256, 2048), (768, 256)]:  # LM-256 FFN / qkv, 4064 tokens
         shapes += [("fwd", 4064, N, K), ("dgrad", 4064, K, N), ("wgrad", N, K, 4064)]
+    for N, K in [(4096, 4096), (11008, 4096), (4096, 11008)]:  # Llama-2-7B projections at 128 tokens
+        shapes += [("fwd", 128, N, K), ("dgrad", 128, K, N)]
     if a.only:
         shapes = [s for s in shapes if s[0] in a.only.split(",")]
     out = [case(*s, a.sweep) for s in shapes]

@@ -63,3 +63,47 @@ def test_killed_rank_fails_the_job_within_timeout(tmp_path):
     assert r.returncode != 0
     assert time.time() - t0 < 280
     assert "injected fault" in r.stderr or "exitcode" in r.stderr
+
+
+def test_kernel_check_proxy_names_the_faulting_op(monkeypatch):
+    """HYPERION_KERNEL_CHECK: every native call is followed by a device sync (outside capture) and
+    NaN-producing ops are named (the launch-blocking / sanitizer role)."""
+    import torch
+
+    from hyperion.ops import _native
+
+    class Fake:
+        __file__ = "fake.so"
+
+        @staticmethod
+        def good(x):
+            return x * 2
+
+        @staticmethod
+        def bad(x):
+            return (x * float("nan"), x)
+
+    syncs = []
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: syncs.append(1))
+    m = _native.CheckedModule(Fake(), nan=True)
+    assert torch.equal(m.good(torch.ones(3)), torch.full((3,), 2.0))
+    assert len(syncs) == 1 and m.__file__ == "fake.so"
+    try:
+        m.bad(torch.ones(3))
+    except _native.KernelCheckError as e:
+        assert "bad" in str(e) and "NaN" in str(e)
+    else:
+        raise AssertionError("NaN output not reported")
+
+    def boom(*a):
+        raise RuntimeError("HIP error: an illegal memory access was encountered")
+
+    monkeypatch.setattr(torch.cuda, "synchronize", boom)
+    try:
+        _native.CheckedModule(Fake()).good(torch.ones(1))
+    except _native.KernelCheckError as e:
+        assert "good" in str(e) and "illegal memory access" in str(e)
+    else:
+        raise AssertionError("device fault not attributed")
