@@ -11,7 +11,7 @@ No setuptools/BuildExtension (that path hipifies sources); this drives ``hipcc``
 
 Usage: ``python -m hyperion.csrc.build [--force] [-j N] [--debug]``.
 
-``--debug`` builds ``_C_debug.so`` (objects under ``csrc/build_debug/``): ``-O1 -g``, ``HYP_DEBUG``
+``--debug`` builds ``_C_debug.so`` (objects under ``csrc/build_debug/``): ``-O1``, ``HYP_DEBUG``
 device checks (``HYP_DASSERT``: staging addresses inside their operands, shape invariants) — the
 kernel bounds-check build of SURVEY §5.2, loaded instead of ``_C`` when ``HYPERION_DEBUG_BUILD=1``.
 """
@@ -81,7 +81,7 @@ def _common_flags(inc, abi, debug: bool = False) -> List[str]:
         "-I" + CSRC,
     ]
     if debug:
-        flags += ["-g", "-DHYP_DEBUG=1", "-DHYP_MODULE_NAME=_C_debug"]
+        flags += ["-DHYP_DEBUG=1", "-DHYP_MODULE_NAME=_C_debug"]
     return flags
 
 
