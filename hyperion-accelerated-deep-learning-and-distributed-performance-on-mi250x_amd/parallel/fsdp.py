@@ -111,7 +111,10 @@ class _FlatGroup:
         for n in self.numels[:-1]:
             self.offsets.append(self.offsets[-1] + n)
         self.numel = sum(self.numels)
-        W, r = fsdp.world, fsdp.rank
+        # resident: a frozen group kept whole on every rank (FSDP(replicate_frozen=...)): never
+        # gathered, never freed — the base weights of a LoRA fine-tune fit 288 GB of HBM many times
+        self.resident = (not trainable) and fsdp.replicate_frozen
+        W, r = (1, 0) if self.resident else (fsdp.world, fsdp.rank)
         # shards of a multiple of 64 elements: every rank's slice of the gathered buffer (and every
         # reduce-scatter output) starts 128-byte aligned for RCCL and the vector kernels
         self.padded = int(math.ceil(max(self.numel, 1) / (W * 64)) * W * 64)
@@ -127,7 +130,7 @@ class _FlatGroup:
                 flat[o : o + n].copy_(p.detach().reshape(-1))
             shard = flat[r * self.shard_numel : (r + 1) * self.shard_numel].clone()
         self.flat_param = nn.Parameter(shard, requires_grad=trainable)
-        self.full = torch.empty(self.padded, dtype=self.cdtype, device=dev)
+        self.full = self.flat_param.data if self.resident else torch.empty(self.padded, dtype=self.cdtype, device=dev)
         self._full_bytes = self.full.untyped_storage().nbytes()
         self.full_grad = torch.empty(self.padded, dtype=self.rdtype, device=dev) if trainable else None
         self._grad_bytes = self.full_grad.untyped_storage().nbytes() if trainable else 0
@@ -149,12 +152,15 @@ class _FlatGroup:
         # module parameters become views of the full buffer (the same Parameter objects)
         for p, o, n, shp in zip(params, self.offsets, self.numels, self.shapes):
             p.data = self.full[o : o + n].view(shp)
-        self.free_full()
+        if not self.resident:
+            self.free_full()
         if trainable:
             self.full_grad.untyped_storage().resize_(0)
 
     # -- storage ------------------------------------------------------------------------
     def free_full(self) -> None:
+        if self.resident:
+            return
         if self.gather_work is not None:
             self.wait_gather()
         if self.gathered:
@@ -162,7 +168,7 @@ class _FlatGroup:
             self.gathered = False
 
     def gather(self, async_op: bool = False) -> None:
-        if self.gathered or self.gather_work is not None:
+        if self.resident or self.gathered or self.gather_work is not None:
             return
         st = self.full.untyped_storage()
         if st.nbytes() != self._full_bytes:
@@ -332,6 +338,7 @@ class FullyShardedDataParallel(nn.Module):
         backward_prefetch: bool = True,
         sync_module_states: bool = True,
         comm=None,
+        replicate_frozen=False,
     ):
         super().__init__()
         if sharding_strategy not in ("FULL_SHARD", "SHARD_GRAD_OP"):
@@ -346,6 +353,17 @@ class FullyShardedDataParallel(nn.Module):
         self.device = torch.device(device_id)
         module.to(self.device)
         self.mp = mixed_precision or MixedPrecision()
+        # replicate_frozen: frozen (requires_grad=False) parameters stay whole on every rank in the
+        # compute dtype — no all-gathers for them, ever; trainable ones are sharded as usual.
+        # "auto": when the frozen bytes take at most a quarter of the device's memory (MI355X:
+        # Llama-2-7B's 13.5 GB bf16 base vs 288 GB HBM — the LoRA step then moves only adapter
+        # traffic over xGMI instead of re-gathering 13.5 GB per forward and per backward).
+        if replicate_frozen == "auto":
+            frozen_bytes = sum(p.numel() for p in module.parameters() if not p.requires_grad) * \
+                torch.finfo(self.mp.param_dtype or torch.float32).bits // 8
+            cap = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
+            replicate_frozen = self.world > 1 and cap > 0 and frozen_bytes <= cap // 4
+        self.replicate_frozen = bool(replicate_frozen)
         self.sharding = sharding_strategy
         self.reshard_after_forward = sharding_strategy == "FULL_SHARD"
         self.forward_prefetch = forward_prefetch
@@ -531,7 +549,7 @@ class FullyShardedDataParallel(nn.Module):
         full_params: Dict[int, torch.Tensor] = {}
         for g in self.flat_groups():
             full = torch.empty(g.padded, dtype=g.flat_param.dtype, device=self.device)
-            if self.world > 1:
+            if self.world > 1 and not g.resident:
                 dist.all_gather_into_tensor(full, g.flat_param.detach(), group=self.group)
             else:
                 full.copy_(g.flat_param.detach())
@@ -557,7 +575,8 @@ class FullyShardedDataParallel(nn.Module):
             flat = torch.zeros(g.padded, dtype=g.flat_param.dtype, device=self.device)
             for p, o, n in zip(g.params, g.offsets, g.numels):
                 flat[o : o + n].copy_(sd[names[id(p)]].reshape(-1).to(self.device, flat.dtype))
-            g.flat_param.data.copy_(flat[self.rank * g.shard_numel : (self.rank + 1) * g.shard_numel])
+            r = 0 if g.resident else self.rank
+            g.flat_param.data.copy_(flat[r * g.shard_numel : (r + 1) * g.shard_numel])
         self.invalidate_gather_cache()
         for n, t in self.module.state_dict(keep_vars=True).items():
             if id(t) not in self._unit_of_param and n in sd:

@@ -372,7 +372,8 @@ def train_gpt2_fsdp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFA
 def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = DEFAULT_BASE_DIR,
                      hf_token: Optional[str] = None, model_id: str = "NousResearch/Llama-2-7b-hf", lora: bool = False,
                      batch_size: int = 1, progress_every: int = 50, opts: Optional[RunOptions] = None,
-                     config=None, lora_parallel: str = "fsdp", mask_pad_labels: bool = False) -> Dict:
+                     config=None, lora_parallel: str = "fsdp", mask_pad_labels: bool = False,
+                     replicate_frozen="auto") -> Dict:
     """C26: Llama fine-tune.  ``lora=True``: frozen bf16 base + r16 adapters on q/k/v/o.
 
     ``lora_parallel='fsdp'`` (default; the BASELINE.json config) shards the frozen base and
@@ -380,6 +381,9 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
     model).  ``lora=False``: full bf16 FSDP with ``LlamaDecoderLayer`` units.  ``hf_token`` /
     ``model_id`` are accepted for CLI compatibility; weights are random-init (no network).
     ``mask_pad_labels`` fixes the reference's unmasked pad labels (:517) when set.
+    ``replicate_frozen`` ("auto" | True | False): under FSDP keep the frozen base whole on every rank
+    when it fits (auto: <= 1/4 of HBM — 13.5 GB of 288 GB on MI355X), so only the adapters are
+    sharded and communicated; False shards the base like the reference's torch FSDP.
     """
     from ..models.llama import LlamaConfig, LlamaDecoderLayer, LlamaForCausalLM
     from ..models.lora import apply_lora, save_adapter
@@ -408,7 +412,8 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
         model = base.to(pdt)
         model = DDP(model) if world > 1 else model
     else:
-        model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt))
+        model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt),
+                     replicate_frozen=replicate_frozen if lora else False)
     opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, isinstance(model, FSDP), opts)
     res = _maybe_resume(opts, model, opt, None, out, "llama")

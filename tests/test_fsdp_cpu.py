@@ -131,3 +131,46 @@ def test_fsdp_frozen_params_not_sharded_into_optimizer():
     # world * 64 elements (aligned shards), then sharded over the 2 ranks
     assert (32 * 48 + 48) <= n_opt < (32 * 48 + 48) + 2 * 64
     assert changed and all("linear1" in k for k in changed)
+
+
+def _replicated_frozen_train(rank, world, replicate):
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.parallel.fsdp import FSDP, transformer_auto_wrap_policy
+
+    m0 = _make_model()
+    for n, p in m0.named_parameters():
+        if "linear1" not in n:
+            p.requires_grad_(False)
+    m = FSDP(m0, auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}), device_id=torch.device("cpu"),
+             replicate_frozen=replicate)
+    gathers = []
+    comm_ag = m.comm.all_gather
+
+    def counting_all_gather(out, inp, *a, **k):
+        gathers.append(out.numel())
+        return comm_ag(out, inp, *a, **k)
+
+    m.comm.all_gather = counting_all_gather
+    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-2)
+    for step in range(3):
+        x, y = _batch(step)
+        opt.zero_grad()
+        m.forward_loss(x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4], ignore_index=-100).backward()
+        opt.step()
+    resident = [g.resident for g in m.flat_groups() if not g.trainable]
+    return m.full_state_dict(rank0_only=False), resident, sum(gathers)
+
+
+def test_fsdp_replicate_frozen_matches_sharded_and_skips_frozen_gathers():
+    """replicate_frozen: the frozen base stays whole on every rank (no all-gathers for it), the
+    adapters are sharded as usual, and training matches the fully sharded run."""
+    shard = run_world(_replicated_frozen_train, 2, (False,))
+    repl = run_world(_replicated_frozen_train, 2, (True,))
+    sd_s, res_s, ag_s = shard[0]
+    sd_r, res_r, ag_r = repl[0]
+    assert res_r and all(res_r) and not any(res_s)
+    assert ag_r < ag_s  # only the trainable groups are gathered
+    for k in sd_s:
+        torch.testing.assert_close(sd_r[k], sd_s[k], rtol=1e-5, atol=1e-6)
+    for k in sd_r:  # replicas agree
+        assert torch.equal(repl[1][0][k], sd_r[k])
