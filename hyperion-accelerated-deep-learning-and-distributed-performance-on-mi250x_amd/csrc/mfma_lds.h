@@ -59,6 +59,15 @@ __device__ __forceinline__ int tr_row_to_k(int row) {
   return (row & ~31) | (((row >> 2) & 3) << 3) | (((row >> 4) & 1) << 2) | (row & 3);
 }
 
+// Debug builds (HYP_DEBUG: device printf checks) spill: hipcc may store an asm-read result to
+// scratch right after the asm statement, before the asynchronous LDS read has returned — so there
+// every asm LDS read waits for itself (HYP_LDS_SYNC).  Release kernels are verified spill-free.
+#ifdef HYP_DEBUG
+#define HYP_LDS_SYNC "\n\ts_waitcnt lgkmcnt(0)"
+#else
+#define HYP_LDS_SYNC ""
+#endif
+
 // ds_read_b64_tr_b16 as inline asm.  The builtin form makes hipcc (ROCm 7.2) wait vmcnt(0) before
 // the read whenever a global_load_lds is in flight — it cannot prove the DMA's LDS destination does
 // not alias — which drained the NEXT stage's prefetch before every k-step of the weight-gradient
@@ -69,7 +78,7 @@ __device__ __forceinline__ s16x4 ds_read_tr16_asm(const uint16_t* addr) {
   typedef short s16x4_t __attribute__((ext_vector_type(4)));
   s16x4_t v;
   const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)addr;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" HYP_LDS_SYNC : "=v"(v) : "v"(a) : "memory");
   return v;
 }
 
@@ -104,7 +113,7 @@ __device__ __forceinline__ s16x4 ds_read_tr16_imm(unsigned addr) {
   static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
   typedef short s16x4_t __attribute__((ext_vector_type(4)));
   s16x4_t v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" HYP_LDS_SYNC : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
   return v;
 }
 

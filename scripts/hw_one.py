@@ -2,7 +2,7 @@
 (each a few launches), plus an event-timed sweep of the STREAM launch modes (grid-stride vs one
 tile per workgroup, non-temporal vs default stores) against torch's add.
 
-    python scripts/hw_one.py [gemm|stream|sweep]
+    python scripts/hw_one.py [gemm|gemm_tiled|gemm_tiled_wgrad|stream|sweep]
 """
 import json
 import os
@@ -39,6 +39,19 @@ if what == "gemm":
     b = (torch.rand(n, n, device="cuda", generator=g) * 2 - 1).bfloat16()
     t = ev(lambda: C.gemm_nt(a, b, None, 1.0, 64), reps=5, warm=2)
     print(json.dumps({"gemm_nt_8192_bf16_TF": 2 * n ** 3 / t / 1e12}))
+elif what == "gemm_tiled":  # gemm_tiles.hip 256x256 fast kernel, 8192^3 NT
+    n = 8192
+    g = torch.Generator(device="cuda").manual_seed(0)
+    a = (torch.rand(n, n, device="cuda", generator=g) * 2 - 1).bfloat16()
+    b = (torch.rand(n, n, device="cuda", generator=g) * 2 - 1).bfloat16()
+    t = ev(lambda: C.gemm(a, b, tile=0, splits=1), reps=5, warm=2)
+    print(json.dumps({"gemm_tiled_8192_bf16_TF": 2 * n ** 3 / t / 1e12}))
+elif what == "gemm_tiled_wgrad":  # ViT-B/16 fc1 weight gradient: [3072 x 768] = dyᵀ x over 6304 tokens
+    g = torch.Generator(device="cuda").manual_seed(0)
+    dy = (torch.rand(6304, 3072, device="cuda", generator=g) * 2 - 1).bfloat16()
+    x = (torch.rand(6304, 768, device="cuda", generator=g) * 2 - 1).bfloat16()
+    t = ev(lambda: C.gemm(dy, x, a_tr=True, b_tr=True, tile=1, splits=3), reps=20, warm=3)
+    print(json.dumps({"gemm_tiled_vit_fc1_wgrad_TF": 2 * 6304 * 3072 * 768 / t / 1e12}))
 elif what == "stream":
     n = 500_000_000
     x, y, z = torch.rand(n, device="cuda"), torch.rand(n, device="cuda"), torch.empty(n, device="cuda")
