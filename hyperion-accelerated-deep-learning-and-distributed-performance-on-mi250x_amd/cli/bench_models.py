@@ -58,8 +58,11 @@ def main(argv=None) -> int:
         from hyperion.bench.models import bench_vit_step
 
         summary["vit_b16_bf16_ckpt"] = bench_vit_step(checkpointing=True)
+        summary["vit_b16_bf16_ckpt_graph"] = bench_vit_step(checkpointing=True, graph=True)
         summary["vit_b16_bf16"] = bench_vit_step(checkpointing=False)
-        print(summary["vit_b16_bf16_ckpt"], summary["vit_b16_bf16"], flush=True)
+        summary["vit_b16_bf16_graph"] = bench_vit_step(checkpointing=False, graph=True)
+        print(summary["vit_b16_bf16_ckpt"], summary["vit_b16_bf16_ckpt_graph"], summary["vit_b16_bf16"],
+              summary["vit_b16_bf16_graph"], flush=True)
         dump()
     if "llama" in parts:
         from hyperion.bench.models import bench_llama_lora_step
