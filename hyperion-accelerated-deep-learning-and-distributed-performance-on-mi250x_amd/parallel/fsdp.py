@@ -592,7 +592,9 @@ class FullyShardedDataParallel(nn.Module):
         return {
             "world_size": self.world,
             "rank": self.rank,
-            "flat_params": [g.flat_param.detach().cpu().clone() for g in groups],
+            # resident (replicated frozen) groups: rank 0 holds the copy (no N-fold checkpoint)
+            "flat_params": [None if (g.resident and self.rank != 0) else g.flat_param.detach().cpu().clone()
+                            for g in groups],
             "meta": [{"tag": g.tag, "names": [names.get(id(p), "?") for p in g.params],
                       "shapes": [tuple(s) for s in g.shapes], "numel": g.numel, "padded": g.padded} for g in groups],
             "buffers": {n: b.detach().cpu().clone() for n, b in self.module.named_buffers()},
@@ -603,7 +605,10 @@ class FullyShardedDataParallel(nn.Module):
         if sd["world_size"] != self.world:
             raise ValueError(f"sharded checkpoint has world_size {sd['world_size']}, running with {self.world}")
         for g, t in zip(self.flat_groups(), sd["flat_params"]):
-            g.flat_param.data.copy_(t.to(self.device))
+            if t is not None:
+                g.flat_param.data.copy_(t.to(self.device))
+            if g.resident and self.world > 1:  # rank 0's copy of a replicated frozen group
+                dist.broadcast(g.flat_param.data, src=0, group=self.group)
         self.invalidate_gather_cache()
         bufs = dict(self.module.named_buffers())
         for n, t in sd.get("buffers", {}).items():

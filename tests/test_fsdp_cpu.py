@@ -174,3 +174,38 @@ def test_fsdp_replicate_frozen_matches_sharded_and_skips_frozen_gathers():
         torch.testing.assert_close(sd_r[k], sd_s[k], rtol=1e-5, atol=1e-6)
     for k in sd_r:  # replicas agree
         assert torch.equal(repl[1][0][k], sd_r[k])
+
+
+def _replicated_roundtrip(rank, world, tmp):
+    import os
+
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.parallel.fsdp import FSDP, transformer_auto_wrap_policy
+
+    def make():
+        m0 = _make_model()
+        for n, p in m0.named_parameters():
+            if "linear1" not in n:
+                p.requires_grad_(False)
+        return FSDP(m0, auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}),
+                    device_id=torch.device("cpu"), replicate_frozen=True)
+
+    m = make()
+    want = m.full_state_dict(rank0_only=False)
+    sd = m.sharded_state_dict()
+    frozen_copies = sum(t is not None for t, g in zip(sd["flat_params"], m.flat_groups()) if g.resident)
+    torch.save(sd, os.path.join(tmp, f"s{rank}.pt"))
+    torch.distributed.barrier()
+    m2 = make()
+    with torch.no_grad():
+        for g in m2.flat_groups():
+            g.flat_param.data.zero_()
+    m2.load_sharded_state_dict(torch.load(os.path.join(tmp, f"s{rank}.pt"), weights_only=True))
+    got = m2.full_state_dict(rank0_only=False)
+    return frozen_copies, all(torch.equal(got[k], want[k]) for k in want)
+
+
+def test_fsdp_replicated_frozen_sharded_checkpoint_single_copy(tmp_path):
+    res = run_world(_replicated_roundtrip, 2, (str(tmp_path),))
+    assert res[0][0] > 0 and res[1][0] == 0  # only rank 0 stores the replicated frozen base
+    assert res[0][1] and res[1][1]  # and every rank gets it back
