@@ -370,10 +370,12 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
   lds_reads_done();
 
   auto mfma_half = [&](int half, const u16x8 (&a)[FH]) {
+    __builtin_amdgcn_s_setprio(1);  // T5: the MFMA cluster wins issue arbitration over the partner wave's loads
 #pragma unroll
     for (int i = 0; i < FH; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[half * FH + i][j] = mma16<T>(a[i], bc[j], acc[half * FH + i][j]);
+    __builtin_amdgcn_s_setprio(0);
   };
   // steady state: stages 0 .. nk-2 (no MFMA under a branch: accumulators stay in place, no phi copies)
   for (int t = 0; t < nk - 1; ++t) {
@@ -394,8 +396,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
         for (int q = g * PPG; q < kL && q < (g + 1) * PPG; ++q) stage_piece(t + kNB, q);
       }
       __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[FH + g][j] = mma16<T>(a1[g], bc[j], acc[FH + g][j]);
+      __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
     // stage t+1's fragments after the last group, into the registers a1 / bc free (a second
