@@ -16,7 +16,9 @@ from __future__ import annotations
 
 import argparse
 import os
+import subprocess
 import sys
+from typing import List, Optional
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -44,8 +46,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--resume", default=None, help="checkpoint path, or 'auto' = this run kind's latest checkpoint")
     ap.add_argument("--ckpt_every", type=int, default=None, help="write the latest checkpoint every N steps")
     ap.add_argument("--max_restarts", type=int, default=0,
-                    help="single process: re-run a failed trainer up to N times with --resume auto (multi-process: "
-                         "use torchrun --max-restarts N together with --resume auto)")
+                    help="single process: run each attempt in a FRESH child process and re-run a failed trainer up "
+                         "to N times with --resume auto (the supervising parent never touches the GPU); "
+                         "multi-process: use torchrun --max-restarts N together with --resume auto")
     ap.add_argument("--ckpt_mode", default="full", choices=["full", "sharded"])
     ap.add_argument("--lora_parallel", default="fsdp", choices=["fsdp", "ddp"])
     ap.add_argument("--seed", type=int, default=0)
@@ -61,7 +64,57 @@ def _env():
         return None
 
 
+def _child_argv(argv: List[str], model: str, resume: Optional[str]) -> List[str]:
+    """``argv`` without --max_restarts, with --model pinned to ``model`` and --resume to ``resume``."""
+    out, skip = [], False
+    for i, a in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        key = a.split("=", 1)[0]
+        if key in ("--max_restarts", "--model", "--resume"):
+            skip = "=" not in a
+            continue
+        out.append(a)
+    out += ["--model", model]
+    if resume:
+        out += ["--resume", resume]
+    return out
+
+
+def _repo_root() -> str:
+    """Directory holding the ``hyperion`` import shim (so the child resolves the same package)."""
+    import hyperion
+
+    src = getattr(hyperion, "_SRC", None) or os.path.dirname(os.path.abspath(hyperion.__file__))
+    return os.path.dirname(src)
+
+
+def supervise(argv: List[str], models: List[str], max_restarts: int, resume: Optional[str]) -> int:
+    """Restart policy for a single-process run: each attempt is a NEW interpreter, so a
+    sticky HIP fault, an aborted communicator, captured graphs or module-global caches of the failed
+    attempt can never leak into the retry.  This process only waits on children."""
+    for m in models:
+        attempt, res = 0, resume
+        while True:
+            cmd = [sys.executable, "-m", "hyperion.cli.run_distributed"] + _child_argv(argv, m, res)
+            env = dict(os.environ, HYPERION_RESTART_ATTEMPT=str(attempt))
+            env["PYTHONPATH"] = os.pathsep.join(p for p in (_repo_root(), env.get("PYTHONPATH", "")) if p)
+            rc = subprocess.run(cmd, env=env).returncode
+            if rc == 0:
+                break
+            if attempt >= max_restarts:
+                print(f"[run_distributed] {m} failed (exit {rc}); no restarts left", file=sys.stderr, flush=True)
+                return rc
+            attempt += 1
+            res = "auto"
+            print(f"[run_distributed] {m} failed (exit {rc}); restart {attempt}/{max_restarts} in a fresh process "
+                  "from the latest checkpoint", file=sys.stderr, flush=True)
+    return 0
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = build_parser().parse_args(argv)
     if args.config:
         from hyperion.config import apply_to_args, load_config
@@ -91,23 +144,18 @@ def main(argv=None) -> int:
     if env is None:
         env = (0, 1, 0)  # plain `python -m`: a single process (the reference exited here)
     rank, world, _local = env
+    todo = ["language_ddp", "cifar", "language_fsdp", "llama"] if args.model == "all" else [args.model]
+    if args.max_restarts > 0:
+        if world > 1:
+            print("--max_restarts is for single-process runs; with torchrun use --max-restarts N and --resume auto",
+                  file=sys.stderr)
+            return 2
+        return supervise(argv, todo, args.max_restarts, args.resume)
     opts = RunOptions(synthetic=args.synthetic, dataset_size=args.dataset_size, max_steps_per_epoch=args.max_steps,
                       precision=args.precision, seed=args.seed, save=not args.no_save, ckpt_mode=args.ckpt_mode,
                       resume=args.resume, causal=args.causal, ckpt_every=args.ckpt_every)
-    todo = ["language_ddp", "cifar", "language_fsdp", "llama"] if args.model == "all" else [args.model]
     for m in todo:
-        attempt = 0
-        while True:
-            try:
-                _run_one(m, rank, world, args, opts)
-                break
-            except Exception as e:  # noqa: BLE001 - restart policy
-                if world > 1 or attempt >= args.max_restarts:
-                    raise
-                attempt += 1
-                print(f"[run_distributed] {m} failed ({e!r}); restart {attempt}/{args.max_restarts} from the latest "
-                      "checkpoint", file=sys.stderr, flush=True)
-                opts.resume = "auto"
+        _run_one(m, rank, world, args, opts)
     if rank == 0:
         create_scaling_report(os.path.join(args.base_dir, "data", "distributed"))
     return 0

@@ -4,6 +4,8 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <mutex>
+
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -33,6 +35,36 @@ inline int dtype_code(const at::Tensor& t) {
     TORCH_CHECK(_e == hipSuccess, "hyperion HIP error: ", hipGetErrorString(_e), " at ", __FILE__, \
                 ":", __LINE__);                                                                      \
   } while (0)
+
+// 4 KiB of zeros per device that the tiled GEMM / implicit-GEMM conv kernels read for out-of-range
+// operand rows and padding taps.  Allocated
+// with hipMalloc outside torch's caching allocator and never freed (no destructor runs after HIP
+// teardown at exit), and zeroed SYNCHRONOUSLY on a private stream: a first call under hipGraph
+// capture would otherwise take the buffer from the graph's pool with the zero-fill merely
+// recorded, so eager GEMMs before the first replay would read garbage.  The calls run
+// in relaxed capture mode, so they are legal (and not captured) while another stream captures.
+inline const void* device_zero_page(const at::Device& dev) {
+  static void* z[64] = {nullptr};
+  static std::mutex mu;
+  const int i = dev.index() < 0 ? 0 : dev.index();
+  TORCH_CHECK(i < 64, "device_zero_page: device index out of range");
+  std::lock_guard<std::mutex> g(mu);
+  if (z[i] == nullptr) {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    HYP_CHECK_HIP(hipThreadExchangeStreamCaptureMode(&mode));
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    hipError_t e = hipMalloc(&p, 4096);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMemsetAsync(p, 0, 4096, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (s) (void)hipStreamDestroy(s);
+    HYP_CHECK_HIP(hipThreadExchangeStreamCaptureMode(&mode));  // restore the caller's mode
+    HYP_CHECK_HIP(e);
+    z[i] = p;
+  }
+  return z[i];
+}
 
 #define HYP_CHECK_CUDA_TENSOR(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 

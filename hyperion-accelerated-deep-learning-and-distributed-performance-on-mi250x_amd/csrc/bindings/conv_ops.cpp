@@ -7,13 +7,6 @@
 namespace hypbind {
 namespace {
 
-at::Tensor& zero_page(const at::Device& dev) {
-  static at::Tensor z[16];
-  const int i = dev.index() < 0 ? 0 : dev.index();
-  if (!z[i].defined()) z[i] = at::zeros({4096}, at::TensorOptions().device(dev).dtype(at::kByte));
-  return z[i];
-}
-
 // Effective split-K count for a conv of nk reduction steps (conv_fwd's own rounding: no empty splits).
 int plan_splits(int M, int K, int nk, int bm, int bn, int64_t splits_req) {
   int sp = splits_req > 0 ? (int)splits_req : (splits_req == 0 ? 1 : hyp::conv_fwd_splits(M, K, nk, bm, bn));
@@ -53,7 +46,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   at::Tensor acc, slabs;
   if (stats) acc = stats_sums(sums, K, x);
   if (splits > 1) slabs = at::empty({splits, M, K}, x.options().dtype(at::kFloat));
-  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), device_zero_page(x.device()),
                               stats ? acc.data_ptr<double>() : nullptr, stats ? acc.data_ptr<double>() + K : nullptr, N, H,
                               W, C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, splits,
                               splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream()));
@@ -99,7 +92,7 @@ at::Tensor conv_fwd_affine(const at::Tensor& x, const at::Tensor& w, int64_t sh,
   ep.shift = shift.data_ptr<float>();
   ep.residual = has_res ? residual->data_ptr() : nullptr;
   ep.act = act ? 1 : 0;
-  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), device_zero_page(x.device()),
                               nullptr, nullptr, N, H, W, C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn,
                               0, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f, &ep));
   return y;
@@ -151,7 +144,7 @@ std::vector<at::Tensor> linear_ce_lse(const at::Tensor& x, const at::Tensor& w, 
   auto loss_rows = at::empty({M}, fopt);
   ce.part = reinterpret_cast<float2*>(part.data_ptr<float>());
   ce.zt = zt.data_ptr<float>();
-  HYP_CHECK_HIP(hyp::linear_ce(dtype_code(x), 1, x.data_ptr(), w.data_ptr(), nullptr, zero_page(x.device()).data_ptr(),
+  HYP_CHECK_HIP(hyp::linear_ce(dtype_code(x), 1, x.data_ptr(), w.data_ptr(), nullptr, device_zero_page(x.device()),
                                (int)M, (int)E, kcols, (int)V, ce, cur_stream(), (int)bn));
   HYP_CHECK_HIP(hyp::ce_lse_combine(ce.part, tiles, (int)M, ce.zt, ce.target, ignore, lse.data_ptr<float>(),
                                     loss_rows.data_ptr<float>(), cur_stream()));
@@ -178,7 +171,7 @@ at::Tensor linear_ce_grad(const at::Tensor& x, const at::Tensor& w, const c10::o
   auto dz = at::empty({M, kcols}, x.options());
   const char* wrow = static_cast<const char*>(w.data_ptr()) + c0 * E * w.element_size();
   TORCH_CHECK(bn == 64 || bn == 128, "linear_ce_grad: bn 64 or 128");
-  HYP_CHECK_HIP(hyp::linear_ce(dtype_code(x), 2, x.data_ptr(), wrow, dz.data_ptr(), zero_page(x.device()).data_ptr(),
+  HYP_CHECK_HIP(hyp::linear_ce(dtype_code(x), 2, x.data_ptr(), wrow, dz.data_ptr(), device_zero_page(x.device()),
                                (int)M, (int)E, kcols, (int)n, ce, cur_stream(), (int)bn));
   return dz;
 }
@@ -260,7 +253,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
     bnb.sums = bn_sums->data_ptr<double>();
   }
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
-                              zero_page(dy.device()).data_ptr(), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
+                              device_zero_page(dy.device()), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
                               dph, dpw, bm, bn, 1, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr,
                               cur_stream(), 1.f, nullptr, (add && (splits == 1 || fuse_bn)) ? addend->data_ptr() : nullptr,
                               fuse_bn ? &bnb : nullptr));
@@ -335,7 +328,7 @@ at::Tensor linear_nt(const at::Tensor& x, const at::Tensor& w, int64_t splits_re
   TORCH_CHECK(sp >= 2 || (ep.U == nullptr && alpha == 1.0), "linear_nt: epilogue needs K >= 128");
   at::Tensor part;
   if (sp > 1) part = at::empty({(int64_t)sp * M * N}, x.options().dtype(at::kFloat));
-  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), zero_page(x.device()).data_ptr(),
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), device_zero_page(x.device()),
                               nullptr, nullptr, M, 1, 1, K, N, 1, 1, 1, 1, 1, 1, 0, 0, bm, bn, 0, sp,
                               sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream(), (float)alpha, &ep));
   return y;
@@ -362,7 +355,7 @@ at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_r
   at::Tensor part;
   if (sp > 1) part = at::empty({(int64_t)sp * M * K}, dy.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
-                              zero_page(dy.device()).data_ptr(), nullptr, nullptr, M, 1, 1, N, K, 1, 1, 1, 1, 1, 1, 0,
+                              device_zero_page(dy.device()), nullptr, nullptr, M, 1, 1, N, K, 1, 1, 1, 1, 1, 1, 0,
                               0, bm, bn, 1, sp, sp > 1 ? part.data_ptr<float>() : nullptr, cur_stream(), (float)alpha,
                               &ep));
   return dx;
@@ -398,7 +391,7 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int6
   at::Tensor part;
   if (splits > 1) part = at::empty({(int64_t)splits * K * R * S * C}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::conv_wgrad(dtype_code(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
-                                splits > 1 ? part.data_ptr<float>() : nullptr, zero_page(x.device()).data_ptr(), N, H,
+                                splits > 1 ? part.data_ptr<float>() : nullptr, device_zero_page(x.device()), N, H,
                                 W, C, K, P, Q, (int)R, (int)S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, splits, per,
                                 cur_stream(), (float)alpha));
   return dw;

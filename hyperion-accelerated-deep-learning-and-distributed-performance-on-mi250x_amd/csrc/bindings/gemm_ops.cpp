@@ -25,13 +25,6 @@ at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::S
   return c;
 }
 
-const at::Tensor& gemm_zero_page(const at::Device& dev) {
-  static at::Tensor z[16];
-  const int i = dev.index() < 0 ? 0 : dev.index();
-  if (!z[i].defined()) z[i] = at::zeros({256}, at::TensorOptions().device(dev).dtype(at::kByte));
-  return z[i];
-}
-
 // Operand view: a 2D tensor with unit stride in its last dim.  row form (tr = false): X[i, k] at
 // row i; tr form: X is [K, I] with X(i, k) = X[k, i].
 void check_operand(const at::Tensor& t, const char* name) {
@@ -87,7 +80,7 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, 
   g.beta = (float)beta;
   g.tile = (int)tile;
   g.splits = (int)splits;
-  g.zero = gemm_zero_page(a.device()).data_ptr();
+  g.zero = device_zero_page(a.device());
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->dim() == 1 && bias->numel() == N && bias->is_contiguous(), "gemm: bias must be [N] contiguous");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm: bias must be 16-byte aligned");

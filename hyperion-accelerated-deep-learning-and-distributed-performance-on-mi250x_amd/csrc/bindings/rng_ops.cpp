@@ -3,12 +3,44 @@
 #include <ATen/core/Generator.h>
 #include <ATen/hip/HIPGeneratorImpl.h>
 
+#include <map>
 #include <mutex>
+#include <utility>
 
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
 namespace hypbind {
+
+// Under capture the generator hands out POINTERS to its extragraph (seed, offset) tensors, which
+// every CUDAGraph::replay() rewrites in its prologue.  A record taken in graph 1 (forward) but
+// consumed in graph 2 (a split backward, train/step.py) would therefore read graph 2's offset and
+// regenerate a DIFFERENT mask.  So the first rng_state() of each capture snapshots (seed, offset)
+// into a 16-byte device buffer with two captured D2D copies at that point of the graph, and every
+// record of that capture points at the snapshot: replay N of graph 1 writes it, graph 2's backward
+// of the same step reads it (one pair of 8-byte copies per captured graph, not per dropout site).
+namespace {
+const int64_t* capture_snapshot(int64_t device, const at::PhiloxCudaState& st) {
+  static std::mutex mu;
+  static std::map<std::pair<int64_t, unsigned long long>, at::Tensor> snaps;
+  hipStream_t stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  HYP_CHECK_HIP(hipStreamGetCaptureInfo(stream, &status, &id));
+  TORCH_CHECK(status == hipStreamCaptureStatusActive, "rng_state: captured philox state outside an active capture");
+  std::lock_guard<std::mutex> g(mu);
+  auto key = std::make_pair(device, id);
+  auto it = snaps.find(key);
+  if (it == snaps.end()) {
+    auto snap = at::empty({2}, at::TensorOptions().device(at::Device(at::kCUDA, (c10::DeviceIndex)device)).dtype(at::kLong));
+    int64_t* d = snap.data_ptr<int64_t>();
+    HYP_CHECK_HIP(hipMemcpyAsync(d, st.seed_.ptr, sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
+    HYP_CHECK_HIP(hipMemcpyAsync(d + 1, st.offset_.ptr, sizeof(int64_t), hipMemcpyDeviceToDevice, stream));
+    it = snaps.emplace(key, snap).first;  // kept for the process lifetime (16 B per capture)
+  }
+  return it->second.data_ptr<int64_t>();
+}
+}  // namespace
 
 // The generator's (seed, offset) for `increment` random draws per element-thread, advancing it —
 // the call torch's own dropout makes.  Returned as a CPU int64 [6] record (seed, offset,
@@ -23,10 +55,11 @@ at::Tensor rng_state(int64_t device, int64_t increment) {
   auto t = at::empty({6}, at::TensorOptions().dtype(at::kLong));
   int64_t* p = t.data_ptr<int64_t>();
   if (st.captured_) {
+    const int64_t* snap = capture_snapshot(device, st);
     p[0] = 0;
     p[1] = 0;
-    p[2] = reinterpret_cast<int64_t>(st.seed_.ptr);
-    p[3] = reinterpret_cast<int64_t>(st.offset_.ptr);
+    p[2] = reinterpret_cast<int64_t>(snap);
+    p[3] = reinterpret_cast<int64_t>(snap + 1);
     p[4] = (int64_t)st.offset_intragraph_;
     p[5] = 1;
   } else {

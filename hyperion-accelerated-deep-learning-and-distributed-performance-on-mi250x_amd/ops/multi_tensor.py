@@ -97,18 +97,41 @@ class MultiTensorTable:
         self.key = self.key_of(groups)
 
 
+def _capturing(dev) -> bool:
+    return dev is not None and dev.type == "cuda" and torch.cuda.is_current_stream_capturing()
+
+
 class TableCache:
-    """Keeps the most recent table per role; rebuilds when pointers change."""
+    """Keeps the most recent table per role; rebuilds (or re-points) when pointers change.
+
+    A table that a hipGraph capture used is PINNED: the captured kernel reads its device pointer
+    buffer at every replay, so it is never re-pointed or dropped afterwards (the cache, owned by
+    the optimizer / model whose graph it is, keeps it alive).  An eager call with other pointers
+    after that gets a table of its own, so it can never redirect the graph's kernel to other
+    (possibly freed) tensors.
+    """
 
     def __init__(self):
         self._tables: Dict[str, MultiTensorTable] = {}
+        self._pinned: Dict[str, List[MultiTensorTable]] = {}
 
     def get(self, role: str, groups: Sequence[Sequence[torch.Tensor]]) -> MultiTensorTable:
         key = MultiTensorTable.key_of(groups)
+        capturing = _capturing(groups[0][0].device if groups and groups[0] else None)
         t = self._tables.get(role)
-        if t is not None and t.key != key and t.layout == MultiTensorTable.layout_of(groups):
-            t.repoint(groups)
-        elif t is None or t.key != key:
-            t = MultiTensorTable(groups)
+        if t is None or t.key != key:
+            hit = next((p for p in self._pinned.get(role, ()) if p.key == key), None)
+            if hit is not None:
+                t = hit
+            elif t is not None and not getattr(t, "pinned", False) and t.layout == MultiTensorTable.layout_of(groups):
+                t.repoint(groups)
+            else:
+                t = MultiTensorTable(groups)  # raises under capture (no allocation in the graph pool)
             self._tables[role] = t
+        if capturing and not getattr(t, "pinned", False):
+            t.pinned = True
+            self._pinned.setdefault(role, []).append(t)
         return t
+
+    def pinned(self) -> List[MultiTensorTable]:
+        return [t for ts in self._pinned.values() for t in ts]

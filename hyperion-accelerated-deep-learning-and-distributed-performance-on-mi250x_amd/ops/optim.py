@@ -19,6 +19,7 @@ Also provides multi-tensor global-norm clipping that takes the norm over *all* g
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Iterable, List, Optional
 
 import torch
@@ -177,14 +178,17 @@ class FusedAdam(torch.optim.Optimizer):
         self._host_step = int(state_dict.pop("hyperion_step", 0))
         super().load_state_dict(state_dict)
         self._step_t = None
-        self._tables = TableCache()
+        # the table cache is kept: tables a captured graph uses stay pinned; new state tensors
+        # simply key new tables
 
 
 def FusedAdamW(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
     return FusedAdam(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=True)
 
 
-_clip_tables = TableCache()
+# clip tables per model: keyed (weakly) by the first parameter, so two same-shaped models never
+# share -- and, once captured, never re-point -- each other's pointer table
+_clip_tables: "weakref.WeakKeyDictionary[torch.Tensor, TableCache]" = weakref.WeakKeyDictionary()
 
 
 @torch.no_grad()
@@ -200,14 +204,18 @@ def clip_grad_norm_(
     is all-reduced over ``group`` before clipping — the reference's ``clip_grad_norm_`` on FSDP
     modules skipped this and clipped by the local shard norm.
     """
-    grads: List[torch.Tensor] = [g for g in (grad_of(p) for p in parameters) if g is not None]
+    params = [p for p in parameters if grad_of(p) is not None]
+    grads: List[torch.Tensor] = [grad_of(p) for p in params]
     if not grads:
         return torch.zeros(())
     dev = grads[0].device
     native = _native.use_native(grads[0], op="clip") and all(_dense(g) and g.dtype == grads[0].dtype for g in grads)
     if native:
         try:
-            tab = _clip_tables.get("clip", [grads])
+            cache = _clip_tables.get(params[0])
+            if cache is None:
+                cache = _clip_tables[params[0]] = TableCache()
+            tab = cache.get("clip", [grads])
         except ValueError:
             native = False
     if native:

@@ -72,6 +72,14 @@ def size_based_auto_wrap_policy(min_num_params: int = 100_000) -> Callable[[nn.M
     return policy
 
 
+def _group_rank0(group) -> int:
+    """GLOBAL rank of the group's rank 0 (``dist.broadcast``'s ``src`` is a global rank; the
+    sharded state dict elects group-rank 0, which is not global rank 0 in a subgroup)."""
+    if group is None or group is dist.group.WORLD:
+        return 0
+    return dist.get_global_rank(group, 0)
+
+
 @dataclass
 class MixedPrecision:
     param_dtype: Optional[torch.dtype] = None
@@ -370,8 +378,9 @@ class FullyShardedDataParallel(nn.Module):
         self.backward_prefetch = backward_prefetch
         if sync_module_states and self.world > 1:
             with torch.no_grad():
+                src = _group_rank0(process_group)
                 for t in list(module.parameters()) + list(module.buffers()):
-                    dist.broadcast(t.data, src=0, group=process_group)
+                    dist.broadcast(t.data, src=src, group=process_group)
         if self.mp.buffer_dtype is not None:
             for m in module.modules():
                 for name, b in list(m.named_buffers(recurse=False)):
@@ -607,8 +616,8 @@ class FullyShardedDataParallel(nn.Module):
         for g, t in zip(self.flat_groups(), sd["flat_params"]):
             if t is not None:
                 g.flat_param.data.copy_(t.to(self.device))
-            if g.resident and self.world > 1:  # rank 0's copy of a replicated frozen group
-                dist.broadcast(g.flat_param.data, src=0, group=self.group)
+            if g.resident and self.world > 1:  # group-rank 0's copy of a replicated frozen group
+                dist.broadcast(g.flat_param.data, src=_group_rank0(self.group), group=self.group)
         self.invalidate_gather_cache()
         bufs = dict(self.module.named_buffers())
         for n, t in sd.get("buffers", {}).items():

@@ -61,12 +61,22 @@ def _local_gpu(rank: int) -> int:
     return lr % max(n, 1)
 
 
+_TIMEOUT_S = 600.0
+
+
+def current_timeout_s() -> float:
+    """The collective timeout the last ``setup()`` used (the native communicator's deadline)."""
+    return _TIMEOUT_S
+
+
 def default_backend() -> str:
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
 def setup(rank: int, world_size: int, backend: Optional[str] = None, timeout_s: float = 600.0) -> torch.device:
     """Create the process group (env:// rendezvous) and bind this process to its GPU."""
+    global _TIMEOUT_S
+    _TIMEOUT_S = float(timeout_s)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     # dmabuf-only IPC on the MI355X hosts; keep legacy IPC off for RCCL (see README)

@@ -7,6 +7,11 @@ the process-group timeout), ``nan`` (returns True so the caller poisons its loss
 configured timeout instead of hanging (the reference disabled the watchdog:
 ``TORCH_NCCL_ASYNC_ERROR_HANDLING=0``, ``run_language_fsdp.sh:10``).
 
+``stall`` is the GPU-side fault of the native communicator (``parallel/comm.py``): the given rank's
+comm stream sleeps ``HYPERION_FAULT_STALL_S`` seconds (default 30) on the device ahead of its
+``step``-th collective (here ``step`` counts that communicator's collectives), so peers — or, at
+world 1, the rank itself — miss the collective deadline and the watchdog must fail it cleanly.
+
 ``HYPERION_FAULT_MARKER=path`` makes the fault one-shot across restarts: it fires only while the
 marker file does not exist and creates it when it fires (restart + auto-resume tests: the resumed
 run replays the same step numbers and must not fail again).
@@ -24,7 +29,7 @@ def parse(spec: Optional[str] = None) -> Optional[Tuple[int, int, str]]:
     if not spec:
         return None
     r, s, k = spec.split(":")
-    if k not in ("exit", "raise", "hang", "nan"):
+    if k not in ("exit", "raise", "hang", "nan", "stall"):
         raise ValueError(f"unknown fault kind {k!r}")
     return int(r), int(s), k
 
@@ -33,9 +38,17 @@ class InjectedFault(RuntimeError):
     pass
 
 
+def comm_stall_s(rank: int, seq: int, spec: Optional[str] = None) -> float:
+    """Seconds of device stall to inject before this rank's seq-th native collective (0 = none)."""
+    f = parse(spec)
+    if f is None or f[2] != "stall" or f[0] != rank or f[1] != seq:
+        return 0.0
+    return float(os.environ.get("HYPERION_FAULT_STALL_S", "30"))
+
+
 def maybe_inject(rank: int, step: int, spec: Optional[str] = None) -> bool:
     f = parse(spec)
-    if f is None or f[0] != rank or f[1] != step:
+    if f is None or f[0] != rank or f[1] != step or f[2] == "stall":
         return False
     marker = os.environ.get("HYPERION_FAULT_MARKER")
     if marker:

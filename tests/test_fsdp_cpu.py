@@ -209,3 +209,45 @@ def test_fsdp_replicated_frozen_sharded_checkpoint_single_copy(tmp_path):
     res = run_world(_replicated_roundtrip, 2, (str(tmp_path),))
     assert res[0][0] > 0 and res[1][0] == 0  # only rank 0 stores the replicated frozen base
     assert res[0][1] and res[1][1]  # and every rank gets it back
+
+
+def _replicated_roundtrip_subgroup(rank, world, tmp):
+    """FSDP over the subgroup {1, 2} (global rank 0 not in it): the replicated frozen base is stored
+    by group-rank 0 (global rank 1) and broadcast back from it on load (the broadcast
+    used global src=0)."""
+    import os
+
+    import torch.distributed as dist
+
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.parallel.fsdp import FSDP, transformer_auto_wrap_policy
+
+    sub = dist.new_group([1, 2])
+    if rank == 0:
+        return None
+
+    def make():
+        m0 = _make_model()
+        for n, p in m0.named_parameters():
+            if "linear1" not in n:
+                p.requires_grad_(False)
+        return FSDP(m0, auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}),
+                    device_id=torch.device("cpu"), replicate_frozen=True, process_group=sub)
+
+    m = make()
+    want = m.full_state_dict(rank0_only=False)
+    sd = m.sharded_state_dict()
+    torch.save(sd, os.path.join(tmp, f"s{rank}.pt"))
+    dist.barrier(group=sub)
+    m2 = make()
+    with torch.no_grad():
+        for g in m2.flat_groups():
+            g.flat_param.data.zero_()
+    m2.load_sharded_state_dict(torch.load(os.path.join(tmp, f"s{rank}.pt"), weights_only=True))
+    got = m2.full_state_dict(rank0_only=False)
+    return all(torch.equal(got[k], want[k]) for k in want)
+
+
+def test_fsdp_replicated_frozen_subgroup_broadcast_source(tmp_path):
+    res = run_world(_replicated_roundtrip_subgroup, 3, (str(tmp_path),))
+    assert res[0] is None and res[1] and res[2]

@@ -64,3 +64,34 @@ def test_native_comm_orders_against_compute_stream(pg):
     torch.cuda.synchronize()
     assert float(y[0]) == 40.0 and float(y[-1]) == 40.0
     c.destroy()
+
+
+def test_native_comm_watchdog_times_out_stalled_collective(pg, monkeypatch):
+    """A device-side stall on the comm stream (HYPERION_FAULT=0:2:stall) makes the 2nd collective
+    miss a 0.5 s deadline: the watchdog aborts the communicator and the next wait() raises a clean
+    RuntimeError naming the collective, instead of hanging."""
+    import time
+
+    from hyperion.parallel.comm import NativeComm
+
+    monkeypatch.setenv("HYPERION_FAULT", "0:2:stall")
+    monkeypatch.setenv("HYPERION_FAULT_STALL_S", "3")
+    c = NativeComm(torch.device("cuda", 0), timeout_s=0.5)
+    x = torch.ones(256, device="cuda")
+    c.all_reduce(x, "sum").wait()  # seq 1: healthy
+    torch.cuda.synchronize()
+    assert c.error() == ""
+    t0 = time.monotonic()
+    w = c.all_reduce(x, "sum")  # seq 2: its comm stream sleeps ~3 s first
+    while c.error() == "" and time.monotonic() - t0 < 20.0:
+        time.sleep(0.01)
+    took = time.monotonic() - t0
+    assert "all_reduce #2" in c.error() and "timeout" in c.error(), c.error()
+    assert took < 2.9, took  # detected at the deadline, not after the stall drained
+    with pytest.raises(RuntimeError, match="all_reduce #2"):
+        w.wait()
+    with pytest.raises(RuntimeError, match="communicator failed"):
+        c.all_reduce(x, "sum")
+    torch.cuda.synchronize()  # the stall kernel drains; the device stays usable
+    assert float((x * 2).sum()) == 512.0
+    c.destroy()

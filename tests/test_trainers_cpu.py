@@ -139,6 +139,14 @@ def test_cli_max_restarts_recovers_single_process(tmp_path, monkeypatch):
     assert (tmp_path / "data" / "distributed" / "language_ddp_latest.pt").exists()
 
 
+def test_cli_restart_argv_rewrites_model_and_resume():
+    from hyperion.cli.run_distributed import _child_argv
+
+    a = ["--model", "all", "--epochs", "2", "--max_restarts", "3", "--resume=ckpt.pt", "--seed", "1"]
+    assert _child_argv(a, "cifar", None) == ["--epochs", "2", "--seed", "1", "--model", "cifar"]
+    assert _child_argv(a, "cifar", "auto")[-2:] == ["--resume", "auto"]
+
+
 def _gpt2_fsdp(rank, world, base):
     from hyperion.train.distributed import train_language_model_fsdp
     from hyperion.models.simple_lm import gpt2_small_lm
