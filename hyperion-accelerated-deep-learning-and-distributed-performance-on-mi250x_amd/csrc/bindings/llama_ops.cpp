@@ -44,6 +44,29 @@ std::vector<at::Tensor> rope(const at::Tensor& q, const at::Tensor& k, const c10
   return {qo, ko};
 }
 
+// in place on strided [B, S, H, D] views (e.g. the q / k columns of a packed [B*S, 3*H*D] buffer):
+// the kernel reads each lane's pairs before writing them back
+void rope_inplace(at::Tensor& q, at::Tensor& k, const c10::optional<at::Tensor>& positions, double theta,
+                  bool inverse) {
+  check_rope_operand(q, "rope_ q");
+  check_rope_operand(k, "rope_ k");
+  TORCH_CHECK(q.sizes() == k.sizes() && q.scalar_type() == k.scalar_type(), "rope_: q/k mismatch");
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D % 16 == 0, "rope_: head_dim must be a multiple of 16");
+  const int64_t* pos = nullptr;
+  at::Tensor pc;
+  if (positions.has_value() && positions->defined()) {
+    pc = positions->to(at::kLong).contiguous();
+    TORCH_CHECK(pc.numel() == q.size(0) * q.size(1), "rope_: positions must be [B, S]");
+    pos = pc.data_ptr<int64_t>();
+  }
+  const at::DeviceGuard guard(q.device());
+  HYP_CHECK_HIP(hyp::rope_apply(dtype_code(q), q.data_ptr(), k.data_ptr(), q.data_ptr(), k.data_ptr(),
+                                q.size(0) * q.size(1), (int)q.size(1), (int)q.size(2), (int)k.size(2), (int)D,
+                                q.stride(1), k.stride(1), q.stride(2), k.stride(2), pos, (float)theta, inverse ? 1 : 0,
+                                cur_stream()));
+}
+
 at::Tensor swiglu_fwd(const at::Tensor& g, const at::Tensor& u) {
   TORCH_CHECK(g.is_cuda() && g.sizes() == u.sizes() && g.scalar_type() == u.scalar_type(), "swiglu: g/u mismatch");
   TORCH_CHECK(g.numel() % 8 == 0, "swiglu: numel must be a multiple of 8");
@@ -69,6 +92,7 @@ std::vector<at::Tensor> swiglu_bwd(const at::Tensor& dh, const at::Tensor& g, co
 
 void register_llama_ops(pybind11::module& m) {
   m.def("rope", &rope, "rotary position embedding on q and k (HF rotate_half convention)");
+  m.def("rope_", &rope_inplace, "in-place rotary embedding on strided q / k views");
   m.def("swiglu_fwd", &swiglu_fwd, "silu(g) * u");
   m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward -> (dg, du)");
 }

@@ -23,4 +23,5 @@ PYBIND11_MODULE(HYP_MODULE_NAME, m) {
   hypbind::register_comm(m);
   hypbind::register_conv_ops(m);
   hypbind::register_rng_ops(m);
+  hypbind::register_ws_ops(m);
 }

@@ -11,4 +11,5 @@ void register_gemm_ops(pybind11::module& m);
 void register_comm(pybind11::module& m);
 void register_conv_ops(pybind11::module& m);
 void register_rng_ops(pybind11::module& m);
+void register_ws_ops(pybind11::module& m);
 }  // namespace hypbind

@@ -174,6 +174,22 @@ __device__ __forceinline__ uint32_t rng_u32(uint64_t key, uint64_t ctr) {
   return (uint32_t)(splitmix64(key + 0xD1B54A32D192ED03ull * (ctr + 1)) >> 32);
 }
 
+// LoRA-dropout keep mask (ops/llama_fused.py): one cheap 32-bit hash per element index, keyed by the
+// call's rng_key — regenerated identically by every forward and backward kernel that needs it.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// keep (probability 1 - thr / 2^32) for element `idx` = (proj * M + m) * K + k
+__device__ __forceinline__ bool lora_keep(uint64_t key, uint32_t idx, uint32_t thr) {
+  return lowbias32(lowbias32(idx ^ (uint32_t)key) ^ (uint32_t)(key >> 32)) >= thr;
+}
+
 // ---- wave / block reductions ------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -290,3 +290,35 @@ hipError_t dropout_apply(int dtype, int mode, const void* x, void* out, int64_t 
                          hipStream_t st);
 }  // namespace hyp
 
+namespace hyp {
+// ---- wstream.hip -----------------------------------------------------------------------------
+// Weight-streaming GEMM for few-token activations: x slice resident in LDS, W streamed to VGPRs.
+// nn = false: y = x Wᵀ (W [N, K]); nn = true: y = x W (W [K, N]).  Writes fp32 partial slabs
+// [S][MB*mf][N/16][64][4] (fragment order); ws_reduce sums them (+ epilogue) into [M, N].
+bool ws_supported(int M, int N, int K, bool nn);
+void ws_plan(int M, int N, int K, bool nn, int* mf, int* kr, int* G, int* nf);
+hipError_t ws_gemm(int dtype, bool nn, const void* x, int64_t ldx, const void* w, int64_t ldw, float* part,
+                   const void* zero, int M, int N, int K, int mf, int kr, int G, int nf, hipStream_t st);
+// out[m, n] = alpha Σ_s part + beta addend[m, n] + uscale Σ_r U[m, seg r + rr] V[n, rr] (seg = n / segw)
+hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t ldo, const void* addend, float alpha,
+                     float beta, const float* U, const void* V, int r, int segw, float uscale, int M, int N, int S,
+                     int MFtot, hipStream_t st);
+// Fused epilogues of the slabs (see wstream.hip): 0 plain, 1 LoRA up (+ RoPE), 2 SwiGLU fwd,
+// 3 SwiGLU bwd (NN), 4 LoRA data gradient (NN).
+hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, int M, int N, void* out, int64_t ldo,
+                       void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
+                       const void* const* lw, int P, int r, int segw, float lscale, int rope_segs, int seq,
+                       float theta, const RngState* rng, float p_drop, hipStream_t st);
+}  // namespace hyp
+
+namespace hyp {
+// ---- lora_fused.hip --------------------------------------------------------------------------
+// rank-r halves of the fused LoRA projections (P projections sharing one input; see the file).
+// t / du: fp32 [M, P r] accumulated atomically (zero them first).
+hipError_t lora_down(int dtype, const void* x, int64_t ldx, const void* const* A, int P, int r, float* t, int ldt, int M,
+                     int K, const RngState* rng, float p_drop, hipStream_t st);
+hipError_t lora_bwd_t(int dtype, const void* dy, int64_t ldy, int N, const void* const* B, void* const* dB, int P,
+                      int r, const float* t, int ldt, float* du, int M, float c, hipStream_t st);
+hipError_t lora_bwd_a(int dtype, const void* x, int64_t ldx, int K, void* const* dA, int P, int r, const float* du,
+                      int ldt, int M, const RngState* rng, float p_drop, hipStream_t st);
+}  // namespace hyp

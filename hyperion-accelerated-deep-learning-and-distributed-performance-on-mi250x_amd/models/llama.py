@@ -19,6 +19,7 @@ non-recursing policy, K8).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -26,6 +27,8 @@ import torch
 import torch.nn as nn
 from torch.utils.checkpoint import checkpoint
 
+from ..ops import _native
+from ..ops import llama_fused as _fused
 from ..ops.embedding import Embedding
 from ..ops.attention import attention
 from ..ops.cross_entropy import LinearCrossEntropy
@@ -33,6 +36,10 @@ from ..ops.layernorm import RMSNorm
 from ..ops.linear import Linear as HypLinear
 from ..ops.rope import apply_rope
 from ..ops.swiglu import swiglu
+
+
+# HYPERION_LLAMA_FUSED=0 keeps every layer on the module path (A/B runs, numerics tests)
+FUSED = os.environ.get("HYPERION_LLAMA_FUSED", "1") != "0"
 
 
 @dataclass
@@ -112,7 +119,16 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
 
     def forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor, positions=None, kpm=None):
-        """Residual-stream form: block input = ``stream + delta``; returns ``(mlp_out, new_stream)``."""
+        """Residual-stream form: block input = ``stream + delta``; returns ``(mlp_out, new_stream)``.
+
+        Frozen-base layers (the LoRA fine-tune) at few tokens run as ONE fused autograd node
+        (``ops/llama_fused.py``: weight-streaming GEMMs over the concatenated q/k/v and gate/up
+        weights, LoRA / RoPE / SwiGLU in their epilogues); everything else takes the module path."""
+        if positions is None and FUSED:
+            out = _fused.llama_layer_fused(self, delta, stream, kpm)
+            if out is not None:
+                _native.count("llama_fused_layer")
+                return out
         ln1 = self.input_layernorm
         if delta is None:
             h, s = ln1(stream), stream

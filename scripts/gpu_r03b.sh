@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 3: weight-streaming GEMM numerics + shape bench, then smoke, headline bench, GPU suite, bench kernel stats
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+fatal() { local rc=$1; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc"; exit $rc; fi; }
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_wstream.py tests/test_gpu_llama_fused.py -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ws.log 2>&1; rc=$?; echo "ws tests rc=$rc"; grep -E "FAILED|Error|error" gpurun_out/pytest_ws.log | head -20; tail -3 gpurun_out/pytest_ws.log; fatal $rc
+timeout -k 10 300 python3 -u scripts/ws_bench.py > gpurun_out/ws_bench.log 2>&1; rc=$?; echo "ws bench rc=$rc"; cat gpurun_out/ws_bench.log | cut -c1-400; fatal $rc
+timeout -k 10 300 python3 __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log | cut -c1-200; fatal $rc
+timeout -k 10 300 python3 bench.py --steps 50 --warmup 10 --json-out gpurun_out/bench_graph.json > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log | cut -c1-220; fatal $rc
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR" gpurun_out/pytest_gpu.log | head -20; tail -3 gpurun_out/pytest_gpu.log; fatal $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/trace_bench" -o run -- python3 "$PWD/bench.py" --steps 6 --warmup 4 > gpurun_out/trace_bench.log 2>&1; rc=$?; echo "trace rc=$rc"
