@@ -376,8 +376,12 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
                      replicate_frozen="auto") -> Dict:
     """C26: Llama fine-tune.  ``lora=True``: frozen bf16 base + r16 adapters on q/k/v/o.
 
-    ``lora_parallel='fsdp'`` (default; the BASELINE.json config) shards the frozen base and
-    reduce-scatters only the adapters; ``'ddp'`` reproduces the reference (DDP over a replicated
+    ``lora_parallel='fsdp'`` (default; the BASELINE.json config) wraps the model in FSDP with one
+    unit per decoder layer and reduce-scatters only the adapters.  Whether the frozen base is
+    sharded too is ``replicate_frozen``'s call (below): with the default ``"auto"`` it is
+    REPLICATED whenever it fits (Llama-2-7B on MI355X: 13.5 GB of 288 GB), which makes the run
+    FSDP over the adapters only — DDP-like traffic; ``replicate_frozen=False`` shards the base
+    like the reference's torch FSDP.  ``'ddp'`` reproduces the reference (DDP over a replicated
     model).  ``lora=False``: full bf16 FSDP with ``LlamaDecoderLayer`` units.  ``hf_token`` /
     ``model_id`` are accepted for CLI compatibility; weights are random-init (no network).
     ``mask_pad_labels`` fixes the reference's unmasked pad labels (:517) when set.
