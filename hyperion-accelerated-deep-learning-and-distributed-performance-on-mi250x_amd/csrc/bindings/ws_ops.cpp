@@ -125,12 +125,25 @@ std::vector<const void*> ptr_list(const std::vector<at::Tensor>& ts, at::ScalarT
   return v;
 }
 
-void ws_epilogue_py(const at::Tensor& part, int64_t S, int64_t MFtot, int64_t M, int64_t N, int64_t epi,
+void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_t MFtot, int64_t M, int64_t N, int64_t epi,
                     const at::Tensor& out, const c10::optional<at::Tensor>& out2, const c10::optional<at::Tensor>& aux,
                     const c10::optional<at::Tensor>& t, const std::vector<at::Tensor>& lw, int64_t segw, double lscale,
-                    int64_t rope_segs, int64_t seq, double theta, const c10::optional<at::Tensor>& rng, double p_drop) {
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= S * MFtot * (N / 16) * 256,
-              "ws_epilogue: fp32 slabs");
+                    int64_t rope_segs, int64_t seq, double theta, const c10::optional<at::Tensor>& rng, double p_drop,
+                    c10::optional<bool> nn, const c10::optional<at::Tensor>& yin) {
+  const bool dense = !(part_opt.has_value() && part_opt->defined());
+  const float* part_ptr = nullptr;
+  if (!dense) {
+    const at::Tensor& part = *part_opt;
+    TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= S * MFtot * (N / 16) * 256,
+                "ws_epilogue: fp32 slabs");
+    part_ptr = part.data_ptr<float>();
+  } else {
+    TORCH_CHECK(yin.has_value() && yin->defined() && yin->dim() == 2 && yin->size(0) == M && yin->size(1) == N &&
+                    yin->stride(1) == 1 && yin->scalar_type() == out.scalar_type(),
+                "ws_epilogue: without slabs, yin must be the [M, N] GEMM result in the activation dtype");
+    MFtot = (M + 15) / 16;
+    S = 0;
+  }
   const auto dt = out.scalar_type();
   const int64_t I = N;  // EPI 2: out is gu [M, N], out2 h [M, N/2]; EPI 3: out is dgu [M, 2N]
   check_out(out, M, epi == 3 ? 2 * N : N, dt, "out");
@@ -172,11 +185,13 @@ void ws_epilogue_py(const at::Tensor& part, int64_t S, int64_t MFtot, int64_t M,
   const bool has_rng = rng.has_value() && rng->defined() && p_drop > 0;
   if (has_rng) rs = unpack_rng(*rng);
   TORCH_CHECK(epi != 1 || (segw >= 128 && N % segw == 0), "ws_epilogue: segment width");
-  const at::DeviceGuard guard(part.device());
-  HYP_CHECK_HIP(hyp::ws_epilogue(dtype_code(out), (int)epi, part.data_ptr<float>(), (int)S, (int)MFtot, (int)M,
+  const at::DeviceGuard guard(out.device());
+  HYP_CHECK_HIP(hyp::ws_epilogue(dtype_code(out), (int)epi, part_ptr, (int)S, (int)MFtot, (int)M,
                                  (int)N, out.data_ptr(), out.stride(0), o2, ldo2, ax, ldax, tp, ldt,
                                  lp.empty() ? nullptr : lp.data(), P, r, (int)segw, (float)lscale, (int)rope_segs,
-                                 (int)seq, (float)theta, has_rng ? &rs : nullptr, (float)p_drop, cur_stream()));
+                                 (int)seq, (float)theta, has_rng ? &rs : nullptr, (float)p_drop,
+                                 nn.has_value() ? *nn : (epi == 3 || epi == 4), dense ? yin->data_ptr() : nullptr,
+                                 dense ? yin->stride(0) : 0, cur_stream()));
 }
 
 void lora_down_py(const at::Tensor& x, const std::vector<at::Tensor>& A, at::Tensor& t,
@@ -254,7 +269,7 @@ void register_ws_ops(pybind11::module& m) {
         "part"_a, "S"_a, "MFtot"_a, "M"_a, "N"_a, "epi"_a, "out"_a, "out2"_a = pybind11::none(),
         "aux"_a = pybind11::none(), "t"_a = pybind11::none(), "lw"_a = std::vector<at::Tensor>{}, "segw"_a = 0,
         "lscale"_a = 1.0, "rope_segs"_a = 0, "seq"_a = 0, "theta"_a = 10000.0, "rng"_a = pybind11::none(),
-        "p_drop"_a = 0.0);
+        "p_drop"_a = 0.0, "nn"_a = pybind11::none(), "yin"_a = pybind11::none());
   m.def("lora_down", &lora_down_py, "t[m, p r + j] += Σ_k keep_p x A_p (fp32 atomics)", "x"_a, "A"_a, "t"_a,
         "rng"_a = pybind11::none(), "p_drop"_a = 0.0);
   m.def("lora_bwd_t", &lora_bwd_t_py, "du' += c dy_p B_p (atomics); dB_p = c dy_pᵀ t_p", "dy"_a, "N"_a, "B"_a, "dB"_a,

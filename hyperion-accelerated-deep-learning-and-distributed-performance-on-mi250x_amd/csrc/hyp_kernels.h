@@ -304,11 +304,13 @@ hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t l
                      float beta, const float* U, const void* V, int r, int segw, float uscale, int M, int N, int S,
                      int MFtot, hipStream_t st);
 // Fused epilogues of the slabs (see wstream.hip): 0 plain, 1 LoRA up (+ RoPE), 2 SwiGLU fwd,
-// 3 SwiGLU bwd (NN), 4 LoRA data gradient (NN).
+// 3 SwiGLU bwd (NN), 4 LoRA data gradient (NN).  part == null: the GEMM result is the row-major
+// yin [M, N] (a vendor GEMM's output) instead of slabs.
 hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, int M, int N, void* out, int64_t ldo,
                        void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
                        const void* const* lw, int P, int r, int segw, float lscale, int rope_segs, int seq,
-                       float theta, const RngState* rng, float p_drop, hipStream_t st);
+                       float theta, const RngState* rng, float p_drop, bool nn, const void* yin, int64_t ldy,
+                       hipStream_t st);
 }  // namespace hyp
 
 namespace hyp {

@@ -318,7 +318,9 @@ __global__ __launch_bounds__(256) void ws_reduce_k(const WsRed a) {
 //          dgu[m, n + I] = dh silu(g)
 //   EPI 4  LoRA data gradient (NN): out = Σ + Σ_p keep_p(m, n) Σ_rr du[m, p r + rr] A_p[rr, n]
 struct WsEpi {
-  const float* part;
+  const float* part;      // fp32 slabs, or null: the GEMM result is the row-major yin (a vendor GEMM's)
+  const void* yin;
+  int64_t ldy;
   int S, MFtot, M, N;     // GEMM output width N (EPI 2: 2 I; EPI 3: I)
   void* out;
   int64_t ldo;
@@ -338,9 +340,9 @@ struct WsEpi {
   int drop;
 };
 
-template <typename T, int EPI>
+template <typename T, int EPI, bool NN>
 __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
-  constexpr bool NN = EPI == 3 || EPI == 4;
+  static_assert(EPI == 0 || (EPI == 3 || EPI == 4) == NN, "slab layout: EPI 1/2 are NT, 3/4 NN, 0 either");
   constexpr bool PAIR = EPI == 1 || EPI == 2;
   __shared__ float lt[16 * 64];           // t / du rows of the block (P r <= 64)
   __shared__ float lw_s[4 * 16 * 128];    // EPI 1: B rows [128 cols][r]; EPI 4: A_p [r][64 cols] per p
@@ -395,6 +397,13 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
   const int64_t slab = (int64_t)a.MFtot * F * 256;
   auto sum_quad = [&](int c) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (a.part == nullptr) {  // dense input: the 4 rows of this quad's column
+      const int col = NN ? (c >> 2) * 64 + 4 * (lane & 15) + (c & 3) : c * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[e] = ld1<T>(static_cast<const T*>(a.yin) + (int64_t)min(m0 + e, a.M - 1) * a.ldy + col);
+      return acc;
+    }
     const float* p = a.part + (((int64_t)mf * F + c) * 64 + lane) * 4;
     for (int s = 0; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * slab);
     return acc;
@@ -595,8 +604,11 @@ hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t l
 hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, int M, int N, void* out, int64_t ldo,
                        void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
                        const void* const* lw, int P, int r, int segw, float lscale, int rope_segs, int seq,
-                       float theta, const RngState* rng, float p_drop, hipStream_t st) {
+                       float theta, const RngState* rng, float p_drop, bool nn, const void* yin, int64_t ldy,
+                       hipStream_t st) {
   if (dtype != kBF16 && dtype != kF16) return hipErrorInvalidValue;
+  if (part == nullptr && yin == nullptr) return hipErrorInvalidValue;
+  if (epi != 0 && nn != (epi == 3 || epi == 4)) return hipErrorInvalidValue;  // the slab layout of that GEMM
   if (MFtot * 16 < M || N % 64 != 0 || epi < 0 || epi > 4) return hipErrorInvalidValue;
   const bool lora = t != nullptr;
   if ((epi == 4 || (epi == 1 && lora)) && (t == nullptr || P < 1 || P > 4 || r < 1 || r > 16 || P * r > 64 || lw == nullptr))
@@ -606,6 +618,8 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
   if (epi == 3 && aux == nullptr) return hipErrorInvalidValue;
   WsEpi a{};
   a.part = part;
+  a.yin = yin;
+  a.ldy = ldy;
   a.S = S;
   a.MFtot = MFtot;
   a.M = M;
@@ -631,13 +645,16 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
   a.thr = (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f);
   const int mfv = (M + 15) / 16;
   dim3 grid(epi == 1 ? N / 128 : (epi == 2 ? N / 128 : N / 64), mfv);
-#define HYP_EPI(TT)                                                                      \
-  switch (epi) {                                                                         \
-    case 0: hipLaunchKernelGGL((ws_epi_k<TT, 0>), grid, dim3(256), 0, st, a); break;   \
-    case 1: hipLaunchKernelGGL((ws_epi_k<TT, 1>), grid, dim3(256), 0, st, a); break;   \
-    case 2: hipLaunchKernelGGL((ws_epi_k<TT, 2>), grid, dim3(256), 0, st, a); break;   \
-    case 3: hipLaunchKernelGGL((ws_epi_k<TT, 3>), grid, dim3(256), 0, st, a); break;   \
-    default: hipLaunchKernelGGL((ws_epi_k<TT, 4>), grid, dim3(256), 0, st, a); break;  \
+#define HYP_EPI(TT)                                                                            \
+  switch (epi) {                                                                               \
+    case 0:                                                                                    \
+      if (nn) hipLaunchKernelGGL((ws_epi_k<TT, 0, true>), grid, dim3(256), 0, st, a);          \
+      else hipLaunchKernelGGL((ws_epi_k<TT, 0, false>), grid, dim3(256), 0, st, a);            \
+      break;                                                                                   \
+    case 1: hipLaunchKernelGGL((ws_epi_k<TT, 1, false>), grid, dim3(256), 0, st, a); break;   \
+    case 2: hipLaunchKernelGGL((ws_epi_k<TT, 2, false>), grid, dim3(256), 0, st, a); break;   \
+    case 3: hipLaunchKernelGGL((ws_epi_k<TT, 3, true>), grid, dim3(256), 0, st, a); break;    \
+    default: hipLaunchKernelGGL((ws_epi_k<TT, 4, true>), grid, dim3(256), 0, st, a); break;   \
   }
   if (dtype == kBF16) {
     HYP_EPI(bf16_t)

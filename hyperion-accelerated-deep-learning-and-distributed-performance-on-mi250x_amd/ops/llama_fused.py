@@ -40,6 +40,7 @@ import torch.nn as nn
 from . import _native
 
 WS_MAX_M = int(os.environ.get("HYPERION_WS_MAX_M", "512"))
+DEBUG: Optional[dict] = None  # tests / scripts: set to a dict to capture the backward intermediates
 
 
 def _adjacent(ws: List[torch.Tensor]) -> bool:
@@ -72,27 +73,29 @@ def _lora_parts(mod: nn.Module):
     return mod.lora_A[a].weight, mod.lora_B[a].weight, float(mod.scaling[a]), float(mod.p)
 
 
+def _fuse_layer(m: nn.Module) -> int:
+    at, mlp = m.self_attn, m.mlp
+    n = 0
+    for mods in ((at.q_proj, at.k_proj, at.v_proj), (mlp.gate_proj, mlp.up_proj)):
+        ws = [_base_weight(x) for x in mods]
+        if any(w.requires_grad for w in ws) or _adjacent(ws):
+            continue
+        with torch.no_grad():
+            buf = torch.cat([w.detach() for w in ws], 0)
+            o = 0
+            for w in ws:
+                w.data = buf[o:o + w.shape[0]]
+                o += w.shape[0]
+        n += 1
+    return n
+
+
 def fuse_llama_weights(model: nn.Module) -> int:
     """Re-home every decoder layer's frozen q/k/v and gate/up weights into concatenated buffers
     (``p.data`` becomes a view; Parameter objects, keys and values are unchanged).  Returns the
-    number of layers changed.  Call before building optimizers / graphs; FSDP units need nothing."""
-    n = 0
-    for m in model.modules():
-        if not (hasattr(m, "self_attn") and hasattr(m, "mlp")):
-            continue
-        at, mlp = m.self_attn, m.mlp
-        for mods in ((at.q_proj, at.k_proj, at.v_proj), (mlp.gate_proj, mlp.up_proj)):
-            ws = [_base_weight(x) for x in mods]
-            if any(w.requires_grad for w in ws) or _adjacent(ws):
-                continue
-            with torch.no_grad():
-                buf = torch.cat([w.detach() for w in ws], 0)
-                o = 0
-                for w in ws:
-                    w.data = buf[o:o + w.shape[0]]
-                    o += w.shape[0]
-            n += 1
-    return n
+    number of groups changed.  The fused node also does this lazily on its first eager call;
+    Hyperion's FSDP flat buffers already hold them adjacent."""
+    return sum(_fuse_layer(m) for m in model.modules() if hasattr(m, "self_attn") and hasattr(m, "mlp"))
 
 
 class _Spec:
@@ -146,7 +149,11 @@ def fused_spec(layer: nn.Module, x: torch.Tensor, kpm: Optional[torch.Tensor]) -
         if lp[0][0].shape[0] > 16:
             return None
     if not (_adjacent(ws[:3]) and _adjacent(ws[4:6])):
-        return None
+        if torch.cuda.is_current_stream_capturing() or not _fuse_layer(layer):
+            return None
+        ws = [_base_weight(m) for m in qkv + [at.o_proj, mlp.gate_proj, mlp.up_proj, mlp.down_proj]]
+        if not (_adjacent(ws[:3]) and _adjacent(ws[4:6])):
+            return None
     s = _Spec()
     s.W_qkv, s.W_o, s.W_gu, s.W_d = _cat_view(ws[:3]), ws[3], _cat_view(ws[4:6]), ws[6]
     s.w1, s.w2 = _ln_w32(layer, "input_layernorm"), _ln_w32(layer, "post_attention_layernorm")
@@ -164,8 +171,49 @@ def fused_spec(layer: nn.Module, x: torch.Tensor, kpm: Optional[torch.Tensor]) -
     return s
 
 
-def _gemm(C, x, w, nn_: bool = False):
-    return C.ws_gemm_part(x, w, nn=nn_)
+# Per-shape GEMM plan: ("ws", mf, kr, G, nf) — the weight-streaming kernel with that plan (0 =
+# automatic) — or ("vendor",) — hipBLASLt, its bf16 output then run through the same epilogue kernel
+# (``ws_epilogue(yin=...)``).  Filled from cold-weight sweeps (scripts/ws_bench.py,
+# profiles/r03/ws_bench.json); ``HYPERION_WS_PLAN=ws|vendor`` forces one side for A/B runs.
+_PLAN_OVERRIDE = os.environ.get("HYPERION_WS_PLAN", "")
+# (nn, output width, reduction length) -> plan; measured at 128 tokens (scripts/ws_bench.py, cold
+# weights, GEMM + epilogue): hipBLASLt streams the wide forward projections (q/k/v 12288 x 4096:
+# 31.9 us, gate/up 22016 x 4096: 46.7 us — no split-K, activations re-read from L2) faster than
+# the slab kernel (43.5 / 74.1 us); every data gradient (hipBLASLt NN 38.6-114 us) and the
+# 4096-wide forwards stay on the weight-streaming kernel.
+PLANS = {
+    (False, 12288, 4096): ("vendor",),
+    (False, 22016, 4096): ("vendor",),
+    (False, 4096, 11008): ("ws", 8, 512, 11, 1),
+}
+
+
+def plan_for(nn_: bool, M: int, N: int, K: int) -> tuple:
+    if _PLAN_OVERRIDE == "vendor":
+        return ("vendor",)
+    if _PLAN_OVERRIDE == "ws":
+        return ("ws", 0, 0, 0, 0)
+    return PLANS.get((nn_, N, K), ("ws", 0, 0, 0, 0))
+
+
+class _Proj:
+    """One projection's GEMM result: fp32 slabs of the weight-streaming kernel, or a dense vendor output."""
+
+    __slots__ = ("part", "S", "MFt", "y")
+
+    def __init__(self, C, x, w, nn_: bool = False):
+        M, K = x.shape
+        N = w.shape[1] if nn_ else w.shape[0]
+        p = plan_for(nn_, M, N, K)
+        self.part = self.y = None
+        self.S = self.MFt = 0
+        if p[0] == "vendor":
+            self.y = x @ w if nn_ else x @ w.t()
+        else:
+            self.part, self.S, self.MFt = C.ws_gemm_part(x, w, nn=nn_, mf=p[1], kr=p[2], G=p[3], nf=p[4])
+
+    def epi(self, C, M, N, epi, out, **kw):
+        C.ws_epilogue(self.part, self.S, self.MFt, M, N, epi, out, yin=self.y, **kw)
 
 
 class _LlamaLayerFn(torch.autograd.Function):
@@ -190,9 +238,9 @@ class _LlamaLayerFn(torch.autograd.Function):
                 rq, ro = _native.rng_state(dev), _native.rng_state(dev)
             t_qkv = torch.zeros(M, 3 * spec.r, device=dev, dtype=torch.float32)
             C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p)
-        part, nS, MFt = C.ws_gemm_part(h, spec.W_qkv)
+        pj = _Proj(C, h, spec.W_qkv)
         qkv = torch.empty(M, 3 * H, device=dev, dtype=dt)
-        C.ws_epilogue(part, nS, MFt, M, 3 * H, 1, qkv, t=t_qkv, lw=[Bq, Bk, Bv] if lora else [], segw=H,
+        pj.epi(C, M, 3 * H, 1, qkv, t=t_qkv, lw=[Bq, Bk, Bv] if lora else [], segw=H,
                       lscale=spec.c, rope_segs=2, seq=S, theta=spec.theta)
         q5 = qkv.view(Bsz, S, 3, spec.nh, spec.hd)
         q, k, v = q5[:, :, 0], q5[:, :, 1], q5[:, :, 2]
@@ -202,17 +250,17 @@ class _LlamaLayerFn(torch.autograd.Function):
         if lora:
             t_o = torch.zeros(M, spec.r, device=dev, dtype=torch.float32)
             C.lora_down(o2, [Ao], t_o, ro, spec.p)
-        part, nS, MFt = C.ws_gemm_part(o2, spec.W_o)
+        pj = _Proj(C, o2, spec.W_o)
         a = torch.empty(M, H, device=dev, dtype=dt)
-        C.ws_epilogue(part, nS, MFt, M, H, 1, a, t=t_o, lw=[Bo] if lora else [], segw=H, lscale=spec.c)
+        pj.epi(C, M, H, 1, a, t=t_o, lw=[Bo] if lora else [], segw=H, lscale=spec.c)
         h2, s2, _, rstd2 = C.ln_fwd(a, s, spec.w2, None, spec.eps, True)
-        part, nS, MFt = C.ws_gemm_part(h2, spec.W_gu)
+        pj = _Proj(C, h2, spec.W_gu)
         gu = torch.empty(M, 2 * spec.I, device=dev, dtype=dt)
         hh = torch.empty(M, spec.I, device=dev, dtype=dt)
-        C.ws_epilogue(part, nS, MFt, M, 2 * spec.I, 2, gu, out2=hh)
-        part, nS, MFt = C.ws_gemm_part(hh, spec.W_d)
+        pj.epi(C, M, 2 * spec.I, 2, gu, out2=hh)
+        pj = _Proj(C, hh, spec.W_d)
         d = torch.empty(M, H, device=dev, dtype=dt)
-        C.ws_epilogue(part, nS, MFt, M, H, 0, d)
+        pj.epi(C, M, H, 0, d)
         ctx.spec = spec
         ctx.cfg = (Bsz, S, delta is not None, scale, rq, ro)
         ctx.save_for_backward(h, s, rstd1, qkv, o, lse, s2, rstd2, gu, kpm, t_qkv, t_o, Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo)
@@ -231,13 +279,13 @@ class _LlamaLayerFn(torch.autograd.Function):
         dd2 = dd.reshape(M, H).to(dt).contiguous() if dd is not None else torch.zeros(M, H, device=dev, dtype=dt)
         ds2c = ds2.reshape(M, H).to(dt).contiguous() if ds2 is not None else None
         # down projection: dhh = dd W_d, SwiGLU backward in the epilogue -> dgu [M, 2I]
-        part, nS, MFt = C.ws_gemm_part(dd2, spec.W_d, nn=True)
+        pj = _Proj(C, dd2, spec.W_d, True)
         dgu = torch.empty(M, 2 * I, device=dev, dtype=dt)
-        C.ws_epilogue(part, nS, MFt, M, I, 3, dgu, aux=gu)
+        pj.epi(C, M, I, 3, dgu, aux=gu)
         # gate/up: dh2 = dgu [W_gate; W_up]
-        part, nS, MFt = C.ws_gemm_part(dgu, spec.W_gu, nn=True)
+        pj = _Proj(C, dgu, spec.W_gu, True)
         dh2 = torch.empty(M, H, device=dev, dtype=dt)
-        C.ws_epilogue(part, nS, MFt, M, H, 0, dh2)
+        pj.epi(C, M, H, 0, dh2, nn=True)
         dsum2 = C.ln_bwd(dh2, s2, spec.w2, rstd2, rstd2, ds2c, False, False, True)[0]  # grad of s2 = a + s
         # O projection (+ LoRA)
         grads = [None] * 8
@@ -246,14 +294,14 @@ class _LlamaLayerFn(torch.autograd.Function):
             du_o = torch.zeros(M, spec.r, device=dev, dtype=torch.float32)
             dAo, dBo = torch.empty_like(Ao), torch.empty_like(Bo)
             C.lora_bwd_t(dsum2, H, [Bo], [dBo], t_o, du_o, spec.c)
-        part, nS, MFt = C.ws_gemm_part(dsum2, spec.W_o, nn=True)
+        pj = _Proj(C, dsum2, spec.W_o, True)
         do = torch.empty(M, H, device=dev, dtype=dt)
         if lora:
-            C.ws_epilogue(part, nS, MFt, M, H, 4, do, t=du_o, lw=[Ao], rng=ro, p_drop=spec.p)
+            pj.epi(C, M, H, 4, do, t=du_o, lw=[Ao], rng=ro, p_drop=spec.p)
             C.lora_bwd_a(o.view(M, H), [dAo], du_o, ro, spec.p)
             grads[6], grads[7] = dAo, dBo
         else:
-            C.ws_epilogue(part, nS, MFt, M, H, 0, do)
+            pj.epi(C, M, H, 0, do, nn=True)
         # attention backward straight into the packed gradient, RoPE backward in place
         q5 = qkv.view(Bsz, S, 3, spec.nh, spec.hd)
         dqkv = torch.empty(M, 3 * H, device=dev, dtype=dt)
@@ -269,15 +317,18 @@ class _LlamaLayerFn(torch.autograd.Function):
             dA = [torch.empty_like(Aq), torch.empty_like(Ak), torch.empty_like(Av)]
             dB = [torch.empty_like(Bq), torch.empty_like(Bk), torch.empty_like(Bv)]
             C.lora_bwd_t(dqkv, H, [Bq, Bk, Bv], dB, t_qkv, du_qkv, spec.c)
-        part, nS, MFt = C.ws_gemm_part(dqkv, spec.W_qkv, nn=True)
+        pj = _Proj(C, dqkv, spec.W_qkv, True)
         dh = torch.empty(M, H, device=dev, dtype=dt)
         if lora:
-            C.ws_epilogue(part, nS, MFt, M, H, 4, dh, t=du_qkv, lw=[Aq, Ak, Av], rng=rq, p_drop=spec.p)
+            pj.epi(C, M, H, 4, dh, t=du_qkv, lw=[Aq, Ak, Av], rng=rq, p_drop=spec.p)
             C.lora_bwd_a(h, dA, du_qkv, rq, spec.p)
             grads[0], grads[1], grads[2], grads[3], grads[4], grads[5] = dA[0], dB[0], dA[1], dB[1], dA[2], dB[2]
         else:
-            C.ws_epilogue(part, nS, MFt, M, H, 0, dh)
+            pj.epi(C, M, H, 0, dh, nn=True)
         dsum1 = C.ln_bwd(dh, s, spec.w1, rstd1, rstd1, dsum2, False, False, True)[0]
+        if DEBUG is not None:
+            DEBUG.update(dgu=dgu, dh2=dh2, dsum2=dsum2, do=do, dqkv=dqkv, dh=dh, dsum1=dsum1, h=h, s=s, qkv=qkv, o=o,
+                         s2=s2, gu=gu, dd=dd2, ds2=ds2c, t_qkv=t_qkv, t_o=t_o, du_o=du_o, du_qkv=du_qkv)
         d_in = dsum1.view(Bsz, S, H)
         return (d_in if has_delta else None, d_in, None, None, *grads)
 

@@ -61,6 +61,9 @@ class RunOptions:
     num_workers: int = 2
     causal: bool = False                    # reference LM had no causal mask
     timeout_s: float = 600.0
+    # hipGraph-captured steps on GPU (the fwd + bwd + optimizer of one step replayed as one or two
+    # graph launches; DDP: all-reduces eager between the two graphs).  None = on for CUDA.
+    graph: Optional[bool] = None
     log: Callable[[str], None] = field(default=print)
 
 
@@ -97,7 +100,9 @@ def _amp(precision: str):
 
 
 class _EpochRunner:
-    """Shared hot loop: device-side loss accumulation, fault hook, timing."""
+    """Shared hot loop: device-side loss accumulation, fault hook, timing, and (on GPU) a
+    hipGraph-captured step — the reference trainers' loops then replay one or two graphs per step
+    instead of dispatching ~10^3 kernels from Python (trainers on the fast path)."""
 
     def __init__(self, rank, world, device, model, opt, scaler, amp_dtype, clip, sharded_clip, opts: RunOptions):
         self.rank, self.world, self.device = rank, world, device
@@ -107,21 +112,64 @@ class _EpochRunner:
         self.opts = opts
         self.global_step = 0
         self.save_latest: Optional[Callable[[int, int], None]] = None  # (epoch, batches done in it)
+        want = opts.graph if opts.graph is not None else device.type == "cuda"
+        self.graph = bool(want) and device.type == "cuda" and torch.cuda.is_available()
+        self._captured: Optional[_CapturedStep] = None
+        self.graph_reason = ""  # why a requested graph fell back to eager (logged once)
 
     def after_step(self, epoch: int, done_in_epoch: int) -> None:
         """Periodic latest checkpoint (``RunOptions.ckpt_every``): collective for FSDP, every rank calls."""
         if self.save_latest is not None and self.opts.ckpt_every and self.global_step % self.opts.ckpt_every == 0:
             self.save_latest(epoch, done_in_epoch)
 
-    def step(self, loss_fn) -> torch.Tensor:
+    def _autocast(self):
+        return torch.autocast(self.device.type, dtype=self.amp_dtype or torch.float32,
+                              enabled=self.amp_dtype is not None
+                              and not (self.device.type == "cpu" and self.amp_dtype == torch.float16))
+
+    def _graphable(self) -> bool:
+        from ..parallel.ddp import DistributedDataParallel
+        from ..parallel.fsdp import FullyShardedDataParallel
+
+        why = ""
+        if isinstance(self.model, FullyShardedDataParallel):
+            why = "FSDP step (hook-driven collectives)"
+        elif isinstance(self.model, DistributedDataParallel) and not (self.model.bucketed and
+                                                                      not self.model.broadcast_buffers):
+            why = "DDP with per-forward buffer broadcasts"
+        elif self.world > 1 and not isinstance(self.model, DistributedDataParallel):
+            why = "non-Hyperion data parallel wrapper"
+        elif os.environ.get("HYPERION_FAULT"):
+            why = "fault injection needs host-side per-step control"
+        if why and not self.graph_reason:
+            self.graph_reason = why
+            if self.rank == 0:
+                self.opts.log(f"[graph] eager steps: {why}")
+        return not why
+
+    def step(self, loss_fn, inputs: Optional[tuple] = None):
+        """``loss_fn(*inputs) -> (loss, extra)``; returns ``(loss fp32 detached, extra)``.  With
+        ``inputs`` and a capturable model the step is replayed from a hipGraph."""
+        if self.graph and inputs is not None and self._graphable():
+            if self._captured is None:
+                self._captured = _CapturedStep(self, loss_fn, inputs)
+            self.global_step += 1
+            return self._captured(inputs)
+        inputs = inputs or ()
         self.opt.zero_grad(set_to_none=True)
-        with torch.autocast(self.device.type, dtype=self.amp_dtype or torch.float32, enabled=self.amp_dtype is not None
-                            and not (self.device.type == "cpu" and self.amp_dtype == torch.float16)):
-            loss, extra = loss_fn()
+        with self._autocast():
+            loss, extra = loss_fn(*inputs)
         if maybe_inject(self.rank, self.global_step):
             loss = loss * float("nan")
+        self._backward_update(loss)
+        self.global_step += 1
+        return loss.detach().float(), extra
+
+    def _backward_update(self, loss, allreduce: Optional[Callable[[], None]] = None) -> None:
         if self.scaler is not None and self.scaler.enabled:
             self.scaler.scale(loss).backward()
+            if allreduce is not None:
+                allreduce()
             if self.clip is not None:
                 self.scaler.unscale_(self.opt)
                 self._clip()
@@ -129,17 +177,113 @@ class _EpochRunner:
             self.scaler.update()
         else:
             loss.backward()
+            if allreduce is not None:
+                allreduce()
             if self.clip is not None:
                 self._clip()
             self.opt.step()
-        self.global_step += 1
-        return loss.detach().float(), extra
 
     def _clip(self) -> None:
         if hasattr(self.model, "clip_grad_norm_"):
             self.model.clip_grad_norm_(self.clip)
         else:
             clip_grad_norm_(self.model.parameters(), self.clip, sharded=self.sharded_clip)
+
+
+class _CapturedStep:
+    """One trainer step as hipGraph(s): warm-up on a side stream, then capture.
+
+    Single process: ONE graph (zero, forward, backward, unscale/clip, optimizer, scaler update).
+    Hyperion DDP: graph 1 = forward + backward (gradient hooks only pack buckets,
+    ``defer_allreduce``), the bucket all-reduces run eagerly on the comm stream, graph 2 = clip +
+    optimizer — no RCCL call is recorded into a graph (same split as ``train/step.py``).
+    Inputs are copied into persistent buffers each step; outputs are the captured step's tensors.
+    """
+
+    def __init__(self, runner: "_EpochRunner", loss_fn, inputs: tuple, warmup: int = 3):
+        from ..ops.multi_tensor import flush_pending
+        from ..parallel.ddp import DistributedDataParallel
+
+        self.r = runner
+        self.fn = loss_fn
+        self.static = [t.clone() if isinstance(t, torch.Tensor) else t for t in inputs]
+        m = runner.model
+        self.ddp = m if isinstance(m, DistributedDataParallel) and runner.world > 1 else None
+        if self.ddp is not None:
+            self.ddp.defer_allreduce = True
+        scaled = runner.scaler is not None and runner.scaler.enabled
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            runner.opt.zero_grad(set_to_none=True)
+            for _ in range(warmup):
+                self._full(zero_in_place=True)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        if not scaled:  # let autograd steal fresh gradients inside the capture (no per-param add)
+            runner.opt.zero_grad(set_to_none=True)
+        zero_flag = getattr(runner.opt, "zero_grad_in_step", None)
+        if zero_flag and not scaled:
+            runner.opt.zero_grad_in_step = False
+        self.g1 = torch.cuda.CUDAGraph()
+        self.g2: Optional[torch.cuda.CUDAGraph] = None
+        try:
+            if self.ddp is None:
+                with torch.cuda.graph(self.g1):
+                    self.out = self._full(zero_in_place=scaled)
+            else:
+                with torch.cuda.graph(self.g1):
+                    self.out = self._fwd_bwd(zero_in_place=scaled)
+                self.g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g2, pool=self.g1.pool()):
+                    self._update()
+        finally:
+            flush_pending()
+            if zero_flag is not None:
+                runner.opt.zero_grad_in_step = zero_flag
+        torch.cuda.synchronize()
+
+    def _fwd_bwd(self, zero_in_place: bool):
+        r = self.r
+        if zero_in_place:
+            r.opt.zero_grad(set_to_none=False)
+        with r._autocast():
+            loss, extra = self.fn(*self.static)
+        if r.scaler is not None and r.scaler.enabled:
+            r.scaler.scale(loss).backward()
+        else:
+            loss.backward()
+        return loss.detach().float(), extra
+
+    def _update(self) -> None:
+        r = self.r
+        if r.scaler is not None and r.scaler.enabled:
+            if r.clip is not None:
+                r.scaler.unscale_(r.opt)
+                r._clip()
+            r.scaler.step(r.opt)
+            r.scaler.update()
+        else:
+            if r.clip is not None:
+                r._clip()
+            r.opt.step()
+
+    def _full(self, zero_in_place: bool):
+        out = self._fwd_bwd(zero_in_place)
+        if self.ddp is not None:
+            self.ddp.allreduce_buckets()
+        self._update()
+        return out
+
+    def __call__(self, inputs: tuple):
+        for st, t in zip(self.static, inputs):
+            if isinstance(st, torch.Tensor) and st.data_ptr() != t.data_ptr():
+                st.copy_(t, non_blocking=True)
+        self.g1.replay()
+        if self.g2 is not None:
+            self.ddp.allreduce_buckets()
+            self.g2.replay()
+        return self.out
 
 
 def _sync(device):
@@ -184,15 +328,15 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
                 break
             if res.skip_batch(ep, i):
                 continue  # done before the checkpoint this run resumed from
-            x, y = ids[:, :-1], ids[:, 1:]
             ddp_fwd = model if world > 1 else None
 
-            def lm_loss():
+            def lm_loss(ids):
+                x, y = ids[:, :-1], ids[:, 1:]
                 if ddp_fwd is not None:  # DDP hooks need the wrapper's forward: run through it
                     return ddp_fwd(x, targets=y, ignore_index=GPT2_PAD), None
                 return inner.forward_loss(x, y, ignore_index=GPT2_PAD), None
 
-            loss, _ = runner.step(lm_loss)
+            loss, _ = runner.step(lm_loss, (ids,))
             loss_sum += loss
             n += 1
             runner.after_step(ep, i + 1)
@@ -259,11 +403,11 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
             if device.type == "cuda":
                 img = img.contiguous(memory_format=torch.channels_last)
 
-            def cifar_loss():
+            def cifar_loss(img, lbl):
                 logits = model(img)
                 return F.cross_entropy(logits.float(), lbl), logits.detach()
 
-            loss, logits = runner.step(cifar_loss)
+            loss, logits = runner.step(cifar_loss, (img, lbl))
             stats[0] += loss
             stats[1] += (logits.argmax(1) == lbl).sum()
             stats[2] += lbl.numel()
@@ -332,8 +476,8 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
                 break
             if res.skip_batch(ep, i):
                 continue
-            x, y = ids[:, :-1], ids[:, 1:]
-            loss, _ = runner.step(lambda: (model.forward_loss(x, y, ignore_index=GPT2_PAD), None))
+            loss, _ = runner.step(lambda ids: (model.forward_loss(ids[:, :-1], ids[:, 1:], ignore_index=GPT2_PAD), None),
+                                  (ids,))
             loss_sum += loss
             n += 1
             runner.after_step(ep, i + 1)
@@ -441,10 +585,10 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
             ids = ids % cfg.vocab_size  # GPT-2-tokenized synthetic ids folded into the Llama vocab
             labels = ids.masked_fill(msk == 0, -100) if mask_pad_labels else ids.clone()
 
-            def llama_loss():
+            def llama_loss(ids, msk, labels):
                 return model(ids, attention_mask=msk, labels=labels).loss, None
 
-            loss, _ = runner.step(llama_loss)
+            loss, _ = runner.step(llama_loss, (ids, msk, labels))
             loss_sum += loss
             n += 1
             runner.after_step(ep, i + 1)

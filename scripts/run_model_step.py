@@ -18,6 +18,8 @@ elif which == "llama":
     r = M.bench_llama_lora_step(steps=3, warmup=2, graph=False)
 elif which == "llamagraph":
     r = M.bench_llama_lora_step(steps=5, warmup=3, graph=True)
+elif which == "llamagraph20":
+    r = M.bench_llama_lora_step(steps=20, warmup=3, graph=True)
 elif which == "lmgraph":
     r = M.bench_lm_step(precision="bf16", graph=True, steps=20, warmup=5)
 elif which == "lm":

@@ -56,6 +56,9 @@ for name, N, K in shapes:
     r["ws_nn"] = timed(lambda w: C.ws_linear(dy, w, nn=True), pool)
     r["ws_nt_gemm_only"] = timed(lambda w: C.ws_gemm_part(x, w), pool)
     r["ws_nn_gemm_only"] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True), pool)
+    # M split in two 64-row blocks with twice the slice length: half the slab bytes
+    r["ws_nt_mf4"] = timed(lambda w: C.ws_linear(x, w, mf=4, kr=1024, G=max(1, 256 // (2 * -(-K // 1024)))), pool)
+    r["ws_nn_mf4"] = timed(lambda w: C.ws_linear(dy, w, nn=True, mf=4, kr=1024, G=max(1, 256 // (2 * -(-N // 1024)))), pool)
     if N <= 12288:
         r["r02_linear_nt"] = timed(lambda w: C.linear_nt(x, w), pool)
         r["r02_linear_nn"] = timed(lambda w: C.linear_nn(dy, w), pool)
@@ -64,24 +67,28 @@ for name, N, K in shapes:
     plan_nt = C.ws_plan(M, N, K, False)
     plan_nn = C.ws_plan(M, K, N, True)
     r["plan_nt"], r["plan_nn"] = plan_nt, plan_nn
-    # sweep: slice length / column groups / fragments per chunk
+    # sweep: m-block rows (mf), slice length, column groups, fragments per chunk
     sweep = {}
-    for kr in (256, 384, 512):
-        S = -(-K // kr)
-        for G in sorted({max(1, 256 // S), max(1, 512 // S), max(1, 128 // S)}):
-            for nf in (1, 2, 4):
+    for mf, krs in ((8, (256, 512)), (4, (512, 1024)), (2, (1024, 2048))):
+        MB = -(-M // (16 * mf))
+        for kr in krs:
+            S = -(-K // kr)
+            for G in sorted({max(1, 256 // (S * MB)), max(1, 512 // (S * MB))}):
+                for nf in (1, 2, 4):
+                    k = f"nt_mf{mf}_kr{kr}_G{G}_nf{nf}"
+                    try:
+                        sweep[k] = timed(lambda w: C.ws_gemm_part(x, w, mf=mf, kr=kr, G=G, nf=nf), pool, 2)
+                    except RuntimeError as ex:  # unsupported plan
+                        sweep[k] = str(ex)[:60]
+            S = -(-N // kr)
+            for G in sorted({max(1, 256 // (S * MB)), max(1, 512 // (S * MB))}):
+                k = f"nn_mf{mf}_kr{kr}_G{G}"
                 try:
-                    sweep[f"nt_kr{kr}_G{G}_nf{nf}"] = timed(lambda w: C.ws_gemm_part(x, w, kr=kr, G=G, nf=nf), pool, 2)
-                except RuntimeError as ex:  # unsupported plan
-                    sweep[f"nt_kr{kr}_G{G}_nf{nf}"] = str(ex)[:60]
-        S = -(-N // kr)
-        for G in sorted({max(1, 256 // S), max(1, 512 // S), max(1, 128 // S)}):
-            try:
-                sweep[f"nn_kr{kr}_G{G}"] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True, kr=kr, G=G), pool, 2)
-            except RuntimeError as ex:
-                sweep[f"nn_kr{kr}_G{G}"] = str(ex)[:60]
+                    sweep[k] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True, mf=mf, kr=kr, G=G), pool, 2)
+                except RuntimeError as ex:
+                    sweep[k] = str(ex)[:60]
     r["sweep"] = sweep
-    for k in ("ws_nt", "ws_nn", "ws_nt_gemm_only", "ws_nn_gemm_only", "r02_linear_nt", "r02_linear_nn",
+    for k in ("ws_nt", "ws_nn", "ws_nt_mf4", "ws_nn_mf4", "ws_nt_gemm_only", "ws_nn_gemm_only", "r02_linear_nt", "r02_linear_nn",
               "hipblaslt_nt", "hipblaslt_nn"):
         if k in r:
             r[k + "_TBs"] = wb / r[k] / 1e6
@@ -91,7 +98,7 @@ for name, N, K in shapes:
     print(f"{name:8s} M={M} N={N} K={K} ws_nt {r['ws_nt']:.1f}us ({r['ws_nt_TBs']:.2f} TB/s; gemm "
           f"{r['ws_nt_gemm_only']:.1f}) ws_nn {r['ws_nn']:.1f}us ({r['ws_nn_TBs']:.2f}; gemm {r['ws_nn_gemm_only']:.1f}) "
           f"r02 {r.get('r02_linear_nt', 0):.1f}/{r.get('r02_linear_nn', 0):.1f} hipblaslt {r['hipblaslt_nt']:.1f}/"
-          f"{r['hipblaslt_nn']:.1f} best_nt {best_nt} best_nn {best_nn}", flush=True)
+          f"{r['hipblaslt_nn']:.1f} mf4 {r['ws_nt_mf4']:.1f}/{r['ws_nn_mf4']:.1f} best_nt {best_nt} best_nn {best_nn}", flush=True)
     out.append(r)
     del pool
     torch.cuda.empty_cache()
