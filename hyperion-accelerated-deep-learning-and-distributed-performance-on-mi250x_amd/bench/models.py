@@ -164,14 +164,16 @@ def _ensure_pg() -> None:
                             device_id=torch.device("cuda", torch.cuda.current_device()))
 
 
-def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps: int = 10, warmup: int = 3) -> Dict:
+def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps: int = 10, warmup: int = 3,
+                    graph: bool = False, replicate_frozen="auto", persistent=None) -> Dict:
     """One FSDP FULL_SHARD training step exactly as the FSDP trainers run it (C25 / BASELINE config
     4 / C26): Hyperion's FSDP over the native RCCL communicator, bf16 mixed precision (param /
     reduce / buffer), FusedAdamW, global-norm clip 1.0.  ``model``: ``lm256`` (size-based wrap,
     100k params), ``gpt2_small`` (one unit per transformer layer), ``llama7b_lora`` (LoRA r16,
     one unit per decoder layer, frozen base weights sharded too).  World size = the launcher's
     (1 on a single GPU: the gathers / reduce-scatters are then identity collectives, but every
-    flat-buffer pack, cast and hook runs)."""
+    flat-buffer pack, cast and hook runs).  ``graph=True``: the step is captured once as graph
+    segments with the collectives as eager holes (``train/segments.py``; persistent FSDP buffers)."""
     import torch.distributed as dist
 
     from ..data.synthetic import SyntheticWikiText2
@@ -200,7 +202,9 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
         policy = (size_based_auto_wrap_policy(100_000) if model == "lm256"
                   else transformer_auto_wrap_policy({TransformerEncoderLayer}))
         vocab = 50257
-    m = FSDP(base, auto_wrap_policy=policy, device_id=dev, mixed_precision=MixedPrecision(bf, bf, bf))
+    m = FSDP(base, auto_wrap_policy=policy, device_id=dev, mixed_precision=MixedPrecision(bf, bf, bf),
+             replicate_frozen=replicate_frozen if model == "llama7b_lora" else False,
+             persistent=True if graph else persistent)
     params = [p for p in m.parameters() if p.requires_grad]
     opt = FusedAdam(params, lr=1e-4, weight_decay=0.01, adamw=True)
     ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=dist.get_rank())
@@ -218,10 +222,18 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
         opt.step()
         return loss.detach()
 
+    seg = None
+    if graph:
+        from ..train.segments import SegmentedStep
+
+        seg = SegmentedStep(step, warmup=2, module=m)
     torch.cuda.reset_peak_memory_stats()
-    t = _timeit(step, steps, warmup)
+    t = _timeit(seg if seg is not None else step, steps, warmup)
     world = dist.get_world_size()
     tok = batch * (seq if model == "llama7b_lora" else seq - 1)
-    return {"model": model, "fsdp": True, "world": world, "batch_per_gpu": batch, "seq": seq, "ms_per_step": t * 1e3,
+    return {"model": model, "fsdp": True, "world": world, "graph": graph, "persistent": m.persistent,
+            "replicate_frozen": m.replicate_frozen,
+            "segments": seg.seg.num_segments if seg is not None and seg.seg is not None else 0,
+            "batch_per_gpu": batch, "seq": seq, "ms_per_step": t * 1e3,
             "samples_per_s": world * batch / t, "tokens_per_s": world * tok / t,
             "trainable_params": sum(p.numel() for p in params), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}

@@ -188,7 +188,19 @@ def FusedAdamW(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2)
 
 # clip tables per model: keyed (weakly) by the first parameter, so two same-shaped models never
 # share -- and, once captured, never re-point -- each other's pointer table
-_clip_tables: "weakref.WeakKeyDictionary[torch.Tensor, TableCache]" = weakref.WeakKeyDictionary()
+# (a WeakKeyDictionary cannot hold tensors: its weakref keys compare their referents with the
+# elementwise Tensor.__eq__ on a hash-bucket collision)
+_clip_tables: "dict[int, tuple]" = {}
+
+
+def _clip_cache(p0: torch.Tensor) -> TableCache:
+    ent = _clip_tables.get(id(p0))
+    if ent is None or ent[0]() is not p0:
+        key = id(p0)
+        ref = weakref.ref(p0, lambda _r, k=key: _clip_tables.pop(k, None))
+        ent = (ref, TableCache())
+        _clip_tables[key] = ent
+    return ent[1]
 
 
 @torch.no_grad()
@@ -212,10 +224,7 @@ def clip_grad_norm_(
     native = _native.use_native(grads[0], op="clip") and all(_dense(g) and g.dtype == grads[0].dtype for g in grads)
     if native:
         try:
-            cache = _clip_tables.get(params[0])
-            if cache is None:
-                cache = _clip_tables[params[0]] = TableCache()
-            tab = cache.get("clip", [grads])
+            tab = _clip_cache(params[0]).get("clip", [grads])
         except ValueError:
             native = False
     if native:
@@ -226,7 +235,9 @@ def clip_grad_norm_(
         for g in grads:
             total_sq += g.float().pow(2).sum()
     if sharded and dist.is_available() and dist.is_initialized():
-        dist.all_reduce(total_sq, group=group)
+        from ..train import segments as _seg
+
+        _seg.eager(lambda: dist.all_reduce(total_sq, group=group))  # a hole of a segmented capture
     if native:
         _native.native().clip_mt(tab.ptrs, tab.sizes, tab.blocks, tab.chunk, total_sq, float(max_norm), code)
     else:

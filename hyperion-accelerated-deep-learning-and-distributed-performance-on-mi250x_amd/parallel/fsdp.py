@@ -48,6 +48,7 @@ import torch.nn as nn
 
 from ..ops import streams as _streams
 from ..ops.optim import clip_grad_norm_
+from ..train import segments as _seg
 from .comm import get_comm
 
 
@@ -105,6 +106,27 @@ def _select_units(root: nn.Module, policy: Optional[Callable]) -> List[nn.Module
 
 
 # ------------------------------------------------------------------------------------ unit
+class _SlotWork:
+    """A collective issued through ``segments.eager``: under a segmented capture the issue is an
+    eager action that refills ``slot`` on every replay, and ``wait()`` is its own action reading
+    the replay's current handle (so the collective overlaps the segments in between)."""
+
+    __slots__ = ("slot",)
+
+    def __init__(self, fn):
+        slot = [None]
+
+        def issue():
+            slot[0] = fn()
+
+        _seg.eager(issue)
+        self.slot = slot
+
+    def wait(self):
+        slot = self.slot
+        _seg.eager(lambda: slot[0].wait())
+
+
 class _FlatGroup:
     """One flat parameter: the trainable (fp32 master shard) or frozen (param-dtype shard) params of a unit."""
 
@@ -160,14 +182,17 @@ class _FlatGroup:
         # module parameters become views of the full buffer (the same Parameter objects)
         for p, o, n, shp in zip(params, self.offsets, self.numels, self.shapes):
             p.data = self.full[o : o + n].view(shp)
-        if not self.resident:
+        if not (self.resident or fsdp.persistent):
             self.free_full()
         if trainable:
-            self.full_grad.untyped_storage().resize_(0)
+            if fsdp.persistent:
+                self.full_grad.zero_()
+            else:
+                self.full_grad.untyped_storage().resize_(0)
 
     # -- storage ------------------------------------------------------------------------
     def free_full(self) -> None:
-        if self.resident:
+        if self.resident or self.fsdp.persistent:  # persistent: the storage stays, the content stays valid
             return
         if self.gather_work is not None:
             self.wait_gather()
@@ -194,7 +219,8 @@ class _FlatGroup:
             out.copy_(send)
             self.gathered = True
             return
-        self.gather_work = self.fsdp.comm.all_gather(out, send)
+        comm = self.fsdp.comm
+        self.gather_work = _SlotWork(lambda: comm.all_gather(out, send))
         if not async_op:
             self.wait_gather()
 
@@ -247,7 +273,8 @@ class _FlatGroup:
             self.rs_out = self._grad_shard
         else:
             self.rs_out = self._rs_buf if self._rs_buf is not None else torch.empty_like(self._grad_shard)
-        self.rs_work = self.fsdp.comm.reduce_scatter(self.rs_out, buf, "avg")
+        comm, rs_out = self.fsdp.comm, self.rs_out
+        self.rs_work = _SlotWork(lambda: comm.reduce_scatter(rs_out, buf, "avg"))
 
     def finish_reduce(self) -> None:
         if not self.reduced:
@@ -266,7 +293,8 @@ class _FlatGroup:
             else:
                 self.flat_param.grad.add_(g)
         self.rs_out = None
-        self.full_grad.untyped_storage().resize_(0)
+        if not self.fsdp.persistent:
+            self.full_grad.untyped_storage().resize_(0)
 
 
 class _Unit:
@@ -347,6 +375,7 @@ class FullyShardedDataParallel(nn.Module):
         sync_module_states: bool = True,
         comm=None,
         replicate_frozen=False,
+        persistent=None,
     ):
         super().__init__()
         if sharding_strategy not in ("FULL_SHARD", "SHARD_GRAD_OP"):
@@ -372,8 +401,22 @@ class FullyShardedDataParallel(nn.Module):
             cap = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
             replicate_frozen = self.world > 1 and cap > 0 and frozen_bytes <= cap // 4
         self.replicate_frozen = bool(replicate_frozen)
+        # persistent: every unit's gathered parameters and gradient buffer stay allocated (no
+        # storage release / re-allocation per step) and the parameters gathered for the forward are
+        # reused by the backward (one all-gather per unit per step instead of two).  That is the
+        # memory-for-traffic trade 288 GB of HBM affords for the models here, and it makes the step
+        # capturable (train/segments.py).  "auto"/None: on GPU when every unit's full parameters +
+        # gradients take at most a quarter of the device memory.
+        if persistent is None or persistent == "auto":
+            if self.device.type == "cuda":
+                need = sum(p.numel() for p in module.parameters()) * (
+                    torch.finfo(self.mp.param_dtype or torch.float32).bits // 8 + 4)
+                persistent = need <= torch.cuda.get_device_properties(self.device).total_memory // 4
+            else:
+                persistent = False
+        self.persistent = bool(persistent)
         self.sharding = sharding_strategy
-        self.reshard_after_forward = sharding_strategy == "FULL_SHARD"
+        self.reshard_after_forward = sharding_strategy == "FULL_SHARD" and not self.persistent
         self.forward_prefetch = forward_prefetch
         self.backward_prefetch = backward_prefetch
         if sync_module_states and self.world > 1:
@@ -500,12 +543,16 @@ class FullyShardedDataParallel(nn.Module):
             u.finish()
             for g in u.groups:
                 g.send_valid = False  # the optimizer steps next: recast on the next forward gather
+                if self.persistent and not g.resident:
+                    g.gathered = False  # ... and re-gather (the persistent buffer keeps its storage)
         self._in_backward = False
 
     def invalidate_gather_cache(self) -> None:
         """Call after changing the flat shards outside an optimizer step that follows backward."""
         for g in self.flat_groups():
             g.send_valid = False
+            if self.persistent and not g.resident:
+                g.gathered = False
 
     # -- forward ----------------------------------------------------------------------------
     def _root_pre(self) -> None:

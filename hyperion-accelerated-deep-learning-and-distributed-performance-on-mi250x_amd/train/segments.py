@@ -1,0 +1,137 @@
+"""Segmented hipGraph capture: a training step recorded as graphs with eager "holes".
+
+Reference context: the reference's FSDP trainers run every step eagerly under torch FSDP, one
+Python hook per unit per phase (``02_development/distributed_utils.py:318-354, 477-524``; SURVEY
+C25/C26, §2.2 FSDP).  A Hyperion FSDP step cannot be ONE graph: its all-gathers and
+reduce-scatters are eager RCCL (or gloo) calls issued from autograd hooks, and recording RCCL into a
+graph is not what the multi-rank tests can exercise.  Instead the step is captured ONCE as a list of
+segments: every time the step is about to issue (or wait for) a collective, the current capture
+ends, the collective runs for real and is appended to the schedule as an eager action, and a new
+capture begins.  Replaying the step = replay segment 0, run action 0, replay segment 1, ... — the
+~10^3 kernels of the step cost a few dozen graph launches, and every collective still overlaps
+the compute segments between its issue and its wait (issue and wait are separate actions).
+
+All segments share one memory pool, so a tensor produced in segment i and consumed in segment j
+keeps its address on every replay; the actions must only touch persistent buffers (FSDP's
+``persistent`` mode keeps the full-parameter and gradient buffers allocated for exactly this).
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional
+
+import torch
+
+_ACTIVE: Optional["SegmentedGraph"] = None
+
+
+def active() -> Optional["SegmentedGraph"]:
+    """The capture in progress, if any (collective call sites route through :func:`eager`)."""
+    return _ACTIVE
+
+
+def eager(fn: Callable[[], object]):
+    """Run ``fn`` now; under a segmented capture, as an eager action between two segments."""
+    seg = _ACTIVE
+    if seg is None:
+        return fn()
+    return seg.hole(fn)
+
+
+class SegmentedGraph:
+    """Capture ``body()`` as graph segments split at :func:`eager` calls; ``replay()`` re-runs it."""
+
+    def __init__(self):
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.actions: List[Callable[[], object]] = []  # actions[i] runs after graphs[i]
+        self.stream: Optional[torch.cuda.Stream] = None
+        self._pool = None
+        self.out = None
+
+    # -- capture ----------------------------------------------------------------------------
+    def _begin(self) -> None:
+        g = torch.cuda.CUDAGraph()
+        if self._pool is None:
+            g.capture_begin()
+            self._pool = g.pool()
+        else:
+            g.capture_begin(pool=self._pool)
+        self.graphs.append(g)
+
+    def _end(self) -> None:
+        self.graphs[-1].capture_end()
+
+    def hole(self, fn: Callable[[], object]):
+        """End the current segment, run ``fn`` eagerly (recorded), start the next segment."""
+        self._end()
+        res = fn()
+        self.actions.append(fn)
+        self._begin()
+        return res
+
+    def capture(self, body: Callable[[], object]):
+        global _ACTIVE
+        assert _ACTIVE is None, "nested segmented capture"
+        self.stream = torch.cuda.Stream()
+        self.stream.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        with torch.cuda.stream(self.stream):
+            _ACTIVE = self
+            try:
+                self._begin()
+                self.out = body()
+                self._end()
+            finally:
+                _ACTIVE = None
+        torch.cuda.current_stream().wait_stream(self.stream)
+        torch.cuda.synchronize()
+        return self.out
+
+    # -- replay -----------------------------------------------------------------------------
+    def replay(self):
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i, g in enumerate(self.graphs):
+                g.replay()
+                if i < len(self.actions):
+                    self.actions[i]()
+        torch.cuda.current_stream().wait_stream(s)
+        return self.out
+
+    @property
+    def num_segments(self) -> int:
+        return len(self.graphs)
+
+
+class SegmentedStep:
+    """``step()`` = ``fn()`` captured as segments after ``warmup`` eager calls (GraphedClosure's
+    contract: ``fn`` zeroes grads in place or lets the captured backward steal fresh ones, reads
+    persistent inputs, returns a tensor)."""
+
+    def __init__(self, fn: Callable[[], torch.Tensor], warmup: int = 3, module: Optional[torch.nn.Module] = None):
+        self.fn = fn
+        self.warmup = warmup
+        self.module = module
+        self.seg: Optional[SegmentedGraph] = None
+
+    def __call__(self) -> torch.Tensor:
+        if self.seg is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(self.warmup):
+                    self.fn()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            from ..ops.multi_tensor import flush_pending
+
+            if self.module is not None:
+                for p in self.module.parameters():
+                    p.grad = None
+            seg = SegmentedGraph()
+            try:
+                seg.capture(self.fn)
+            finally:
+                flush_pending()
+            self.seg = seg
+        return self.seg.replay()

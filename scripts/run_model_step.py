@@ -8,7 +8,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hyperion.bench import models as M  # noqa: E402
 
 which = sys.argv[1]
-if which == "vit":
+if which == "fsdp":  # fsdp <lm256|gpt2_small|llama7b_lora> [graph] [shardbase]
+    model = sys.argv[2]
+    kw = dict(graph="graph" in sys.argv[3:])
+    if "shardbase" in sys.argv[3:]:
+        kw["replicate_frozen"] = False
+    if model == "gpt2_small":
+        kw["batch"] = 16
+    if model == "llama7b_lora":
+        kw["batch"] = 1
+    r = M.bench_fsdp_step(model, steps=10, warmup=3, **kw)
+elif which == "vit":
     r = M.bench_vit_step(checkpointing=False, steps=5, warmup=3)
 elif which == "vitgraph":
     r = M.bench_vit_step(checkpointing=False, steps=20, warmup=5, graph=True)
