@@ -51,11 +51,10 @@ class SegmentedGraph:
     def _begin(self) -> None:
         g = torch.cuda.CUDAGraph()
         if self._pool is None:
-            g.capture_begin()
-            self._pool = g.pool()
-        else:
-            g.capture_begin(pool=self._pool)
+            # a fresh handle up front: CUDAGraph.pool() is only valid after a finished capture
+            self._pool = torch.cuda.graph_pool_handle()
         self.graphs.append(g)
+        g.capture_begin(pool=self._pool)
 
     def _end(self) -> None:
         self.graphs[-1].capture_end()
@@ -80,6 +79,16 @@ class SegmentedGraph:
                 self._begin()
                 self.out = body()
                 self._end()
+            except BaseException:
+                # close a capture the body left open, so the failure surfaces as this exception and
+                # not as a terminate() from the graph's destructor
+                if torch.cuda.is_current_stream_capturing():
+                    try:
+                        self.graphs[-1].capture_end()
+                    except Exception:
+                        pass
+                self.graphs.clear()
+                raise
             finally:
                 _ACTIVE = None
         torch.cuda.current_stream().wait_stream(self.stream)
