@@ -6,6 +6,7 @@ samples/s, tokens/s, ms/step and peak memory.  Used by ``cli/bench_models`` and 
 """
 from __future__ import annotations
 
+import math
 import time
 from typing import Dict
 
@@ -229,6 +230,9 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
         seg = SegmentedStep(step, warmup=2, module=m)
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(seg if seg is not None else step, steps, warmup)
+    final_loss = float((seg if seg is not None else step)())  # one more step: the timed schedule trains
+    if not math.isfinite(final_loss):
+        raise RuntimeError(f"bench_fsdp_step({model}, graph={graph}): non-finite loss {final_loss}")
     world = dist.get_world_size()
     tok = batch * (seq if model == "llama7b_lora" else seq - 1)
     return {"model": model, "fsdp": True, "world": world, "graph": graph, "persistent": m.persistent,
@@ -236,4 +240,5 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
             "segments": seg.seg.num_segments if seg is not None and seg.seg is not None else 0,
             "batch_per_gpu": batch, "seq": seq, "ms_per_step": t * 1e3,
             "samples_per_s": world * batch / t, "tokens_per_s": world * tok / t,
-            "trainable_params": sum(p.numel() for p in params), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
+            "trainable_params": sum(p.numel() for p in params), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20,
+            "final_loss": final_loss}

@@ -43,28 +43,39 @@ inline int dtype_code(const at::Tensor& t) {
 // capture would otherwise take the buffer from the graph's pool with the zero-fill merely
 // recorded, so eager GEMMs before the first replay would read garbage.  The calls run
 // in relaxed capture mode, so they are legal (and not captured) while another stream captures.
-inline const void* device_zero_page(const at::Device& dev) {
-  static void* z[64] = {nullptr};
+// kind 0: the 4 KiB zero page; kind 1: 64 KiB of int32 work counters (see device_counters)
+inline void* device_zeroed_block(const at::Device& dev, int kind) {
+  static void* z[2][64] = {{nullptr}};
   static std::mutex mu;
   const int i = dev.index() < 0 ? 0 : dev.index();
-  TORCH_CHECK(i < 64, "device_zero_page: device index out of range");
+  TORCH_CHECK(i < 64 && kind >= 0 && kind < 2, "device_zeroed_block: bad device index / kind");
+  const size_t bytes = kind == 0 ? 4096 : 65536;
   std::lock_guard<std::mutex> g(mu);
-  if (z[i] == nullptr) {
+  if (z[kind][i] == nullptr) {
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     HYP_CHECK_HIP(hipThreadExchangeStreamCaptureMode(&mode));
     void* p = nullptr;
     hipStream_t s = nullptr;
-    hipError_t e = hipMalloc(&p, 4096);
+    hipError_t e = hipMalloc(&p, bytes);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMemsetAsync(p, 0, 4096, s);
+    if (e == hipSuccess) e = hipMemsetAsync(p, 0, bytes, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (s) (void)hipStreamDestroy(s);
     HYP_CHECK_HIP(hipThreadExchangeStreamCaptureMode(&mode));  // restore the caller's mode
     HYP_CHECK_HIP(e);
-    z[i] = p;
+    z[kind][i] = p;
   }
-  return z[i];
+  return z[kind][i];
 }
+
+inline const void* device_zero_page(const at::Device& dev) { return device_zeroed_block(dev, 0); }
+
+// 16K int32 counters per device for last-arriver reductions (a kernel's workgroups count in on a
+// slot; the last one reduces and RESETS the slot to zero, so every launch — eager or a graph
+// replay — finds its slots zeroed).  Slot ranges are fixed per op (kCounterSlot*); users must be
+// stream-ordered: two kernels sharing slots must never run concurrently.
+constexpr int kCounterSlotLoraDown = 0;  // [0, 4096)
+inline int* device_counters(const at::Device& dev) { return static_cast<int*>(device_zeroed_block(dev, 1)); }
 
 #define HYP_CHECK_CUDA_TENSOR(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 

@@ -195,7 +195,7 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
 }
 
 void lora_down_py(const at::Tensor& x, const std::vector<at::Tensor>& A, at::Tensor& t,
-                  const c10::optional<at::Tensor>& rng, double p_drop) {
+                  const c10::optional<at::Tensor>& rng, double p_drop, const c10::optional<at::Tensor>& zero) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "lora_down: x [M, K] row-major");
   auto lp = ptr_list(A, x.scalar_type(), "lora_down A");
@@ -208,8 +208,22 @@ void lora_down_py(const at::Tensor& x, const std::vector<at::Tensor>& A, at::Ten
   const bool has_rng = rng.has_value() && rng->defined() && p_drop > 0;
   if (has_rng) rs = unpack_rng(*rng);
   const at::DeviceGuard guard(x.device());
+  float* zp = nullptr;
+  int nz = 0;
+  if (zero.has_value() && zero->defined()) {
+    TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous() && zero->device() == x.device(),
+                "lora_down: zero must be a contiguous fp32 tensor on x's device");
+    zp = zero->data_ptr<float>();
+    nz = (int)zero->numel();
+  }
+  // k-split: ~256 workgroups over the (projection, 16-row tile) grid, >= 512 reduction elements each
+  const int M = (int)x.size(0), K = (int)x.size(1), tiles = P * ((M + 15) / 16);
+  int ks = 1;
+  while (ks < 16 && tiles * ks * 2 <= 256 && K % (128 * ks * 2) == 0 && K / (ks * 2) >= 512) ks *= 2;
+  auto part = at::empty({(int64_t)tiles * ks * 256}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::lora_down(dtype_code(x), x.data_ptr(), x.stride(0), lp.data(), P, r, t.data_ptr<float>(),
-                               (int)t.stride(0), (int)x.size(0), (int)x.size(1), has_rng ? &rs : nullptr, (float)p_drop,
+                               (int)t.stride(0), M, K, has_rng ? &rs : nullptr, (float)p_drop, zp, nz,
+                               part.data_ptr<float>(), device_counters(x.device()) + kCounterSlotLoraDown, ks,
                                cur_stream()));
 }
 
@@ -270,8 +284,8 @@ void register_ws_ops(pybind11::module& m) {
         "aux"_a = pybind11::none(), "t"_a = pybind11::none(), "lw"_a = std::vector<at::Tensor>{}, "segw"_a = 0,
         "lscale"_a = 1.0, "rope_segs"_a = 0, "seq"_a = 0, "theta"_a = 10000.0, "rng"_a = pybind11::none(),
         "p_drop"_a = 0.0, "nn"_a = pybind11::none(), "yin"_a = pybind11::none());
-  m.def("lora_down", &lora_down_py, "t[m, p r + j] += Σ_k keep_p x A_p (fp32 atomics)", "x"_a, "A"_a, "t"_a,
-        "rng"_a = pybind11::none(), "p_drop"_a = 0.0);
+  m.def("lora_down", &lora_down_py, "t[m, p r + j] = Σ_k keep_p x A_p (written); zeroes `zero` in the same launch",
+        "x"_a, "A"_a, "t"_a, "rng"_a = pybind11::none(), "p_drop"_a = 0.0, "zero"_a = pybind11::none());
   m.def("lora_bwd_t", &lora_bwd_t_py, "du' += c dy_p B_p (atomics); dB_p = c dy_pᵀ t_p", "dy"_a, "N"_a, "B"_a, "dB"_a,
         "t"_a, "du"_a, "c"_a);
   m.def("lora_bwd_a", &lora_bwd_a_py, "dA_p = du'_pᵀ (keep_p ∘ x)", "x"_a, "dA"_a, "du"_a, "rng"_a = pybind11::none(),

@@ -316,9 +316,13 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
 namespace hyp {
 // ---- lora_fused.hip --------------------------------------------------------------------------
 // rank-r halves of the fused LoRA projections (P projections sharing one input; see the file).
-// t / du: fp32 [M, P r] accumulated atomically (zero them first).
+// t: fp32 [M, P r] written (k-split over `ksplit` workgroups per tile: fp32 partials in `part`
+// [P * ceil(M/16) * ksplit * 256], last-arriver sum on `counters` slots [0, P * ceil(M/16)); lora_down
+// also zeroes zero[0, nzero): the du buffer); du: accumulated
+// atomically by lora_bwd_t (zero it first).  K % 256 == 0 (lora_down), N % 256 == 0 (lora_bwd_t).
 hipError_t lora_down(int dtype, const void* x, int64_t ldx, const void* const* A, int P, int r, float* t, int ldt, int M,
-                     int K, const RngState* rng, float p_drop, hipStream_t st);
+                     int K, const RngState* rng, float p_drop, float* zero, int nzero, float* part, int* counters,
+                     int ksplit, hipStream_t st);
 hipError_t lora_bwd_t(int dtype, const void* dy, int64_t ldy, int N, const void* const* B, void* const* dB, int P,
                       int r, const float* t, int ldt, float* du, int M, float c, hipStream_t st);
 hipError_t lora_bwd_a(int dtype, const void* x, int64_t ldx, int K, void* const* dA, int P, int r, const float* du,

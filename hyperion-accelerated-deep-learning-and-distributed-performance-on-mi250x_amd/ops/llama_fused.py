@@ -232,12 +232,18 @@ class _LlamaLayerFn(torch.autograd.Function):
             h, s, _, rstd1 = C.ln_fwd(delta.reshape(M, H).contiguous(), xs, spec.w1, None, spec.eps, True)
         lora = spec.lora
         rq = ro = None
-        t_qkv = t_o = None
+        t_qkv = t_o = du_bufs = t_all = None
         if lora:
             if spec.p > 0:
                 rq, ro = _native.rng_state(dev), _native.rng_state(dev)
-            t_qkv = torch.zeros(M, 3 * spec.r, device=dev, dtype=torch.float32)
-            C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p)
+            # t written by lora_down; the backward's du buffers (accumulated atomically by
+            # lora_bwd_t) are zeroed by the same launch — no fill kernels
+            # (t and du share one [M, 4 r] row layout: q/k/v columns then o — lora_bwd_t wants t
+            # and du at one row stride)
+            t_all = torch.empty(M, 4 * spec.r, device=dev, dtype=torch.float32)
+            t_qkv = t_all[:, :3 * spec.r]
+            du_bufs = torch.empty(M, 4 * spec.r, device=dev, dtype=torch.float32)
+            C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p, du_bufs)
         pj = _Proj(C, h, spec.W_qkv)
         qkv = torch.empty(M, 3 * H, device=dev, dtype=dt)
         pj.epi(C, M, 3 * H, 1, qkv, t=t_qkv, lw=[Bq, Bk, Bv] if lora else [], segw=H,
@@ -248,7 +254,7 @@ class _LlamaLayerFn(torch.autograd.Function):
         o, lse = C.attn_fwd(q, k, v, True, scale, 0.0, None, kpm, True)
         o2 = o.view(M, H)
         if lora:
-            t_o = torch.zeros(M, spec.r, device=dev, dtype=torch.float32)
+            t_o = t_all[:, 3 * spec.r:]
             C.lora_down(o2, [Ao], t_o, ro, spec.p)
         pj = _Proj(C, o2, spec.W_o)
         a = torch.empty(M, H, device=dev, dtype=dt)
@@ -263,7 +269,8 @@ class _LlamaLayerFn(torch.autograd.Function):
         pj.epi(C, M, H, 0, d)
         ctx.spec = spec
         ctx.cfg = (Bsz, S, delta is not None, scale, rq, ro)
-        ctx.save_for_backward(h, s, rstd1, qkv, o, lse, s2, rstd2, gu, kpm, t_qkv, t_o, Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo)
+        ctx.save_for_backward(h, s, rstd1, qkv, o, lse, s2, rstd2, gu, kpm, t_qkv, t_o, du_bufs if lora else None, Aq, Bq,
+                              Ak, Bk, Av, Bv, Ao, Bo)
         return d.view(Bsz, S, H), s2.view(Bsz, S, H)
 
     @staticmethod
@@ -271,7 +278,8 @@ class _LlamaLayerFn(torch.autograd.Function):
         C = _native.native()
         spec: _Spec = ctx.spec
         Bsz, S, has_delta, scale, rq, ro = ctx.cfg
-        (h, s, rstd1, qkv, o, lse, s2, rstd2, gu, kpm, t_qkv, t_o, Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo) = ctx.saved_tensors
+        (h, s, rstd1, qkv, o, lse, s2, rstd2, gu, kpm, t_qkv, t_o, du_bufs, Aq, Bq, Ak, Bk, Av, Bv, Ao,
+         Bo) = ctx.saved_tensors
         H, I = spec.H, spec.I
         M = Bsz * S
         dt, dev = h.dtype, h.device
@@ -291,7 +299,7 @@ class _LlamaLayerFn(torch.autograd.Function):
         grads = [None] * 8
         du_o = None
         if lora:
-            du_o = torch.zeros(M, spec.r, device=dev, dtype=torch.float32)
+            du_o = du_bufs[:, 3 * spec.r:]  # zeroed by the forward's lora_down (row stride 4 r)
             dAo, dBo = torch.empty_like(Ao), torch.empty_like(Bo)
             C.lora_bwd_t(dsum2, H, [Bo], [dBo], t_o, du_o, spec.c)
         pj = _Proj(C, dsum2, spec.W_o, True)
@@ -313,7 +321,7 @@ class _LlamaLayerFn(torch.autograd.Function):
         # q/k/v: dh = dqkv [W_q; W_k; W_v] + Σ_p keep_p ∘ (du'_p A_p)
         du_qkv = None
         if lora:
-            du_qkv = torch.zeros(M, 3 * spec.r, device=dev, dtype=torch.float32)
+            du_qkv = du_bufs[:, :3 * spec.r]
             dA = [torch.empty_like(Aq), torch.empty_like(Ak), torch.empty_like(Av)]
             dB = [torch.empty_like(Bq), torch.empty_like(Bk), torch.empty_like(Bv)]
             C.lora_bwd_t(dqkv, H, [Bq, Bk, Bv], dB, t_qkv, du_qkv, spec.c)

@@ -143,7 +143,8 @@ class _FlatGroup:
         self.numel = sum(self.numels)
         # resident: a frozen group kept whole on every rank (FSDP(replicate_frozen=...)): never
         # gathered, never freed — the base weights of a LoRA fine-tune fit 288 GB of HBM many times
-        self.resident = (not trainable) and fsdp.replicate_frozen
+        # (at world 1 every frozen group is resident: its one shard IS the full tensor — no copy)
+        self.resident = (not trainable) and (fsdp.replicate_frozen or fsdp.world == 1)
         W, r = (1, 0) if self.resident else (fsdp.world, fsdp.rank)
         # shards of a multiple of 64 elements: every rank's slice of the gathered buffer (and every
         # reduce-scatter output) starts 128-byte aligned for RCCL and the vector kernels
@@ -184,6 +185,8 @@ class _FlatGroup:
             p.data = self.full[o : o + n].view(shp)
         if not (self.resident or fsdp.persistent):
             self.free_full()
+        elif not self.resident:
+            self.gathered = False  # persistent: the full buffer is allocated but not filled yet
         if trainable:
             if fsdp.persistent:
                 self.full_grad.zero_()
@@ -542,6 +545,8 @@ class FullyShardedDataParallel(nn.Module):
         for u in self.units:
             u.finish()
             for g in u.groups:
+                if not g.trainable:
+                    continue  # frozen weights never change: a persistent gathered copy stays valid
                 g.send_valid = False  # the optimizer steps next: recast on the next forward gather
                 if self.persistent and not g.resident:
                     g.gathered = False  # ... and re-gather (the persistent buffer keeps its storage)

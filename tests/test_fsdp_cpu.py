@@ -36,7 +36,7 @@ def _reference_train(steps, lr=1e-2, clip=None):
     return {k: v.detach().clone() for k, v in m.state_dict().items()}
 
 
-def _fsdp_train(rank, world, steps, policy_kind, clip, strategy):
+def _fsdp_train(rank, world, steps, policy_kind, clip, strategy, persistent=None):
     from hyperion.models.transformer import TransformerEncoderLayer
     from hyperion.parallel.fsdp import FSDP, size_based_auto_wrap_policy, transformer_auto_wrap_policy
 
@@ -45,7 +45,12 @@ def _fsdp_train(rank, world, steps, policy_kind, clip, strategy):
               # every Linear its own unit (the reference's min_num_params=100_000 at full size):
               # the FFN / attention projections must be CALLED as modules for the gather hooks
               "leaf": size_based_auto_wrap_policy(500), "none": None}[policy_kind]
-    m = FSDP(_make_model(), auto_wrap_policy=policy, device_id=torch.device("cpu"), sharding_strategy=strategy)
+    m = FSDP(_make_model(), auto_wrap_policy=policy, device_id=torch.device("cpu"), sharding_strategy=strategy,
+             persistent=persistent)
+    if persistent:
+        for g in m.flat_groups():  # an allocated-but-unfilled full buffer must never be read as gathered
+            if not g.resident:
+                g.full.fill_(float("nan"))
     opt = torch.optim.SGD(m.parameters(), lr=1e-1, momentum=0.9, weight_decay=0.01)
     per = 8 // world
     for s in range(steps):
@@ -73,6 +78,16 @@ def test_fsdp_matches_single_process(policy, strategy):
         torch.testing.assert_close(sd[k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
     if policy == "layer":
         assert len(res[0]["units"]) == 3  # 2 encoder layers + root (embed, fc)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_persistent_matches_single_process(world):
+    """persistent mode (full params / grad buffers kept allocated, one gather per unit per step): the
+    first forward gathers into the fresh buffer (poisoned with NaN here) like every later one."""
+    ref = _reference_train(3)
+    res = run_world(_fsdp_train, world, (3, "layer", None, "FULL_SHARD", True))
+    for k in ref:
+        torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
 
 
 def test_fsdp_global_grad_clip_matches_single_process():
