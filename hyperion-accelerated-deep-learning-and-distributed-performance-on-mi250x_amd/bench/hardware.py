@@ -11,8 +11,11 @@ Reference (``Phase 1/01_hardware_exploration.ipynb``):
 Hyperion runs each in two methodologies so the comparison is honest both ways:
 ``method='reference'`` reproduces the single-shot, allocation-inside-the-timer measurement;
 ``method='proper'`` warms up, times with hipEvents and reports the median of ``repeat`` runs.
-Kernels: ``hyperion`` = the hand-written gfx950 MFMA GEMM (``gemm_mfma.hip``) / STREAM kernels
-(``stream_bw.hip``); ``torch`` = hipBLASLt/rocBLAS and PyTorch's elementwise add, for A/B.
+Kernels: ``hyperion`` = the hand-written gfx950 GEMMs — bf16/fp16 on the deep-pipelined tiled MFMA
+GEMM (``gemm_tiles.hip``; the proper method reports the best of its tile shapes, the reference
+method the static plan), fp32 on the fp32-input MFMA GEMM (``gemm_f32.hip``: exact fp32 products,
+no TF32-like shortcut exists on gfx950) — and the STREAM kernels (``stream_bw.hip``); ``torch`` =
+hipBLASLt/rocBLAS and PyTorch's elementwise add, for A/B.
 Results use the reference CSV schemas (``precision_results.csv``: ``Size,Precision,Time (s),TFLOPS``;
 ``bandwidth_results.csv``: ``Size (M elements),Bandwidth (GB/s)``) plus ``Method``/``Kernel`` columns.
 """
@@ -50,37 +53,55 @@ def _events_ms(fn, repeat: int, warmup: int) -> List[float]:
 
 
 def matmul_tflops(n: int, precision: str, kernel: str = "hyperion", method: str = "proper", repeat: int = 20,
-                  warmup: int = 5, bk: int = 64) -> Dict:
-    """TFLOPS of one n×n×n product (2n³ FLOP)."""
+                  warmup: int = 5, tiles=(0, 1, 2, 3)) -> Dict:
+    """TFLOPS of one n×n×n product (2n³ FLOP).  Hyperion computes C = A·Bᵀ with B stored [N, K] (the
+    transpose is layout, not work: same 2n³ FLOPs)."""
     from ..ops import _native
 
     dev = torch.device("cuda")
     dt = _DT[precision]
-    use_hyp = kernel == "hyperion" and dt != torch.float32
+    use_hyp = kernel == "hyperion"
+    C = _native.native() if use_hyp else None
 
     def make():
         a = torch.rand(n, n, device=dev, dtype=dt) * 2 - 1
         b = torch.rand(n, n, device=dev, dtype=dt) * 2 - 1
         return a, b
 
+    def hyp_fn(a, b, tile=-1):
+        if dt == torch.float32:
+            return lambda: C.gemm_f32_nt(a, b)  # noqa: E731
+        return lambda: C.gemm(a, b, tile=tile, splits=1 if tile >= 0 else -1)  # noqa: E731
+
+    best_tile = None
     if method == "reference":
         _sync()
         t0 = time.perf_counter()
         a, b = make()  # allocation inside the timer, single un-warmed call (reference :223-231)
-        c = _native.native().gemm_nt(a, b, None, 1.0, bk) if use_hyp else torch.matmul(a, b)
+        c = hyp_fn(a, b)() if use_hyp else torch.matmul(a, b)
         _sync()
         t = time.perf_counter() - t0
         del c
     else:
         a, b = make()
-        if use_hyp:
-            # C = A · Bᵀ with B stored [N, K] (the transpose is layout, not work: same 2n³ FLOPs)
-            fn = lambda: _native.native().gemm_nt(a, b, None, 1.0, bk)  # noqa: E731
+        if use_hyp and dt != torch.float32:
+            # the tiled kernel's tile shapes (the autotune space of ops/gemm.py): report the best
+            res = {}
+            for tile in tiles:
+                try:
+                    res[tile] = statistics.median(_events_ms(hyp_fn(a, b, tile), repeat, warmup)) / 1e3
+                except RuntimeError:  # tile not valid for this shape
+                    pass
+            best_tile = min(res, key=res.get)
+            t = res[best_tile]
         else:
-            fn = lambda: torch.matmul(a, b)  # noqa: E731
-        t = statistics.median(_events_ms(fn, repeat, warmup)) / 1e3
+            fn = hyp_fn(a, b) if use_hyp else (lambda: torch.matmul(a, b))  # noqa: E731
+            t = statistics.median(_events_ms(fn, repeat, warmup)) / 1e3
+    kname = "torch"
+    if use_hyp:
+        kname = "hyperion_f32_mfma" if dt == torch.float32 else "hyperion_tiled_mfma"
     return {"Size": n, "Precision": precision.upper() if precision != "bf16" else "BF16", "Time (s)": t,
-            "TFLOPS": 2 * n**3 / t / 1e12, "Method": method, "Kernel": "hyperion_mfma" if use_hyp else "torch"}
+            "TFLOPS": 2 * n**3 / t / 1e12, "Method": method, "Kernel": kname, "Tile": best_tile}
 
 
 def test_precision_formats(sizes: Sequence[int] = (1024, 2048, 4096, 8192), precisions=("fp32", "fp16", "bf16"),
@@ -90,8 +111,6 @@ def test_precision_formats(sizes: Sequence[int] = (1024, 2048, 4096, 8192), prec
     for method in methods:
         for kern in kernels:
             for p in precisions:
-                if kern == "hyperion" and p == "fp32":
-                    continue  # fp32 GEMM stays on the library (no xf32 MFMA on gfx950)
                 for n in sizes:
                     r = matmul_tflops(n, p, kern, method)
                     rows.append(r)

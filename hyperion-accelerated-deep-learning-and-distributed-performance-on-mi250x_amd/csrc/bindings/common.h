@@ -72,9 +72,8 @@ inline const void* device_zero_page(const at::Device& dev) { return device_zeroe
 
 // 16K int32 counters per device for last-arriver reductions (a kernel's workgroups count in on a
 // slot; the last one reduces and RESETS the slot to zero, so every launch — eager or a graph
-// replay — finds its slots zeroed).  Slot ranges are fixed per op (kCounterSlot*); users must be
-// stream-ordered: two kernels sharing slots must never run concurrently.
-constexpr int kCounterSlotLoraDown = 0;  // [0, 4096)
+// replay — finds its slots zeroed).  Users must be stream-ordered: two kernels sharing slots must
+// never run concurrently.
 inline int* device_counters(const at::Device& dev) { return static_cast<int*>(device_zeroed_block(dev, 1)); }
 
 #define HYP_CHECK_CUDA_TENSOR(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")

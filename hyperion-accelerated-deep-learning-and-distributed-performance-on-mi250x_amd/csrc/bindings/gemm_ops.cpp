@@ -25,6 +25,24 @@ at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::S
   return c;
 }
 
+// fp32 a [M, K], b [N, K] -> a @ b.T on the fp32-input MFMA (gemm_f32.hip)
+at::Tensor gemm_f32_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::ScalarType> out_dtype, double alpha) {
+  HYP_CHECK_CUDA_TENSOR(a);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_f32_nt: expected a [M,K], b [N,K]");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_f32_nt: K must be contiguous");
+  TORCH_CHECK(a.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "gemm_f32_nt: fp32 inputs");
+  const int M = (int)a.size(0), N = (int)b.size(0), K = (int)a.size(1);
+  TORCH_CHECK(hyp::gemm_f32_nt_supported(M, N, K, (int)a.stride(0), (int)b.stride(0)),
+              "gemm_f32_nt: shape not supported (M, N multiples of 128; K multiple of 32; 16-byte rows)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "gemm_f32_nt: 16-byte aligned bases required");
+  const at::DeviceGuard guard(a.device());
+  auto c = at::empty({M, N}, a.options().dtype(out_dtype.has_value() ? *out_dtype : at::kFloat));
+  HYP_CHECK_HIP(hyp::gemm_f32_nt(dtype_code(c), a.data_ptr<float>(), b.data_ptr<float>(), c.data_ptr(), M, N, K,
+                                 (int)a.stride(0), (int)b.stride(0), N, (float)alpha, cur_stream()));
+  return c;
+}
+
 // Operand view: a 2D tensor with unit stride in its last dim.  row form (tr = false): X[i, k] at
 // row i; tr form: X is [K, I] with X(i, k) = X[k, i].
 void check_operand(const at::Tensor& t, const char* name) {
@@ -127,6 +145,8 @@ void register_gemm_ops(pybind11::module& m) {
         pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0, pybind11::arg("out") = pybind11::none(),
         pybind11::arg("tile") = -1, pybind11::arg("splits") = -1);
   m.def("gemm_plan", &gemm_plan, "(tile, splits) the automatic plan picks for an M x N x K GEMM");
+  m.def("gemm_f32_nt", &gemm_f32_nt, "C = alpha * A @ B.T, fp32 in, on the fp32-input MFMA", pybind11::arg("a"),
+        pybind11::arg("b"), pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("alpha") = 1.0);
   m.def("gemm_nt", &gemm_nt, "C = alpha * A @ B.T on MFMA (bf16/f16 in)", pybind11::arg("a"), pybind11::arg("b"),
         pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("alpha") = 1.0, pybind11::arg("bk") = 64);
 }

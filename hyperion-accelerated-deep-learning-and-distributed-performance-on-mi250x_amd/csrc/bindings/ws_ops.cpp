@@ -125,6 +125,26 @@ std::vector<const void*> ptr_list(const std::vector<at::Tensor>& ts, at::ScalarT
   return v;
 }
 
+// A rank-r fp32 buffer: [M, >= W] (one slice) or a split-partial stack [S, M, >= W] (slices summed by
+// the consumer); unit stride in the last dim.
+struct RankRView {
+  float* p;
+  int ld, S;
+  int64_t sstride;
+};
+
+RankRView rank_r_view(const at::Tensor& t, int64_t M, int64_t W, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && (t.dim() == 2 || t.dim() == 3) && t.stride(-1) == 1,
+              what, ": fp32 [M, W] or [splits, M, W] with unit stride in the last dim");
+  TORCH_CHECK(t.size(-2) == M && t.size(-1) >= W, what, ": shape must be [.., M, >= ", W, "]");
+  RankRView v;
+  v.p = t.data_ptr<float>();
+  v.ld = (int)t.stride(-2);
+  v.S = t.dim() == 3 ? (int)t.size(0) : 1;
+  v.sstride = t.dim() == 3 ? t.stride(0) : 0;
+  return v;
+}
+
 void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_t MFtot, int64_t M, int64_t N, int64_t epi,
                     const at::Tensor& out, const c10::optional<at::Tensor>& out2, const c10::optional<at::Tensor>& aux,
                     const c10::optional<at::Tensor>& t, const std::vector<at::Tensor>& lw, int64_t segw, double lscale,
@@ -164,12 +184,11 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
     ldax = aux->stride(0);
   }
   const float* tp = nullptr;
-  int ldt = 0, r = 0, P = 0;
+  int ldt = 0, r = 0, P = 0, t_S = 1;
+  int64_t t_ss = 0;
   std::vector<const void*> lp;
   if (epi == 4 || (epi == 1 && t.has_value() && t->defined())) {
-    TORCH_CHECK(t.has_value() && t->defined() && t->scalar_type() == at::kFloat && t->dim() == 2 &&
-                    t->stride(1) == 1 && t->size(0) == M,
-                "ws_epilogue: t fp32 [M, P r]");
+    TORCH_CHECK(t.has_value() && t->defined(), "ws_epilogue: this epilogue needs t");
     lp = ptr_list(lw, dt, "ws_epilogue lw");
     P = (int)lw.size();
     TORCH_CHECK(P >= 1 && P <= 4, "ws_epilogue: 1..4 LoRA projections");
@@ -177,9 +196,11 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
     for (const auto& w : lw)
       TORCH_CHECK(epi == 1 ? (w.size(1) == r && w.size(0) == segw) : (w.size(0) == r && w.size(1) == N),
                   "ws_epilogue: LoRA operand shapes (B_p [segw, r] / A_p [r, N])");
-    TORCH_CHECK(t->size(1) >= P * r, "ws_epilogue: t too narrow");
-    tp = t->data_ptr<float>();
-    ldt = (int)t->stride(0);
+    const RankRView tv = rank_r_view(*t, M, P * r, "ws_epilogue t");
+    tp = tv.p;
+    ldt = tv.ld;
+    t_ss = tv.sstride;
+    t_S = tv.S;
   }
   hyp::RngState rs{};
   const bool has_rng = rng.has_value() && rng->defined() && p_drop > 0;
@@ -187,7 +208,7 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
   TORCH_CHECK(epi != 1 || (segw >= 128 && N % segw == 0), "ws_epilogue: segment width");
   const at::DeviceGuard guard(out.device());
   HYP_CHECK_HIP(hyp::ws_epilogue(dtype_code(out), (int)epi, part_ptr, (int)S, (int)MFtot, (int)M,
-                                 (int)N, out.data_ptr(), out.stride(0), o2, ldo2, ax, ldax, tp, ldt,
+                                 (int)N, out.data_ptr(), out.stride(0), o2, ldo2, ax, ldax, tp, ldt, t_ss, t_S,
                                  lp.empty() ? nullptr : lp.data(), P, r, (int)segw, (float)lscale, (int)rope_segs,
                                  (int)seq, (float)theta, has_rng ? &rs : nullptr, (float)p_drop,
                                  nn.has_value() ? *nn : (epi == 3 || epi == 4), dense ? yin->data_ptr() : nullptr,
@@ -195,36 +216,19 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
 }
 
 void lora_down_py(const at::Tensor& x, const std::vector<at::Tensor>& A, at::Tensor& t,
-                  const c10::optional<at::Tensor>& rng, double p_drop, const c10::optional<at::Tensor>& zero) {
+                  const c10::optional<at::Tensor>& rng, double p_drop) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "lora_down: x [M, K] row-major");
   auto lp = ptr_list(A, x.scalar_type(), "lora_down A");
   const int P = (int)A.size(), r = (int)A[0].size(0);
   for (const auto& a : A) TORCH_CHECK(a.dim() == 2 && a.size(0) == r && a.size(1) == x.size(1), "lora_down: A_p [r, K]");
-  TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2 && t.stride(1) == 1 && t.size(0) == x.size(0) &&
-                  t.size(1) >= P * r,
-              "lora_down: t fp32 [M, >= P r]");
+  const RankRView tv = rank_r_view(t, x.size(0), P * r, "lora_down t");
   hyp::RngState rs{};
   const bool has_rng = rng.has_value() && rng->defined() && p_drop > 0;
   if (has_rng) rs = unpack_rng(*rng);
   const at::DeviceGuard guard(x.device());
-  float* zp = nullptr;
-  int nz = 0;
-  if (zero.has_value() && zero->defined()) {
-    TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous() && zero->device() == x.device(),
-                "lora_down: zero must be a contiguous fp32 tensor on x's device");
-    zp = zero->data_ptr<float>();
-    nz = (int)zero->numel();
-  }
-  // k-split: ~256 workgroups over the (projection, 16-row tile) grid, >= 512 reduction elements each
-  const int M = (int)x.size(0), K = (int)x.size(1), tiles = P * ((M + 15) / 16);
-  int ks = 1;
-  while (ks < 16 && tiles * ks * 2 <= 256 && K % (128 * ks * 2) == 0 && K / (ks * 2) >= 512) ks *= 2;
-  auto part = at::empty({(int64_t)tiles * ks * 256}, x.options().dtype(at::kFloat));
-  HYP_CHECK_HIP(hyp::lora_down(dtype_code(x), x.data_ptr(), x.stride(0), lp.data(), P, r, t.data_ptr<float>(),
-                               (int)t.stride(0), M, K, has_rng ? &rs : nullptr, (float)p_drop, zp, nz,
-                               part.data_ptr<float>(), device_counters(x.device()) + kCounterSlotLoraDown, ks,
-                               cur_stream()));
+  HYP_CHECK_HIP(hyp::lora_down(dtype_code(x), x.data_ptr(), x.stride(0), lp.data(), P, r, tv.p, tv.ld, tv.sstride, tv.S,
+                               (int)x.size(0), (int)x.size(1), has_rng ? &rs : nullptr, (float)p_drop, cur_stream()));
 }
 
 void lora_bwd_t_py(const at::Tensor& dy, int64_t N, const std::vector<at::Tensor>& B, const std::vector<at::Tensor>& dB,
@@ -237,14 +241,13 @@ void lora_bwd_t_py(const at::Tensor& dy, int64_t N, const std::vector<at::Tensor
   const int P = (int)B.size(), r = (int)B[0].size(1);
   for (size_t i = 0; i < B.size(); ++i)
     TORCH_CHECK(B[i].size(0) == N && B[i].size(1) == r && dB[i].sizes() == B[i].sizes(), "lora_bwd_t: B_p [N, r]");
-  TORCH_CHECK(t.scalar_type() == at::kFloat && du.scalar_type() == at::kFloat && t.stride(0) == du.stride(0) &&
-                  t.size(0) == dy.size(0) && du.size(0) == dy.size(0),
-              "lora_bwd_t: t / du fp32 [M, P r] with one row stride");
+  const RankRView tv = rank_r_view(t, dy.size(0), P * r, "lora_bwd_t t");
+  const RankRView uv = rank_r_view(du, dy.size(0), P * r, "lora_bwd_t du");
   std::vector<void*> dbw;
   for (auto* q : dbp) dbw.push_back(const_cast<void*>(q));
   const at::DeviceGuard guard(dy.device());
-  HYP_CHECK_HIP(hyp::lora_bwd_t(dtype_code(dy), dy.data_ptr(), dy.stride(0), (int)N, bp.data(), dbw.data(), P, r,
-                                t.data_ptr<float>(), (int)t.stride(0), du.data_ptr<float>(), (int)dy.size(0), (float)c,
+  HYP_CHECK_HIP(hyp::lora_bwd_t(dtype_code(dy), dy.data_ptr(), dy.stride(0), (int)N, bp.data(), dbw.data(), P, r, tv.p,
+                                tv.ld, tv.sstride, tv.S, uv.p, uv.ld, uv.sstride, uv.S, (int)dy.size(0), (float)c,
                                 cur_stream()));
 }
 
@@ -255,16 +258,15 @@ void lora_bwd_a_py(const at::Tensor& x, const std::vector<at::Tensor>& dA, const
   auto dap = ptr_list(dA, x.scalar_type(), "lora_bwd_a dA");
   const int P = (int)dA.size(), r = (int)dA[0].size(0);
   for (const auto& a : dA) TORCH_CHECK(a.size(0) == r && a.size(1) == x.size(1), "lora_bwd_a: dA_p [r, K]");
-  TORCH_CHECK(du.scalar_type() == at::kFloat && du.size(0) == x.size(0) && du.size(1) >= P * r, "lora_bwd_a: du fp32");
+  const RankRView uv = rank_r_view(du, x.size(0), P * r, "lora_bwd_a du");
   std::vector<void*> daw;
   for (auto* q : dap) daw.push_back(const_cast<void*>(q));
   hyp::RngState rs{};
   const bool has_rng = rng.has_value() && rng->defined() && p_drop > 0;
   if (has_rng) rs = unpack_rng(*rng);
   const at::DeviceGuard guard(x.device());
-  HYP_CHECK_HIP(hyp::lora_bwd_a(dtype_code(x), x.data_ptr(), x.stride(0), (int)x.size(1), daw.data(), P, r,
-                                du.data_ptr<float>(), (int)du.stride(0), (int)x.size(0), has_rng ? &rs : nullptr,
-                                (float)p_drop, cur_stream()));
+  HYP_CHECK_HIP(hyp::lora_bwd_a(dtype_code(x), x.data_ptr(), x.stride(0), (int)x.size(1), daw.data(), P, r, uv.p, uv.ld,
+                                uv.sstride, uv.S, (int)x.size(0), has_rng ? &rs : nullptr, (float)p_drop, cur_stream()));
 }
 }  // namespace
 
@@ -284,9 +286,10 @@ void register_ws_ops(pybind11::module& m) {
         "aux"_a = pybind11::none(), "t"_a = pybind11::none(), "lw"_a = std::vector<at::Tensor>{}, "segw"_a = 0,
         "lscale"_a = 1.0, "rope_segs"_a = 0, "seq"_a = 0, "theta"_a = 10000.0, "rng"_a = pybind11::none(),
         "p_drop"_a = 0.0, "nn"_a = pybind11::none(), "yin"_a = pybind11::none());
-  m.def("lora_down", &lora_down_py, "t[m, p r + j] = Σ_k keep_p x A_p (written); zeroes `zero` in the same launch",
-        "x"_a, "A"_a, "t"_a, "rng"_a = pybind11::none(), "p_drop"_a = 0.0, "zero"_a = pybind11::none());
-  m.def("lora_bwd_t", &lora_bwd_t_py, "du' += c dy_p B_p (atomics); dB_p = c dy_pᵀ t_p", "dy"_a, "N"_a, "B"_a, "dB"_a,
+  m.def("lora_down", &lora_down_py,
+        "t[m, p r + j] = Σ_k keep_p x A_p; t [M, W] or a k-split partial stack [S, M, W] (slice q = split q)", "x"_a,
+        "A"_a, "t"_a, "rng"_a = pybind11::none(), "p_drop"_a = 0.0);
+  m.def("lora_bwd_t", &lora_bwd_t_py, "du' = c dy_p B_p (n-split partial stack if du is 3D); dB_p = c dy_pᵀ t_p (t: stack summed)", "dy"_a, "N"_a, "B"_a, "dB"_a,
         "t"_a, "du"_a, "c"_a);
   m.def("lora_bwd_a", &lora_bwd_a_py, "dA_p = du'_pᵀ (keep_p ∘ x)", "x"_a, "dA"_a, "du"_a, "rng"_a = pybind11::none(),
         "p_drop"_a = 0.0);

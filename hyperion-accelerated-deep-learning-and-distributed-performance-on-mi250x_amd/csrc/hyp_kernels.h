@@ -128,6 +128,12 @@ bool gemm_nt_supported(int M, int N, int K, int lda, int ldb, int bk);
 hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, void* C, int M, int N, int K, int lda,
                    int ldb, int ldc, float alpha, int bk, hipStream_t st);
 
+// ---- gemm_f32.hip -----------------------------------------------------------------------------
+// C = alpha A·Bᵀ, fp32 in (fp32-input MFMA, exact fp32 products/accumulation); M, N % 128, K % 32
+bool gemm_f32_nt_supported(int M, int N, int K, int lda, int ldb);
+hipError_t gemm_f32_nt(int out_dtype, const float* A, const float* B, void* C, int M, int N, int K, int lda, int ldb,
+                       int ldc, float alpha, hipStream_t st);
+
 // ---- gemm_tiles.hip --------------------------------------------------------------------------
 // C[M,N] = epi(alpha Σ_k A(m,k) B(n,k)); A(m,k) at A + m*lda + k (a_tr = 0) or A + k*lda + m (a_tr = 1),
 // B likewise.  epi: + beta*C_old, + bias[n] (bias_dtype), aux = pre-activation, act (0 none, 1 relu,
@@ -308,23 +314,23 @@ hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t l
 // yin [M, N] (a vendor GEMM's output) instead of slabs.
 hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, int M, int N, void* out, int64_t ldo,
                        void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
-                       const void* const* lw, int P, int r, int segw, float lscale, int rope_segs, int seq,
-                       float theta, const RngState* rng, float p_drop, bool nn, const void* yin, int64_t ldy,
-                       hipStream_t st);
+                       int64_t t_sstride, int t_splits, const void* const* lw, int P, int r, int segw, float lscale,
+                       int rope_segs, int seq, float theta, const RngState* rng, float p_drop, bool nn,
+                       const void* yin, int64_t ldy, hipStream_t st);
 }  // namespace hyp
 
 namespace hyp {
 // ---- lora_fused.hip --------------------------------------------------------------------------
 // rank-r halves of the fused LoRA projections (P projections sharing one input; see the file).
-// t: fp32 [M, P r] written (k-split over `ksplit` workgroups per tile: fp32 partials in `part`
-// [P * ceil(M/16) * ksplit * 256], last-arriver sum on `counters` slots [0, P * ceil(M/16)); lora_down
-// also zeroes zero[0, nzero): the du buffer); du: accumulated
-// atomically by lora_bwd_t (zero it first).  K % 256 == 0 (lora_down), N % 256 == 0 (lora_bwd_t).
-hipError_t lora_down(int dtype, const void* x, int64_t ldx, const void* const* A, int P, int r, float* t, int ldt, int M,
-                     int K, const RngState* rng, float p_drop, float* zero, int nzero, float* part, int* counters,
-                     int ksplit, hipStream_t st);
+// t and du: fp32 split-partial stacks [splits][M][ld] (slice stride sstride; splits = 1: a plain
+// [M, ld] matrix): producers write one slice per split, consumers sum the slices.
+// K % 32 == 0 (lora_down), N % 64 == 0 (lora_bwd_t), K % 64 == 0 (lora_bwd_a).
+hipError_t lora_down(int dtype, const void* x, int64_t ldx, const void* const* A, int P, int r, float* t, int ldt,
+                     int64_t t_sstride, int t_splits, int M, int K, const RngState* rng, float p_drop, hipStream_t st);
 hipError_t lora_bwd_t(int dtype, const void* dy, int64_t ldy, int N, const void* const* B, void* const* dB, int P,
-                      int r, const float* t, int ldt, float* du, int M, float c, hipStream_t st);
+                      int r, const float* t, int ldt, int64_t t_sstride, int t_splits, float* du, int ldu,
+                      int64_t du_sstride, int du_splits, int M, float c, hipStream_t st);
 hipError_t lora_bwd_a(int dtype, const void* x, int64_t ldx, int K, void* const* dA, int P, int r, const float* du,
-                      int ldt, int M, const RngState* rng, float p_drop, hipStream_t st);
+                      int ldu, int64_t du_sstride, int du_splits, int M, const RngState* rng, float p_drop,
+                      hipStream_t st);
 }  // namespace hyp

@@ -6,8 +6,8 @@
 // stored dropout mask per projection.  Here, for the P projections that read the same input x
 // (q, k, v: P = 3; o: P = 1), with c' = scaling / (1 - p) and keep_p the regenerated dropout mask
 // (lora_keep in hyp_common.h; never stored):
-//   lora_down   t'[m, p r + j] = Σ_k keep_p(m, k) x[m, k] A_p[j, k]          (fp32, MFMA, written)
-//   lora_bwd_t  du'[m, p r + j] += c' Σ_n dy_p[m, n] B_p[n, j]   (atomics),  dB_p = c' dy_pᵀ t'_p
+//   lora_down   t'[m, p r + j] = Σ_k keep_p(m, k) x[m, k] A_p[j, k]          (fp32, MFMA, k-split partials)
+//   lora_bwd_t  du'[m, p r + j] = c' Σ_n dy_p[m, n] B_p[n, j]   (n-split partials),  dB_p = c' dy_pᵀ t'_p
 //   lora_bwd_a  dA_p[j, k] = Σ_m du'[m, p r + j] keep_p(m, k) x[m, k]
 // and the up term c' t' Bᵀ / the data-gradient term keep ∘ (du' A) ride in ws_epilogue.
 #include "hyp_common.h"
@@ -24,52 +24,94 @@ struct LoraPtrs {
   const void* p[4];
 };
 
-// lora_down: block (p, 16-row m-tile, k-split q < KS), 4 waves splitting the block's K range; A
-// fragments are the (masked) x rows and B fragments the rows of A_p, both straight from global
-// memory (16 contiguous bytes per lane).  Each block leaves its 16 x 16 partial tile (summed over
-// its waves through LDS) in `part`; the LAST block of the (p, m-tile) to count in on its counter
-// slot sums the KS partials in fixed order and WRITES t (deterministic; no atomics on t and no
-// zero-fill launch), then resets the slot.  The launch also zeroes z[0, nz) — the du buffer the
-// backward's lora_bwd_t accumulates into.
-template <typename T>
-__global__ __launch_bounds__(256) void lora_down_k(const T* __restrict__ x, int64_t ldx, LoraPtrs A, float* t, int ldt,
-                                                   int M, int K, int P, int r, RngState rs, uint32_t thr, int drop,
-                                                   float* z, int nz, float* part, int* cnt, int KS) {
-  __shared__ f32x4 red[4][64];
-  __shared__ int is_last;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {
-    const int nb = gridDim.x * gridDim.y * gridDim.z;
-    const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    for (int i = b * 256 + tid; i < nz; i += nb * 256) z[i] = 0.f;
+// Rank-r buffers (t', du') are fp32 [S][M][ld] split-partial stacks: the producer writes split q
+// into slice q (no atomics, no zero-fill, no cross-workgroup synchronisation — workgroup fences
+// cost microseconds per workgroup on the 8-XCD part), every consumer sums the S slices as it
+// stages the rows it needs (ws_epilogue's LoRA terms, lora_bwd_t, lora_bwd_a).
+struct RankR {
+  float* p;
+  int ld;            // row stride
+  int64_t sstride;   // slice stride
+  int S;             // slices
+};
+
+// Stage rows [row0, row0 + 128) x ranks [col0, col0 + 16) of a stack (its slices summed; zeros past
+// `rows` and past r) into dst[128][16]: each of the 256 threads owns two float4 cells and issues all
+// of its slice loads before summing (a per-element loop would wait a memory round trip per slice).
+// Needs ld, col0 and sstride % 4 == 0 (host-checked).
+__device__ __forceinline__ void stage_rank_rows(const RankR& u, int row0, int rows, int col0, int r, float (*dst)[16],
+                                                int tid) {
+  float4 acc[2] = {float4{0.f, 0.f, 0.f, 0.f}, float4{0.f, 0.f, 0.f, 0.f}};
+  for (int q0 = 0; q0 < u.S; q0 += 4) {
+    float4 v[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int cell = tid + 256 * c, row = cell >> 2, j4 = (cell & 3) * 4;
+      const bool ok = row < rows;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = min(q0 + i, u.S - 1);
+        v[c][i] = ok ? *reinterpret_cast<const float4*>(u.p + q * u.sstride + (int64_t)(row0 + row) * u.ld + col0 + j4)
+                     : float4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (q0 + i < u.S) {
+          acc[c].x += v[c][i].x; acc[c].y += v[c][i].y; acc[c].z += v[c][i].z; acc[c].w += v[c][i].w;
+        }
   }
-  const int p = blockIdx.x, mt = blockIdx.y, q = blockIdx.z, m0 = mt * 16;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int cell = tid + 256 * c, row = cell >> 2, j4 = (cell & 3) * 4;
+    float4 o = acc[c];
+    if (j4 + 0 >= r) o.x = 0.f;
+    if (j4 + 1 >= r) o.y = 0.f;
+    if (j4 + 2 >= r) o.z = 0.f;
+    if (j4 + 3 >= r) o.w = 0.f;
+    *reinterpret_cast<float4*>(&dst[row][j4]) = o;
+  }
+}
+
+// lora_down: block (p, 16-row m-tile, k-split q), 4 waves over the block's K range; A fragments =
+// (masked) x rows, B fragments = rows of A_p, both straight from global memory (16 contiguous bytes
+// per lane, every load of a wave in flight at once); the 4 wave tiles are summed through LDS and the
+// block's 16 x 16 partial is written to slice q of t'.
+template <typename T>
+__global__ __launch_bounds__(256) void lora_down_k(const T* __restrict__ x, int64_t ldx, LoraPtrs A, RankR t, int M,
+                                                   int K, int P, int r, RngState rs, uint32_t thr, int drop) {
+  __shared__ f32x4 red[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int p = blockIdx.x, m0 = blockIdx.y * 16, q = blockIdx.z;
   const uint64_t key = drop ? rng_key(rs) : 0ull;
   const int l15 = lane & 15, g4 = lane >> 4;
   const int m = m0 + l15;
   const bool mok = m < M, jok = l15 < r;
   const T* xr = x + (int64_t)(mok ? m : 0) * ldx;
   const T* ar = static_cast<const T*>(A.p[p]) + (int64_t)(jok ? l15 : 0) * K;
-  const int kw = K / (KS * 4);  // % 32 == 0 (host check)
-  const int kb = (q * 4 + wave) * kw, ke = kb + kw;
+  // 32-wide k-steps of this split, round-robin over the 4 waves
+  const int nks = K >> 5, per = (nks + t.S - 1) / t.S;
+  const int ks0 = q * per, ks1 = min(nks, ks0 + per);
   const uint32_t ibase = (uint32_t)(((int64_t)p * M + m) * K);
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = kb; k < ke; k += 128) {
-    u16x8 a[4], b[4];
+  for (int k0 = ks0 + wave; k0 < ks1; k0 += 32) {  // up to 8 k-steps (16 loads) in flight
+    u16x8 a[8], b[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // all loads of the group in flight together
-      const int kk = min(k + 32 * u, ke - 32) + g4 * 8;
+    for (int u = 0; u < 8; ++u) {
+      const int kk = min(k0 + 4 * u, ks1 - 1) * 32 + g4 * 8;
       a[u] = *reinterpret_cast<const u16x8*>(xr + kk);
       b[u] = *reinterpret_cast<const u16x8*>(ar + kk);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (k + 32 * u >= ke) break;
+    for (int u = 0; u < 8; ++u) {
+      if (k0 + 4 * u >= ks1) break;
       u16x8 av = a[u], bv = b[u];
       if (!mok) av = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (!jok) bv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (drop) {
-        const int kk = k + 32 * u + g4 * 8;
+        const int kk = (k0 + 4 * u) * 32 + g4 * 8;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (!lora_keep(key, ibase + (uint32_t)(kk + e), thr)) av[e] = 0;
@@ -79,118 +121,117 @@ __global__ __launch_bounds__(256) void lora_down_k(const T* __restrict__ x, int6
   }
   red[wave][lane] = acc;
   __syncthreads();
-  const int tile = p * gridDim.y + mt;
-  f32x4* tp = reinterpret_cast<f32x4*>(part) + (int64_t)tile * KS * 64;
   if (wave == 0) {
-    f32x4 s = red[0][lane];
+    const f32x4 sum = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    // sum[e] = t'_q[m0 + 4 g4 + e][p r + l15]
 #pragma unroll
-    for (int w = 1; w < 4; ++w) s += red[w][lane];
-    tp[q * 64 + lane] = s;
-  }
-  __threadfence();  // release: this block's partial is visible device-wide before it counts in
-  __syncthreads();
-  if (tid == 0) {
-    const int old = atomicAdd(cnt + tile, 1);
-    is_last = old == KS - 1;
-    if (is_last) cnt[tile] = 0;  // every block of the tile has counted: reset for the next launch
-  }
-  __syncthreads();
-  if (!is_last || wave != 0) return;
-  __threadfence();  // acquire: the other blocks' partials
-  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int i = 0; i < KS; ++i) s += __builtin_nontemporal_load(tp + i * 64 + lane);
-  // s[e] = t[m0 + 4 g4 + e][p r + l15]
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int mm = m0 + 4 * g4 + e;
-    if (mm < M && jok) t[(int64_t)mm * ldt + p * r + l15] = s[e];
+    for (int e = 0; e < 4; ++e) {
+      const int mm = m0 + 4 * g4 + e;
+      if (mm < M && jok) t.p[q * t.sstride + (int64_t)mm * t.ld + p * r + l15] = sum[e];
+    }
   }
 }
 
-// lora_bwd_t: block (p, 256-column slice of dy_p), 512 threads.  The dy tile (128 rows per pass)
-// is staged in LDS with 16-byte loads all in flight at once; then, with every LDS read a 16-byte
-// vector feeding 8-16 FMAs:
-//   dB rows of the slice, reduced over all M in the block (thread = (column, 8 ranks));
-//   the slice's share of du' (thread = (row, 4 ranks)), added atomically — 16-way per element at
-//   N = 4096 (du zeroed by the forward's lora_down).
-constexpr int kBtN = 256, kBtM = 128;
+// lora_bwd_t: ONE launch, two workgroup roles (256 threads each).
+//  du role, block (p, 16-row m-tile, n-split q): slice q of du'[m, p r + j] = c Σ_{n in split} dy_p[m, n] B_p[n, j]
+//    on MFMA — A fragments = dy rows from global (16 B per lane), B fragments = 8 rows of B_p (2-byte
+//    loads: 16 lanes cover one 32-byte row); 4 waves round-robin over the split's 32-wide steps.
+//  dB role, block (p, 64-column slice): dB_p[n, j] = c Σ_m dy[m, n] t'[m, j] — the dy tile staged in LDS
+//    (four 16-byte loads per thread, all in flight), t' (its slices summed) beside it; thread =
+//    (column, 4 ranks), every LDS read a broadcast or a 16-byte vector.
+constexpr int kBtN = 64, kBtM = 128;
 template <typename T>
-__global__ __launch_bounds__(512) void lora_bwd_t_k(const T* __restrict__ dy, int64_t ldy, int N, LoraPtrs B,
-                                                    LoraPtrs dB, const float* __restrict__ t, int ldt, float* du,
-                                                    int M, int r, float c) {
+__global__ __launch_bounds__(256) void lora_bwd_t_k(const T* __restrict__ dy, int64_t ldy, int N, LoraPtrs B,
+                                                    LoraPtrs dB, RankR t, RankR du, int M, int r, float c,
+                                                    int n_du_blocks, int mtiles) {
   __shared__ __attribute__((aligned(16))) uint16_t ys[kBtM][kBtN + 8];
   __shared__ __attribute__((aligned(16))) float ts[kBtM][16];
-  __shared__ __attribute__((aligned(16))) float bs[kBtN][16];
-  const int tid = threadIdx.x;
-  const int p = blockIdx.y, n0 = blockIdx.x * kBtN;
-  const T* Bp = static_cast<const T*>(B.p[p]);
-  for (int i = tid; i < kBtN * 16; i += 512) {
-    const int nn = i >> 4, j = i & 15;
-    bs[nn][j] = j < r ? ld1<T>(Bp + (int64_t)(n0 + nn) * r + j) : 0.f;
-  }
-  const int dn = tid & 255, djh = (tid >> 8) * 8;  // dB: column dn, ranks djh .. djh+7
-  float db[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if ((int)blockIdx.x < n_du_blocks) {
+    f32x4* red = reinterpret_cast<f32x4*>(&ts[0][0]);  // [4][64] f32x4 = 4 KB
+    const int l15 = lane & 15, g4 = lane >> 4;
+    const int per_p = mtiles * du.S;
+    const int p = blockIdx.x / per_p, rem = blockIdx.x - p * per_p;
+    const int mt = rem / du.S, q = rem - mt * du.S, m0 = mt * 16;
+    const int m = m0 + l15;
+    const bool mok = m < M, jok = l15 < r;
+    const T* yr = dy + (int64_t)(mok ? m : 0) * ldy + (int64_t)p * N;
+    const uint16_t* Bp = static_cast<const uint16_t*>(B.p[p]) + (jok ? l15 : 0);
+    const int nks = N >> 5, per = (nks + du.S - 1) / du.S;
+    const int ks0 = q * per, ks1 = min(nks, ks0 + per);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = ks0 + wave; k0 < ks1; k0 += 16) {  // 4 k-steps: 4 row loads + 32 B-element loads in flight
+      u16x8 av4[4], bv4[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) db[j] = 0.f;
+      for (int u = 0; u < 4; ++u) {
+        const int nn = min(k0 + 4 * u, ks1 - 1) * 32 + g4 * 8;
+        av4[u] = *reinterpret_cast<const u16x8*>(yr + nn);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv4[u][e] = Bp[(int64_t)(nn + e) * r];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k0 + 4 * u >= ks1) break;
+        u16x8 av = av4[u], bv = bv4[u];
+        if (!mok) av = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (!jok) bv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        acc = mfl::mma16<T>(av, bv, acc);
+      }
+    }
+    red[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      const f32x4 sum = red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int mm = m0 + 4 * g4 + e;
+        if (mm < M && jok) du.p[q * du.sstride + (int64_t)mm * du.ld + p * r + l15] = c * sum[e];
+      }
+    }
+    return;
+  }
+  // ---- dB role
+  const int nsl = N / kBtN;
+  const int idx = blockIdx.x - n_du_blocks, p = idx / nsl, n0 = (idx - p * nsl) * kBtN;
+  const int dn = tid & 63, j0 = (tid >> 6) * 4;
+  float db[4] = {0.f, 0.f, 0.f, 0.f};
   const T* dyp = dy + (int64_t)p * N + n0;
   for (int mc = 0; mc < M; mc += kBtM) {
     const int rows = min(kBtM, M - mc);
     __syncthreads();
-    uint4 v[8];
+    uint4 v[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 512 * i, row = idx >> 5, ch = idx & 31;
+    for (int i = 0; i < 4; ++i) {  // [128 rows][64 cols]: 8 chunks per row
+      const int id = tid + 256 * i, row = id >> 3, ch = id & 7;
       v[i] = row < rows ? *reinterpret_cast<const uint4*>(dyp + (int64_t)(mc + row) * ldy + ch * 8)
                         : uint4{0u, 0u, 0u, 0u};
     }
-    for (int i = tid; i < kBtM * 16; i += 512) {
-      const int row = i >> 4, j = i & 15;
-      ts[row][j] = (row < rows && j < r) ? t[(int64_t)(mc + row) * ldt + p * r + j] : 0.f;
-    }
+    stage_rank_rows(t, mc, rows, p * r, r, ts, tid);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 512 * i, row = idx >> 5, ch = idx & 31;
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i, row = id >> 3, ch = id & 7;
       *reinterpret_cast<uint4*>(&ys[row][ch * 8]) = v[i];
     }
     __syncthreads();
-    // dB[n][j] += Σ_m dy[m][n] t[m][j]
+#pragma unroll 8
     for (int mm = 0; mm < rows; ++mm) {
       const float yv = ld1<T>(reinterpret_cast<const T*>(&ys[mm][dn]));
-      const float4 t0 = *reinterpret_cast<const float4*>(&ts[mm][djh]);
-      const float4 t1 = *reinterpret_cast<const float4*>(&ts[mm][djh + 4]);
-      db[0] += yv * t0.x; db[1] += yv * t0.y; db[2] += yv * t0.z; db[3] += yv * t0.w;
-      db[4] += yv * t1.x; db[5] += yv * t1.y; db[6] += yv * t1.z; db[7] += yv * t1.w;
-    }
-    // du'[m][j] += c Σ_{n in slice} dy[m][n] B[n][j]   (thread = row mm, ranks jq .. jq+3)
-    const int mm = tid >> 2, jq = (tid & 3) * 4;
-    if (mm < rows) {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int n = 0; n < kBtN; n += 8) {
-        float yv[8];
-        Vec8<T>::load(reinterpret_cast<const T*>(&ys[mm][n]), yv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float4 bv = *reinterpret_cast<const float4*>(&bs[n + e][jq]);
-          s[0] += yv[e] * bv.x; s[1] += yv[e] * bv.y; s[2] += yv[e] * bv.z; s[3] += yv[e] * bv.w;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (jq + j < r) atomicAdd(du + (int64_t)(mc + mm) * ldt + p * r + jq + j, c * s[j]);
+      const float4 tv = *reinterpret_cast<const float4*>(&ts[mm][j0]);
+      db[0] += yv * tv.x; db[1] += yv * tv.y; db[2] += yv * tv.z; db[3] += yv * tv.w;
     }
   }
   T* dBp = static_cast<T*>(const_cast<void*>(dB.p[p]));
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    if (djh + j < r) st1<T>(dBp + (int64_t)(n0 + dn) * r + djh + j, c * db[j]);
+  for (int j = 0; j < 4; ++j)
+    if (j0 + j < r) st1<T>(dBp + (int64_t)(n0 + dn) * r + j0 + j, c * db[j]);
 }
 
 // lora_bwd_a: block (p, 64-column slice of x): dA_p[:, slice] = Σ_m du'[m, p r + j] keep_p(m, k) x[m, k];
-// up to 128 rows per pass, the x tile arriving with four 16-byte loads per thread issued together.
+// up to 128 rows per pass, the x tile arriving with four 16-byte loads per thread issued together,
+// du' (its slices summed) staged beside it.
 template <typename T>
-__global__ __launch_bounds__(256) void lora_bwd_a_k(const T* __restrict__ x, int64_t ldx, int K, LoraPtrs dA,
-                                                    const float* __restrict__ du, int ldt, int M, int r, RngState rs,
-                                                    uint32_t thr, int drop) {
+__global__ __launch_bounds__(256) void lora_bwd_a_k(const T* __restrict__ x, int64_t ldx, int K, LoraPtrs dA, RankR du,
+                                                    int M, int r, RngState rs, uint32_t thr, int drop) {
   __shared__ float xs[128][65];  // [m chunk][k]
   __shared__ __attribute__((aligned(16))) float us[128][16];
   const int tid = threadIdx.x;
@@ -203,20 +244,13 @@ __global__ __launch_bounds__(256) void lora_bwd_a_k(const T* __restrict__ x, int
     uint4 v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, ch = idx & 7, m = mc + row;
+      const int id = tid + 256 * i, row = id >> 3, ch = id & 7, m = mc + row;
       v[i] = m < M ? *reinterpret_cast<const uint4*>(x + (int64_t)m * ldx + k0 + ch * 8) : uint4{0u, 0u, 0u, 0u};
     }
-    float uv[8];
-    {
-      const int row = tid >> 1, q = (tid & 1) * 8, m = mc + row;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) uv[e] = (m < M && q + e < r) ? du[(int64_t)m * ldt + p * r + q + e] : 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) us[row][q + e] = uv[e];
-    }
+    stage_rank_rows(du, mc, min(128, M - mc), p * r, r, us, tid);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, ch = idx & 7, m = mc + row;
+      const int id = tid + 256 * i, row = id >> 3, ch = id & 7, m = mc + row;
       float f[8];
       Vec8<T>::load(reinterpret_cast<const T*>(&v[i]), f);
 #pragma unroll
@@ -249,56 +283,72 @@ LoraPtrs pack(const void* const* v, int P) {
 
 }  // namespace
 
-hipError_t lora_down(int dtype, const void* x, int64_t ldx, const void* const* A, int P, int r, float* t, int ldt, int M,
-                     int K, const RngState* rng, float p_drop, float* zero, int nzero, float* part, int* counters,
-                     int ksplit, hipStream_t st) {
-  if ((dtype != kBF16 && dtype != kF16) || P < 1 || P > 4 || r < 1 || r > 16 || M < 1 || ksplit < 1 ||
-      K % (128 * ksplit) != 0 || ldx % 8 != 0 || (nzero > 0 && zero == nullptr) || part == nullptr ||
-      counters == nullptr || P * ((M + 15) / 16) > 4096)
+static RankR rank_r(float* p, int ld, int64_t sstride, int S) {
+  RankR u;
+  u.p = p;
+  u.ld = ld;
+  u.sstride = sstride;
+  u.S = S;
+  return u;
+}
+
+hipError_t lora_down(int dtype, const void* x, int64_t ldx, const void* const* A, int P, int r, float* t, int ldt,
+                     int64_t t_sstride, int t_splits, int M, int K, const RngState* rng, float p_drop, hipStream_t st) {
+  if ((dtype != kBF16 && dtype != kF16) || P < 1 || P > 4 || r < 1 || r > 16 || M < 1 || K % 32 != 0 ||
+      ldx % 8 != 0 || t_splits < 1 || t_splits > K / 32)
     return hipErrorInvalidValue;
   const int drop = (rng != nullptr && p_drop > 0.f) ? 1 : 0;
   const RngState rs = drop ? *rng : RngState{};
   const uint32_t thr = (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f);
-  dim3 grid(P, (M + 15) / 16, ksplit);
+  dim3 grid(P, (M + 15) / 16, t_splits);
+  const RankR tt = rank_r(t, ldt, t_sstride, t_splits);
   if (dtype == kBF16)
-    hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), ldx, pack(A, P), t,
-                       ldt, M, K, P, r, rs, thr, drop, zero, nzero, part, counters, ksplit);
+    hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), ldx, pack(A, P), tt,
+                       M, K, P, r, rs, thr, drop);
   else
-    hipLaunchKernelGGL(lora_down_k<f16_t>, grid, dim3(256), 0, st, static_cast<const f16_t*>(x), ldx, pack(A, P), t,
-                       ldt, M, K, P, r, rs, thr, drop, zero, nzero, part, counters, ksplit);
+    hipLaunchKernelGGL(lora_down_k<f16_t>, grid, dim3(256), 0, st, static_cast<const f16_t*>(x), ldx, pack(A, P), tt,
+                       M, K, P, r, rs, thr, drop);
   return hipGetLastError();
 }
 
 hipError_t lora_bwd_t(int dtype, const void* dy, int64_t ldy, int N, const void* const* B, void* const* dB, int P,
-                      int r, const float* t, int ldt, float* du, int M, float c, hipStream_t st) {
-  if ((dtype != kBF16 && dtype != kF16) || P < 1 || P > 4 || r < 1 || r > 16 || N % kBtN != 0 || M < 1 || ldy % 8 != 0)
+                      int r, const float* t, int ldt, int64_t t_sstride, int t_splits, float* du, int ldu,
+                      int64_t du_sstride, int du_splits, int M, float c, hipStream_t st) {
+  if ((dtype != kBF16 && dtype != kF16) || P < 1 || P > 4 || r < 1 || r > 16 || N % kBtN != 0 || M < 1 ||
+      ldy % 8 != 0 || t_splits < 1 || du_splits < 1 || du_splits > N / 32 || ldt % 4 != 0 || t_sstride % 4 != 0 ||
+      (P > 1 && r % 4 != 0) || reinterpret_cast<uintptr_t>(t) % 16 != 0)
     return hipErrorInvalidValue;
-  dim3 grid(N / kBtN, P);
+  const int mtiles = (M + 15) / 16, n_du = P * mtiles * du_splits, n_db = P * (N / kBtN);
   LoraPtrs bp = pack(B, P), dbp = pack(const_cast<const void* const*>(reinterpret_cast<void* const*>(dB)), P);
+  const RankR tt = rank_r(const_cast<float*>(t), ldt, t_sstride, t_splits), uu = rank_r(du, ldu, du_sstride, du_splits);
   if (dtype == kBF16)
-    hipLaunchKernelGGL(lora_bwd_t_k<bf16_t>, grid, dim3(512), 0, st, static_cast<const bf16_t*>(dy), ldy, N, bp, dbp,
-                       t, ldt, du, M, r, c);
+    hipLaunchKernelGGL(lora_bwd_t_k<bf16_t>, dim3(n_du + n_db), dim3(256), 0, st, static_cast<const bf16_t*>(dy), ldy,
+                       N, bp, dbp, tt, uu, M, r, c, n_du, mtiles);
   else
-    hipLaunchKernelGGL(lora_bwd_t_k<f16_t>, grid, dim3(512), 0, st, static_cast<const f16_t*>(dy), ldy, N, bp, dbp, t,
-                       ldt, du, M, r, c);
+    hipLaunchKernelGGL(lora_bwd_t_k<f16_t>, dim3(n_du + n_db), dim3(256), 0, st, static_cast<const f16_t*>(dy), ldy,
+                       N, bp, dbp, tt, uu, M, r, c, n_du, mtiles);
   return hipGetLastError();
 }
 
 hipError_t lora_bwd_a(int dtype, const void* x, int64_t ldx, int K, void* const* dA, int P, int r, const float* du,
-                      int ldt, int M, const RngState* rng, float p_drop, hipStream_t st) {
-  if ((dtype != kBF16 && dtype != kF16) || P < 1 || P > 4 || r < 1 || r > 16 || K % 64 != 0 || M < 1 || ldx % 8 != 0)
+                      int ldu, int64_t du_sstride, int du_splits, int M, const RngState* rng, float p_drop,
+                      hipStream_t st) {
+  if ((dtype != kBF16 && dtype != kF16) || P < 1 || P > 4 || r < 1 || r > 16 || K % 64 != 0 || M < 1 || ldx % 8 != 0 ||
+      du_splits < 1 || ldu % 4 != 0 || du_sstride % 4 != 0 || (P > 1 && r % 4 != 0) ||
+      reinterpret_cast<uintptr_t>(du) % 16 != 0)
     return hipErrorInvalidValue;
   const int drop = (rng != nullptr && p_drop > 0.f) ? 1 : 0;
   const RngState rs = drop ? *rng : RngState{};
   const uint32_t thr = (uint32_t)fminf(p_drop * 4294967296.f, 4294967295.f);
   dim3 grid(K / 64, P);
   LoraPtrs dap = pack(const_cast<const void* const*>(reinterpret_cast<void* const*>(dA)), P);
+  const RankR uu = rank_r(const_cast<float*>(du), ldu, du_sstride, du_splits);
   if (dtype == kBF16)
-    hipLaunchKernelGGL(lora_bwd_a_k<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), ldx, K, dap, du,
-                       ldt, M, r, rs, thr, drop);
+    hipLaunchKernelGGL(lora_bwd_a_k<bf16_t>, grid, dim3(256), 0, st, static_cast<const bf16_t*>(x), ldx, K, dap, uu, M,
+                       r, rs, thr, drop);
   else
-    hipLaunchKernelGGL(lora_bwd_a_k<f16_t>, grid, dim3(256), 0, st, static_cast<const f16_t*>(x), ldx, K, dap, du, ldt,
-                       M, r, rs, thr, drop);
+    hipLaunchKernelGGL(lora_bwd_a_k<f16_t>, grid, dim3(256), 0, st, static_cast<const f16_t*>(x), ldx, K, dap, uu, M,
+                       r, rs, thr, drop);
   return hipGetLastError();
 }
 

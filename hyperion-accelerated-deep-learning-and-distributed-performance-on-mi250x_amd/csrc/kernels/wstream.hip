@@ -328,8 +328,10 @@ struct WsEpi {
   int64_t ldo2;
   const void* aux;        // EPI 3: gu [M, 2 I]
   int64_t ld_aux;
-  const float* t;         // EPI 1: t' / EPI 4: du'  [M, P r] fp32
+  const float* t;         // EPI 1: t' / EPI 4: du'  [t_splits][M][ldt] fp32 split partials (summed here)
   int ldt;
+  int64_t t_sstride;
+  int t_splits;
   const void* lw[4];      // EPI 1: B_p [segw, r]; EPI 4: A_p [r, N]
   int P, r, segw;
   float lscale;
@@ -344,7 +346,7 @@ template <typename T, int EPI, bool NN>
 __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
   static_assert(EPI == 0 || (EPI == 3 || EPI == 4) == NN, "slab layout: EPI 1/2 are NT, 3/4 NN, 0 either");
   constexpr bool PAIR = EPI == 1 || EPI == 2;
-  __shared__ float lt[16 * 64];           // t / du rows of the block (P r <= 64)
+  __shared__ __attribute__((aligned(16))) float lt[16 * 64];  // t / du rows of the block (P r <= 64)
   __shared__ float lw_s[4 * 16 * 128];    // EPI 1: B rows [128 cols][r]; EPI 4: A_p [r][64 cols] per p
   __shared__ __attribute__((aligned(16))) uint16_t tile[3][16][128 + 8];
   const int tid = threadIdx.x, lane = tid & 63, f = tid >> 6;
@@ -369,11 +371,29 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
 
   // ---- stage LoRA operands
   if ((EPI == 1 && a.t != nullptr) || EPI == 4) {
-    const int pr = a.P * a.r;
-    for (int i = tid; i < 16 * pr; i += 256) {
-      const int rr = i / pr, j = i - rr * pr;
-      const int m = mrow0 + rr;
-      lt[rr * 64 + j] = m < a.M ? a.t[(int64_t)m * a.ldt + j] : 0.f;
+    // 16 rows x P r (<= 64) ranks as float4 cells, one per thread; all slice loads in flight before
+    // the sum (the stacks are host-checked to 16-byte alignment)
+    const int pr = a.P * a.r, c4 = pr >> 2;
+    {
+      const int rr = tid / 16, j4 = (tid & 15) * 4, m = mrow0 + rr;
+      const bool ok = j4 < pr && m < a.M;
+      float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+      for (int q0 = 0; q0 < a.t_splits; q0 += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = min(q0 + i, a.t_splits - 1);
+          v[i] = ok ? *reinterpret_cast<const float4*>(a.t + q * a.t_sstride + (int64_t)m * a.ldt + j4)
+                    : float4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (q0 + i < a.t_splits) {
+            acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
+          }
+      }
+      if (j4 < 64) *reinterpret_cast<float4*>(&lt[rr * 64 + j4]) = acc;
+      (void)c4;
     }
     if (EPI == 1) {  // B rows of the 64 (+64 partner) columns: lw_s[c][rr], c < 128
       const int ncols = 128;
@@ -603,15 +623,17 @@ hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t l
 
 hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, int M, int N, void* out, int64_t ldo,
                        void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
-                       const void* const* lw, int P, int r, int segw, float lscale, int rope_segs, int seq,
-                       float theta, const RngState* rng, float p_drop, bool nn, const void* yin, int64_t ldy,
-                       hipStream_t st) {
+                       int64_t t_sstride, int t_splits, const void* const* lw, int P, int r, int segw, float lscale,
+                       int rope_segs, int seq, float theta, const RngState* rng, float p_drop, bool nn,
+                       const void* yin, int64_t ldy, hipStream_t st) {
   if (dtype != kBF16 && dtype != kF16) return hipErrorInvalidValue;
   if (part == nullptr && yin == nullptr) return hipErrorInvalidValue;
   if (epi != 0 && nn != (epi == 3 || epi == 4)) return hipErrorInvalidValue;  // the slab layout of that GEMM
   if (MFtot * 16 < M || N % 64 != 0 || epi < 0 || epi > 4) return hipErrorInvalidValue;
   const bool lora = t != nullptr;
-  if ((epi == 4 || (epi == 1 && lora)) && (t == nullptr || P < 1 || P > 4 || r < 1 || r > 16 || P * r > 64 || lw == nullptr))
+  if ((epi == 4 || (epi == 1 && lora)) && (t == nullptr || P < 1 || P > 4 || r < 1 || r > 16 || P * r > 64 || lw == nullptr ||
+                                            (P * r) % 4 != 0 || ldt % 4 != 0 || t_sstride % 4 != 0 ||
+                                            reinterpret_cast<uintptr_t>(t) % 16 != 0))
     return hipErrorInvalidValue;
   if (epi == 1 && (N % 128 != 0 || segw < 128 || segw % 128 != 0 || (lora && N / segw > P))) return hipErrorInvalidValue;
   if (epi == 2 && (N % 128 != 0 || out2 == nullptr)) return hipErrorInvalidValue;
@@ -632,6 +654,8 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
   a.ld_aux = ld_aux;
   a.t = t;
   a.ldt = ldt;
+  a.t_sstride = t_sstride;
+  a.t_splits = t_splits < 1 ? 1 : t_splits;
   for (int i = 0; i < 4; ++i) a.lw[i] = (lw != nullptr && i < P) ? lw[i] : nullptr;
   a.P = P;
   a.r = r;

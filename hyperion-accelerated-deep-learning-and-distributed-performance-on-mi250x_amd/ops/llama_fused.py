@@ -40,7 +40,13 @@ import torch.nn as nn
 from . import _native
 
 WS_MAX_M = int(os.environ.get("HYPERION_WS_MAX_M", "512"))
+RANK_SPLITS = 4  # slices of the rank-r split-partial stacks (t: k-splits of lora_down, du: n-splits)
 DEBUG: Optional[dict] = None  # tests / scripts: set to a dict to capture the backward intermediates
+
+
+def _summed(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """A rank-r split-partial stack [S, M, W] as the [M, W] matrix it stands for."""
+    return t.sum(0) if t is not None and t.dim() == 3 else t
 
 
 def _adjacent(ws: List[torch.Tensor]) -> bool:
@@ -236,14 +242,13 @@ class _LlamaLayerFn(torch.autograd.Function):
         if lora:
             if spec.p > 0:
                 rq, ro = _native.rng_state(dev), _native.rng_state(dev)
-            # t written by lora_down; the backward's du buffers (accumulated atomically by
-            # lora_bwd_t) are zeroed by the same launch — no fill kernels
-            # (t and du share one [M, 4 r] row layout: q/k/v columns then o — lora_bwd_t wants t
-            # and du at one row stride)
-            t_all = torch.empty(M, 4 * spec.r, device=dev, dtype=torch.float32)
-            t_qkv = t_all[:, :3 * spec.r]
-            du_bufs = torch.empty(M, 4 * spec.r, device=dev, dtype=torch.float32)
-            C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p, du_bufs)
+            # t (k-split) and du (n-split) as fp32 split-partial stacks [S, M, 4 r] — q/k/v columns
+            # then o — written slice by slice by lora_down / lora_bwd_t and summed by every consumer:
+            # no atomics, no fill kernels, and the rank-r work spreads over ~100-200 workgroups
+            t_all = torch.empty(RANK_SPLITS, M, 4 * spec.r, device=dev, dtype=torch.float32)
+            t_qkv = t_all[:, :, :3 * spec.r]
+            du_bufs = torch.empty(RANK_SPLITS, M, 4 * spec.r, device=dev, dtype=torch.float32)
+            C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p)
         pj = _Proj(C, h, spec.W_qkv)
         qkv = torch.empty(M, 3 * H, device=dev, dtype=dt)
         pj.epi(C, M, 3 * H, 1, qkv, t=t_qkv, lw=[Bq, Bk, Bv] if lora else [], segw=H,
@@ -254,7 +259,7 @@ class _LlamaLayerFn(torch.autograd.Function):
         o, lse = C.attn_fwd(q, k, v, True, scale, 0.0, None, kpm, True)
         o2 = o.view(M, H)
         if lora:
-            t_o = t_all[:, 3 * spec.r:]
+            t_o = t_all[:, :, 3 * spec.r:]
             C.lora_down(o2, [Ao], t_o, ro, spec.p)
         pj = _Proj(C, o2, spec.W_o)
         a = torch.empty(M, H, device=dev, dtype=dt)
@@ -299,7 +304,7 @@ class _LlamaLayerFn(torch.autograd.Function):
         grads = [None] * 8
         du_o = None
         if lora:
-            du_o = du_bufs[:, 3 * spec.r:]  # zeroed by the forward's lora_down (row stride 4 r)
+            du_o = du_bufs[:, :, 3 * spec.r:]
             dAo, dBo = torch.empty_like(Ao), torch.empty_like(Bo)
             C.lora_bwd_t(dsum2, H, [Bo], [dBo], t_o, du_o, spec.c)
         pj = _Proj(C, dsum2, spec.W_o, True)
@@ -321,7 +326,7 @@ class _LlamaLayerFn(torch.autograd.Function):
         # q/k/v: dh = dqkv [W_q; W_k; W_v] + Σ_p keep_p ∘ (du'_p A_p)
         du_qkv = None
         if lora:
-            du_qkv = du_bufs[:, :3 * spec.r]
+            du_qkv = du_bufs[:, :, :3 * spec.r]
             dA = [torch.empty_like(Aq), torch.empty_like(Ak), torch.empty_like(Av)]
             dB = [torch.empty_like(Bq), torch.empty_like(Bk), torch.empty_like(Bv)]
             C.lora_bwd_t(dqkv, H, [Bq, Bk, Bv], dB, t_qkv, du_qkv, spec.c)
@@ -336,7 +341,8 @@ class _LlamaLayerFn(torch.autograd.Function):
         dsum1 = C.ln_bwd(dh, s, spec.w1, rstd1, rstd1, dsum2, False, False, True)[0]
         if DEBUG is not None:
             DEBUG.update(dgu=dgu, dh2=dh2, dsum2=dsum2, do=do, dqkv=dqkv, dh=dh, dsum1=dsum1, h=h, s=s, qkv=qkv, o=o,
-                         s2=s2, gu=gu, dd=dd2, ds2=ds2c, t_qkv=t_qkv, t_o=t_o, du_o=du_o, du_qkv=du_qkv)
+                         s2=s2, gu=gu, dd=dd2, ds2=ds2c, t_qkv=_summed(t_qkv), t_o=_summed(t_o), du_o=_summed(du_o),
+                         du_qkv=_summed(du_qkv))
         d_in = dsum1.view(Bsz, S, H)
         return (d_in if has_delta else None, d_in, None, None, *grads)
 

@@ -47,17 +47,17 @@ for P in (3, 1):
     B = [torch.randn(K, r, device=dev, dtype=bf) * 0.1 for _ in range(P)]
     dB = [torch.empty_like(b) for b in B]
     dA = [torch.empty_like(a) for a in A]
-    t = torch.zeros(M, 4 * r, device=dev)
-    du = torch.zeros(M, 4 * r, device=dev)
+    t = torch.zeros(4, M, 4 * r, device=dev)  # split-partial stacks as the fused layer uses them
+    du = torch.zeros(4, M, 4 * r, device=dev)
     z = torch.empty(M, 4 * r, device=dev)
     dy = torch.randn(M, P * K, device=dev, dtype=bf)
     rs = _native.rng_state(x.device)
-    res[f"P{P}_down_nodrop"] = per_call_us(lambda: C.lora_down(x, A, t[:, :P * r]))
-    res[f"P{P}_down_drop"] = per_call_us(lambda: C.lora_down(x, A, t[:, :P * r], rs, 0.05))
-    res[f"P{P}_down_drop_zero"] = per_call_us(lambda: C.lora_down(x, A, t[:, :P * r], rs, 0.05, z))
-    res[f"P{P}_bwd_t"] = per_call_us(lambda: C.lora_bwd_t(dy, K, B, dB, t[:, :P * r], du[:, :P * r], 2.0))
-    res[f"P{P}_bwd_a_nodrop"] = per_call_us(lambda: C.lora_bwd_a(x, dA, du[:, :P * r]))
-    res[f"P{P}_bwd_a_drop"] = per_call_us(lambda: C.lora_bwd_a(x, dA, du[:, :P * r], rs, 0.05))
+    tv, uv = t[:, :, :P * r], du[:, :, :P * r]
+    res[f"P{P}_down_nodrop"] = per_call_us(lambda: C.lora_down(x, A, tv))
+    res[f"P{P}_down_drop"] = per_call_us(lambda: C.lora_down(x, A, tv, rs, 0.05))
+    res[f"P{P}_bwd_t"] = per_call_us(lambda: C.lora_bwd_t(dy, K, B, dB, tv, uv, 2.0))
+    res[f"P{P}_bwd_a_nodrop"] = per_call_us(lambda: C.lora_bwd_a(x, dA, uv))
+    res[f"P{P}_bwd_a_drop"] = per_call_us(lambda: C.lora_bwd_a(x, dA, uv, rs, 0.05))
     res[f"P{P}_torch_fill"] = per_call_us(lambda: z.zero_())
     res[f"P{P}_torch_add"] = per_call_us(lambda: z.add_(1.0))
 print(json.dumps(res), flush=True)

@@ -48,3 +48,20 @@ def test_stream_kernels_bandwidth_sane():
 
     r = stream_bandwidth(50_000_000, "add", "hyperion", "proper", repeat=5, warmup=2)
     assert r["Bandwidth (GB/s)"] > 1000  # MI355X HBM3E ≈ 8 TB/s; anything near the MI250X figure is a bug
+
+
+@pytest.mark.parametrize("shape", [(128, 128, 32), (256, 384, 96), (1024, 512, 2048)])
+def test_gemm_f32_nt_matches_fp64(shape):
+    """fp32-input MFMA GEMM (gemm_f32.hip): exact fp32 products, fp32 accumulation — error vs fp64
+    at the level of a k-ordered fp32 fma chain."""
+    from hyperion.ops import _native
+
+    M, N, K = shape
+    torch.manual_seed(0)
+    a = torch.rand(M, K, device="cuda") * 2 - 1
+    b = torch.rand(N, K, device="cuda") * 2 - 1
+    c = _native.native().gemm_f32_nt(a, b)
+    ref = a.double() @ b.double().t()
+    bound = 4e-7 * (a.abs().double() @ b.abs().double().t()) + 1e-30
+    assert ((c.double() - ref).abs() <= bound * 8).all()
+    assert _native.native().gemm_f32_nt(a, b, out_dtype=torch.bfloat16).dtype == torch.bfloat16

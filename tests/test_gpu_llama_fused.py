@@ -48,6 +48,36 @@ def test_lora_rank_r_kernels_match_fp32():
         assert _rel(dA[p], du[:, p * r:(p + 1) * r].t() @ x.float()) < 2e-2
 
 
+@pytest.mark.parametrize("splits", [2, 4])
+def test_lora_rank_r_split_stacks_match_fp32(splits):
+    """t / du as split-partial stacks [S, M, W] (what the fused layer uses): lora_down and lora_bwd_t
+    write one slice per split, every consumer sums them."""
+    torch.manual_seed(1)
+    C = _C()
+    M, K, N, r, P = 128, 1024, 512, 16, 3
+    bf = torch.bfloat16
+    x = torch.randn(M, K, device="cuda", dtype=bf)
+    A = [torch.randn(r, K, device="cuda", dtype=bf) * 0.1 for _ in range(P)]
+    t = torch.full((splits, M, 4 * r), float("nan"), device="cuda")[:, :, :P * r]
+    C.lora_down(x, A, t)
+    ref_t = torch.cat([x.float() @ a.float().t() for a in A], 1)
+    assert _rel(t.sum(0), ref_t) < 1e-2
+    dy = torch.randn(M, P * N, device="cuda", dtype=bf)
+    B = [torch.randn(N, r, device="cuda", dtype=bf) * 0.1 for _ in range(P)]
+    dB = [torch.empty_like(b) for b in B]
+    du = torch.full((splits, M, 4 * r), float("nan"), device="cuda")[:, :, :P * r]
+    C.lora_bwd_t(dy, N, B, dB, t, du, 1.5)
+    tsum = t.sum(0)
+    for p in range(P):
+        dyp = dy[:, p * N:(p + 1) * N].float()
+        assert _rel(du.sum(0)[:, p * r:(p + 1) * r], 1.5 * dyp @ B[p].float()) < 1e-2
+        assert _rel(dB[p], 1.5 * dyp.t() @ tsum[:, p * r:(p + 1) * r]) < 2e-2
+    dA = [torch.empty_like(a) for a in A]
+    C.lora_bwd_a(x, dA, du)
+    for p in range(P):
+        assert _rel(dA[p], du.sum(0)[:, p * r:(p + 1) * r].t() @ x.float()) < 2e-2
+
+
 def test_lora_dropout_mask_rate_and_regeneration():
     """keep rate 1 - p; the same rng record regenerates the same mask in every kernel."""
     from hyperion.ops import _native
