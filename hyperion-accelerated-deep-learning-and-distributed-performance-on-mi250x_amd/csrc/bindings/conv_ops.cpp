@@ -361,10 +361,46 @@ at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_r
   return dx;
 }
 
+// Deferred weight-gradient reduce (per device): the split-K reduce of the last conv_wgrad(defer=True)
+// waits here and rides on the next conv_wgrad launch as extra workgroups; conv_wgrad_flush() runs
+// it standalone.  The partials tensor and the OUTPUT's storage are held until the kernel that uses
+// them is queued (stream order protects the reuse of their memory after that).  The output is held
+// by storage, not as a tensor: an extra tensor reference would stop AccumulateGrad from stealing
+// the gradient (it would clone the not-yet-reduced values instead).
+struct PendingWgrad {
+  at::Tensor part;
+  c10::Storage out_storage;
+  void* out = nullptr;
+  int out_dtype = 0;
+  int64_t n = 0;
+  int splits = 0;
+  float alpha = 1.f;
+  hipStream_t stream = nullptr;
+};
+// leaked on purpose: no tensor destructor may run after the HIP runtime is torn down at exit
+PendingWgrad* const g_pending_wgrad = new PendingWgrad[64];
+
+bool conv_wgrad_flush_dev(int dev) {
+  PendingWgrad& p = g_pending_wgrad[dev];
+  if (!p.part.defined()) return false;
+  PendingWgrad q = std::move(p);
+  p = PendingWgrad{};
+  HYP_CHECK_HIP(hyp::splitk_reduce(q.out_dtype, q.part.data_ptr<float>(), q.out, q.n, q.splits, q.stream, q.alpha));
+  return true;
+}
+
+bool conv_wgrad_flush() {
+  bool any = false;
+  for (int d = 0; d < 64; ++d) any |= conv_wgrad_flush_dev(d);
+  return any;
+}
+
 // dy [N,K,P,Q] channels-last, x [N,C,H,W] channels-last -> dW [K,C,R,S] channels-last (x's dtype)
 // bm / bn / splits < 0: automatic plan (conv_wgrad_plan); explicit values are for tuning sweeps.
+// defer: leave this gradient's split-K reduce pending (see PendingWgrad); the values of the
+// returned tensor are final only after the next conv_wgrad launch or conv_wgrad_flush().
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int64_t S, int64_t sh, int64_t sw,
-                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_, double alpha) {
+                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_, double alpha, bool defer) {
   HYP_CHECK_CUDA_TENSOR(x);
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4D tensors");
@@ -390,10 +426,37 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int6
   }
   at::Tensor part;
   if (splits > 1) part = at::empty({(int64_t)splits * K * R * S * C}, x.options().dtype(at::kFloat));
+  const int dev = x.device().index() < 0 ? 0 : x.device().index();
+  PendingWgrad& pend = g_pending_wgrad[dev];
+  hipStream_t stream = cur_stream();
+  if (pend.part.defined() && pend.stream != stream) conv_wgrad_flush_dev(dev);  // other stream: no chaining
+  hyp::WgradPendingReduce pr{};
+  PendingWgrad taken;
+  if (pend.part.defined()) {
+    taken = std::move(pend);
+    pend = PendingWgrad{};
+    pr.part = taken.part.data_ptr<float>();
+    pr.out = taken.out;
+    pr.n = taken.n;
+    pr.splits = taken.splits;
+    pr.alpha = taken.alpha;
+    pr.dtype = taken.out_dtype;
+  }
+  const bool defer_now = defer && splits > 1;
   HYP_CHECK_HIP(hyp::conv_wgrad(dtype_code(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                                 splits > 1 ? part.data_ptr<float>() : nullptr, device_zero_page(x.device()), N, H,
                                 W, C, K, P, Q, (int)R, (int)S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, splits, per,
-                                cur_stream(), (float)alpha));
+                                stream, (float)alpha, pr.part != nullptr ? &pr : nullptr, defer_now));
+  if (defer_now) {
+    pend.part = part;
+    pend.out_storage = dw.storage();
+    pend.out = dw.data_ptr();
+    pend.out_dtype = dtype_code(dw);
+    pend.n = (int64_t)K * R * S * C;
+    pend.splits = splits;
+    pend.alpha = (float)alpha;
+    pend.stream = stream;
+  }
   return dw;
 }
 
@@ -545,7 +608,10 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
-        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("alpha") = 1.0);
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("alpha") = 1.0,
+        pybind11::arg("defer") = false);
+  m.def("conv_wgrad_flush", &conv_wgrad_flush,
+        "run a deferred weight-gradient split-K reduce now (returns whether one was pending)");
   m.def("bn_fwd_sums", &bn_fwd_sums, "BN apply (inline finalize) from conv-epilogue statistics sums");
 }
 

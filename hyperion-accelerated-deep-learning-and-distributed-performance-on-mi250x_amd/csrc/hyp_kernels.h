@@ -246,9 +246,22 @@ int conv_fwd_splits(int M, int K, int nk, int bm, int bn);
 // splits > 1, reduced + cast into dw by a second kernel).
 bool conv_wgrad_supported(int C, int K);
 void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* splits, int* steps_per_split);
+// A weight gradient's split-K reduce (out = alpha * Σ_s part[s] in dtype) deferred into the NEXT
+// conv_wgrad launch, which runs it in extra workgroups beside its own tiles (one launch less per
+// layer; ops/conv.py chains them and flushes the last one at the end of backward).
+struct WgradPendingReduce {
+  const float* part;
+  void* out;
+  int64_t n;
+  int splits;
+  float alpha;
+  int dtype;
+  int blocks;  // filled by conv_wgrad
+};
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
-                      int bn, int splits, int steps_per_split, hipStream_t st, float alpha = 1.f);
+                      int bn, int splits, int steps_per_split, hipStream_t st, float alpha,
+                      const WgradPendingReduce* pending = nullptr, bool defer_reduce = false);
 }  // namespace hyp
 
 namespace hyp {

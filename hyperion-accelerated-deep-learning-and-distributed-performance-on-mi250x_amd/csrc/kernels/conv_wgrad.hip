@@ -45,7 +45,46 @@ struct WgradArgs {
   uint64_t mq, mpq;  // magic multipliers: floor(m / Q) = (m * mq) >> 36 (same for P*Q)
   float alpha;       // output scale (splits == 1: applied in the store; else in the reduce)
   int dn, dpq;       // one 64-pixel stage = dn images + dpq pixels (kBP = dn * P*Q + dpq)
+  WgradPendingReduce pr;  // an EARLIER weight gradient's split-K reduce, run by extra workgroups
+  int nwg_main;           // workgroups of this gradient (blockIdx.x >= nwg_main: the pending reduce)
 };
+
+// The deferred split-K reduce of a previous weight gradient (WgradPendingReduce): workgroup b of
+// the extra range sums quads [64 b, 64 b + 64) (stride: every extra workgroup) — 4 split lanes per
+// quad combined in lane order through LDS, the fixed order of splitk_reduce4_k (deterministic).
+__device__ __forceinline__ void pending_reduce_block(const WgradPendingReduce& pr, int b, int nb, f32x4* red) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t nq = pr.n / 4, sn = nq;
+  for (int64_t q0 = (int64_t)b * 64; q0 < nq; q0 += (int64_t)nb * 64) {
+    const int64_t iq = q0 + tx;
+    const bool ok = iq < nq;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    if (ok) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(pr.part) + iq;
+      int s = ty;
+      for (; s + 4 < pr.splits; s += 8) {
+        a0 += __builtin_nontemporal_load(src + (int64_t)s * sn);
+        a1 += __builtin_nontemporal_load(src + (int64_t)(s + 4) * sn);
+      }
+      if (s < pr.splits) a0 += __builtin_nontemporal_load(src + (int64_t)s * sn);
+    }
+    f32x4 acc = a0 + a1;
+    __syncthreads();
+    if (ty > 0) red[(ty - 1) * 64 + tx] = acc;
+    __syncthreads();
+    if (ty == 0 && ok) {
+      acc = ((acc + red[tx]) + red[64 + tx]) + red[128 + tx];
+      acc *= pr.alpha;
+      if (pr.dtype == kBF16) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st1<bf16_t>(static_cast<bf16_t*>(pr.out) + iq * 4 + e, acc[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st1<f16_t>(static_cast<f16_t*>(pr.out) + iq * 4 + e, acc[e]);
+      }
+    }
+  }
+}
 
 // floor(x / d) with magic = ceil(2^36 / d): exact while x * d < 2^36 (host: M < 2^22, P*Q < 2^14)
 __device__ __forceinline__ int fdiv(int x, uint64_t magic) { return (int)(((uint64_t)(uint32_t)x * magic) >> 36); }
@@ -113,6 +152,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
+  if ((int)blockIdx.x >= a.nwg_main) {
+    pending_reduce_block(a.pr, blockIdx.x - a.nwg_main, gridDim.x - a.nwg_main, reinterpret_cast<f32x4*>(smem));
+    return;
+  }
   const int RSC = a.R * a.S * a.C;
   const int tiles_k = (a.K + BM - 1) / BM, tiles_c = RSC / BN, ntiles = tiles_k * tiles_c;
   const int nwg = ntiles * a.splits;
@@ -275,6 +318,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_dense_k(const WgradArgs a
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
+  if ((int)blockIdx.x >= a.nwg_main) {
+    pending_reduce_block(a.pr, blockIdx.x - a.nwg_main, gridDim.x - a.nwg_main, reinterpret_cast<f32x4*>(smem));
+    return;
+  }
   const int K = a.K, C = a.C, M = a.M;
   const int tiles_k = (K + BM - 1) / BM, tiles_c = C / BN, ntiles = tiles_k * tiles_c;
   const int bid = xcd_remap(blockIdx.x, ntiles * a.splits);
@@ -686,7 +733,7 @@ int g_wgrad_kp = 0;      // pixels per LDS stage of the dense kernel
 template <typename T, int BM, int BN, bool DENSE>
 hipError_t launch_d(const WgradArgs& a, hipStream_t st, int nb, int kp) {
   const int tiles = ((a.K + BM - 1) / BM) * (a.R * a.S * a.C / BN);
-  const dim3 grid(tiles * a.splits);
+  const dim3 grid(tiles * a.splits + a.pr.blocks);
   if (DENSE && g_wgrad_lean) {
     if (kp == 128) {  // 3 stages of 128 pixels fit 160 KiB of LDS up to 128 x 64 tiles
       if constexpr (BM + BN <= 192) {
@@ -748,7 +795,8 @@ void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* s
 
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
-                      int bn, int splits, int steps_per_split, hipStream_t st, float alpha) {
+                      int bn, int splits, int steps_per_split, hipStream_t st, float alpha,
+                      const WgradPendingReduce* pending, bool defer_reduce) {
   if (!conv_wgrad_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (C % bn != 0 || (bm != 64 && bm != 128) || (bn != 64 && bn != 128) || splits < 1) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
@@ -761,6 +809,16 @@ hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float*
               splits > 1 ? static_cast<void*>(partials) : dw, static_cast<const uint16_t*>(zero), N, H, W, C, K, P, Q,
               R, S, sh, sw, ph, pw, (int)M64, splits, steps_per_split, magic36(Q), magic36(P * Q), alpha,
               kBP / (P * Q), kBP % (P * Q)};
+  a.pr = WgradPendingReduce{};
+  if (pending != nullptr && pending->part != nullptr) {
+    if (pending->n % 4 != 0 || pending->splits < 1 || (pending->dtype != kBF16 && pending->dtype != kF16))
+      return hipErrorInvalidValue;
+    a.pr = *pending;
+    // one extra workgroup per 64 output quads, at most 256 (they loop)
+    const int64_t want = (pending->n / 4 + 63) / 64;
+    a.pr.blocks = (int)(want < 256 ? want : 256);
+  }
+  a.nwg_main = ((K + bm - 1) / bm) * (R * S * C / bn) * splits;
   hipError_t e;
   if (dtype == kBF16) {
     if (bm == 128 && bn == 128) e = launch<bf16_t, 128, 128>(a, st);
@@ -773,7 +831,7 @@ hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float*
     else if (bn == 128) e = launch<f16_t, 64, 128>(a, st);
     else e = launch<f16_t, 64, 64>(a, st);
   }
-  if (e != hipSuccess || splits == 1) return e;
+  if (e != hipSuccess || splits == 1 || defer_reduce) return e;
   return splitk_reduce(dtype, partials, dw, (int64_t)K * R * S * C, splits, st, alpha);  // C % 64 == 0: n % 4 == 0
 }
 

@@ -183,7 +183,40 @@ def branch_sum_link(x: torch.Tensor) -> Optional[BranchSumLink]:
     return BranchSumLink(x) if FUSE_SHORTCUT_GRAD else None
 
 
-def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+# Deferred weight-gradient reduce: a split-K weight gradient's reduce kernel is not launched; it rides
+# on the NEXT conv_wgrad launch as extra workgroups (csrc/kernels/conv_wgrad.hip WgradPendingReduce),
+# ~50 launches fewer per ResNet-50 backward.  Safe only when nothing reads the gradient before that
+# launch: the weight must be a leaf whose .grad is None (AccumulateGrad steals the tensor — no add
+# or cast kernel reads it), and every in-backward reader of .grad (DDP / FSDP gradient hooks) calls
+# flush_wgrad() first; the last pending reduce runs at the end of the backward pass (engine callback).
+DEFER_WGRAD_REDUCE = os.environ.get("HYPERION_WGRAD_DEFER", "1") == "1"
+_defer_state = {"pending": False, "queued": False}
+
+
+def flush_wgrad() -> None:
+    """Run a deferred weight-gradient reduce now (no-op when none is pending)."""
+    _defer_state["queued"] = False
+    if _defer_state["pending"]:
+        _defer_state["pending"] = False
+        _native.native().conv_wgrad_flush()
+
+
+def _can_defer(w_param: Optional[torch.Tensor]) -> bool:
+    # (grad mode off: a create_graph backward would make AccumulateGrad clone, not steal)
+    if not (DEFER_WGRAD_REDUCE and w_param is not None and w_param.grad is None and not _streams.enabled()
+            and not torch.is_grad_enabled()):
+        return False
+    if not _defer_state["queued"]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush_wgrad)
+        except RuntimeError:  # not inside a backward pass: nobody would flush
+            return False
+        _defer_state["queued"] = True
+    return True
+
+
+def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
+           w_param: Optional[torch.Tensor] = None) -> torch.Tensor:
     # csrc/kernels/conv_wgrad.hip: split-K MFMA GEMM over the output pixels with transposed LDS
     # reads (one kernel + one deterministic partial-sum/cast kernel; MIOpen used 3-4 launches).
     # (hipBLASLt on the 1x1 case dYᵀ·X runs a 10⁵-long reduction without split-K: 10x slower.)
@@ -193,7 +226,11 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) 
             and _native.use_native(x, op="wgrad")):
         dyc = dy.contiguous(memory_format=torch.channels_last)
         _native.count("wgrad")
-        return _native.native().conv_wgrad(dyc, x, R, S, stride[0], stride[1], padding[0], padding[1])
+        defer = _can_defer(w_param)
+        dw = _native.native().conv_wgrad(dyc, x, R, S, stride[0], stride[1], padding[0], padding[1], defer=defer)
+        if defer:
+            _defer_state["pending"] = True
+        return dw
     _native.count("wgrad_vendor")
     return torch.ops.aten.convolution_backward(dy, x, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
@@ -225,6 +262,7 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.cfg = (stride, padding, act, residual is not None)
         ctx.links = (link_in, link_out, branch, bidx)
         ctx.prod = prod  # the BNGradLink of the fused layer that produced x (or None)
+        ctx.w_param = w if (w.is_leaf and w.requires_grad) else None  # (deferred wgrad reduce)
         # this layer's own link for the conv that will consume `out` (reached as out.grad_fn.bnlink)
         mode = (2 if residual is not None else 1) if act else 0
         ctx.bnlink = (BNGradLink(yc, bn_w, bn_b, mean, invstd, mode, ctx.bsums)
@@ -276,7 +314,7 @@ class _ConvBNActFn(torch.autograd.Function):
                 # producer sees a summed gradient and takes its full path)
                 dx = _dgrad(dyc, x, w, stride, padding, addend=add, bn=prod)
         if dw is None and ctx.needs_input_grad[1]:
-            dw = _wgrad(dyc, x, w, stride, padding)
+            dw = _wgrad(dyc, x, w, stride, padding, w_param=ctx.w_param)
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
                 dres, None, None, None, None, None, None, None, None, None, None)
 

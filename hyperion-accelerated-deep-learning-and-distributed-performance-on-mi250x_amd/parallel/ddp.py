@@ -41,6 +41,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import streams as _streams
+from ..ops.conv import flush_wgrad as _flush_wgrad
 from ..utils.nvtx import range_push, range_pop
 from .comm import get_comm
 
@@ -183,6 +184,7 @@ class DistributedDataParallel(nn.Module):
     def _grad_ready(self, p: nn.Parameter) -> None:
         if not self._sync or p.grad is None:
             return
+        _flush_wgrad()  # a deferred weight-gradient reduce may still owe this gradient its values
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)

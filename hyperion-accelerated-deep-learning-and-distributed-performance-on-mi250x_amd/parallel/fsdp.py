@@ -47,6 +47,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import streams as _streams
+from ..ops.conv import flush_wgrad as _flush_wgrad
 from ..ops.optim import clip_grad_norm_
 from ..train import segments as _seg
 from .comm import get_comm
@@ -251,6 +252,7 @@ class _FlatGroup:
             return False
         buf = self._grad_buf()
         o, n = self.offsets[i], self.numels[i]
+        _flush_wgrad()  # a deferred weight-gradient reduce may still owe this gradient its values
         if p.grad.is_cuda:
             _streams.join(p.grad.device)  # produced on the weight-gradient side stream
         with torch.no_grad():

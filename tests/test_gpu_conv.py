@@ -569,3 +569,69 @@ def test_resnet_training_mode_forward_under_no_grad():
     with torch.no_grad():
         y = m(x)
     assert torch.isfinite(y.float()).all()
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_deferred_wgrad_reduce_is_exact(accumulate):
+    """Weight-gradient split-K reduces chained into the next conv_wgrad launch (ops/conv.py
+    DEFER_WGRAD_REDUCE) give bit-identical gradients to the standalone reduce kernels (two bottleneck
+    blocks, BN-backward fusion off so the A/B is bitwise); with gradients already allocated
+    (accumulation: AccumulateGrad reads dW at once) nothing is deferred."""
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import Bottleneck
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(Bottleneck(256, 64), Bottleneck(256, 64)).cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    x0 = torch.randn(8, 256, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, 256, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run(defer):
+        hconv.DEFER_WGRAD_REDUCE = defer
+        hconv.FUSE_BN_BACKWARD = False
+        try:
+            for p in m.parameters():
+                p.grad = torch.ones_like(p) if accumulate else None
+            m(x0).backward(gy)
+            torch.cuda.synchronize()
+            assert not hconv._defer_state["pending"]
+            return [p.grad.float().clone() for p in m.parameters()]
+        finally:
+            hconv.DEFER_WGRAD_REDUCE = True
+            hconv.FUSE_BN_BACKWARD = True
+
+    ref = run(False)
+    got = run(True)
+    for u, v in zip(ref, got):
+        assert torch.equal(u, v)
+
+
+def test_deferred_wgrad_reduce_resnet50_matches():
+    """The chained reduces across a whole ResNet-50 backward: gradients agree with the standalone
+    reduce path to the run-to-run noise of the BN statistics atomics."""
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import resnet50
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=16).cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    x0 = torch.randn(8, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, 16, device="cuda").bfloat16()
+
+    def run(defer):
+        hconv.DEFER_WGRAD_REDUCE = defer
+        try:
+            for p in m.parameters():
+                p.grad = None
+            m(x0).backward(gy)
+            torch.cuda.synchronize()
+            return [p.grad.float().clone() for p in m.parameters()]
+        finally:
+            hconv.DEFER_WGRAD_REDUCE = True
+
+    ref, ref2, got = run(False), run(False), run(True)
+    for u, u2, v in zip(ref, ref2, got):
+        noise = (u2 - u).norm().item()
+        assert (v - u).norm().item() <= 4 * noise + 1e-2 * u.norm().item() + 1e-6
