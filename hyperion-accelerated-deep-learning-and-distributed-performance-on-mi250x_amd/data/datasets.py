@@ -50,6 +50,17 @@ class WikiText2TorchDataset(Dataset):
         m = torch.ones_like(ids) if m is None else torch.as_tensor(m, dtype=torch.long)
         return ids, m
 
+    def tensors(self):
+        """[N, 128] token ids and mask (fixed-length rows: the tokenizer padded to max_length)."""
+        if self._ids is not None:
+            ids = torch.as_tensor(self._ids, dtype=torch.long)
+            m = torch.ones_like(ids) if self._mask is None else torch.as_tensor(self._mask, dtype=torch.long)
+            return ids, m
+        cols = self.ds.with_format("torch")  # HF datasets: columnar, no per-sample Python
+        ids = cols["input_ids"].long()
+        m = cols["attention_mask"].long() if "attention_mask" in self.ds.column_names else torch.ones_like(ids)
+        return ids, m
+
 
 class CIFAR10TorchDataset(Dataset):
     def __init__(self, data: Sequence):
@@ -61,6 +72,9 @@ class CIFAR10TorchDataset(Dataset):
     def __getitem__(self, i: int):
         img, label = self.data[i]
         return img, label
+
+    def tensors(self):
+        return torch.stack([d[0] for d in self.data]), torch.as_tensor([int(d[1]) for d in self.data])
 
 
 class TensorPairDataset(Dataset):
@@ -75,6 +89,9 @@ class TensorPairDataset(Dataset):
 
     def __getitem__(self, i: int):
         return self.x[i], self.y[i]
+
+    def tensors(self):
+        return self.x, self.y
 
 
 def load_wikitext2(path: str, split: Optional[str] = None):

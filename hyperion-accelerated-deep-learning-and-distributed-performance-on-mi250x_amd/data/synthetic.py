@@ -47,6 +47,9 @@ class SyntheticWikiText2(Dataset):
     def __getitem__(self, i: int):
         return self.input_ids[i], self.attention_mask[i]
 
+    def tensors(self):
+        return self.input_ids, self.attention_mask
+
 
 class SyntheticCIFAR10(Dataset):
     def __init__(self, n: int = CIFAR10_TRAIN, num_classes: int = 10, image: int = 32, seed: int = 0):
@@ -59,6 +62,9 @@ class SyntheticCIFAR10(Dataset):
 
     def __getitem__(self, i: int):
         return self.x[i], int(self.y[i])
+
+    def tensors(self):
+        return self.x, self.y
 
 
 class SyntheticImageNet(Dataset):
@@ -76,3 +82,6 @@ class SyntheticImageNet(Dataset):
 
     def __getitem__(self, i: int):
         return self.x[i], self.y[i]
+
+    def tensors(self):
+        return self.x, self.y

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 from torch.utils.data import DataLoader
 
 from ..data import DistributedSampler, SyntheticCIFAR10, SyntheticWikiText2, WikiText2TorchDataset, load_wikitext2
-from ..data.loader import DevicePrefetcher
+from ..data.loader import DevicePrefetcher, DeviceTensorLoader, dataset_tensors
 from ..models.simple_lm import GPT2_PAD, GPT2_VOCAB, simple_lm_256
 from ..ops.optim import FusedAdam, clip_grad_norm_
 from ..parallel.launch import cleanup, setup
@@ -64,6 +64,9 @@ class RunOptions:
     # hipGraph-captured steps on GPU (the fwd + bwd + optimizer of one step replayed as one or two
     # graph launches; DDP: all-reduces eager between the two graphs).  None = on for CUDA.
     graph: Optional[bool] = None
+    # GPU: tensor datasets resident in HBM and batched on the device (data/loader.py
+    # DeviceTensorLoader) instead of DataLoader workers + per-step H2D copies
+    device_data: bool = True
     log: Callable[[str], None] = field(default=print)
 
 
@@ -75,6 +78,10 @@ def _out_dir(base_dir: str) -> str:
 
 def _loader(ds, world, rank, batch, opts: RunOptions, device, drop_last=False):
     sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=opts.seed)
+    if device.type == "cuda" and opts.device_data:
+        tensors = dataset_tensors(ds)
+        if tensors is not None:  # the whole dataset resident in HBM, batched on the device
+            return sampler, DeviceTensorLoader(tensors, sampler, batch, device, drop_last=drop_last)
     dl = DataLoader(ds, batch_size=batch, sampler=sampler, num_workers=opts.num_workers if device.type == "cuda" else 0,
                     pin_memory=device.type == "cuda", drop_last=drop_last, persistent_workers=False)
     return sampler, DevicePrefetcher(dl, device)
@@ -132,8 +139,8 @@ class _EpochRunner:
         from ..parallel.fsdp import FullyShardedDataParallel
 
         why = ""
-        if isinstance(self.model, FullyShardedDataParallel):
-            why = "FSDP step (hook-driven collectives)"
+        if isinstance(self.model, FullyShardedDataParallel) and not self.model.persistent:
+            why = "FSDP step without persistent buffers (storage released / re-allocated per unit)"
         elif isinstance(self.model, DistributedDataParallel) and not (self.model.bucketed and
                                                                       not self.model.broadcast_buffers):
             why = "DDP with per-forward buffer broadcasts"
@@ -153,8 +160,9 @@ class _EpochRunner:
         if self.graph and inputs is not None and self._graphable():
             if self._captured is None:
                 self._captured = _CapturedStep(self, loss_fn, inputs)
-            self.global_step += 1
-            return self._captured(inputs)
+            if self._captured.fits(inputs):  # (a short last batch runs eagerly)
+                self.global_step += 1
+                return self._captured(inputs)
         inputs = inputs or ()
         self.opt.zero_grad(set_to_none=True)
         with self._autocast():
@@ -197,14 +205,19 @@ class _CapturedStep:
     Hyperion DDP: graph 1 = forward + backward (gradient hooks only pack buckets,
     ``defer_allreduce``), the bucket all-reduces run eagerly on the comm stream, graph 2 = clip +
     optimizer — no RCCL call is recorded into a graph (same split as ``train/step.py``).
+    Hyperion FSDP (persistent buffers): the whole step as graph segments with every all-gather /
+    reduce-scatter / clip all-reduce an eager hole between them (``train/segments.py``).
     Inputs are copied into persistent buffers each step; outputs are the captured step's tensors.
     """
 
     def __init__(self, runner: "_EpochRunner", loss_fn, inputs: tuple, warmup: int = 3):
         from ..ops.multi_tensor import flush_pending
         from ..parallel.ddp import DistributedDataParallel
+        from ..parallel.fsdp import FullyShardedDataParallel
+        from .segments import SegmentedGraph
 
         self.r = runner
+        self.seg: Optional[SegmentedGraph] = None
         self.fn = loss_fn
         self.static = [t.clone() if isinstance(t, torch.Tensor) else t for t in inputs]
         m = runner.model
@@ -228,7 +241,10 @@ class _CapturedStep:
         self.g1 = torch.cuda.CUDAGraph()
         self.g2: Optional[torch.cuda.CUDAGraph] = None
         try:
-            if self.ddp is None:
+            if isinstance(m, FullyShardedDataParallel):
+                self.seg = SegmentedGraph()
+                self.out = self.seg.capture(lambda: self._full(zero_in_place=scaled))
+            elif self.ddp is None:
                 with torch.cuda.graph(self.g1):
                     self.out = self._full(zero_in_place=scaled)
             else:
@@ -275,10 +291,17 @@ class _CapturedStep:
         self._update()
         return out
 
+    def fits(self, inputs: tuple) -> bool:
+        return all(not isinstance(st, torch.Tensor) or (isinstance(t, torch.Tensor) and t.shape == st.shape)
+                   for st, t in zip(self.static, inputs))
+
     def __call__(self, inputs: tuple):
         for st, t in zip(self.static, inputs):
             if isinstance(st, torch.Tensor) and st.data_ptr() != t.data_ptr():
                 st.copy_(t, non_blocking=True)
+        if self.seg is not None:
+            self.seg.replay()
+            return self.out
         self.g1.replay()
         if self.g2 is not None:
             self.ddp.allreduce_buckets()

@@ -102,3 +102,25 @@ def test_prepare_cifar10_binary(tmp_path):
     pairs = load_cifar10_pt(str(tmp_path / "out" / "cifar10_train.pt"))
     x, y = pairs[0]
     assert x.shape == (3, 32, 32) and y == 0 and float(x.min()) >= -1.0 and float(x.max()) <= 1.0
+
+
+def test_device_tensor_loader_matches_dataloader_batches():
+    """DeviceTensorLoader (whole dataset resident, batched by index_select) yields exactly the
+    DataLoader's batches for the same DistributedSampler — every rank, every epoch, short last batch."""
+    import torch
+    from torch.utils.data import DataLoader
+
+    from hyperion.data import DistributedSampler, SyntheticCIFAR10, SyntheticWikiText2
+    from hyperion.data.loader import DeviceTensorLoader, dataset_tensors
+
+    for ds in (SyntheticWikiText2(n=70, seed=3), SyntheticCIFAR10(n=70, seed=3)):
+        for rank in (0, 1):
+            s = DistributedSampler(ds, num_replicas=2, rank=rank, shuffle=True, seed=5)
+            dev = DeviceTensorLoader(dataset_tensors(ds), s, 8, torch.device("cpu"))
+            ref = DataLoader(ds, batch_size=8, sampler=s)
+            for ep in (0, 1):
+                s.set_epoch(ep)
+                a, b = list(dev), list(ref)
+                assert len(a) == len(b) == len(dev)
+                for x, y in zip(a, b):
+                    assert all(torch.equal(u, torch.as_tensor(v)) for u, v in zip(x, y))
