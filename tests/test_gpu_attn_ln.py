@@ -21,7 +21,9 @@ def _ref_attn(q, k, v, causal, kpm=None):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,S,H,D", [(2, 16, 8, 64), (3, 127, 4, 64), (2, 128, 2, 128), (1, 200, 3, 64)])
+@pytest.mark.parametrize(
+    "B,S,H,D", [(2, 16, 8, 64), (3, 127, 4, 64), (2, 128, 2, 128), (1, 200, 3, 64), (1, 197, 2, 64), (1, 600, 2, 128)]
+)
 @pytest.mark.parametrize("causal", [False, True])
 def test_attention_fwd_bwd(dtype, B, S, H, D, causal):
     from hyperion.ops.attention import _AttnFn
