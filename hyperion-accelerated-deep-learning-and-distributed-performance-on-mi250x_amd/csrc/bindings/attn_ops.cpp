@@ -74,7 +74,10 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   const at::DeviceGuard guard(q.device());
   auto fopt = q.options().dtype(at::kFloat);
   auto delta = at::empty({(int64_t)B * H * S}, fopt);
-  auto dq_acc = at::empty({(int64_t)B * H * S * D}, fopt);
+  // fp32 dQ workspace only when several key blocks add into one dQ row (attn_bwd_k stores dQ
+  // directly for S <= 128)
+  at::Tensor dq_acc;
+  if (S > 128) dq_acc = at::empty({(int64_t)B * H * S * D}, fopt);
   at::Tensor kpm_u8;
   if (kpm.has_value() && kpm->defined()) kpm_u8 = kpm->to(at::kByte).contiguous();
   hyp::AttnBwdParams p{};
@@ -90,7 +93,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   p.sdvb = dv.stride(0); p.sdvs = dv.stride(1); p.sdvh = dv.stride(2);
   p.lse = lse.data_ptr<float>();
   p.delta = delta.data_ptr<float>();
-  p.dq_acc = dq_acc.data_ptr<float>();
+  p.dq_acc = dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr;
   p.kpm = kpm_u8.defined() ? kpm_u8.data_ptr<uint8_t>() : nullptr;
   p.B = B; p.H = H; p.S = S; p.D = D;
   p.scale = (float)scale;

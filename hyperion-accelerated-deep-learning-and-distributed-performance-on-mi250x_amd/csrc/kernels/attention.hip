@@ -11,11 +11,8 @@
 // Forward: 128 query rows per workgroup on the 32x32x16 MFMA (details at attn_fwd_k); dropout on P
 // by a counter-based hash of (seed, b, h, q, key) — regenerated in backward; writes O and the
 // log2-domain log-sum-exp per row.
-// Backward (one workgroup = 64 keys of one (b, h); wave w owns 16 keys; loop over query tiles):
-//   * S and dP recomputed with the query on rows, key on the lane; their C tiles are directly the
-//     B operands of dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS (accumulator-as-operand, §3) — no LDS trip;
-//   * dQ = dS·K goes through one bf16 LDS image of dS and is accumulated across key blocks with
-//     fp32 atomics into a [B,H,S,D] workspace, converted by a final pass.
+// Backward: 128 keys per workgroup on the 32x32x16 MFMA (details at attn_bwd_k); dQ stored directly
+// when one key block covers the sequence, else accumulated with fp32 atomics.
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -371,158 +368,267 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_k(AttnBwdParams p) {
   for (int d = lane; d < D; d += 64) acc += MM<T>::tof(o[d]) * MM<T>::tof(g[d]);
   acc = wave_sum(acc);
   if (lane == 0) p.delta[row] = acc;
-  float* dq = p.dq_acc + row * D;
-  for (int d = lane; d < D; d += 64) dq[d] = 0.f;
+  if (p.dq_acc) {
+    float* dq = p.dq_acc + row * D;
+    for (int d = lane; d < D; d += 64) dq[d] = 0.f;
+  }
 }
 
-template <typename T, int D>
-__global__ __launch_bounds__(256) void attn_bwd_k(AttnBwdParams p) {
-  constexpr int NKK = D / 32;
-  constexpr int NN = D / 16;
-  __shared__ __attribute__((aligned(16))) uint16_t Qs[KB * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t dOs[KB * D];
-  __shared__ __attribute__((aligned(16))) uint16_t dOt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t dSs[KB * (KB + 8)];
-  __shared__ float lse_s[KB];
-  __shared__ float delta_s[KB];
+// One workgroup = 4 wave64s = BKB = 128 keys of one (b, h); wave w owns keys kw0 = k0 + 32 w .. +31
+// and keeps dKᵀ, dVᵀ of them in registers ([d][key] 32x32 blocks: key on the lane) while the
+// workgroup sweeps query slices of QS rows (32 for D = 128, 64 for D = 64) — 32x32x16 MFMAs:
+//  * S = Q·Kᵀ and dP = dO·Vᵀ with the KEY on the lane (A = Q / dO rows from LDS, B = this wave's
+//    K rows from LDS / V rows held in registers): their accumulators are directly the B operands
+//    of dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS (§3 accumulator-as-operand; Aᵀ by ds_read_b64_tr_b16 from the
+//    same Q / dO images);
+//  * dS crosses LDS once, as a [key][q] image written 8 bytes per lane, and dQ = dS·K is one
+//    32x32 block per wave (A = dS by transposed reads, B = K by transposed reads of the K image);
+//  * S <= 128 (one key block per (b, h): Llama / LM sequence lengths): dQ is complete inside the
+//    workgroup and is stored directly — no fp32 workspace, no atomics, no conversion pass;
+//    longer sequences add it with fp32 atomics into dq_acc (zeroed by attn_bwd_pre_k, converted by
+//    attn_bwd_post_k);
+//  * Q / dO slices (and their LSE / delta rows) arrive by LDS-DMA into a 2-deep ring, one barrier
+//    pair per slice; XCD-grouped blocks, heaviest (causal) key block first.
+constexpr int BKB = 128;
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 4, c16 = lane & 15;
-  const int bh = blockIdx.y, b = bh / p.H, hd = bh - b * p.H;
-  const int k0 = blockIdx.x * KB;
-  const int key = k0 + 16 * w + c16;  // this lane's key (C-tile column)
+// D = 128 keeps 128 accumulator + 32 V-operand registers per lane live across the sweep: one wave
+// per SIMD with the whole register file (a 256-register cap spilled the V operand to scratch);
+// D = 64 fits two workgroups per CU.
+template <typename T, int D, bool DROP, bool DIRECT>
+__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParams p) {
+  constexpr int NS = D / 16;    // k-steps over the head dim
+  constexpr int NDB = D / 32;   // 32-wide head-dim blocks
+  constexpr int NCH = D / 8;    // 16-byte chunks per row
+  constexpr int QS = 4096 / D;  // query rows per slice
+  constexpr int NQB = QS / 32;  // 32-row query blocks per slice
+  constexpr int SPC = QS * D * 2 / 1024;   // 1-KiB DMA pieces per Q (or dO) slice
+  constexpr int KPC = BKB * D * 2 / 1024;  // ... per K tile
+  constexpr int DSU = QS / 4;              // 8-byte units per dSᵀ row
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[BKB * D];
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[2][QS * D];
+  __shared__ __attribute__((aligned(16))) uint16_t dOs[2][QS * D];
+  __shared__ __attribute__((aligned(16))) uint16_t dSt[BKB * QS];
+  __shared__ __attribute__((aligned(16))) float lse_s[2][64];
+  __shared__ __attribute__((aligned(16))) float del_s[2][64];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int nkb = (p.S + BKB - 1) / BKB;
+  const int total = nkb * p.B * p.H;
+  int bid = blockIdx.x;
+  {
+    const int q8 = total / 8, r8 = total % 8, xcd = bid % 8, idx = bid / 8;
+    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
+  }
+  const int bh = bid / nkb, kblk = bid - bh * nkb;
+  const int b = bh / p.H, hd = bh - b * p.H;
+  const int k0 = kblk * BKB, kw0 = k0 + 32 * w, key = kw0 + r;
   const uint16_t* qb = static_cast<const uint16_t*>(p.q) + b * p.sqb + hd * p.sqh;
   const uint16_t* kb = static_cast<const uint16_t*>(p.k) + b * p.skb + hd * p.skh;
   const uint16_t* vb = static_cast<const uint16_t*>(p.v) + b * p.svb + hd * p.svh;
   const uint16_t* gb = static_cast<const uint16_t*>(p.dout) + b * p.sdob + hd * p.sdoh;
+  const float* lse_g = p.lse + (int64_t)bh * p.S;
+  const float* del_g = p.delta + (int64_t)bh * p.S;
 
-  u16x8 kf[NKK], vf[NKK];
-#pragma unroll
-  for (int kk = 0; kk < NKK; ++kk) {
-    u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-    kf[kk] = key < p.S ? *reinterpret_cast<const u16x8*>(kb + (int64_t)key * p.sks + 8 * h + 32 * kk) : z;
-    vf[kk] = key < p.S ? *reinterpret_cast<const u16x8*>(vb + (int64_t)key * p.svs + 8 * h + 32 * kk) : z;
-  }
-  stage_tile<D, false, true>(kb, p.sks, k0, p.S, nullptr, Kt);
-
-  f32x4 dvt[NN], dkt[NN];
-#pragma unroll
-  for (int n = 0; n < NN; ++n) dvt[n] = dkt[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float inv_keep = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
-  const uint32_t thr = (uint32_t)(p.p_drop * 4294967296.0);
-  const uint64_t seed = p.p_drop > 0.f ? rng_key(p.rng) : 0;  // graph-safe generator state
-  const bool key_masked = key >= p.S || (p.kpm && p.kpm[(int64_t)b * p.S + key] != 0);
-
-  const int nq = (p.S + KB - 1) / KB;
-  const int qt0 = p.causal ? k0 / KB : 0;
-  TileRegs<D> qr, gr;  // the next query tile, in flight while the current one computes
-  float lse_r = INFINITY, delta_r = 0.f;
-  auto load_q = [&](int q0n) {
-    load_tile<D>(qb, p.sqs, q0n, p.S, qr);
-    load_tile<D>(gb, p.sdos, q0n, p.S, gr);
-    if (threadIdx.x < KB) {
-      const int qq = q0n + threadIdx.x;
-      lse_r = qq < p.S ? p.lse[(int64_t)bh * p.S + qq] : INFINITY;
-      delta_r = qq < p.S ? p.delta[(int64_t)bh * p.S + qq] : 0.f;
+  auto dma_rows = [&](const uint16_t* base, int64_t sstride, int row0, uint16_t* img, int npieces) {
+    for (int pc = w; pc < npieces; pc += 4) {
+      const int t = 2 * pc + (lane >> 5);
+      const int row = 8 * (t / (NCH / 4)) + ((lane & 31) >> 2);
+      const int ch = 4 * (t % (NCH / 4)) + ((lane & 3) ^ ((row >> 2) & 3));
+      const int64_t gr = min(row0 + row, p.S - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(base + gr * sstride + ch * 8),
+                                       (void __attribute__((address_space(3)))*)(img + pc * 512), 16, 0, 0);
     }
   };
-  if (qt0 < nq) load_q(qt0 * KB);
-  for (int qt = qt0; qt < nq; ++qt) {
-    const int q0 = qt * KB;
-    __syncthreads();
-    store_tile<D, true, true>(qr, Qs, Qt);
-    store_tile<D, true, true>(gr, dOs, dOt);
-    if (threadIdx.x < KB) {
-      lse_s[threadIdx.x] = lse_r;
-      delta_s[threadIdx.x] = delta_r;
+  auto dma_slice = [&](int q0, int buf) {
+    dma_rows(qb, p.sqs, q0, Qs[buf], SPC);
+    dma_rows(gb, p.sdos, q0, dOs[buf], SPC);
+    if (w < 2) {
+      const float* src = (w == 0 ? lse_g : del_g) + min(q0 + lane, p.S - 1);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (void __attribute__((address_space(3)))*)(w == 0 ? lse_s[buf] : del_s[buf]),
+                                       4, 0, 0);
     }
-    if (qt + 1 < nq) load_q(q0 + KB);
-    __syncthreads();
+  };
 
-    float pd[4][4], ds[4][4];
+  // this wave's V rows as the B operand of dP (key on the lane)
+  u16x8 vf[NS];
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < NS; ++s) {
+    u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    vf[s] = key < p.S ? *reinterpret_cast<const u16x8*>(vb + (int64_t)key * p.svs + 16 * s + 8 * hh) : z;
+  }
+  const bool key_ok = key < p.S && !(p.kpm && p.kpm[(int64_t)b * p.S + key] != 0);
+  const float inv_keep = DROP ? 1.f / (1.f - p.p_drop) : 1.f;
+  const uint32_t thr = (uint32_t)(p.p_drop * 4294967296.0);
+  const uint64_t seed = DROP ? rng_key(p.rng) : 0;  // graph-safe generator state
+
+  const int qstart = p.causal ? (k0 / QS) * QS : 0;
+  const int nsl = qstart < p.S ? (p.S - qstart + QS - 1) / QS : 0;
+  dma_rows(kb, p.sks, k0, Ks, KPC);
+  if (nsl > 0) dma_slice(qstart, 0);
+
+  f32x16 dvt[NDB], dkt[NDB];
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        s = MM<T>::mfma(read_row_chunk(Qs, D, 16 * qq + c16, h + 4 * kk), kf[kk], s);
-        dp = MM<T>::mfma(read_row_chunk(dOs, D, 16 * qq + c16, h + 4 * kk), vf[kk], dp);
-      }
+  for (int n = 0; n < NDB; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * qq + 4 * h + r;
-        const int qg = q0 + ql;
-        bool ok = !key_masked;
-        if (p.causal) ok = ok && key <= qg;
-        const float pv = ok ? exp2f(s[r] * p.scale_log2 - lse_s[ql]) : 0.f;
-        float dpv = dp[r];
-        float pdv = pv;
-        if (p.p_drop > 0.f) {
-          const uint64_t idx = (((uint64_t)bh * p.S + qg) * p.S) + key;
-          const bool keep = hash_keep(seed, idx) >= thr;
-          pdv = keep ? pv * inv_keep : 0.f;
-          dpv = keep ? dpv * inv_keep : 0.f;
+    for (int e = 0; e < 16; ++e) dvt[n][e] = dkt[n][e] = 0.f;
+
+  // per-lane LDS bases (reads of a wave differ by lane-independent constants)
+  const int tr_row = 4 * hh + ((lane & 15) >> 2);
+  const int tr_ch = 2 * ((lane >> 4) & 1) + ((lane & 3) >> 1);
+  int rbase[2], tbase[2];  // row reads (k-step parity) / transposed reads (+8 rows) of a Q-like image
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rbase[i] = (r >> 3) * 8 * D + (r & 7) * 32 + (((2 * i + hh) ^ ((r >> 2) & 3)) << 3);
+    tbase[i] = i * 8 * D + tr_row * 32 + ((tr_ch ^ (hh + 2 * i)) << 3) + 4 * (lane & 1);
+  }
+  // dQ block of this wave and the dSᵀ image swizzle (8-byte units of 4 queries)
+  const int dq_qb = w / NDB, dq_db = w % NDB;
+  auto dsw = [](int row) { return QS == 32 ? ((row >> 1) & 7) : ((row & 15) ^ (((row >> 1) & 1) << 3)); };
+  // dQ operands by transposed reads, key k-step ks (16 keys) at + 16 QS ks / + 16 D ks:
+  //   A = dS[q][key] from the dSᵀ image, B = K[key][d] from the K image; lane (group g, i = 4 qq + pp)
+  //   addresses key row 16 ks + 8 hh + 4 t + qq, query / head-dim columns 16 (g & 1) + 4 pp .. +3
+  int dqa[2], dqb[2];
+  {
+    const int gq = 16 * ((lane >> 4) & 1), qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = 8 * hh + 4 * t + qq;
+      const int u = (32 * dq_qb + gq) / 4 + pp;
+      dqa[t] = row * QS + 4 * (u ^ dsw(row));
+      dqb[t] = img_off<D>(row, 4 * dq_db + (gq >> 3) + (pp >> 1)) + 4 * (pp & 1);
+    }
+  }
+  // dSᵀ write of register group g (block qbk): row 32 w + r, unit 8 qbk + 2 g + hh
+  const int ds_row = 32 * w + r;
+
+  for (int sl = 0; sl < nsl; ++sl) {
+    const int q0 = qstart + sl * QS, cur = sl & 1;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of slice sl (and the K tile) has landed ...
+    __syncthreads();                // ... every wave's; slice sl-1's buffers and dSt are free
+    if (sl + 1 < nsl) dma_slice(q0 + QS, cur ^ 1);
+    const uint16_t* Qc = Qs[cur];
+    const uint16_t* Gc = dOs[cur];
+#pragma unroll
+    for (int qbk = 0; qbk < NQB; ++qbk) {
+      const int qbase = q0 + 32 * qbk;
+      if (p.causal && kw0 > qbase + 31) {  // wave-uniform: the whole block is masked
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int u = 8 * qbk + 2 * g + hh;
+          *reinterpret_cast<uint2*>(dSt + ds_row * QS + 4 * (u ^ dsw(ds_row))) = make_uint2(0u, 0u);
         }
-        pd[qq][r] = pdv;
-        ds[qq][r] = pv * (dpv - delta_s[ql]);
+        continue;
+      }
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sacc[e] = dpacc[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int qo = rbase[s & 1] + 32 * D * qbk + 256 * (s >> 1);
+        const u16x8 kf = *reinterpret_cast<const u16x8*>(Ks + rbase[s & 1] + 32 * D * w + 256 * (s >> 1));
+        sacc = MM32<T>::mfma(*reinterpret_cast<const u16x8*>(Qc + qo), kf, sacc);
+        dpacc = MM32<T>::mfma(*reinterpret_cast<const u16x8*>(Gc + qo), vf[s], dpacc);
+      }
+      // P, dS; register e holds query qbase + crow(e), crow(e) = (e & 3) + 8 (e >> 2) + 4 hh
+      const bool edge = !key_ok || (p.causal && kw0 + 31 > qbase) || qbase + 32 > p.S;
+      u16x8 pb[2], sb[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ql = 32 * qbk + 8 * g + 4 * hh;  // slice-local query of register 4g
+        const float4 ls = *reinterpret_cast<const float4*>(&lse_s[cur][ql]);
+        const float4 dl = *reinterpret_cast<const float4*>(&del_s[cur][ql]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * g + i;
+          float pv = exp2f(fmaf(sacc[e], p.scale_log2, -(&ls.x)[i]));
+          if (edge) {
+            const int qg = q0 + ql + i;
+            if (!key_ok || qg >= p.S || (p.causal && key > qg)) pv = 0.f;
+          }
+          float dpv = dpacc[e], pdv = pv;
+          if constexpr (DROP) {
+            const int qg = q0 + ql + i;
+            const uint64_t idx = (((uint64_t)bh * p.S + qg) * p.S) + key;
+            const bool keep = hash_keep(seed, idx) >= thr;
+            pdv = keep ? pv * inv_keep : 0.f;
+            dpv = keep ? dpv * inv_keep : 0.f;
+          }
+          pb[e >> 3][e & 7] = MM<T>::cvt(pdv);
+          sb[e >> 3][e & 7] = MM<T>::cvt(pv * (dpv - (&dl.x)[i]));
+        }
+      }
+      // dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS  (k = query, the accumulator's permuted order)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int n = 0; n < NDB; ++n) {
+          const int off = 32 * D * qbk + 16 * D * s2 + 256 * n;
+          const u16x4 glo = read_tr(Gc, tbase[0] + off), ghi = read_tr(Gc, tbase[1] + off);
+          const u16x4 qlo = read_tr(Qc, tbase[0] + off), qhi = read_tr(Qc, tbase[1] + off);
+          const u16x8 ga = {glo[0], glo[1], glo[2], glo[3], ghi[0], ghi[1], ghi[2], ghi[3]};
+          const u16x8 qa = {qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]};
+          dvt[n] = MM32<T>::mfma(ga, pb[s2], dvt[n]);
+          dkt[n] = MM32<T>::mfma(qa, sb[s2], dkt[n]);
+        }
+      // dSᵀ image: registers 4g..4g+3 = queries 32 qbk + 8 g + 4 hh + 0..3 of key row 32 w + r
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int u = 8 * qbk + 2 * g + hh;
+        const u16x8& src = sb[g >> 1];
+        const int o4 = 4 * (g & 1);
+        const uint2 v = make_uint2((uint32_t)src[o4] | ((uint32_t)src[o4 + 1] << 16),
+                                   (uint32_t)src[o4 + 2] | ((uint32_t)src[o4 + 3] << 16));
+        *reinterpret_cast<uint2*>(dSt + ds_row * QS + 4 * (u ^ dsw(ds_row))) = v;
       }
     }
-    // dVᵀ += dOᵀ·P_drop ; dKᵀ += Qᵀ·dS    (k = query, permuted order within each 32-step)
+    __syncthreads();  // dSᵀ complete
+    // dQ[32 dq_qb + .., 32 dq_db + ..] = Σ_key dS·K over the workgroup's 128 keys
+    {
+      f32x16 acc;
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      u16x8 bp, bs;
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        bp[r] = MM<T>::cvt(pd[2 * s2][r]);
-        bp[4 + r] = MM<T>::cvt(pd[2 * s2 + 1][r]);
-        bs[r] = MM<T>::cvt(ds[2 * s2][r]);
-        bs[4 + r] = MM<T>::cvt(ds[2 * s2 + 1][r]);
+      for (int ks = 0; ks < BKB / 16; ++ks) {
+        const u16x4 a0 = read_tr(dSt, dqa[0] + 16 * QS * ks), a1 = read_tr(dSt, dqa[1] + 16 * QS * ks);
+        const u16x4 b0 = read_tr(Ks, dqb[0] + 16 * D * ks), b1 = read_tr(Ks, dqb[1] + 16 * D * ks);
+        const u16x8 a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const u16x8 bk = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        acc = MM32<T>::mfma(a, bk, acc);
       }
+      // acc[e] = dQ[query q0 + 32 dq_qb + crow(e)][head dim 32 dq_db + r]
+      const int d = 32 * dq_db + r;
 #pragma unroll
-      for (int n = 0; n < NN; ++n) {
-        const int d = 16 * n + c16;
-        dvt[n] = MM<T>::mfma(read_t_pair(dOt, d, 32 * s2 + 4 * h, 32 * s2 + 16 + 4 * h), bp, dvt[n]);
-        dkt[n] = MM<T>::mfma(read_t_pair(Qt, d, 32 * s2 + 4 * h, 32 * s2 + 16 + 4 * h), bs, dkt[n]);
-      }
-    }
-    // dQ: dS image [q][key] in LDS, then wave w reduces its 16 query rows over the 64 keys
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dSs[(16 * qq + 4 * h + r) * (KB + 8) + 16 * w + c16] = MM<T>::cvt(ds[qq][r]);
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < NN; ++n) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const u16x8 a = *reinterpret_cast<const u16x8*>(dSs + (16 * w + c16) * (KB + 8) + 32 * s2 + 8 * h);
-        const u16x8 bk = *reinterpret_cast<const u16x8*>(Kt + (16 * n + c16) * TS + 32 * s2 + 8 * h);
-        acc = MM<T>::mfma(a, bk, acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qg = q0 + 16 * w + 4 * h + r;
-        if (qg < p.S) atomicAdd(p.dq_acc + ((int64_t)bh * p.S + qg) * D + 16 * n + c16, acc[r] * p.scale);
+      for (int e = 0; e < 16; ++e) {
+        const int qg = q0 + 32 * dq_qb + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (qg < p.S) {
+          if constexpr (DIRECT) {
+            uint16_t* dq = static_cast<uint16_t*>(p.dq) + b * p.sdqb + hd * p.sdqh + (int64_t)qg * p.sdqs;
+            dq[d] = MM<T>::cvt(acc[e] * p.scale);
+          } else {
+            atomicAdd(p.dq_acc + ((int64_t)bh * p.S + qg) * D + d, acc[e] * p.scale);
+          }
+        }
       }
     }
   }
-  // write dK, dV: lane holds [d = 16n + 4h + r][key] for r = 0..3 (4 consecutive d)
+  // dK, dV: lane holds [d = 32 n + 8 g + 4 hh + 0..3][key]
   if (key < p.S) {
     uint16_t* dk = static_cast<uint16_t*>(p.dk) + b * p.sdkb + hd * p.sdkh + (int64_t)key * p.sdks;
     uint16_t* dv = static_cast<uint16_t*>(p.dv) + b * p.sdvb + hd * p.sdvh + (int64_t)key * p.sdvs;
 #pragma unroll
-    for (int n = 0; n < NN; ++n) {
-      u16x4 kv, vv;
+    for (int n = 0; n < NDB; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        kv[r] = MM<T>::cvt(dkt[n][r] * p.scale);
-        vv[r] = MM<T>::cvt(dvt[n][r]);
+      for (int g = 0; g < 4; ++g) {
+        u16x4 kv, vv;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          kv[i] = MM<T>::cvt(dkt[n][4 * g + i] * p.scale);
+          vv[i] = MM<T>::cvt(dvt[n][4 * g + i]);
+        }
+        *reinterpret_cast<u16x4*>(dk + 32 * n + 8 * g + 4 * hh) = kv;
+        *reinterpret_cast<u16x4*>(dv + 32 * n + 8 * g + 4 * hh) = vv;
       }
-      *reinterpret_cast<u16x4*>(dk + 16 * n + 4 * h) = kv;
-      *reinterpret_cast<u16x4*>(dv + 16 * n + 4 * h) = vv;
-    }
   }
 }
 
@@ -553,9 +659,20 @@ hipError_t fwd_launch(const AttnParams& p, hipStream_t st) {
 template <typename T, int D>
 hipError_t bwd_launch(const AttnBwdParams& p, hipStream_t st) {
   const int64_t rows = (int64_t)p.B * p.H * p.S;
+  const bool direct = p.S <= BKB;
+  if (!direct && !p.dq_acc) return hipErrorInvalidValue;
   hipLaunchKernelGGL((attn_bwd_pre_k<T, D>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, p);
-  const dim3 grid((p.S + KB - 1) / KB, p.B * p.H);
-  hipLaunchKernelGGL((attn_bwd_k<T, D>), grid, dim3(256), 0, st, p);
+  const dim3 grid(((p.S + BKB - 1) / BKB) * p.B * p.H);
+  const bool drop = p.p_drop > 0.f;
+  if (direct) {
+    AttnBwdParams q = p;
+    q.dq_acc = nullptr;
+    if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, true>), grid, dim3(256), 0, st, q);
+    else hipLaunchKernelGGL((attn_bwd_k<T, D, false, true>), grid, dim3(256), 0, st, q);
+    return hipGetLastError();
+  }
+  if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, false>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((attn_bwd_k<T, D, false, false>), grid, dim3(256), 0, st, p);
   const int64_t tot = rows * (D / 4);
   hipLaunchKernelGGL((attn_bwd_post_k<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p);
   return hipGetLastError();
