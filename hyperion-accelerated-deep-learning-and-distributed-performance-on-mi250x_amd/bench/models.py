@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import math
 import time
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 
@@ -25,8 +25,12 @@ def _timeit(step, steps: int, warmup: int) -> float:
 
 
 def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", steps: int = 20, warmup: int = 5,
-                  model: str = "lm256", causal: bool = False, graph: bool = False) -> Dict:
-    """SimpleTransformerLM (C14) training step as in train_language_model_ddp (single GPU)."""
+                  model: str = "lm256", causal: bool = False, graph: bool = False,
+                  compute_copies: Optional[bool] = None) -> Dict:
+    """SimpleTransformerLM (C14) training step as in train_language_model_ddp (single GPU).
+    ``compute_copies`` (default for bf16): the parameters live in bf16 with fp32 masters inside
+    FusedAdam (train.amp.cast_for_compute, as the ViT bench) instead of fp32 parameters cast by
+    autocast on every step; fp16 keeps the reference's autocast + loss-scaler methodology."""
     from ..data.synthetic import SyntheticWikiText2
     from ..models.simple_lm import GPT2_PAD, gpt2_small_lm, simple_lm_256
     from ..ops.optim import FusedAdam
@@ -35,15 +39,20 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
     dev = torch.device("cuda")
     torch.manual_seed(0)
     m = (simple_lm_256(causal=causal) if model == "lm256" else gpt2_small_lm()).to(dev)
-    opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True, zero_grad_in_step=graph)
     dt = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[precision]
+    copies = (precision == "bf16") if compute_copies is None else bool(compute_copies and dt is not None)
+    if copies:
+        from ..train.amp import cast_for_compute
+
+        cast_for_compute(m, dt)
+    opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True, zero_grad_in_step=graph)
     scaler = LossScaler(enabled=precision == "fp16", device=dev)
     ids = SyntheticWikiText2(n=batch, seq_len=seq, seed=0).input_ids.to(dev)
     x, y = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
 
     def body():
         opt.zero_grad(set_to_none=not graph)
-        with torch.autocast("cuda", dtype=dt or torch.float32, enabled=dt is not None):
+        with torch.autocast("cuda", dtype=dt or torch.float32, enabled=dt is not None and not copies):
             loss = m.forward_loss(x, y, ignore_index=GPT2_PAD)
         if scaler.enabled:
             scaler.scale(loss).backward()
@@ -59,7 +68,8 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
     step = GraphedClosure(body, warmup=2, module=m) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
-    return {"model": model, "batch": batch, "seq": seq, "precision": precision, "graph": graph, "ms_per_step": t * 1e3,
+    return {"model": model, "batch": batch, "seq": seq, "precision": precision, "graph": graph,
+            "compute_copies": copies, "ms_per_step": t * 1e3,
             "samples_per_s": batch / t, "tokens_per_s": batch * (seq - 1) / t,
             "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
@@ -219,7 +229,7 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
             with torch.autocast("cuda", dtype=bf):
                 loss = m.forward_loss(ids[:, :-1], ids[:, 1:], ignore_index=GPT2_PAD)
         loss.backward()
-        m.clip_grad_norm_(1.0)
+        m.clip_grad_norm_(1.0, defer_to=opt)  # the coefficient is applied inside the Adam kernel
         opt.step()
         return loss.detach()
 

@@ -353,25 +353,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
 }
 
 // ============================================================================ backward
-// delta[bh, q] = Σ_d dO·O ; also zero the fp32 dQ accumulator rows
+// delta[bh, q] = Σ_d dO·O ; also zero the fp32 dQ accumulator rows (when there is one).
+// D / 8 lanes per row, one 16-byte load of O and of dO per lane, a shuffle reduction in the group.
 template <typename T, int D>
 __global__ __launch_bounds__(256) void attn_bwd_pre_k(AttnBwdParams p) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*H*S
-  if (row >= (int64_t)p.B * p.H * p.S) return;
-  const int q = (int)(row % p.S);
-  const int bh = (int)(row / p.S);
-  const int b = bh / p.H, hd = bh - b * p.H;
-  const uint16_t* o = static_cast<const uint16_t*>(p.o) + b * p.sob + hd * p.soh + (int64_t)q * p.sos;
-  const uint16_t* g = static_cast<const uint16_t*>(p.dout) + b * p.sdob + hd * p.sdoh + (int64_t)q * p.sdos;
+  constexpr int LPR = D / 8;  // lanes per row
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;  // over B*H*S
+  const int c = threadIdx.x % LPR;
+  const bool ok = row < (int64_t)p.B * p.H * p.S;
   float acc = 0.f;
-  for (int d = lane; d < D; d += 64) acc += MM<T>::tof(o[d]) * MM<T>::tof(g[d]);
-  acc = wave_sum(acc);
-  if (lane == 0) p.delta[row] = acc;
-  if (p.dq_acc) {
-    float* dq = p.dq_acc + row * D;
-    for (int d = lane; d < D; d += 64) dq[d] = 0.f;
+  if (ok) {
+    const int q = (int)(row % p.S);
+    const int bh = (int)(row / p.S);
+    const int b = bh / p.H, hd = bh - b * p.H;
+    const u16x8 o = *reinterpret_cast<const u16x8*>(static_cast<const uint16_t*>(p.o) + b * p.sob + hd * p.soh +
+                                                    (int64_t)q * p.sos + 8 * c);
+    const u16x8 g = *reinterpret_cast<const u16x8*>(static_cast<const uint16_t*>(p.dout) + b * p.sdob +
+                                                    hd * p.sdoh + (int64_t)q * p.sdos + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += MM<T>::tof(o[e]) * MM<T>::tof(g[e]);
+    if (p.dq_acc) {
+      float4* dq = reinterpret_cast<float4*>(p.dq_acc + row * D + 8 * c);
+      dq[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      dq[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) acc += __shfl_xor(acc, m, 64);
+  if (ok && c == 0) p.delta[row] = acc;
 }
 
 // One workgroup = 4 wave64s = BKB = 128 keys of one (b, h); wave w owns keys kw0 = k0 + 32 w .. +31
@@ -661,7 +670,7 @@ hipError_t bwd_launch(const AttnBwdParams& p, hipStream_t st) {
   const int64_t rows = (int64_t)p.B * p.H * p.S;
   const bool direct = p.S <= BKB;
   if (!direct && !p.dq_acc) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((attn_bwd_pre_k<T, D>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, p);
+  hipLaunchKernelGGL((attn_bwd_pre_k<T, D>), dim3((unsigned)((rows * (D / 8) + 255) / 256)), dim3(256), 0, st, p);
   const dim3 grid(((p.S + BKB - 1) / BKB) * p.B * p.H);
   const bool drop = p.p_drop > 0.f;
   if (direct) {

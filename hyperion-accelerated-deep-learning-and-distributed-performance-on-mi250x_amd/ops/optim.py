@@ -70,6 +70,9 @@ class FusedAdam(torch.optim.Optimizer):
         # optional device scalars set by the AMP scaler
         self.inv_scale: Optional[torch.Tensor] = None
         self.found_inf: Optional[torch.Tensor] = None
+        # a global-norm clip coefficient left for this step by clip_grad_norm_(defer_to=self): the
+        # kernel applies it while it reads the gradients (no separate scaling pass); consumed by step()
+        self.clip_coef: Optional[torch.Tensor] = None
 
     def _state(self, p: torch.Tensor):
         st = self.state[p]
@@ -96,6 +99,10 @@ class FusedAdam(torch.optim.Optimizer):
         if first is None:
             return loss
         native = _native.use_native(first, op="adam")
+        inv_scale = self.inv_scale
+        if self.clip_coef is not None:
+            inv_scale = self.clip_coef if inv_scale is None else self.clip_coef * inv_scale
+            self.clip_coef = None
         if native:
             if self._step_t is None or self._step_t.device != first.device:
                 self._step_t = torch.full((), float(self._host_step - 1), dtype=torch.float32, device=first.device)
@@ -129,17 +136,17 @@ class FusedAdam(torch.optim.Optimizer):
                     _native.native().adam_mt(
                         tab.ptrs, tab.sizes, tab.blocks, tab.T, tab.chunk,
                         float(lr) if lr_t is None else 0.0, b1, b2, group["eps"], group["weight_decay"],
-                        bool(group["adamw"]), lr_t, self._step_t, self.inv_scale, self.found_inf,
+                        bool(group["adamw"]), lr_t, self._step_t, inv_scale, self.found_inf,
                         _native.DTYPE_CODE[gdt], _native.DTYPE_CODE[pdt], bool(self.zero_grad_in_step),
                     )
                 else:
-                    self._reference_step(group, ps, gs, ms, vs, masters)
+                    self._reference_step(group, ps, gs, ms, vs, masters, inv_scale)
                     if self.zero_grad_in_step:
                         for g in gs:
                             g.zero_()
         return loss
 
-    def _reference_step(self, group, ps, gs, ms, vs, masters=None):
+    def _reference_step(self, group, ps, gs, ms, vs, masters=None, inv_scale=None):
         """PyTorch reference (CPU / fallback); identical math to the kernel."""
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             # the host-side step count would be baked into the graph (frozen bias correction)
@@ -153,7 +160,7 @@ class FusedAdam(torch.optim.Optimizer):
         step = self._host_step
         bc1 = 1 - b1**step
         bc2_sqrt = math.sqrt(1 - b2**step)
-        inv = float(self.inv_scale) if self.inv_scale is not None else 1.0
+        inv = float(inv_scale) if inv_scale is not None else 1.0
         for i, (p, g, m, v) in enumerate(zip(ps, gs, ms, vs)):
             w = masters[i] if masters is not None else p
             g = g.float() * inv
@@ -209,12 +216,15 @@ def clip_grad_norm_(
     max_norm: float,
     group: Optional["dist.ProcessGroup"] = None,
     sharded: bool = False,
+    defer_to: Optional[FusedAdam] = None,
 ) -> torch.Tensor:
     """Clip by the global L2 norm.
 
     ``sharded=True``: each rank holds a disjoint shard of the gradients (FSDP); the squared norm
     is all-reduced over ``group`` before clipping — the reference's ``clip_grad_norm_`` on FSDP
     modules skipped this and clipped by the local shard norm.
+    ``defer_to``: a FusedAdam whose next ``step()`` applies the clip coefficient as it reads the
+    gradients (one pass over them fewer); the ``.grad`` tensors themselves are left unclipped.
     """
     params = [p for p in parameters if grad_of(p) is not None]
     grads: List[torch.Tensor] = [grad_of(p) for p in params]
@@ -238,7 +248,9 @@ def clip_grad_norm_(
         from ..train import segments as _seg
 
         _seg.eager(lambda: dist.all_reduce(total_sq, group=group))  # a hole of a segmented capture
-    if native:
+    if defer_to is not None:
+        defer_to.clip_coef = (max_norm / (total_sq.reshape(1).sqrt() + 1e-6)).clamp(max=1.0)
+    elif native:
         _native.native().clip_mt(tab.ptrs, tab.sizes, tab.blocks, tab.chunk, total_sq, float(max_norm), code)
     else:
         coef = (max_norm / (total_sq.sqrt() + 1e-6)).clamp(max=1.0)

@@ -180,6 +180,7 @@ class _FlatGroup:
                         if trainable and self.rdtype != torch.float32 else None)
         self._grad_shard = torch.empty(self.shard_numel, dtype=torch.float32, device=dev) if trainable else None
         self.grad_ready: Set[int] = set()
+        self._pending: List[Tuple[int, torch.Tensor]] = []  # (param index, grad) not yet in full_grad
         self.reduced = False
         # module parameters become views of the full buffer (the same Parameter objects)
         for p, o, n, shp in zip(params, self.offsets, self.numels, self.shapes):
@@ -210,6 +211,11 @@ class _FlatGroup:
         st = self.full.untyped_storage()
         if st.nbytes() != self._full_bytes:
             st.resize_(self._full_bytes)
+        if self.fsdp.world == 1:  # identity gather: one cast-copy of the shard, no staging buffer
+            with torch.no_grad():
+                self.full.data.copy_(self.flat_param.detach())
+            self.gathered = True
+            return
         if self._send_buf is None:
             send = self.flat_param.detach()
         else:
@@ -219,10 +225,6 @@ class _FlatGroup:
                 self.send_valid = True
             send = self._send_buf
         out = self.full.data  # fresh version counter: autograd's saved views stay valid
-        if self.fsdp.world == 1:
-            out.copy_(send)
-            self.gathered = True
-            return
         comm = self.fsdp.comm
         self.gather_work = _SlotWork(lambda: comm.all_gather(out, send))
         if not async_op:
@@ -244,27 +246,41 @@ class _FlatGroup:
 
     def start_backward(self) -> None:
         self.grad_ready = set()
+        self._pending = []
         self.reduced = False
 
     def on_grad(self, i: int, p: nn.Parameter) -> bool:
-        """Move one param's grad into the flat buffer; True once the group is complete."""
+        """Take one param's grad for the flat buffer; True once the group is complete.  The grads
+        land together (one multi-tensor copy per group when it completes or reduces) instead of one
+        small device copy per parameter."""
         if self.reduced or i in self.grad_ready:
             return False
-        buf = self._grad_buf()
-        o, n = self.offsets[i], self.numels[i]
         _flush_wgrad()  # a deferred weight-gradient reduce may still owe this gradient its values
         if p.grad.is_cuda:
             _streams.join(p.grad.device)  # produced on the weight-gradient side stream
-        with torch.no_grad():
-            buf[o : o + n].copy_(p.grad.reshape(-1))
+        self._pending.append((i, p.grad))
         p.grad = None
         self.grad_ready.add(i)
-        return len(self.grad_ready) == len(self.params)
+        done = len(self.grad_ready) == len(self.params)
+        if done:
+            self._land_pending()
+        return done
+
+    def _land_pending(self) -> None:
+        if not self._pending:
+            return
+        buf = self._grad_buf()
+        dst = [buf[self.offsets[i] : self.offsets[i] + self.numels[i]].view(self.shapes[i]) for i, _ in self._pending]
+        src = [g for _, g in self._pending]
+        with torch.no_grad():
+            torch._foreach_copy_(dst, src)
+        self._pending = []
 
     def reduce(self) -> None:
         if self.reduced:
             return
         self.reduced = True
+        self._land_pending()
         buf = self._grad_buf()
         for i, (o, n) in enumerate(zip(self.offsets, self.numels)):
             if i not in self.grad_ready:  # unused this step: contributes zeros
@@ -597,9 +613,11 @@ class FullyShardedDataParallel(nn.Module):
         return attr
 
     # -- gradient clipping ---------------------------------------------------------------------
-    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
-        """Global L2 norm over every rank's shard (fixes the reference's local-shard clip, C25)."""
-        return clip_grad_norm_(list(self.parameters()), max_norm, group=self.group, sharded=self.world > 1)
+    def clip_grad_norm_(self, max_norm: float, defer_to=None) -> torch.Tensor:
+        """Global L2 norm over every rank's shard (fixes the reference's local-shard clip, C25).
+        ``defer_to``: a FusedAdam that applies the coefficient inside its step (ops.optim)."""
+        return clip_grad_norm_(list(self.parameters()), max_norm, group=self.group, sharded=self.world > 1,
+                               defer_to=defer_to)
 
     # -- state dicts (collective: call on EVERY rank) ---------------------------------------------
     @torch.no_grad()

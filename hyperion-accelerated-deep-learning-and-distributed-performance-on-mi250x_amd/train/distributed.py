@@ -188,14 +188,18 @@ class _EpochRunner:
             if allreduce is not None:
                 allreduce()
             if self.clip is not None:
-                self._clip()
+                self._clip(defer=True)
             self.opt.step()
 
-    def _clip(self) -> None:
+    def _clip(self, defer: bool = False) -> None:
+        """``defer``: FusedAdam applies the clip coefficient inside its step (one gradient pass fewer)."""
+        from ..ops.optim import FusedAdam
+
+        d = self.opt if defer and isinstance(self.opt, FusedAdam) else None
         if hasattr(self.model, "clip_grad_norm_"):
-            self.model.clip_grad_norm_(self.clip)
+            self.model.clip_grad_norm_(self.clip, defer_to=d)
         else:
-            clip_grad_norm_(self.model.parameters(), self.clip, sharded=self.sharded_clip)
+            clip_grad_norm_(self.model.parameters(), self.clip, sharded=self.sharded_clip, defer_to=d)
 
 
 class _CapturedStep:

@@ -14,6 +14,8 @@ def short(n):
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 ends = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"]]
+# a step with several Adam launches (bf16 compute copies + fp32 masters): keep the last of each run
+ends = [i for j, i in enumerate(ends) if j + 1 == len(ends) or ends[j + 1] != i + 1]
 st = rows[ends[-2] + 1:ends[-1] + 1] if len(ends) > 1 else rows
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in st:
