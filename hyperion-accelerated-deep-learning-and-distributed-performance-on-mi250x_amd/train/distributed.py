@@ -102,6 +102,15 @@ def _reduce_mean(t: torch.Tensor, world: int) -> torch.Tensor:
     return t
 
 
+def _shared_run_id(name: str, world: int) -> str:
+    """Rank 0's clock names the run on every rank (per-rank clocks can straddle a second boundary
+    and name the checkpoint / optimizer-shard files differently)."""
+    when = [time.time()]
+    if world > 1 and dist.is_available() and dist.is_initialized():
+        dist.broadcast_object_list(when, src=0)
+    return make_run_id(name, world, when[0])
+
+
 def _amp(precision: str):
     return {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[precision]
 
@@ -338,7 +347,7 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
     runner = _EpochRunner(rank, world, device, model, opt, scaler, _amp(precision), None, False, opts)
     inner = model.module if hasattr(model, "module") else model
     res = _maybe_resume(opts, model, opt, scaler, out, "language_ddp")
-    run_id = res.run_id or make_run_id("language_ddp", world)
+    run_id = res.run_id or _shared_run_id("language_ddp", world)
     csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["language_ddp"], enabled=rank == 0,
                      append=res.run_id is not None)
     runner.global_step = res.global_step
@@ -409,7 +418,7 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
     scaler = LossScaler(enabled=precision == "fp16", device=device)
     runner = _EpochRunner(rank, world, device, model, opt, scaler, _amp(precision), None, False, opts)
     res = _maybe_resume(opts, model, opt, scaler, out, "cifar_ddp")
-    run_id = res.run_id or make_run_id("cifar_ddp", world)
+    run_id = res.run_id or _shared_run_id("cifar_ddp", world)
     csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["cifar"], enabled=rank == 0,
                      append=res.run_id is not None)
     runner.global_step = res.global_step
@@ -486,7 +495,7 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, True, opts)
     res = _maybe_resume(opts, model, opt, None, out, run_name)
-    run_id = res.run_id or make_run_id(run_name, world)
+    run_id = res.run_id or _shared_run_id(run_name, world)
     csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS.get(run_name, SCHEMAS["language_fsdp"]),
                      enabled=rank == 0, append=res.run_id is not None)
     runner.global_step = res.global_step
@@ -592,7 +601,7 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
     opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, isinstance(model, FSDP), opts)
     res = _maybe_resume(opts, model, opt, None, out, "llama")
-    run_id = res.run_id or make_run_id("llama", world)
+    run_id = res.run_id or _shared_run_id("llama", world)
     csv = MetricsCSV(os.path.join(out, f"{run_id}_metrics.csv"), SCHEMAS["llama"], enabled=rank == 0,
                      append=res.run_id is not None)
     runner.global_step = res.global_step
