@@ -110,6 +110,28 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
 }
 
 // ---- LayerNorm / RMSNorm ------------------------------------------------------------------
+// affine parameters: fp32, or (wt = 1) the activation dtype; weight and bias must agree
+int affine_mode(const at::Tensor& x, const c10::optional<at::Tensor>& w, const c10::optional<at::Tensor>& b,
+                const char* what) {
+  int mode = -1;
+  for (const auto* t : {&w, &b}) {
+    if (!t->has_value() || !(*t)->defined()) continue;
+    const at::Tensor& a = **t;
+    TORCH_CHECK(a.is_contiguous() && a.device() == x.device() && a.numel() == x.size(-1), what,
+                ": affine parameter must be a contiguous [d] tensor on the input's device");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0, what, ": affine parameter must be 16-byte aligned");
+    const int m = a.scalar_type() == at::kFloat ? 0 : (a.scalar_type() == x.scalar_type() ? 1 : -2);
+    TORCH_CHECK(m >= 0, what, ": affine parameters must be fp32 or the input dtype");
+    TORCH_CHECK(mode < 0 || mode == m, what, ": weight and bias dtypes differ");
+    mode = m;
+  }
+  return mode < 0 ? 0 : mode;
+}
+
+const float* affine_ptr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? static_cast<const float*>(t->data_ptr()) : nullptr;
+}
+
 // x: [..., d] contiguous; returns (y, s (fused residual stream or undefined), mean, rstd)
 std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
                                const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
@@ -132,10 +154,11 @@ std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tens
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({rows}, fopt);
   auto rstd = at::empty({rows}, fopt);
+  const int wt = affine_mode(x, weight, bias, "ln_fwd");
   HYP_CHECK_HIP(hyp::layernorm_forward(dtype_code(x), rms ? 1 : 0, x.data_ptr(), has_res ? residual->data_ptr() : nullptr,
-                                       has_res ? s.data_ptr() : nullptr, y.data_ptr(), ptr_or_null<float>(weight),
-                                       ptr_or_null<float>(bias), rms ? nullptr : mean.data_ptr<float>(),
-                                       rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream()));
+                                       has_res ? s.data_ptr() : nullptr, y.data_ptr(), affine_ptr(weight),
+                                       affine_ptr(bias), rms ? nullptr : mean.data_ptr<float>(),
+                                       rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream(), wt));
   return {y, s, mean, rstd};
 }
 
@@ -152,17 +175,19 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
   hyp::layernorm_bwd_geom(rows, d, &P, &rpw);
   auto fopt = xin.options().dtype(at::kFloat);
   auto part = at::empty({2 * (int64_t)P * d}, fopt);
+  const int wt = affine_mode(xin, weight, c10::nullopt, "ln_bwd");
+  auto wopt = wt ? xin.options() : fopt;  // dγ / dβ in the weight's dtype
   at::Tensor dw, db;
-  if (need_dw) dw = at::empty({d}, fopt);
-  if (need_db && !rms) db = at::empty({d}, fopt);
+  if (need_dw) dw = at::empty({d}, wopt);
+  if (need_db && !rms) db = at::empty({d}, wopt);
   at::Tensor dr;
   if (dres.has_value() && dres->defined()) dr = dres->is_contiguous() ? *dres : dres->contiguous();
   HYP_CHECK_HIP(hyp::layernorm_backward(dtype_code(xin), rms ? 1 : 0, g.data_ptr(), xin.data_ptr(),
-                                        ptr_or_null<float>(weight), rms ? nullptr : mean.data_ptr<float>(),
+                                        affine_ptr(weight), rms ? nullptr : mean.data_ptr<float>(),
                                         rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(),
                                         part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)P * d,
-                                        need_dw ? dw.data_ptr<float>() : nullptr,
-                                        db.defined() ? db.data_ptr<float>() : nullptr, rows, d, P, rpw, cur_stream()));
+                                        need_dw ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr,
+                                        rows, d, P, rpw, cur_stream(), wt));
   return {dx, dw, db};
 }
 

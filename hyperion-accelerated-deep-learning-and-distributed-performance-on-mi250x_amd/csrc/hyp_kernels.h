@@ -60,12 +60,13 @@ namespace hyp {
 // ---- layernorm.hip ---------------------------------------------------------------------------
 bool layernorm_supported(int d);
 void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave);
+// wt = 1: w / b (and dw / db) are in the activation dtype instead of fp32 (pointers reinterpreted)
 hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
                              const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
-                             hipStream_t st);
+                             hipStream_t st, int wt = 0);
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
-                              const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, float* dw,
-                              float* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st);
+                              const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
+                              void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt = 0);
 }  // namespace hyp
 
 namespace hyp {

@@ -40,16 +40,28 @@ struct RowRegs {
   __device__ __forceinline__ void unpack(int k, float (&o)[8]) const { Vec8<T>::load(reinterpret_cast<const T*>(&v[k][0]), o); }
 };
 
-template <int VPL>
-__device__ __forceinline__ void load_affine(const float* p, int d, int lane, float (&o)[VPL][8], float dflt) {
+// 8 affine values from p + c: fp32, or (wt) in the activation dtype T — a module cast wholesale to
+// bf16 (FSDP mixed precision, HF-style Llama) hands over bf16 weights; reading them as such saves
+// the two cast kernels per LayerNorm per direction the fp32-only interface cost
+template <typename T>
+__device__ __forceinline__ void affine8(const float* p, int wt, int c, float (&o)[8]) {
+  if (wt) {
+    Vec8<T>::load(reinterpret_cast<const T*>(p) + c, o);
+  } else {
+    const float4 a = reinterpret_cast<const float4*>(p + c)[0];
+    const float4 b = reinterpret_cast<const float4*>(p + c)[1];
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+    o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+}
+
+template <typename T, int VPL>
+__device__ __forceinline__ void load_affine(const float* p, int wt, int d, int lane, float (&o)[VPL][8], float dflt) {
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     const int c = (k * 64 + lane) * 8;
     if (p != nullptr && c < d) {
-      const float4 a = reinterpret_cast<const float4*>(p + c)[0];
-      const float4 b = reinterpret_cast<const float4*>(p + c)[1];
-      o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
-      o[k][4] = b.x; o[k][5] = b.y; o[k][6] = b.z; o[k][7] = b.w;
+      affine8<T>(p, wt, c, o[k]);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[k][j] = dflt;
@@ -63,13 +75,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_fwd_k(const T* __restr
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ b, float* __restrict__ mean_out,
                                                                   float* __restrict__ rstd_out, int64_t rows, int d,
-                                                                  float eps, int rpw) {
+                                                                  float eps, int rpw, int wt) {
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * rpw;
   if (row0 >= rows) return;
   float wv[VPL][8], bv[VPL][8];
-  load_affine<VPL>(w, d, lane, wv, 1.f);
-  load_affine<VPL>(RMS ? nullptr : b, d, lane, bv, 0.f);
+  load_affine<T, VPL>(w, wt, d, lane, wv, 1.f);
+  load_affine<T, VPL>(RMS ? nullptr : b, wt, d, lane, bv, 0.f);
   RowRegs<T, VPL> cx, cr, nx, nr;
   cx.load(x, row0, d, lane);
   if (HAS_RES) cr.load(r, row0, d, lane);
@@ -141,7 +153,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
                                                                   const float* __restrict__ rstd_in,
                                                                   const T* __restrict__ dres, T* __restrict__ dx,
                                                                   float* __restrict__ pdw, float* __restrict__ pdb,
-                                                                  int64_t rows, int d, int rows_per_wave) {
+                                                                  int64_t rows, int d, int rows_per_wave, int wt) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float gw[VPL][8], gb[VPL][8], wv[VPL][8];
@@ -149,7 +161,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) gw[k][j] = gb[k][j] = 0.f;
-  load_affine<VPL>(w, d, lane, wv, 1.f);
+  load_affine<T, VPL>(w, wt, d, lane, wv, 1.f);
 
   const int64_t row_begin = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * rows_per_wave;
   RowRegs<T, VPL> cg, cxr, cd, ng, nxr, nd;
@@ -264,16 +276,13 @@ __device__ __forceinline__ void wide_load(const T* base, int64_t row, int d, int
   }
 }
 
-template <int VW>
-__device__ __forceinline__ void wide_affine(const float* p, int d, int tid, float (&o)[VW][8], float dflt) {
+template <typename T, int VW>
+__device__ __forceinline__ void wide_affine(const float* p, int wt, int d, int tid, float (&o)[VW][8], float dflt) {
 #pragma unroll
   for (int k = 0; k < VW; ++k) {
     const int c = (k * kWideThreads + tid) * 8;
     if (p != nullptr && c < d) {
-      const float4 a = reinterpret_cast<const float4*>(p + c)[0];
-      const float4 b = reinterpret_cast<const float4*>(p + c)[1];
-      o[k][0] = a.x; o[k][1] = a.y; o[k][2] = a.z; o[k][3] = a.w;
-      o[k][4] = b.x; o[k][5] = b.y; o[k][6] = b.z; o[k][7] = b.w;
+      affine8<T>(p, wt, c, o[k]);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[k][j] = dflt;
@@ -300,12 +309,12 @@ __global__ __launch_bounds__(kWideThreads) void ln_fwd_wide_k(const T* __restric
                                                               T* __restrict__ s_out, T* __restrict__ y,
                                                               const float* __restrict__ w, const float* __restrict__ b,
                                                               float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                              int64_t rows, int d, float eps, int rpb) {
+                                                              int64_t rows, int d, float eps, int rpb, int wt) {
   __shared__ float red[8];
   const int tid = threadIdx.x;
   float wv[VW][8], bv[VW][8];
-  wide_affine<VW>(w, d, tid, wv, 1.f);
-  wide_affine<VW>(RMS ? nullptr : b, d, tid, bv, 0.f);
+  wide_affine<T, VW>(w, wt, d, tid, wv, 1.f);
+  wide_affine<T, VW>(RMS ? nullptr : b, wt, d, tid, bv, 0.f);
   for (int i = 0; i < rpb; ++i) {
     const int64_t row = (int64_t)blockIdx.x * rpb + i;
     if (row >= rows) break;
@@ -369,7 +378,7 @@ __global__ __launch_bounds__(kWideThreads) void ln_bwd_wide_k(const T* __restric
                                                               const float* __restrict__ rstd_in,
                                                               const T* __restrict__ dres, T* __restrict__ dx,
                                                               float* __restrict__ pdw, float* __restrict__ pdb,
-                                                              int64_t rows, int d, int rpb) {
+                                                              int64_t rows, int d, int rpb, int wt) {
   __shared__ float red[8];
   const int tid = threadIdx.x;
   float gw[VW][8], gb[VW][8], wv[VW][8];
@@ -377,7 +386,7 @@ __global__ __launch_bounds__(kWideThreads) void ln_bwd_wide_k(const T* __restric
   for (int k = 0; k < VW; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) gw[k][j] = gb[k][j] = 0.f;
-  wide_affine<VW>(w, d, tid, wv, 1.f);
+  wide_affine<T, VW>(w, wt, d, tid, wv, 1.f);
   for (int i = 0; i < rpb; ++i) {
     const int64_t row = (int64_t)blockIdx.x * rpb + i;
     if (row >= rows) break;
@@ -442,16 +451,16 @@ int wide_rows_per_block(int64_t rows) { return (int)((rows + 1023) / 1024); }
 
 template <typename T, bool RMS>
 hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, const float* b, float* mean,
-                           float* rstd, int64_t rows, int d, float eps, hipStream_t st) {
+                           float* rstd, int64_t rows, int d, float eps, hipStream_t st, int wt) {
   if (d > 2048) {
     const int rpb = wide_rows_per_block(rows);
     const dim3 grid((unsigned)((rows + rpb - 1) / rpb)), block(kWideThreads);
     if (r)
       hipLaunchKernelGGL((ln_fwd_wide_k<T, 2, RMS, true>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, d,
-                         eps, rpb);
+                         eps, rpb, wt);
     else
       hipLaunchKernelGGL((ln_fwd_wide_k<T, 2, RMS, false>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, d,
-                         eps, rpb);
+                         eps, rpb, wt);
     return hipGetLastError();
   }
   const int vpl = (d + 511) / 512;
@@ -464,10 +473,10 @@ hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, c
   case V:                                                                                                    \
     if (r)                                                                                                   \
       hipLaunchKernelGGL((ln_fwd_k<T, V, RMS, true>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, \
-                         d, eps, rpw);                                                                       \
+                         d, eps, rpw, wt);                                                                       \
     else                                                                                                     \
       hipLaunchKernelGGL((ln_fwd_k<T, V, RMS, false>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, \
-                         d, eps, rpw);                                                                       \
+                         d, eps, rpw, wt);                                                                       \
     break;
   switch (vpl) {
     HYP_LN_F(1)
@@ -484,18 +493,18 @@ hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, c
 
 template <typename T, bool RMS>
 hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const float* mean, const float* rstd,
-                           const T* dres, T* dx, float* pdw, float* pdb, float* dw, float* db, int64_t rows, int d,
-                           int P, int rows_per_wave, hipStream_t st) {
+                           const T* dres, T* dx, float* pdw, float* pdb, void* dw, void* db, int64_t rows, int d,
+                           int P, int rows_per_wave, hipStream_t st, int wt, int wdt) {
   if (d > 2048) {  // P blocks of rows_per_wave rows (layernorm_bwd_geom)
     if (dres)
       hipLaunchKernelGGL((ln_bwd_wide_k<T, 2, RMS, true>), dim3(P), dim3(kWideThreads), 0, st, dy, xin, w, mean, rstd,
-                         dres, dx, pdw, pdb, rows, d, rows_per_wave);
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave, wt);
     else
       hipLaunchKernelGGL((ln_bwd_wide_k<T, 2, RMS, false>), dim3(P), dim3(kWideThreads), 0, st, dy, xin, w, mean, rstd,
-                         dres, dx, pdw, pdb, rows, d, rows_per_wave);
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave, wt);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, kF32, st);
-    if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, kF32, st);
+    if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, wdt, st);
+    if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, wdt, st);
     return e;
   }
   const int vpl = (d + 511) / 512;
@@ -505,10 +514,10 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
   case V:                                                                                                    \
     if (dres)                                                                                                \
       hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, true>), grid, block, lds, st, dy, xin, w, mean, rstd, dres, dx, \
-                         pdw, pdb, rows, d, rows_per_wave);                                                  \
+                         pdw, pdb, rows, d, rows_per_wave, wt);                                              \
     else                                                                                                     \
       hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, false>), grid, block, lds, st, dy, xin, w, mean, rstd, dres, dx, \
-                         pdw, pdb, rows, d, rows_per_wave);                                                  \
+                         pdw, pdb, rows, d, rows_per_wave, wt);                                              \
     break;
   switch (vpl) {
     HYP_LN_B(1)
@@ -521,8 +530,8 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
   }
 #undef HYP_LN_B
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, kF32, st);
-  if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, kF32, st);
+  if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, wdt, st);
+  if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, wdt, st);
   return e;
 }
 
@@ -561,26 +570,27 @@ void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave) {
 
 hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
                              const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
-                             hipStream_t st) {
+                             hipStream_t st, int wt) {
   if (!layernorm_supported(d)) return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (rms)
-      return ln_fwd_dispatch<T, true>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st);
-    return ln_fwd_dispatch<T, false>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st);
+      return ln_fwd_dispatch<T, true>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st, wt);
+    return ln_fwd_dispatch<T, false>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st, wt);
   });
   return hipSuccess;
 }
 
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
-                              const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, float* dw,
-                              float* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st) {
+                              const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
+                              void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt) {
+  const int wdt = wt ? dtype : kF32;  // dγ / dβ in the weight's dtype
   if (!layernorm_supported(d)) return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (rms)
       return ln_bwd_dispatch<T, true>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                      db, rows, d, P, rows_per_wave, st);
+                                      db, rows, d, P, rows_per_wave, st, wt, wdt);
     return ln_bwd_dispatch<T, false>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                     db, rows, d, P, rows_per_wave, st);
+                                     db, rows, d, P, rows_per_wave, st, wt, wdt);
   });
   return hipSuccess;
 }

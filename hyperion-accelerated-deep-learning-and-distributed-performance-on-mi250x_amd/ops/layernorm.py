@@ -75,18 +75,19 @@ def layer_norm(
     return_sum: bool = False,
 ) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
     d = x.shape[-1]
-    # the kernels take fp32 affine parameters; a model cast wholesale to bf16 (HF-style Llama) hands
-    # us bf16 ones — upcast them (d elements, differentiable) rather than leave the fused path
-    if weight is not None and weight.dtype in (torch.bfloat16, torch.float16):
-        weight = weight.float()
-    if bias is not None and bias.dtype in (torch.bfloat16, torch.float16):
-        bias = bias.float()
+    # the kernels take fp32 affine parameters or parameters in the activation dtype (a model cast
+    # wholesale to bf16: FSDP mixed precision, HF-style Llama) — read as such, dγ / dβ returned in it;
+    # any other mix is upcast (d elements, differentiable) rather than leave the fused path
+    wdt = weight.dtype if weight is not None else (bias.dtype if bias is not None else torch.float32)
+    if wdt not in (torch.float32, x.dtype) or (weight is not None and bias is not None and weight.dtype != bias.dtype):
+        weight = weight.float() if weight is not None else None
+        bias = bias.float() if bias is not None else None
+        wdt = torch.float32
     native = (
         _native.use_native(x, op="ln")
         and x.dtype in _native.DTYPE_CODE
         and _SUPPORTED_D(d)
-        and (weight is None or weight.dtype == torch.float32)
-        and (bias is None or bias.dtype == torch.float32)
+        and all(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in (weight, bias))
         and (residual is None or residual.shape == x.shape)
     )
     if native:

@@ -270,11 +270,15 @@ class _FlatGroup:
         if not self._pending:
             return
         buf = self._grad_buf()
-        dst = [buf[self.offsets[i] : self.offsets[i] + self.numels[i]].view(self.shapes[i]) for i, _ in self._pending]
-        src = [g for _, g in self._pending]
-        with torch.no_grad():
-            torch._foreach_copy_(dst, src)
+        pend = sorted(self._pending, key=lambda ig: ig[0])
         self._pending = []
+        with torch.no_grad():
+            if (len(pend) == len(self.params) and all(g.is_contiguous() and g.dtype == buf.dtype for _, g in pend)):
+                # the whole group, in flat order: one concatenation kernel straight into the buffer
+                torch.cat([g.reshape(-1) for _, g in pend], out=buf.narrow(0, 0, self.numel))
+            else:
+                dst = [buf[self.offsets[i] : self.offsets[i] + self.numels[i]].view(self.shapes[i]) for i, _ in pend]
+                torch._foreach_copy_(dst, [g for _, g in pend])
 
     def reduce(self) -> None:
         if self.reduced:

@@ -107,6 +107,39 @@ def test_layernorm(dtype, d, fused):
         torch.testing.assert_close(rn.grad.float(), rr.grad, atol=tol * 5, rtol=tol * 5)
 
 
+@pytest.mark.parametrize("d", [768, 4096])
+@pytest.mark.parametrize("rms", [False, True])
+def test_layernorm_bf16_affine(d, rms):
+    """bf16 weight / bias (a module cast wholesale to bf16, FSDP mixed precision) read in the kernel;
+    dγ / dβ come back in bf16 (no cast kernels around the op)."""
+    from hyperion.ops.layernorm import layer_norm
+
+    torch.manual_seed(0)
+    x = torch.randn(300, d, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(d, device="cuda") + 0.5).to(torch.bfloat16)
+    b = None if rms else torch.randn(d, device="cuda").to(torch.bfloat16)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = None if rms else b.detach().float().requires_grad_(True)
+    if rms:
+        yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    else:
+        yr = F.layer_norm(xr, (d,), wr, br, 1e-5)
+    xn, wn = x.detach().requires_grad_(True), w.detach().requires_grad_(True)
+    bn = None if rms else b.detach().requires_grad_(True)
+    yn = layer_norm(xn, wn, bn, 1e-5, rms=rms)
+    torch.testing.assert_close(yn.float(), yr, atol=3e-2, rtol=3e-2)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    yn.backward(g.to(torch.bfloat16))
+    assert wn.grad.dtype == torch.bfloat16
+    torch.testing.assert_close(xn.grad.float(), xr.grad, atol=0.15, rtol=0.05)
+    torch.testing.assert_close(wn.grad.float(), wr.grad, atol=0.5, rtol=0.05)
+    if not rms:
+        assert bn.grad.dtype == torch.bfloat16
+        torch.testing.assert_close(bn.grad.float(), br.grad, atol=0.5, rtol=0.05)
+
+
 def test_rmsnorm():
     from hyperion.ops.layernorm import RMSNorm
 
