@@ -40,25 +40,31 @@ void check_ws(const at::Tensor& x, const at::Tensor& w, bool nn, int64_t* M, int
 
 // fp32 partial slabs of x·Wᵀ (nn = false) / x·W (nn = true) -> (part, S, MFtot)
 std::tuple<at::Tensor, int64_t, int64_t> ws_gemm_part(const at::Tensor& x, const at::Tensor& w, bool nn, int64_t mf,
-                                                      int64_t kr, int64_t G, int64_t nf) {
+                                                      int64_t kr, int64_t G, int64_t nf, bool slab16) {
   int64_t M, N, K;
   check_ws(x, w, nn, &M, &N, &K);
   const WsPlan p = plan_for(M, N, K, nn, mf, kr, G, nf);
   const at::DeviceGuard guard(x.device());
-  auto part = at::empty({(int64_t)p.S * p.MFtot * (N / 16) * 256}, x.options().dtype(at::kFloat));
+  auto part = at::empty({(int64_t)p.S * p.MFtot * (N / 16) * 256}, x.options().dtype(slab16 ? at::kBFloat16 : at::kFloat));
   HYP_CHECK_HIP(hyp::ws_gemm(dtype_code(x), nn, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
-                             part.data_ptr<float>(), device_zero_page(x.device()), (int)M, (int)N, (int)K, p.mf, p.kr,
-                             p.G, p.nf, cur_stream()));
+                             static_cast<float*>(part.data_ptr()), device_zero_page(x.device()), (int)M, (int)N, (int)K,
+                             p.mf, p.kr, p.G, p.nf, cur_stream(), slab16 ? 1 : 0));
   return {part, p.S, p.MFtot};
+}
+
+// slab buffer -> (pointer, bf16 flag)
+std::pair<const float*, int> slab_ptr(const at::Tensor& part, int64_t need, const char* what) {
+  TORCH_CHECK(part.is_cuda() && part.is_contiguous() && part.numel() >= need &&
+                  (part.scalar_type() == at::kFloat || part.scalar_type() == at::kBFloat16),
+              what, ": fp32 or bf16 slabs of the weight-streaming GEMM");
+  return {static_cast<const float*>(part.data_ptr()), part.scalar_type() == at::kBFloat16 ? 1 : 0};
 }
 
 at::Tensor ws_reduce(const at::Tensor& part, int64_t M, int64_t N, int64_t S, int64_t MFtot, bool nn,
                      at::ScalarType dtype, double alpha, const c10::optional<at::Tensor>& addend, double beta,
                      const c10::optional<at::Tensor>& U, const c10::optional<at::Tensor>& V, int64_t segw,
                      double uscale, const c10::optional<at::Tensor>& out) {
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
-                  part.numel() >= S * MFtot * (N / 16) * 256,
-              "ws_reduce: fp32 slabs");
+  const auto sp = slab_ptr(part, S * MFtot * (N / 16) * 256, "ws_reduce");
   TORCH_CHECK(MFtot * 16 >= M, "ws_reduce: MFtot too small");
   const at::DeviceGuard guard(part.device());
   at::Tensor o;
@@ -88,16 +94,16 @@ at::Tensor ws_reduce(const at::Tensor& part, int64_t M, int64_t N, int64_t S, in
     v = V->data_ptr();
     r = (int)V->size(1);
   }
-  HYP_CHECK_HIP(hyp::ws_reduce(dtype == at::kBFloat16 ? hyp::kBF16 : hyp::kF16, nn, part.data_ptr<float>(),
+  HYP_CHECK_HIP(hyp::ws_reduce(dtype == at::kBFloat16 ? hyp::kBF16 : hyp::kF16, nn, sp.first,
                                o.data_ptr(), o.stride(0), add, (float)alpha, (float)beta, u, v, r, (int)segw,
-                               (float)uscale, (int)M, (int)N, (int)S, (int)MFtot, cur_stream()));
+                               (float)uscale, (int)M, (int)N, (int)S, (int)MFtot, cur_stream(), sp.second));
   return o;
 }
 
 at::Tensor ws_linear(const at::Tensor& x, const at::Tensor& w, bool nn, double alpha,
                      const c10::optional<at::Tensor>& addend, double beta, int64_t mf, int64_t kr, int64_t G,
                      int64_t nf) {
-  auto res = ws_gemm_part(x, w, nn, mf, kr, G, nf);
+  auto res = ws_gemm_part(x, w, nn, mf, kr, G, nf, false);
   const int64_t M = x.size(0), N = nn ? w.size(1) : w.size(0);
   return ws_reduce(std::get<0>(res), M, N, std::get<1>(res), std::get<2>(res), nn, x.scalar_type(), alpha, addend,
                    beta, c10::nullopt, c10::nullopt, 1, 1.0, c10::nullopt);
@@ -152,11 +158,11 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
                     c10::optional<bool> nn, const c10::optional<at::Tensor>& yin) {
   const bool dense = !(part_opt.has_value() && part_opt->defined());
   const float* part_ptr = nullptr;
+  int sb = 0;
   if (!dense) {
-    const at::Tensor& part = *part_opt;
-    TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= S * MFtot * (N / 16) * 256,
-                "ws_epilogue: fp32 slabs");
-    part_ptr = part.data_ptr<float>();
+    const auto sp = slab_ptr(*part_opt, S * MFtot * (N / 16) * 256, "ws_epilogue");
+    part_ptr = sp.first;
+    sb = sp.second;
   } else {
     TORCH_CHECK(yin.has_value() && yin->defined() && yin->dim() == 2 && yin->size(0) == M && yin->size(1) == N &&
                     yin->stride(1) == 1 && yin->scalar_type() == out.scalar_type(),
@@ -212,7 +218,7 @@ void ws_epilogue_py(const c10::optional<at::Tensor>& part_opt, int64_t S, int64_
                                  lp.empty() ? nullptr : lp.data(), P, r, (int)segw, (float)lscale, (int)rope_segs,
                                  (int)seq, (float)theta, has_rng ? &rs : nullptr, (float)p_drop,
                                  nn.has_value() ? *nn : (epi == 3 || epi == 4), dense ? yin->data_ptr() : nullptr,
-                                 dense ? yin->stride(0) : 0, cur_stream()));
+                                 dense ? yin->stride(0) : 0, cur_stream(), sb));
 }
 
 void lora_down_py(const at::Tensor& x, const std::vector<at::Tensor>& A, at::Tensor& t,
@@ -272,8 +278,9 @@ void lora_bwd_a_py(const at::Tensor& x, const std::vector<at::Tensor>& dA, const
 
 void register_ws_ops(pybind11::module& m) {
   using namespace pybind11::literals;
-  m.def("ws_gemm_part", &ws_gemm_part, "weight-streaming GEMM -> (fp32 fragment-order partial slabs, S, MFtot)",
-        "x"_a, "w"_a, "nn"_a = false, "mf"_a = 0, "kr"_a = 0, "G"_a = 0, "nf"_a = 0);
+  m.def("ws_gemm_part", &ws_gemm_part,
+        "weight-streaming GEMM -> (fragment-order partial slabs: fp32, or bf16 with slab16, S, MFtot)", "x"_a, "w"_a,
+        "nn"_a = false, "mf"_a = 0, "kr"_a = 0, "G"_a = 0, "nf"_a = 0, "slab16"_a = false);
   m.def("ws_reduce", &ws_reduce, "sum weight-streaming partial slabs (+ alpha, addend, rank-r term)", "part"_a, "M"_a,
         "N"_a, "S"_a, "MFtot"_a, "nn"_a, "dtype"_a, "alpha"_a = 1.0, "addend"_a = pybind11::none(), "beta"_a = 1.0,
         "U"_a = pybind11::none(), "V"_a = pybind11::none(), "segw"_a = 1, "uscale"_a = 1.0, "out"_a = pybind11::none());

@@ -314,15 +314,15 @@ namespace hyp {
 // ---- wstream.hip -----------------------------------------------------------------------------
 // Weight-streaming GEMM for few-token activations: x slice resident in LDS, W streamed to VGPRs.
 // nn = false: y = x Wᵀ (W [N, K]); nn = true: y = x W (W [K, N]).  Writes fp32 partial slabs
-// [S][MB*mf][N/16][64][4] (fragment order); ws_reduce sums them (+ epilogue) into [M, N].
+// [S][MB*mf][N/16][64][4] (fragment order; sb = 1: bf16 elements); ws_reduce sums them (+ epilogue) into [M, N].
 bool ws_supported(int M, int N, int K, bool nn);
 void ws_plan(int M, int N, int K, bool nn, int* mf, int* kr, int* G, int* nf);
 hipError_t ws_gemm(int dtype, bool nn, const void* x, int64_t ldx, const void* w, int64_t ldw, float* part,
-                   const void* zero, int M, int N, int K, int mf, int kr, int G, int nf, hipStream_t st);
+                   const void* zero, int M, int N, int K, int mf, int kr, int G, int nf, hipStream_t st, int sb = 0);
 // out[m, n] = alpha Σ_s part + beta addend[m, n] + uscale Σ_r U[m, seg r + rr] V[n, rr] (seg = n / segw)
 hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t ldo, const void* addend, float alpha,
                      float beta, const float* U, const void* V, int r, int segw, float uscale, int M, int N, int S,
-                     int MFtot, hipStream_t st);
+                     int MFtot, hipStream_t st, int sb = 0);
 // Fused epilogues of the slabs (see wstream.hip): 0 plain, 1 LoRA up (+ RoPE), 2 SwiGLU fwd,
 // 3 SwiGLU bwd (NN), 4 LoRA data gradient (NN).  part == null: the GEMM result is the row-major
 // yin [M, N] (a vendor GEMM's output) instead of slabs.
@@ -330,7 +330,7 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
                        void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
                        int64_t t_sstride, int t_splits, const void* const* lw, int P, int r, int segw, float lscale,
                        int rope_segs, int seq, float theta, const RngState* rng, float p_drop, bool nn,
-                       const void* yin, int64_t ldy, hipStream_t st);
+                       const void* yin, int64_t ldy, hipStream_t st, int sb = 0);
 }  // namespace hyp
 
 namespace hyp {

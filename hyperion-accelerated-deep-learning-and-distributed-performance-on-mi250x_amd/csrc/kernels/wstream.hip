@@ -46,6 +46,7 @@ struct WsArgs {
   int S, G, MB;    // slices, workgroups per (slice, m-block), m-blocks
   int chunks;      // column chunks per (slice, m-block)
   int R;           // S * G
+  int sb;          // slabs in bf16 (8-byte quads) instead of fp32
 };
 
 __device__ __forceinline__ int swz_chunk(int c, int r) { return (c & ~15) | ((c ^ r) & 15); }
@@ -57,6 +58,22 @@ __device__ __forceinline__ int swz_chunk(int c, int r) { return (c & ~15) | ((c 
 // too), never short.  s_nop 1: the store's data VGPRs may be rewritten right after (acc reset).
 __device__ __forceinline__ void store_slab(float* dst, f32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+}
+// bf16 slabs (half the partial-sum traffic of the split-K GEMM and of its epilogue; each slab is a
+// fp32 partial over >= 128 reduction terms rounded once, the slabs are summed in fp32)
+__device__ __forceinline__ void store_slab16(uint16_t* dst, f32x4 v) {
+  const uint2 q = make_uint2((uint32_t)float_to_bf16(v[0]) | ((uint32_t)float_to_bf16(v[1]) << 16),
+                             (uint32_t)float_to_bf16(v[2]) | ((uint32_t)float_to_bf16(v[3]) << 16));
+  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(dst), "v"(q) : "memory");
+}
+// one slab quad (4 rows x 1 column) at element offset e of the slab buffer
+__device__ __forceinline__ f32x4 load_slab(const float* part, int sb, int64_t e) {
+  if (sb) {
+    const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(part) + e);
+    return f32x4{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u), __uint_as_float(q.y << 16),
+                 __uint_as_float(q.y & 0xffff0000u)};
+  }
+  return *reinterpret_cast<const f32x4*>(part + e);
 }
 
 template <typename T, int MF, int NF, bool NN, int D, int WAVES>
@@ -216,8 +233,9 @@ __global__ __launch_bounds__(WAVES * 64) void ws_gemm_k(const WsArgs a) {
       if (NN || fr0 + j < F) {
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-          float* dst = a.part + ((((int64_t)s * MFtot + mb * MF + i) * F + fr0 + j) * 64 + lane) * 4;
-          store_slab(dst, acc[i][j]);
+          const int64_t e = ((((int64_t)s * MFtot + mb * MF + i) * F + fr0 + j) * 64 + lane) * 4;
+          if (a.sb) store_slab16(reinterpret_cast<uint16_t*>(a.part) + e, acc[i][j]);
+          else store_slab(a.part + e, acc[i][j]);
         }
       }
 #pragma unroll
@@ -246,7 +264,7 @@ hipError_t launch_gemm(const WsArgs& a, int grid, hipStream_t st) {
 
 // ---- slab reduction: out[m, n] = alpha * Σ_s part[s] (+ beta * addend) (+ rank-r term) ---------------
 struct WsRed {
-  const float* part;
+  const float* part;  // fp32 slabs, or bf16 ones (sb)
   void* out;
   int64_t ldo;
   const void* addend;  // [M, N] (ld ldo) in T, or null
@@ -257,6 +275,7 @@ struct WsRed {
   int r, segw;
   float uscale;
   int M, N, S, MFtot, NN;
+  int sb;  // bf16 slabs
 };
 
 // one thread = one (m-fragment, column-fragment, lane) quad: 4 rows x 1 column
@@ -274,18 +293,18 @@ __global__ __launch_bounds__(256) void ws_reduce_k(const WsRed a) {
   if (m0 >= a.M) return;
   const int64_t slab = (int64_t)a.MFtot * F * 256;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* p = a.part + tid * 4;
+  const int64_t e0 = tid * 4;
   {
     f32x4 acc4[4] = {acc, acc, acc, acc};
     int s = 0;
     for (; s + 8 <= a.S; s += 8) {
       f32x4 v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(p + (s + i) * slab);
+      for (int i = 0; i < 8; ++i) v[i] = load_slab(a.part, a.sb, e0 + (s + i) * slab);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc4[i & 3] += v[i];
     }
-    for (; s < a.S; ++s) acc4[0] += *reinterpret_cast<const f32x4*>(p + s * slab);
+    for (; s < a.S; ++s) acc4[0] += load_slab(a.part, a.sb, e0 + s * slab);
     acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
   }
   float v[4];
@@ -330,7 +349,8 @@ __global__ __launch_bounds__(256) void ws_reduce_k(const WsRed a) {
 //          dgu[m, n + I] = dh silu(g)
 //   EPI 4  LoRA data gradient (NN): out = Σ + Σ_p keep_p(m, n) Σ_rr du[m, p r + rr] A_p[rr, n]
 struct WsEpi {
-  const float* part;      // fp32 slabs, or null: the GEMM result is the row-major yin (a vendor GEMM's)
+  const float* part;      // fp32 (or bf16: sb) slabs, or null: the GEMM result is the row-major yin (a vendor GEMM's)
+  int sb;
   const void* yin;
   int64_t ldy;
   int S, MFtot, M, N;     // GEMM output width N (EPI 2: 2 I; EPI 3: I)
@@ -464,17 +484,17 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
     }
     // 8 slab loads in flight per step, 4 accumulators (fixed order: deterministic); a one-load
     // loop waited a memory round trip per slab (24-43 slabs on the Llama dgrads)
-    const float* p = a.part + (((int64_t)mf * F + c) * 64 + lane) * 4;
+    const int64_t e0 = (((int64_t)mf * F + c) * 64 + lane) * 4;
     f32x4 acc4[4] = {acc, acc, acc, acc};
     int s = 0;
     for (; s + 8 <= a.S; s += 8) {
       f32x4 v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const f32x4*>(p + (s + i) * slab);
+      for (int i = 0; i < 8; ++i) v[i] = load_slab(a.part, a.sb, e0 + (s + i) * slab);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc4[i & 3] += v[i];
     }
-    for (; s < a.S; ++s) acc4[0] += *reinterpret_cast<const f32x4*>(p + s * slab);
+    for (; s < a.S; ++s) acc4[0] += load_slab(a.part, a.sb, e0 + s * slab);
     return (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
   };
   f32x4 v = sum_quad(cf);
@@ -606,7 +626,7 @@ void ws_plan(int M, int N, int K, bool nn, int* mf, int* kr, int* G, int* nf) {
 }
 
 hipError_t ws_gemm(int dtype, bool nn, const void* x, int64_t ldx, const void* w, int64_t ldw, float* part,
-                   const void* zero, int M, int N, int K, int mf, int kr, int G, int nf, hipStream_t st) {
+                   const void* zero, int M, int N, int K, int mf, int kr, int G, int nf, hipStream_t st, int sb) {
   if (!ws_supported(M, N, K, nn) || (dtype != kBF16 && dtype != kF16)) return hipErrorInvalidValue;
   if (kr < 128 || kr % 128 != 0 || G < 1 || (mf != 2 && mf != 4 && mf != 8)) return hipErrorInvalidValue;
   if (!nn && nf != 1 && nf != 2 && nf != 4) return hipErrorInvalidValue;
@@ -628,6 +648,7 @@ hipError_t ws_gemm(int dtype, bool nn, const void* x, int64_t ldx, const void* w
   a.MB = (M + mf * 16 - 1) / (mf * 16);
   a.chunks = nn ? N / 64 : (N / 16 + nf - 1) / nf;
   a.R = a.S * a.G;
+  a.sb = sb;
   const int grid = a.MB == 1 ? a.R : a.MB * ((a.R + 7) / 8) * 8;
 #define HYP_WS(TT)                                                              \
   if (nn) {                                                                     \
@@ -658,11 +679,11 @@ hipError_t ws_gemm(int dtype, bool nn, const void* x, int64_t ldx, const void* w
 
 hipError_t ws_reduce(int dtype, bool nn, const float* part, void* out, int64_t ldo, const void* addend, float alpha,
                      float beta, const float* U, const void* V, int r, int segw, float uscale, int M, int N, int S,
-                     int MFtot, hipStream_t st) {
+                     int MFtot, hipStream_t st, int sb) {
   if (dtype != kBF16 && dtype != kF16) return hipErrorInvalidValue;
   if (U != nullptr && (V == nullptr || r < 1 || segw < 1 || N % segw != 0)) return hipErrorInvalidValue;
   WsRed a{part, out, ldo, addend, alpha, beta, U, static_cast<const uint16_t*>(V), r, segw, uscale,
-          M, N, S, MFtot, nn ? 1 : 0};
+          M, N, S, MFtot, nn ? 1 : 0, sb};
   const int64_t nquads = (int64_t)MFtot * (N / 16) * 64;
   const int blocks = (int)((nquads + 255) / 256);
   if (dtype == kBF16) hipLaunchKernelGGL(ws_reduce_k<bf16_t>, dim3(blocks), dim3(256), 0, st, a);
@@ -674,7 +695,7 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
                        void* out2, int64_t ldo2, const void* aux, int64_t ld_aux, const float* t, int ldt,
                        int64_t t_sstride, int t_splits, const void* const* lw, int P, int r, int segw, float lscale,
                        int rope_segs, int seq, float theta, const RngState* rng, float p_drop, bool nn,
-                       const void* yin, int64_t ldy, hipStream_t st) {
+                       const void* yin, int64_t ldy, hipStream_t st, int sb) {
   if (dtype != kBF16 && dtype != kF16) return hipErrorInvalidValue;
   if (part == nullptr && yin == nullptr) return hipErrorInvalidValue;
   if (epi != 0 && nn != (epi == 3 || epi == 4)) return hipErrorInvalidValue;  // the slab layout of that GEMM
@@ -689,6 +710,7 @@ hipError_t ws_epilogue(int dtype, int epi, const float* part, int S, int MFtot, 
   if (epi == 3 && aux == nullptr) return hipErrorInvalidValue;
   WsEpi a{};
   a.part = part;
+  a.sb = sb;
   a.yin = yin;
   a.ldy = ldy;
   a.S = S;

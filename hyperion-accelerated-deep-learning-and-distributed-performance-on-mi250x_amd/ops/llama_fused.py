@@ -182,6 +182,11 @@ def fused_spec(layer: nn.Module, x: torch.Tensor, kpm: Optional[torch.Tensor]) -
 # (``ws_epilogue(yin=...)``).  Filled from cold-weight sweeps (scripts/ws_bench.py,
 # profiles/r03/ws_bench.json); ``HYPERION_WS_PLAN=ws|vendor`` forces one side for A/B runs.
 _PLAN_OVERRIDE = os.environ.get("HYPERION_WS_PLAN", "")
+# split-K partial slabs in bf16 (default): the slabs of the data-gradient GEMMs (24-43 slices of 512
+# reduction terms at 128 tokens) were a third of the HBM traffic of those GEMMs and all of their
+# epilogues' reads; each slab is one rounding of a fp32 partial, the slabs are summed in fp32.
+# HYPERION_WS_SLAB=fp32 keeps fp32 slabs (A/B runs)
+SLAB16 = os.environ.get("HYPERION_WS_SLAB", "bf16") != "fp32"
 # (nn, output width, reduction length) -> plan; measured at 128 tokens (scripts/ws_bench.py, cold
 # weights, GEMM + epilogue): hipBLASLt streams the wide forward projections (q/k/v 12288 x 4096:
 # 31.9 us, gate/up 22016 x 4096: 46.7 us — no split-K, activations re-read from L2) faster than
@@ -216,7 +221,8 @@ class _Proj:
         if p[0] == "vendor":
             self.y = x @ w if nn_ else x @ w.t()
         else:
-            self.part, self.S, self.MFt = C.ws_gemm_part(x, w, nn=nn_, mf=p[1], kr=p[2], G=p[3], nf=p[4])
+            self.part, self.S, self.MFt = C.ws_gemm_part(x, w, nn=nn_, mf=p[1], kr=p[2], G=p[3], nf=p[4],
+                                                         slab16=SLAB16)
 
     def epi(self, C, M, N, epi, out, **kw):
         C.ws_epilogue(self.part, self.S, self.MFt, M, N, epi, out, yin=self.y, **kw)

@@ -95,3 +95,26 @@ def test_ws_deterministic():
     a = C.ws_linear(x, w, nn=True)
     b = C.ws_linear(x, w, nn=True)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("nn", [False, True])
+def test_ws_bf16_slabs_match_fp32_slabs(nn):
+    """bf16 partial slabs (the Llama layer's default): same sums as the fp32 slabs within bf16 output
+    rounding, through both the plain reduce and the fused epilogue."""
+    torch.manual_seed(3)
+    C = _C()
+    M, N, K = 128, 1024, 8192
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(K, N, device="cuda") if nn else torch.randn(N, K, device="cuda")).mul_(0.05).bfloat16()
+    p32, S, MFt = C.ws_gemm_part(x, w, nn=nn)
+    p16, S2, MFt2 = C.ws_gemm_part(x, w, nn=nn, slab16=True)
+    assert p16.dtype == torch.bfloat16 and (S, MFt) == (S2, MFt2) and S > 1
+    ref = _ref(x, w, nn)
+    y32 = C.ws_reduce(p32, M, N, S, MFt, nn, torch.bfloat16)
+    y16 = C.ws_reduce(p16, M, N, S, MFt, nn, torch.bfloat16)
+    _close(y32, ref)
+    _close(y16, ref)
+    _close(y16, y32.float(), rel=1e-2)
+    e16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C.ws_epilogue(p16, S, MFt, M, N, 0, e16, nn=nn)
+    _close(e16, y16.float(), rel=1e-2)
