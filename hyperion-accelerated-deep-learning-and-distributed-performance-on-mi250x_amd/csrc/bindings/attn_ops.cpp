@@ -1,4 +1,5 @@
 // Torch bindings: flash attention fwd/bwd and LayerNorm/RMSNorm fwd/bwd.
+#include <cmath>
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
@@ -55,9 +56,10 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
 }
 
 // grads are written into dq/dk/dv (any [B,S,H,D] strided views, e.g. slices of a packed dQKV)
-void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
-              const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, double p_drop, const c10::optional<at::Tensor>& rng,
-              const c10::optional<at::Tensor>& kpm, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
+void attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                   const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, double p_drop,
+                   const c10::optional<at::Tensor>& rng, const c10::optional<at::Tensor>& kpm, at::Tensor& dq,
+                   at::Tensor& dk, at::Tensor& dv, const at::Tensor* rope_cs) {
   check_bshd(q, "q");
   check_bshd(k, "k");
   check_bshd(v, "v");
@@ -106,7 +108,31 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   } else {
     p.rng = hyp::RngState{};
   }
+  p.rope = rope_cs != nullptr ? 1 : 0;
+  p.rope_cs = nullptr;
+  if (rope_cs != nullptr) {
+    TORCH_CHECK(D == 128 && p_drop == 0, "attn_bwd_rope: head_dim 128 without dropout");
+    TORCH_CHECK(rope_cs->is_cuda() && rope_cs->scalar_type() == at::kFloat && rope_cs->is_contiguous() &&
+                    rope_cs->numel() >= (int64_t)S * 128,
+                "attn_bwd_rope: table must be fp32 [>= S, 64, 2] (cos, sin)");
+    p.rope_cs = reinterpret_cast<const float2*>(rope_cs->data_ptr<float>());
+  }
   HYP_CHECK_HIP(hyp::attention_backward(dt, p, cur_stream()));
+}
+
+void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+              const at::Tensor& o, const at::Tensor& lse, bool causal, double scale, double p_drop, const c10::optional<at::Tensor>& rng,
+              const c10::optional<at::Tensor>& kpm, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv) {
+  attn_bwd_impl(dout, q, k, v, o, lse, causal, scale, p_drop, rng, kpm, dq, dk, dv, nullptr);
+}
+
+// the same, with dQ / dK leaving through the inverse rotary embedding (positions = sequence index;
+// cs = the (cos, sin) table [S, 64, 2] of ops.rope.rope_table)
+void attn_bwd_rope(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                   const at::Tensor& o, const at::Tensor& lse, bool causal, double scale,
+                   const c10::optional<at::Tensor>& kpm, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
+                   const at::Tensor& cs) {
+  attn_bwd_impl(dout, q, k, v, o, lse, causal, scale, 0.0, c10::nullopt, kpm, dq, dk, dv, &cs);
 }
 
 // ---- LayerNorm / RMSNorm ------------------------------------------------------------------
@@ -196,6 +222,7 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
 void register_attn_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, "flash attention forward (MFMA)");
   m.def("attn_bwd", &attn_bwd, "flash attention backward (MFMA)");
+  m.def("attn_bwd_rope", &attn_bwd_rope, "flash attention backward with the inverse RoPE fused into dQ / dK");
   m.def("ln_fwd", &ln_fwd, "LayerNorm/RMSNorm forward (+fused residual add)");
   m.def("ln_bwd", &ln_bwd, "LayerNorm/RMSNorm backward");
 }

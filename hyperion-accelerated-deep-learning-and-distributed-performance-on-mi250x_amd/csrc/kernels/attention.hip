@@ -403,7 +403,10 @@ constexpr int BKB = 128;
 // D = 128 keeps 128 accumulator + 32 V-operand registers per lane live across the sweep: one wave
 // per SIMD with the whole register file (a 256-register cap spilled the V operand to scratch);
 // D = 64 fits two workgroups per CU.
-template <typename T, int D, bool DROP, bool DIRECT>
+// ROPE (D = 128): dQ and dK leave through the inverse rotary embedding (the forward applied RoPE to
+// q and k in the projection epilogue) — the rotate-half partner of a dK column is in the same lane,
+// the partner of a dQ block is the block of wave w ^ 2 (exchanged through LDS).
+template <typename T, int D, bool DROP, bool DIRECT, bool ROPE = false>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParams p) {
   constexpr int NS = D / 16;    // k-steps over the head dim
   constexpr int NDB = D / 32;   // 32-wide head-dim blocks
@@ -419,6 +422,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
   __shared__ __attribute__((aligned(16))) uint16_t dSt[BKB * QS];
   __shared__ __attribute__((aligned(16))) float lse_s[2][64];
   __shared__ __attribute__((aligned(16))) float del_s[2][64];
+  __shared__ float rope_x[ROPE ? 4 * 16 * 64 : 1];  // dQ blocks of the 4 waves [wave][e][lane]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int nkb = (p.S + BKB - 1) / BKB;
@@ -597,6 +601,14 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
       f32x16 acc;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      float2 rcs[ROPE ? 16 : 1];  // (cos, sin) of this lane's 16 dQ entries, in flight under the MFMAs
+      if constexpr (ROPE) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int qg = min(q0 + 32 * dq_qb + (e & 3) + 8 * (e >> 2) + 4 * hh, p.S - 1);
+          rcs[e] = p.rope_cs[(int64_t)qg * 64 + ((32 * dq_db + r) & 63)];
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < BKB / 16; ++ks) {
         const u16x4 a0 = read_tr(dSt, dqa[0] + 16 * QS * ks), a1 = read_tr(dSt, dqa[1] + 16 * QS * ks);
@@ -607,6 +619,18 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
       }
       // acc[e] = dQ[query q0 + 32 dq_qb + crow(e)][head dim 32 dq_db + r]
       const int d = 32 * dq_db + r;
+      if constexpr (ROPE) {  // inverse rotation: partner head-dim block dq_db ^ 2 lives in wave w ^ 2
+        static_assert(D == 128, "fused RoPE backward: head_dim 128");
+#pragma unroll
+        for (int e = 0; e < 16; ++e) rope_x[(w * 16 + e) * 64 + lane] = acc[e];
+        __syncthreads();
+        const bool lo = dq_db < 2;  // this block holds x0 (first half of the head)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float other = rope_x[(((w ^ 2) * 16) + e) * 64 + lane];
+          acc[e] = lo ? acc[e] * rcs[e].x + other * rcs[e].y : acc[e] * rcs[e].x - other * rcs[e].y;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int qg = q0 + 32 * dq_qb + (e & 3) + 8 * (e >> 2) + 4 * hh;
@@ -625,6 +649,21 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
   if (key < p.S) {
     uint16_t* dk = static_cast<uint16_t*>(p.dk) + b * p.sdkb + hd * p.sdkh + (int64_t)key * p.sdks;
     uint16_t* dv = static_cast<uint16_t*>(p.dv) + b * p.sdvb + hd * p.sdvh + (int64_t)key * p.sdvs;
+    if constexpr (ROPE) {  // inverse rotation of dK: columns d and d + 64 are blocks n and n + 2 of this lane
+      float2 kcs[2][16];
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) kcs[n][e] = p.rope_cs[(int64_t)key * 64 + 32 * n + 8 * (e >> 2) + 4 * hh + (e & 3)];
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float x0 = dkt[n][e], x1 = dkt[n + 2][e];
+          dkt[n][e] = x0 * kcs[n][e].x + x1 * kcs[n][e].y;
+          dkt[n + 2][e] = x1 * kcs[n][e].x - x0 * kcs[n][e].y;
+        }
+    }
 #pragma unroll
     for (int n = 0; n < NDB; ++n)
 #pragma unroll
@@ -673,14 +712,18 @@ hipError_t bwd_launch(const AttnBwdParams& p, hipStream_t st) {
   hipLaunchKernelGGL((attn_bwd_pre_k<T, D>), dim3((unsigned)((rows * (D / 8) + 255) / 256)), dim3(256), 0, st, p);
   const dim3 grid(((p.S + BKB - 1) / BKB) * p.B * p.H);
   const bool drop = p.p_drop > 0.f;
+  const bool rope = p.rope != 0;
+  if (rope && (D != 128 || drop)) return hipErrorInvalidValue;
   if (direct) {
     AttnBwdParams q = p;
     q.dq_acc = nullptr;
-    if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, true>), grid, dim3(256), 0, st, q);
+    if (rope) hipLaunchKernelGGL((attn_bwd_k<T, D, false, true, D == 128>), grid, dim3(256), 0, st, q);
+    else if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, true>), grid, dim3(256), 0, st, q);
     else hipLaunchKernelGGL((attn_bwd_k<T, D, false, true>), grid, dim3(256), 0, st, q);
     return hipGetLastError();
   }
-  if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, false>), grid, dim3(256), 0, st, p);
+  if (rope) hipLaunchKernelGGL((attn_bwd_k<T, D, false, false, D == 128>), grid, dim3(256), 0, st, p);
+  else if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, false>), grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL((attn_bwd_k<T, D, false, false>), grid, dim3(256), 0, st, p);
   const int64_t tot = rows * (D / 4);
   hipLaunchKernelGGL((attn_bwd_post_k<T, D>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p);

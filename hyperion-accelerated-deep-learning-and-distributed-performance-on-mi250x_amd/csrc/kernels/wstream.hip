@@ -487,6 +487,20 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
     const int64_t e0 = (((int64_t)mf * F + c) * 64 + lane) * 4;
     f32x4 acc4[4] = {acc, acc, acc, acc};
     int s = 0;
+    if (a.sb) {
+      // bf16 slabs: 16 quads (8 bytes each) in flight per round — the 24-43 slabs of a Llama data
+      // gradient take 2-3 memory round trips instead of 3-6
+      const uint16_t* p16 = reinterpret_cast<const uint16_t*>(a.part) + e0;
+      for (; s + 16 <= a.S; s += 16) {
+        uint2 q[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) q[i] = *reinterpret_cast<const uint2*>(p16 + (s + i) * slab);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          acc4[i & 3] += f32x4{__uint_as_float(q[i].x << 16), __uint_as_float(q[i].x & 0xffff0000u),
+                               __uint_as_float(q[i].y << 16), __uint_as_float(q[i].y & 0xffff0000u)};
+      }
+    }
     for (; s + 8 <= a.S; s += 8) {
       f32x4 v[8];
 #pragma unroll

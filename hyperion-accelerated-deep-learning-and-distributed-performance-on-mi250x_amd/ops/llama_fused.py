@@ -38,6 +38,7 @@ import torch
 import torch.nn as nn
 
 from . import _native
+from .rope import rope_table
 
 WS_MAX_M = int(os.environ.get("HYPERION_WS_MAX_M", "512"))
 RANK_SPLITS = 4  # slices of the rank-r split-partial stacks (t: k-splits of lora_down, du: n-splits)
@@ -326,9 +327,13 @@ class _LlamaLayerFn(torch.autograd.Function):
         dqkv = torch.empty(M, 3 * H, device=dev, dtype=dt)
         d5 = dqkv.view(Bsz, S, 3, spec.nh, spec.hd)
         dq, dk, dv = d5[:, :, 0], d5[:, :, 1], d5[:, :, 2]
-        C.attn_bwd(do.view(Bsz, S, spec.nh, spec.hd), q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, lse, True, scale,
-                   0.0, None, kpm, dq, dk, dv)
-        C.rope_(dq, dk, None, spec.theta, True)
+        if spec.hd == 128:  # inverse RoPE fused into the attention backward's dQ / dK stores
+            C.attn_bwd_rope(do.view(Bsz, S, spec.nh, spec.hd), q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, lse, True,
+                            scale, kpm, dq, dk, dv, rope_table(S, spec.hd, spec.theta, dev))
+        else:
+            C.attn_bwd(do.view(Bsz, S, spec.nh, spec.hd), q5[:, :, 0], q5[:, :, 1], q5[:, :, 2], o, lse, True, scale,
+                       0.0, None, kpm, dq, dk, dv)
+            C.rope_(dq, dk, None, spec.theta, True)
         # q/k/v: dh = dqkv [W_q; W_k; W_v] + Σ_p keep_p ∘ (du'_p A_p)
         du_qkv = None
         if lora:

@@ -7,6 +7,7 @@ in fp32 on the fly (no cos/sin cache tensors); backward is the inverse rotation.
 """
 from __future__ import annotations
 
+import math
 from typing import Optional, Tuple
 
 import torch
@@ -28,6 +29,24 @@ def rope_reference(q: torch.Tensor, k: torch.Tensor, positions: Optional[torch.T
         return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
     return rot(q), rot(k)
+
+
+_TABLES: dict = {}
+
+
+def rope_table(S: int, D: int, theta: float, device) -> torch.Tensor:
+    """fp32 [S, D/2, 2] (cos, sin) of position x inv_freq(i), inv_freq = theta^(-2i/D) computed as the
+    kernels do (exp2 of -(2i/D) log2 theta); cached per (S, D, theta, device) — built eagerly before
+    a hipGraph capture reads it (the fused attention backward's inverse RoPE)."""
+    key = (int(S), int(D), float(theta), str(device))
+    t = _TABLES.get(key)
+    if t is None:
+        i = torch.arange(D // 2, device=device, dtype=torch.float32)
+        inv = torch.exp2(-(2.0 * i / D) * math.log2(theta))
+        ang = torch.arange(S, device=device, dtype=torch.float32)[:, None] * inv[None, :]
+        t = torch.stack([torch.cos(ang), torch.sin(ang)], dim=-1).contiguous()
+        _TABLES[key] = t
+    return t
 
 
 class _RopeFn(torch.autograd.Function):

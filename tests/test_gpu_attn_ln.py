@@ -44,6 +44,31 @@ def test_attention_fwd_bwd(dtype, B, S, H, D, causal):
         torch.testing.assert_close(a.grad.float(), b.grad, atol=gt, rtol=gt)
 
 
+@pytest.mark.parametrize("S", [128, 300])
+def test_attention_bwd_fused_inverse_rope(S):
+    """attn_bwd_rope == attn_bwd followed by the inverse RoPE pass (D = 128; direct dQ at S <= 128,
+    atomic dQ above)."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    torch.manual_seed(0)
+    B, H, D = 2, 4, 128
+    q, k, v, do = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16) for _ in range(4))
+    scale = 1.0 / math.sqrt(D)
+    o, lse = C.attn_fwd(q, k, v, True, scale, 0.0, None, None, True)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    C.attn_bwd(do, q, k, v, o, lse, True, scale, 0.0, None, None, dq, dk, dv)
+    C.rope_(dq, dk, None, 10000.0, True)
+    dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    from hyperion.ops.rope import rope_table
+
+    C.attn_bwd_rope(do, q, k, v, o, lse, True, scale, None, dq2, dk2, dv2, rope_table(S, D, 10000.0, q.device))
+    torch.testing.assert_close(dv2, dv, atol=0, rtol=0)
+    for a, b in ((dq2, dq), (dk2, dk)):  # one bf16 rounding fewer on the fused path
+        err = (a.float() - b.float()).abs().max().item()
+        assert err <= 2e-2 * b.float().abs().max().item(), err
+
+
 def test_attention_packed_and_padding_mask():
     from hyperion.ops.attention import attention_packed
 
