@@ -157,7 +157,9 @@ class LlamaModel(nn.Module):
         kpm = None
         positions = None
         if attention_mask is not None:
-            kpm = attention_mask == 0  # True = padded key
+            # nonzero = padded key; uint8 once per forward (the kernels' mask dtype) instead of a
+            # bool -> uint8 copy in each of the 32 layers
+            kpm = (attention_mask == 0).to(torch.uint8)
             # HF computes positions from the mask only when generating; training uses arange
         d: Optional[torch.Tensor] = None
         s = x

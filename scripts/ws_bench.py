@@ -42,6 +42,7 @@ def pool_of(shape, nbytes_min=640 << 20):
 
 
 M = int(os.environ.get("WS_M", "128"))
+SLAB16 = os.environ.get("HYPERION_WS_SLAB", "bf16") != "fp32"  # the Llama layer's slab dtype
 shapes = [  # (name, N out, K in) of y = x Wᵀ; dgrad rows use W [N, K] read as NN
     ("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096), ("down", 4096, 11008),
 ]
@@ -54,8 +55,8 @@ for name, N, K in shapes:
     r = {"name": name, "M": M, "N": N, "K": K, "weight_MB": wb / 1e6}
     r["ws_nt"] = timed(lambda w: C.ws_linear(x, w), pool)
     r["ws_nn"] = timed(lambda w: C.ws_linear(dy, w, nn=True), pool)
-    r["ws_nt_gemm_only"] = timed(lambda w: C.ws_gemm_part(x, w), pool)
-    r["ws_nn_gemm_only"] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True), pool)
+    r["ws_nt_gemm_only"] = timed(lambda w: C.ws_gemm_part(x, w, slab16=SLAB16), pool)
+    r["ws_nn_gemm_only"] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True, slab16=SLAB16), pool)
     # M split in two 64-row blocks with twice the slice length: half the slab bytes
     r["ws_nt_mf4"] = timed(lambda w: C.ws_linear(x, w, mf=4, kr=1024, G=max(1, 256 // (2 * -(-K // 1024)))), pool)
     r["ws_nn_mf4"] = timed(lambda w: C.ws_linear(dy, w, nn=True, mf=4, kr=1024, G=max(1, 256 // (2 * -(-N // 1024)))), pool)
@@ -69,7 +70,7 @@ for name, N, K in shapes:
     r["plan_nt"], r["plan_nn"] = plan_nt, plan_nn
     # sweep: m-block rows (mf), slice length, column groups, fragments per chunk
     sweep = {}
-    for mf, krs in ((8, (256, 512)), (4, (512, 1024)), (2, (1024, 2048))):
+    for mf, krs in ((8, (256, 384, 512)), (4, (512, 1024)), (2, (1024, 2048))):
         MB = -(-M // (16 * mf))
         for kr in krs:
             S = -(-K // kr)
@@ -77,14 +78,14 @@ for name, N, K in shapes:
                 for nf in (1, 2, 4):
                     k = f"nt_mf{mf}_kr{kr}_G{G}_nf{nf}"
                     try:
-                        sweep[k] = timed(lambda w: C.ws_gemm_part(x, w, mf=mf, kr=kr, G=G, nf=nf), pool, 2)
+                        sweep[k] = timed(lambda w: C.ws_gemm_part(x, w, mf=mf, kr=kr, G=G, nf=nf, slab16=SLAB16), pool, 2)
                     except RuntimeError as ex:  # unsupported plan
                         sweep[k] = str(ex)[:60]
             S = -(-N // kr)
             for G in sorted({max(1, 256 // (S * MB)), max(1, 512 // (S * MB))}):
                 k = f"nn_mf{mf}_kr{kr}_G{G}"
                 try:
-                    sweep[k] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True, mf=mf, kr=kr, G=G), pool, 2)
+                    sweep[k] = timed(lambda w: C.ws_gemm_part(dy, w, nn=True, mf=mf, kr=kr, G=G, slab16=SLAB16), pool, 2)
                 except RuntimeError as ex:
                     sweep[k] = str(ex)[:60]
     r["sweep"] = sweep
