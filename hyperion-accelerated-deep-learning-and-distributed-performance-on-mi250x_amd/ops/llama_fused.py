@@ -200,6 +200,19 @@ PLANS = {
 }
 
 
+# cold-weight sweep with bf16 slabs (scripts/ws_bench.py, profiles/r03/ws_bench_bf16_slabs.json):
+# GEMM-only best plans — q/k/v forward now streams faster than hipBLASLt (28.1 vs 32.3 us)
+PLANS_BF16 = {
+    (False, 12288, 4096): ("ws", 8, 512, 32, 1),
+    (False, 4096, 4096): ("ws", 8, 512, 32, 1),
+    (True, 4096, 4096): ("ws", 8, 256, 16, 4),
+    (True, 4096, 22016): ("ws", 8, 384, 4, 4),
+    (True, 11008, 4096): ("ws", 8, 384, 23, 4),
+}
+if SLAB16 and os.environ.get("HYPERION_WS_PLANS", "bf16") == "bf16":
+    PLANS = {**PLANS, **PLANS_BF16}
+
+
 def plan_for(nn_: bool, M: int, N: int, K: int) -> tuple:
     if _PLAN_OVERRIDE == "vendor":
         return ("vendor",)
