@@ -203,18 +203,24 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
   auto part = at::empty({2 * (int64_t)P * d}, fopt);
   const int wt = affine_mode(xin, weight, c10::nullopt, "ln_bwd");
   auto wopt = wt ? xin.options() : fopt;  // dγ / dβ in the weight's dtype
-  at::Tensor dw, db;
-  if (need_dw) dw = at::empty({d}, wopt);
-  if (need_db && !rms) db = at::empty({d}, wopt);
+  // LayerNorm: dγ and dβ come out of one combine pass into one [2, d] buffer (both computed)
+  at::Tensor dw, db, dwdb;
+  if (!rms && (need_dw || need_db)) {
+    dwdb = at::empty({2, d}, wopt);
+    dw = dwdb[0];
+    db = dwdb[1];
+  } else if (need_dw) {
+    dw = at::empty({d}, wopt);
+  }
   at::Tensor dr;
   if (dres.has_value() && dres->defined()) dr = dres->is_contiguous() ? *dres : dres->contiguous();
   HYP_CHECK_HIP(hyp::layernorm_backward(dtype_code(xin), rms ? 1 : 0, g.data_ptr(), xin.data_ptr(),
                                         affine_ptr(weight), rms ? nullptr : mean.data_ptr<float>(),
                                         rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(),
-                                        part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)P * d,
-                                        need_dw ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr,
+                                        part.data_ptr<float>(), db.defined() ? part.data_ptr<float>() + d : nullptr,
+                                        dw.defined() ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr,
                                         rows, d, P, rpw, cur_stream(), wt));
-  return {dx, dw, db};
+  return {dx, need_dw ? dw : at::Tensor(), need_db ? db : at::Tensor()};
 }
 
 }  // namespace

@@ -248,8 +248,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
       a += sw[q * d + c];
       bb += sb[q * d + c];
     }
-    pdw[(int64_t)blockIdx.x * d + c] = a;
-    if (pdb) pdb[(int64_t)blockIdx.x * d + c] = bb;
+    // partial rows [P][d] (dγ only) or [P][2d] (dγ | dβ: one combine pass for both)
+    const int64_t ps = pdb ? 2 * (int64_t)d : d;
+    pdw[(int64_t)blockIdx.x * ps + c] = a;
+    if (pdb) pdb[(int64_t)blockIdx.x * ps + c] = bb;
   }
 }
 
@@ -434,11 +436,12 @@ __global__ __launch_bounds__(kWideThreads) void ln_bwd_wide_k(const T* __restric
   for (int k = 0; k < VW; ++k) {
     const int c = (k * kWideThreads + tid) * 8;
     if (c < d) {
-      float4* pw = reinterpret_cast<float4*>(pdw + (int64_t)blockIdx.x * d + c);
+      const int64_t ps = pdb ? 2 * (int64_t)d : d;  // [P][d] or [P][2d] (dγ | dβ)
+      float4* pw = reinterpret_cast<float4*>(pdw + (int64_t)blockIdx.x * ps + c);
       pw[0] = make_float4(gw[k][0], gw[k][1], gw[k][2], gw[k][3]);
       pw[1] = make_float4(gw[k][4], gw[k][5], gw[k][6], gw[k][7]);
       if (pdb) {
-        float4* pb = reinterpret_cast<float4*>(pdb + (int64_t)blockIdx.x * d + c);
+        float4* pb = reinterpret_cast<float4*>(pdb + (int64_t)blockIdx.x * ps + c);
         pb[0] = make_float4(gb[k][0], gb[k][1], gb[k][2], gb[k][3]);
         pb[1] = make_float4(gb[k][4], gb[k][5], gb[k][6], gb[k][7]);
       }
@@ -495,6 +498,14 @@ template <typename T, bool RMS>
 hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const float* mean, const float* rstd,
                            const T* dres, T* dx, float* pdw, float* pdb, void* dw, void* db, int64_t rows, int d,
                            int P, int rows_per_wave, hipStream_t st, int wt, int wdt) {
+  // with a bias: dγ and dβ partials interleave per block row ([P][2d]) and ONE combine writes
+  // dw | db (the caller's db must directly follow dw)
+  const size_t wbytes = wdt == kF32 ? 4 : 2;
+  if (pdb != nullptr) {
+    pdb = pdw + d;
+    if (dw == nullptr || db == nullptr || static_cast<char*>(db) != static_cast<char*>(dw) + (size_t)d * wbytes)
+      return hipErrorInvalidValue;
+  }
   if (d > 2048) {  // P blocks of rows_per_wave rows (layernorm_bwd_geom)
     if (dres)
       hipLaunchKernelGGL((ln_bwd_wide_k<T, 2, RMS, true>), dim3(P), dim3(kWideThreads), 0, st, dy, xin, w, mean, rstd,
@@ -503,8 +514,7 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
       hipLaunchKernelGGL((ln_bwd_wide_k<T, 2, RMS, false>), dim3(P), dim3(kWideThreads), 0, st, dy, xin, w, mean, rstd,
                          dres, dx, pdw, pdb, rows, d, rows_per_wave, wt);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, wdt, st);
-    if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, wdt, st);
+    if (e == hipSuccess && dw) e = colsum_combine(pdw, P, pdb ? 2 * d : d, dw, wdt, st);
     return e;
   }
   const int vpl = (d + 511) / 512;
@@ -530,8 +540,7 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
   }
 #undef HYP_LN_B
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess && dw) e = colsum_combine(pdw, P, d, dw, wdt, st);
-  if (e == hipSuccess && db && pdb) e = colsum_combine(pdb, P, d, db, wdt, st);
+  if (e == hipSuccess && dw) e = colsum_combine(pdw, P, pdb ? 2 * d : d, dw, wdt, st);
   return e;
 }
 
