@@ -39,6 +39,18 @@ def autocast_ctx(device: torch.device, dtype: Optional[torch.dtype]):
     return torch.autocast(device_type=device.type, dtype=dtype)
 
 
+
+def _has_dropout(module: torch.nn.Module) -> bool:
+    """Any active dropout (nn.Dropout-family modules, or an attention module's dropout rate)."""
+    for m in module.modules():
+        if isinstance(m, torch.nn.modules.dropout._DropoutNd) and m.p > 0:
+            return True
+        for attr in ("dropout_p", "attn_dropout", "dropout"):
+            v = getattr(m, attr, None)
+            if isinstance(v, float) and v > 0:
+                return True
+    return False
+
 class TrainStep:
     """``loss = step(x, y)``; captures a hipGraph on GPU when ``graph=True``."""
 
@@ -88,7 +100,15 @@ class TrainStep:
             return None
         fn = getattr(ddp.module, "graph_stages", None)
         st = fn() if callable(fn) else None
-        return st if st is not None and len(st) == 2 else None
+        if st is None or len(st) != 2:
+            return None
+        # a dropout mask is regenerated in backward from the generator offset that each graph
+        # replay rewrites: forward in graph 1 and the bottom backward in graph 2 would see different
+        # masks — a bottom stage with active dropout keeps the single-graph step
+        bottom = st[0] if isinstance(st[0], torch.nn.Module) else ddp.module  # (a callable: the whole model)
+        if _has_dropout(bottom):
+            return None
+        return st
 
     def _fwd_bwd_top(self, x: torch.Tensor, y: torch.Tensor, stages, zero_in_place: bool = False):
         """Forward through both stages, backward through the top one only."""
