@@ -423,6 +423,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
   __shared__ __attribute__((aligned(16))) float lse_s[2][64];
   __shared__ __attribute__((aligned(16))) float del_s[2][64];
   __shared__ float rope_x[ROPE ? 4 * 16 * 64 : 1];  // dQ blocks of the 4 waves [wave][e][lane]
+  // direct D = 128 (one key block per (b, h): each query slice is visited once): delta = rowsum(dO·O)
+  // is computed here from an O slice staged beside dO — no separate pre-pass launch
+  constexpr bool FDELTA = DIRECT && D == 128;
+  __shared__ __attribute__((aligned(16))) uint16_t Os[FDELTA ? 2 : 1][FDELTA ? QS * D : 8];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int nkb = (p.S + BKB - 1) / BKB;
@@ -452,10 +456,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
                                        (void __attribute__((address_space(3)))*)(img + pc * 512), 16, 0, 0);
     }
   };
+  const uint16_t* ob = static_cast<const uint16_t*>(p.o) + b * p.sob + hd * p.soh;
   auto dma_slice = [&](int q0, int buf) {
     dma_rows(qb, p.sqs, q0, Qs[buf], SPC);
     dma_rows(gb, p.sdos, q0, dOs[buf], SPC);
-    if (w < 2) {
+    if constexpr (FDELTA) dma_rows(ob, p.sos, q0, Os[buf], SPC);
+    if (w < (FDELTA ? 1 : 2)) {
       const float* src = (w == 0 ? lse_g : del_g) + min(q0 + lane, p.S - 1);
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (void __attribute__((address_space(3)))*)(w == 0 ? lse_s[buf] : del_s[buf]),
@@ -522,6 +528,23 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
     if (sl + 1 < nsl) dma_slice(q0 + QS, cur ^ 1);
     const uint16_t* Qc = Qs[cur];
     const uint16_t* Gc = dOs[cur];
+    if constexpr (FDELTA) {  // delta[q] = Σ_d dO·O: 8 threads per query row, 16 columns each
+      const int row = tid >> 3, part = tid & 7;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int off = img_off<D>(row, 2 * part + c);
+        const u16x8 g8 = *reinterpret_cast<const u16x8*>(Gc + off);
+        const u16x8 o8 = *reinterpret_cast<const u16x8*>(Os[cur] + off);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += MM<T>::tof(g8[e]) * MM<T>::tof(o8[e]);
+      }
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      acc += __shfl_xor(acc, 4, 64);
+      if (part == 0) del_s[cur][row] = acc;
+      __syncthreads();
+    }
 #pragma unroll
     for (int qbk = 0; qbk < NQB; ++qbk) {
       const int qbase = q0 + 32 * qbk;
@@ -709,7 +732,8 @@ hipError_t bwd_launch(const AttnBwdParams& p, hipStream_t st) {
   const int64_t rows = (int64_t)p.B * p.H * p.S;
   const bool direct = p.S <= BKB;
   if (!direct && !p.dq_acc) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((attn_bwd_pre_k<T, D>), dim3((unsigned)((rows * (D / 8) + 255) / 256)), dim3(256), 0, st, p);
+  if (!(direct && D == 128))  // (direct D = 128 computes delta in the main kernel)
+    hipLaunchKernelGGL((attn_bwd_pre_k<T, D>), dim3((unsigned)((rows * (D / 8) + 255) / 256)), dim3(256), 0, st, p);
   const dim3 grid(((p.S + BKB - 1) / BKB) * p.B * p.H);
   const bool drop = p.p_drop > 0.f;
   const bool rope = p.rope != 0;
