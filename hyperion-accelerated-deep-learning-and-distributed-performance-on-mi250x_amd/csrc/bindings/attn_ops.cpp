@@ -79,7 +79,11 @@ void attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
   // fp32 dQ workspace only when several key blocks add into one dQ row (attn_bwd_k stores dQ
   // directly for S <= 128)
   at::Tensor dq_acc;
-  if (S > 128) dq_acc = at::empty({(int64_t)B * H * S * D}, fopt);
+  // 2-4 key blocks (ViT-B/16's 197 tokens): one fp32 slab per key block, summed in order by the
+  // conversion pass (deterministic, no zero-fill, no atomics); more blocks: fp32 atomics
+  const int nkb = (S + 127) / 128;
+  const int dq_slabs = (nkb >= 2 && nkb <= 4) ? nkb : 0;
+  if (S > 128) dq_acc = at::empty({(int64_t)(dq_slabs ? dq_slabs : 1) * B * H * S * D}, fopt);
   at::Tensor kpm_u8;
   if (kpm.has_value() && kpm->defined()) kpm_u8 = kpm->to(at::kByte).contiguous();
   hyp::AttnBwdParams p{};
@@ -96,6 +100,7 @@ void attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
   p.lse = lse.data_ptr<float>();
   p.delta = delta.data_ptr<float>();
   p.dq_acc = dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr;
+  p.dq_slabs = dq_acc.defined() ? dq_slabs : 0;
   p.kpm = kpm_u8.defined() ? kpm_u8.data_ptr<uint8_t>() : nullptr;
   p.B = B; p.H = H; p.S = S; p.D = D;
   p.scale = (float)scale;

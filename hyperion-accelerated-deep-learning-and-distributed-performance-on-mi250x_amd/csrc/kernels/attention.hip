@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_k(AttnBwdParams p) {
                                                     hd * p.sdoh + (int64_t)q * p.sdos + 8 * c);
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc += MM<T>::tof(o[e]) * MM<T>::tof(g[e]);
-    if (p.dq_acc) {
+    if (p.dq_acc && p.dq_slabs == 0) {  // (slab mode: every slab row is stored, nothing to clear)
       float4* dq = reinterpret_cast<float4*>(p.dq_acc + row * D + 8 * c);
       dq[0] = make_float4(0.f, 0.f, 0.f, 0.f);
       dq[1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -662,7 +662,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
             uint16_t* dq = static_cast<uint16_t*>(p.dq) + b * p.sdqb + hd * p.sdqh + (int64_t)qg * p.sdqs;
             dq[d] = MM<T>::cvt(acc[e] * p.scale);
           } else {
-            atomicAdd(p.dq_acc + ((int64_t)bh * p.S + qg) * D + d, acc[e] * p.scale);
+            if (p.dq_slabs)  // one fp32 slab per key block, summed in order by attn_bwd_post_k
+              p.dq_acc[(((int64_t)kblk * p.B * p.H + bh) * p.S + qg) * D + d] = acc[e] * p.scale;
+            else
+              atomicAdd(p.dq_acc + ((int64_t)bh * p.S + qg) * D + d, acc[e] * p.scale);
           }
         }
       }
@@ -713,7 +716,18 @@ __global__ __launch_bounds__(256) void attn_bwd_post_k(AttnBwdParams p) {
   const int q = (int)(row % p.S);
   const int bh = (int)(row / p.S);
   const int b = bh / p.H, hd = bh - b * p.H;
-  const float4 v = *reinterpret_cast<const float4*>(p.dq_acc + row * D + d);
+  float4 v;
+  if (p.dq_slabs) {  // key blocks whose slice range covers q (causal: key block j starts at query 128 j)
+    v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t slab = (int64_t)p.B * p.H * p.S * D;
+    const int nk = p.causal ? min(p.dq_slabs, q / BKB + 1) : p.dq_slabs;
+    for (int j = 0; j < nk; ++j) {
+      const float4 u = *reinterpret_cast<const float4*>(p.dq_acc + j * slab + row * D + d);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+  } else {
+    v = *reinterpret_cast<const float4*>(p.dq_acc + row * D + d);
+  }
   uint16_t* dq = static_cast<uint16_t*>(p.dq) + b * p.sdqb + hd * p.sdqh + (int64_t)q * p.sdqs + d;
   u16x4 o = {MM<T>::cvt(v.x), MM<T>::cvt(v.y), MM<T>::cvt(v.z), MM<T>::cvt(v.w)};
   *reinterpret_cast<u16x4*>(dq) = o;
