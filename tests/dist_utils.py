@@ -3,6 +3,7 @@ import io
 import os
 import socket
 import sys
+import tempfile
 import traceback
 
 import torch
@@ -17,13 +18,16 @@ def free_port() -> int:
     return p
 
 
-def _entry(rank, world, port, fn, args, q):
+def _entry(rank, world, port, fn, args, q, store_file=None):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if store_file is not None:  # file rendezvous: no TCP port to race for under pytest-xdist
+            dist.init_process_group("gloo", init_method=f"file://{store_file}", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         out = fn(rank, world, *args)
         buf = io.BytesIO()
         torch.save(out, buf)  # plain bytes: tensors in a Queue would ride on fds that die with the child
@@ -40,7 +44,10 @@ def run_world(fn, world: int = 2, args=(), timeout: float = 180.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    fd, store_file = tempfile.mkstemp(prefix="hyp_dist_", suffix=".store")
+    os.close(fd)
+    os.unlink(store_file)  # the FileStore creates it; a stale file would hold old keys
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, store_file)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -55,4 +62,6 @@ def run_world(fn, world: int = 2, args=(), timeout: float = 180.0):
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
+        if os.path.exists(store_file):
+            os.unlink(store_file)
     return res
