@@ -486,6 +486,79 @@ std::vector<at::Tensor> bn_fwd_sums(const at::Tensor& x, const c10::optional<at:
   return {y, stats[0], stats[1]};
 }
 
+// ---- ResNet stem (csrc/kernels/stem.hip) ----------------------------------------------------
+// x [N, C <= 4, H, W] channels-last -> Xs [N, 16, P + 3, Q + 3] channels-last (space-to-depth)
+at::Tensor stem_s2d(const at::Tensor& x) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) >= 1 && x.size(1) <= 4,
+              "stem_s2d: channels-last [N, C <= 4, H, W]");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "stem_s2d: bf16/f16");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int P = (H - 1) / 2 + 1, Q = (W - 1) / 2 + 1;
+  const at::DeviceGuard guard(x.device());
+  auto out = at::empty({N, 16, P + 3, Q + 3}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  HYP_CHECK_HIP(hyp::stem_s2d(dtype_code(x), x.data_ptr(), out.data_ptr(), N, H, W, C, P + 3, Q + 3, cur_stream()));
+  return out;
+}
+
+namespace {
+void check_stem(const at::Tensor& xs, int64_t K) {
+  HYP_CHECK_CUDA_TENSOR(xs);
+  TORCH_CHECK(xs.dim() == 4 && xs.size(1) == 16 && xs.size(2) > 3 && xs.size(3) > 3 &&
+                  xs.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem conv: Xs must be the channels-last [N, 16, P + 3, Q + 3] output of stem_s2d");
+  TORCH_CHECK(K % 8 == 0, "stem conv: K % 8 == 0");
+}
+}  // namespace
+
+// y [N, K, P, Q] = the stem conv from Xs and W4 [K, 64, 4, 1] (channels-last: memory [k][dr][64]),
+// with the BN-statistics epilogue into `sums` (zeroed fp64 [kStatSlots * 2 * K]).
+at::Tensor stem_conv_fwd(const at::Tensor& xs, const at::Tensor& w4, const at::Tensor& sums) {
+  check_stem(xs, w4.size(0));
+  TORCH_CHECK(w4.dim() == 4 && w4.size(1) == 64 && w4.size(2) == 4 && w4.size(3) == 1 &&
+                  w4.is_contiguous(at::MemoryFormat::ChannelsLast) && w4.scalar_type() == xs.scalar_type(),
+              "stem_conv_fwd: W4 must be a channels-last [K, 64, 4, 1] tensor of Xs's dtype");
+  const int N = xs.size(0), Hs = xs.size(2), Ws = xs.size(3), K = w4.size(0), P = Hs - 3, Q = Ws - 3;
+  const at::DeviceGuard guard(xs.device());
+  auto y = at::empty({N, K, P, Q}, xs.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int M = N * P * Q;
+  int bm = 128, bn = 128;
+  hyp::conv_fwd_tile(M, K, &bm, &bn);
+  const int splits = plan_splits(M, K, 4, bm, bn, -1);
+  at::Tensor slabs;
+  if (splits > 1) slabs = at::empty({splits, M, K}, xs.options().dtype(at::kFloat));
+  at::Tensor acc = stats_sums(sums, K, xs);
+  HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(xs), xs.data_ptr(), w4.data_ptr(), y.data_ptr(), device_zero_page(xs.device()),
+                              acc.data_ptr<double>(), acc.data_ptr<double>() + K, N, Hs, Ws, 64, K, P, Q, 4, 1, 1, 1, 0,
+                              0, bm, bn, 0, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f,
+                              nullptr, nullptr, nullptr, 16));
+  return y;
+}
+
+// dW4 [K, 64, 4, 1] (channels-last) of the stem conv from dY [N, K, P, Q] and Xs.
+at::Tensor stem_conv_wgrad(const at::Tensor& dy, const at::Tensor& xs, int64_t splits_req) {
+  check_stem(xs, dy.size(1));
+  TORCH_CHECK(dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.scalar_type() == xs.scalar_type() &&
+                  dy.size(0) == xs.size(0) && dy.size(2) == xs.size(2) - 3 && dy.size(3) == xs.size(3) - 3,
+              "stem_conv_wgrad: dY must be channels-last [N, K, P, Q] of Xs's dtype");
+  const int N = xs.size(0), Hs = xs.size(2), Ws = xs.size(3), K = dy.size(1), P = Hs - 3, Q = Ws - 3;
+  const at::DeviceGuard guard(xs.device());
+  auto dw = at::empty({K, 64, 4, 1}, xs.options().memory_format(at::MemoryFormat::ChannelsLast));
+  // a 4-tile output over a ~4e5-pixel reduction: split the pixels until ~1024 workgroups stream
+  // (the generic plan's <= 64 splits leave 256 workgroups 98 k-steps deep: 68 us on MI355X)
+  const int bm = 64, bn = 64, tiles = ((K + 63) / 64) * 4, steps = (N * P * Q + 63) / 64;
+  int per = std::max(16, (steps * tiles + 1023) / 1024);
+  if (splits_req > 0) per = (steps + (int)splits_req - 1) / (int)splits_req;
+  const int splits = (steps + per - 1) / per;
+  at::Tensor part;
+  if (splits > 1) part = at::empty({(int64_t)splits * K * 4 * 64}, xs.options().dtype(at::kFloat));
+  HYP_CHECK_HIP(hyp::conv_wgrad(dtype_code(xs), dy.data_ptr(), xs.data_ptr(), dw.data_ptr(),
+                                splits > 1 ? part.data_ptr<float>() : nullptr, device_zero_page(xs.device()), N, Hs, Ws,
+                                64, K, P, Q, 4, 1, 1, 1, 0, 0, bm, bn, splits, per, cur_stream(), 1.f, nullptr, false,
+                                16));
+  return dw;
+}
+
 // ---- pooling (NHWC) -------------------------------------------------------------------------
 std::vector<at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
   HYP_CHECK_CUDA_TENSOR(x);
@@ -591,6 +664,14 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("splits") = -1, pybind11::arg("bn") = -1,
         pybind11::arg("alpha") = 1.0, pybind11::arg("U") = pybind11::none(), pybind11::arg("V") = pybind11::none(),
         pybind11::arg("v_nr") = false, pybind11::arg("mask") = pybind11::none(), pybind11::arg("beta") = 1.0);
+  m.def("conv_set_stamps", [](const c10::optional<at::Tensor>& buf) {
+    hyp::conv_set_stamps(buf.has_value() && buf->defined() ? buf->data_ptr() : nullptr);
+  }, "diagnostic: record a per-workgroup timeline (int64 [>= 6 * workgroups]) of the next conv_fwd launches",
+        pybind11::arg("buf") = pybind11::none());
+  m.def("stem_s2d", &stem_s2d, "ResNet 7x7/s2/p3 stem input as space-to-depth Xs [N, 16, P+3, Q+3]");
+  m.def("stem_conv_fwd", &stem_conv_fwd, "the stem conv (R=4 x 64 over Xs, pixel stride 16) + BN statistics");
+  m.def("stem_conv_wgrad", &stem_conv_wgrad, "dW4 [K, 64, 4, 1] of the stem conv", pybind11::arg("dy"),
+        pybind11::arg("xs"), pybind11::arg("splits") = -1);
   m.def("maxpool2d_fwd", &maxpool2d_fwd, "NHWC max pool (+ window-tap index)");
   m.def("maxpool2d_bwd", &maxpool2d_bwd, "NHWC max pool backward (gather, deterministic)");
   m.def("global_avgpool_fwd", &global_avgpool_fwd, "NHWC global average pool");

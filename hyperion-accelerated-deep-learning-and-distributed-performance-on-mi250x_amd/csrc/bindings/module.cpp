@@ -2,6 +2,7 @@
 #include <torch/extension.h>
 
 #include "bindings/registry.h"
+#include "hyp_kernels.h"
 
 #ifndef HYP_MODULE_NAME
 #define HYP_MODULE_NAME _C
@@ -10,6 +11,7 @@
 PYBIND11_MODULE(HYP_MODULE_NAME, m) {
   m.doc() = "Hyperion-MI355X native kernels (gfx950 HIP) and RCCL communicator";
   m.attr("arch") = "gfx950";
+  m.attr("STAT_SLOTS") = hyp::kStatSlots;
 #ifdef HYP_DEBUG
   m.attr("debug_build") = true;
 #else

@@ -181,7 +181,10 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
                     const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr,
-                    const struct BnBwdEpilogue* bnb = nullptr);
+                    const struct BnBwdEpilogue* bnb = nullptr, int pix = 0);
+// pix (conv_fwd / conv_wgrad): the input's pixel stride in elements when it differs from the
+// 64-multiple reduction slice C (0 = C) — the stem's space-to-depth input (stem.hip): 16-channel
+// pixels read as 64-element runs of 4 adjacent pixels.
 // Fused linear + cross-entropy epilogues of the implicit-GEMM kernel (linear_ce below).
 struct CeEpilogue {
   const float* bias = nullptr;      // [V] fp32 or null, indexed by vocabulary index
@@ -265,7 +268,7 @@ struct WgradPendingReduce {
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
                       int bn, int splits, int steps_per_split, hipStream_t st, float alpha,
-                      const WgradPendingReduce* pending = nullptr, bool defer_reduce = false);
+                      const WgradPendingReduce* pending = nullptr, bool defer_reduce = false, int pix = 0);
 }  // namespace hyp
 
 namespace hyp {
@@ -290,6 +293,11 @@ hipError_t maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, in
 hipError_t maxpool2d_backward(int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C,
                               int k, int s, int pad, hipStream_t st);
 hipError_t global_avgpool_forward(int dtype, const void* x, void* y, int N, int HW, int C, hipStream_t st);
+// diagnostic: per-workgroup timeline of the next conv_fwd launches (6 u64 per workgroup; null = off)
+void conv_set_stamps(void* buf);
+// ---- stem.hip: the 7x7/s2/p3 stem (C <= 4) as a stride-1 R=4 x S=1 conv with pixel stride 16:
+// Xs [N, Hs = P + 3, Ws = Q + 3, 16] (space-to-depth) from x [N, H, W, C] (both channels-last)
+hipError_t stem_s2d(int dtype, const void* x, void* out, int N, int H, int W, int C, int Hs, int Ws, hipStream_t st);
 // out[N,H,W,C] = addend (optional) + comp[N,P,Q,C] scattered to pixels (p*sh, q*sw), zeros elsewhere
 hipError_t upsample_add(int dtype, const void* comp, const void* addend, void* out, int N, int H, int W, int C, int P,
                         int Q, int sh, int sw, hipStream_t st);

@@ -67,6 +67,7 @@ struct ConvArgs {
   double* psq;           // psum + K: Σy²
   int N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw;
   int M;                 // N*P*Q
+  int pix;               // input pixel stride in elements (C, or the stem's 16: see hyp_kernels.h)
   int group;             // M-tiles per tile-order group (see conv_fwd_group)
   int splits, steps_per_split;  // split-K over the reduction (splits > 1: fp32 partials, no STATS)
   float* part;                  // [splits, M, K] fp32 when splits > 1
@@ -77,7 +78,19 @@ struct ConvArgs {
   int aff_act;
   int kvalid;                   // B rows that exist (< K only for a padded linear-CE vocabulary chunk)
   CeEpilogue ce;                // EPI 1 / 2: fused linear + cross-entropy (see linear_ce)
+  unsigned long long* stamps;   // diagnostic timeline (conv_set_stamps), null in normal runs
 };
+
+// Diagnostic per-workgroup timeline: s_memrealtime (100 MHz, chip-wide) at entry, before and
+// after the K loop and at the end, plus HW_ID / XCC_ID — 6 words per workgroup.  Never on in
+// timed runs (the stamp's lgkmcnt(0) forbids overlaps); read its SHARES, not its length.
+__device__ __forceinline__ unsigned long long realtime_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 // DGRAD = false: W is [K, R, S, C] (reduction contiguous; B tiles are row slices, read row-wise).
 // DGRAD = true:  the stride-1 data gradient dX = conv(dY, flip(W) with C <-> K, pad R-1-p), run on
@@ -91,9 +104,14 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (wave tile BM/2 x BN/2)
   constexpr int IA = BM / 32, IB = BN / 32;  // glds instructions per wave per slice
   constexpr int kBuf = (BM + BN) * kBK;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NB * kBuf];
+  // the ring, or (NB == 1: one stage) at least the epilogue's transpose tile + its reduction scratch
+  constexpr int kEpi = BM * (BN + 8) + 16 * BN, kCe = 8 * BM;
+  constexpr int kSmem = NB * kBuf > kEpi ? (NB * kBuf > kCe ? NB * kBuf : kCe) : (kEpi > kCe ? kEpi : kCe);
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kSmem];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  unsigned long long tsa = 0, tsb = 0, tsc = 0;
+  if (a.stamps != nullptr) tsa = realtime_stamp();
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.K + BN - 1) / BN, nwg = tiles_m * tiles_n;
   // split-major logical order: an XCD's contiguous range is tiles of ONE reduction split
@@ -124,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     const int n = mm / PQ, pq = mm - n * PQ, p = pq / a.Q, q = pq - p * a.Q;
     a_h0[i] = p * a.sh - a.ph;
     a_w0[i] = q * a.sw - a.pw;
-    a_off[i] = (((int64_t)n * a.H + a_h0[i]) * a.W + a_w0[i]) * a.C + chunk * 8;
+    a_off[i] = (((int64_t)n * a.H + a_h0[i]) * a.W + a_w0[i]) * a.pix + chunk * 8;
   }
   const int64_t ldw = (int64_t)a.R * a.S * a.C;
   const uint16_t* b_src[IB];
@@ -160,7 +178,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   int64_t st_t = kt0;
   auto stage = [&](uint16_t* buf) {
     const int r = st_r, s = st_s, c0 = st_c0;
-    const int64_t tap = ((int64_t)r * a.W + s) * a.C + c0;
+    const int64_t tap = ((int64_t)r * a.W + s) * a.pix + c0;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       const int h = a_h0[i] + r, w = a_w0[i] + s;
@@ -221,10 +239,20 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   for (int i = 0; i < NB - 1; ++i)
     if (i < nk) stage(smem + i * kBuf);
   const int r16 = lane & 15, c4 = lane >> 4;
+  if (a.stamps != nullptr) tsb = realtime_stamp();
   for (int t = 0; t < nk; ++t) {
-    mfl::wait_stage<IA + IB, NB>(min(NB - 2, nk - 1 - t));
-    mfl::barrier_keep_vm();  // stage t visible to all waves; every wave is done with buffer (t-1) % NB
-    if (t + NB - 1 < nk) stage(smem + ((t + NB - 1) % NB) * kBuf);
+    if (NB == 1) {
+      // single buffer (short reductions: LDS for more resident workgroups instead of a ring):
+      // wait until every wave has read stage t-1, refill, wait for the DMA, publish
+      if (t > 0) mfl::barrier_keep_vm();
+      stage(smem);
+      mfl::wait_vmcnt<0>();
+      mfl::barrier_keep_vm();
+    } else {
+      mfl::wait_stage<IA + IB, NB>(min(NB - 2, nk - 1 - t));
+      mfl::barrier_keep_vm();  // stage t visible to all waves; every wave is done with buffer (t-1) % NB
+      if (t + NB - 1 < nk) stage(smem + ((t + NB - 1) % NB) * kBuf);
+    }
     const uint16_t* as = smem + (t % NB) * kBuf;
     const uint16_t* bs = as + BM * kBK;
 #pragma unroll
@@ -244,6 +272,24 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
   __syncthreads();  // the epilogue reuses the ring
+  if (a.stamps != nullptr) tsc = realtime_stamp();
+  // (the end stamp is written when the kernel returns, on every epilogue path)
+  struct StampEnd {
+    const ConvArgs& a;
+    unsigned long long s0, s1, s2;
+    __device__ ~StampEnd() {
+      if (a.stamps != nullptr && threadIdx.x == 0) {
+        const unsigned long long s3 = realtime_stamp();
+        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 6;
+        o[0] = s0;
+        o[1] = s1;
+        o[2] = s2;
+        o[3] = s3;
+        o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      }
+    }
+  } stamp_end{a, tsa, tsb, tsc};
 
   if (EPI != 0) {
     // ---- fused linear + cross-entropy.  Class n0 + n of this tile is vocabulary index
@@ -533,6 +579,7 @@ hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) 
 }
 
 int g_stages = 0;  // 0 = automatic (conv_set_stages, for tuning sweeps)
+unsigned long long* g_stamps = nullptr;  // diagnostic timeline buffer (conv_set_stamps)
 
 template <typename T, int BM, int BN>
 hipError_t launch(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
@@ -540,6 +587,7 @@ hipError_t launch(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
   // ResNet-50 layer or Llama projection (profiles/conv_r01, profiles/llama_r01) — at 2-5
   // workgroups per CU the other workgroups already hide the glds latency (guide: "regime-gated")
   const int nb = g_stages > 0 ? g_stages : 2;
+  if (nb == 1) return launch_nb<T, BM, BN, 1>(a, stats, dgrad, st);
   if (nb == 2) return launch_nb<T, BM, BN, 2>(a, stats, dgrad, st);
   if (nb == 3) return launch_nb<T, BM, BN, 3>(a, stats, dgrad, st);
   return launch_nb<T, BM, BN, 4>(a, stats, dgrad, st);
@@ -574,7 +622,9 @@ int conv_fwd_group(int M, int K, int RS, int bm, int bn) {
   return max(1, min(tm, (int)(g + 0.5)));
 }
 
-void conv_set_stages(int nb) { g_stages = (nb >= 2 && nb <= 4) ? nb : 0; }
+void conv_set_stamps(void* buf) { g_stamps = static_cast<unsigned long long*>(buf); }
+
+void conv_set_stages(int nb) { g_stages = (nb >= 1 && nb <= 4) ? nb : 0; }
 
 // Below ~2 workgroups per CU a conv runs latency-bound on its long reduction (ResNet-50 layer4
 // 3x3: 200 tiles x 72 K-steps, 55 us).  Split the reduction until ~768 workgroups run, keeping
@@ -592,7 +642,7 @@ int conv_fwd_splits(int M, int K, int nk, int bm, int bn) {
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
-                    const SplitkEpilogue* ep, const void* addend, const BnBwdEpilogue* bnb) {
+                    const SplitkEpilogue* ep, const void* addend, const BnBwdEpilogue* bnb, int pix) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
   if (splits > 1 && part == nullptr) return hipErrorInvalidValue;
@@ -612,6 +662,9 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
              static_cast<const uint16_t*>(zero), psum, psq, N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw, (int)M64};
   a.group = conv_fwd_group(a.M, K, R * S, bm, bn);
   a.kvalid = K;
+  a.stamps = g_stamps;
+  a.pix = pix > 0 ? pix : C;
+  if (pix > 0 && (dgrad || pix % 8 != 0)) return hipErrorInvalidValue;
   const int nk = R * S * (C / kBK);
   splits = max(1, min(splits, nk));
   a.steps_per_split = (nk + splits - 1) / splits;
@@ -670,6 +723,7 @@ hipError_t linear_ce(int dtype, int mode, const void* x, const void* w, void* ou
   constexpr int BM = 128;
   a.group = conv_fwd_group(M, kcols, 1, BM, bn);
   a.kvalid = kvalid;
+  a.pix = E;
   a.splits = 1;
   a.steps_per_split = E / kBK;
   a.ce = ce;

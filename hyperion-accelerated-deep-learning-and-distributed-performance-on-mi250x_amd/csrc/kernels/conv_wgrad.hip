@@ -45,6 +45,7 @@ struct WgradArgs {
   uint64_t mq, mpq;  // magic multipliers: floor(m / Q) = (m * mq) >> 36 (same for P*Q)
   float alpha;       // output scale (splits == 1: applied in the store; else in the reduce)
   int dn, dpq;       // one 64-pixel stage = dn images + dpq pixels (kBP = dn * P*Q + dpq)
+  int pix;           // x's pixel stride in elements (C, or the stem's 16: see hyp_kernels.h)
   WgradPendingReduce pr;  // an EARLIER weight gradient's split-K reduce, run by extra workgroups
   int nwg_main;           // workgroups of this gradient (blockIdx.x >= nwg_main: the pending reduce)
 };
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_k(const WgradArgs a) {
         const int p = fdiv(pqb[i], a.mq), q = pqb[i] - p * a.Q;
         const int h = p * a.sh + r - a.ph, w = q * a.sw + s - a.pw;
         const bool ok = mb[i] < a.M && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        src = ok ? a.x + (((nb_[i] * a.H + h) * a.W + w) * a.C + cb[i]) : zero;
+        src = ok ? a.x + (((nb_[i] * a.H + h) * a.W + w) * a.pix + cb[i]) : zero;
         pqb[i] += a.dpq;
         nb_[i] += a.dn;
         if (pqb[i] >= PQ) {
@@ -796,7 +797,7 @@ void conv_wgrad_plan(int M, int K, int C, int R, int S, int* bm, int* bn, int* s
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
                       int bn, int splits, int steps_per_split, hipStream_t st, float alpha,
-                      const WgradPendingReduce* pending, bool defer_reduce) {
+                      const WgradPendingReduce* pending, bool defer_reduce, int pix) {
   if (!conv_wgrad_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (C % bn != 0 || (bm != 64 && bm != 128) || (bn != 64 && bn != 128) || splits < 1) return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
@@ -809,6 +810,9 @@ hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float*
               splits > 1 ? static_cast<void*>(partials) : dw, static_cast<const uint16_t*>(zero), N, H, W, C, K, P, Q,
               R, S, sh, sw, ph, pw, (int)M64, splits, steps_per_split, magic36(Q), magic36(P * Q), alpha,
               kBP / (P * Q), kBP % (P * Q)};
+  a.pix = pix > 0 ? pix : C;
+  if (pix > 0 && (pix % 8 != 0 || (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)))
+    return hipErrorInvalidValue;  // (the DENSE 1x1 path reads x as a plain [M, C] matrix)
   a.pr = WgradPendingReduce{};
   if (pending != nullptr && pending->part != nullptr) {
     if (pending->n % 4 != 0 || pending->splits < 1 || (pending->dtype != kBF16 && pending->dtype != kF16))

@@ -30,7 +30,8 @@ _ERR: Optional[BaseException] = None
 _TRIED = False
 
 DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
-STAT_SLOTS = 8  # hyp::kStatSlots: BN statistics sums are [STAT_SLOTS, 2, C] fp64 (csrc/hyp_kernels.h)
+STAT_SLOTS = 8  # hyp::kStatSlots: BN statistics sums are [STAT_SLOTS, 2, C] fp64 (csrc/hyp_kernels.h);
+#                 checked against the loaded extension's STAT_SLOTS in _load()
 
 
 def _load():
@@ -44,6 +45,8 @@ def _load():
     except BaseException as e:  # noqa: BLE001 - report any load failure
         _ERR = e
         _MOD = None
+    if _MOD is not None and getattr(_MOD, "STAT_SLOTS", STAT_SLOTS) != STAT_SLOTS:
+        raise RuntimeError(f"{name}: built with kStatSlots={_MOD.STAT_SLOTS}, Python expects {STAT_SLOTS}; rebuild")
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")

@@ -18,8 +18,10 @@ SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
   gradient is the same DGRAD GEMM on the output grid plus one scatter(+add) pass; other strided
   data gradients use the vendor kernels (``aten.convolution_backward``).
 
-Anything outside the kernel's envelope (fp32, C % 64 != 0 such as the RGB stem, groups, dilation,
-eval mode) falls back to ``bn(conv(x), residual)`` — the same math.
+The RGB stem (7x7/s2/p3, C <= 4) is rewritten as space-to-depth + a stride-1 R=4 conv whose
+64-element reduction runs span 4 adjacent 16-channel pixels (``stem.hip``), on the same kernels.  Anything else
+outside the kernel's envelope (fp32, other C % 64 != 0 convs, groups, dilation, eval mode) falls
+back to ``bn(conv(x), residual)`` — the same math.
 """
 from __future__ import annotations
 
@@ -382,6 +384,112 @@ def _conv_bn_eval(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor,
                                             sc, sh, residual, bool(bn.act))
 
 
+# ---- the RGB stem (7x7, stride 2, padding 3, C <= 4): csrc/kernels/stem.hip rewrites it as
+# space-to-depth Xs [N, 16, P+3, Q+3] and a stride-1 R=4 conv whose 64-element reduction runs are 4
+# adjacent Xs pixels (conv_fwd / conv_wgrad with a 16-element pixel stride); W4[k, dr, ds*16 +
+# (2a+b)*C + c] = W[k, c, 2dr+a, 2ds+b] (zero for tap 7).
+_STEM_IDX: dict = {}
+
+
+def _stem_index(C: int, device) -> tuple:
+    """(idx4 [256]: column of [W.view(K, C*49) | 0] feeding each W4 column, inv [C*49]: the W4
+    column of each W element)."""
+    key = (C, str(device))
+    if key not in _STEM_IDX:
+        idx4 = torch.full((4, 4, 16), C * 49, dtype=torch.long)  # the appended zero column
+        inv = torch.empty(C * 49, dtype=torch.long)
+        for dr in range(4):
+            for ds in range(4):
+                for a in range(2):
+                    for b in range(2):
+                        r, q = 2 * dr + a, 2 * ds + b
+                        if r > 6 or q > 6:
+                            continue
+                        for c in range(C):
+                            src = c * 49 + r * 7 + q
+                            idx4[dr, ds, (2 * a + b) * C + c] = src
+                            inv[src] = (dr * 4 + ds) * 16 + (2 * a + b) * C + c
+        _STEM_IDX[key] = (idx4.reshape(-1).to(device), inv.to(device))
+    return _STEM_IDX[key]
+
+
+def stem_weight(w: torch.Tensor) -> torch.Tensor:
+    """W [K, C, 7, 7] -> W4 [K, 64, 4, 1] (channels-last; memory [k][dr][ds*16 + (2a+b)*C + c]).
+    Differentiable (an index gather): the rewritten conv's weight gradient flows back to W."""
+    K, C = w.shape[0], w.shape[1]
+    idx4, _ = _stem_index(C, w.device)
+    wx = torch.nn.functional.pad(w.reshape(K, C * 49), (0, 1))
+    w4 = wx.index_select(1, idx4).reshape(K, 4, 1, 64)
+    return w4.permute(0, 3, 1, 2)
+
+
+def stem_weight_grad(dw4: torch.Tensor, C: int) -> torch.Tensor:
+    """dW [K, C, 7, 7] from dW4 [K, 64, 4, 1] (channels-last): each W element feeds one W4 column."""
+    K = dw4.shape[0]
+    _, inv = _stem_index(C, dw4.device)
+    flat = dw4.permute(0, 2, 3, 1).reshape(K, 256)  # memory order [k][dr][64]
+    return flat.index_select(1, inv).reshape(K, C, 7, 7)
+
+
+def stem_s2d_reference(x: torch.Tensor) -> torch.Tensor:
+    """PyTorch form of ``stem_s2d`` (the kernel's numerics oracle): x [N, C, H, W] -> Xs
+    [N, 16, P+3, Q+3], Xs[n, (2a+b)*C + c, i, j] = x_pad3[n, c, 2i+a, 2j+b]."""
+    N, C, H, W = x.shape
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    Hs, Ws = P + 3, Q + 3
+    xp = torch.nn.functional.pad(x, (3, 2 * Ws - W - 3, 3, 2 * Hs - H - 3))
+    xs = xp.reshape(N, C, Hs, 2, Ws, 2).permute(0, 2, 4, 3, 5, 1).reshape(N, Hs, Ws, 4 * C)
+    xs = torch.nn.functional.pad(xs, (0, 16 - 4 * C))
+    return xs.permute(0, 3, 1, 2)
+
+
+def stem_runs_reference(xs: torch.Tensor) -> torch.Tensor:
+    """What the kernels read with a 16-element pixel stride: X4 [N, 64, P+3, Q], X4[n, ds*16 + e, i, q]
+    = Xs[n, e, i, q + ds] — so the stem is F.conv2d(X4, W4) (used by the CPU check of the rewrite)."""
+    Q = xs.shape[3] - 3
+    return torch.cat([xs[:, :, :, ds:ds + Q] for ds in range(4)], dim=1)
+
+
+def _is_stem(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    return (tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2) and tuple(conv.padding) == (3, 3)
+            and conv.groups == 1 and tuple(conv.dilation) == (1, 1) and conv.bias is None
+            and x.dim() == 4 and 1 <= x.shape[1] <= 4 and not x.requires_grad
+            and x.dtype in (torch.bfloat16, torch.float16) and x.is_cuda and conv.out_channels % 8 == 0)
+
+
+class _StemConvBNActFn(torch.autograd.Function):
+    """stem conv -> BN (training) -> ReLU on the native kernels; no input gradient (the image)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bn_w, bn_b, rm, rv, momentum, eps, act):
+        C = _native.native()
+        K, Cin = w.shape[0], w.shape[1]
+        xs = C.stem_s2d(x.contiguous(memory_format=torch.channels_last))
+        w4 = stem_weight(w.detach())
+        sums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
+        ctx.bsums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
+        yc = C.stem_conv_fwd(xs, w4, sums)
+        out, mean, invstd = C.bn_fwd_sums(yc, None, sums, bn_w, bn_b, rm, rv, momentum, eps, act)
+        ctx.save_for_backward(xs, yc, bn_w, bn_b, mean, invstd)
+        ctx.cfg = (Cin, act)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xs, yc, bn_w, bn_b, mean, invstd = ctx.saved_tensors
+        Cin, act = ctx.cfg
+        bsums, ctx.bsums = ctx.bsums, None
+        C = _native.native()
+        dyc, _, dbw, dbb = C.bn_bwd(dout.contiguous(memory_format=torch.channels_last), yc, None, bn_w, bn_b, mean,
+                                    invstd, True, act, False, sums=bsums)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            _native.count("wgrad")
+            dw = stem_weight_grad(C.stem_conv_wgrad(dyc, xs), Cin)
+        return (None, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None,
+                None, None, None, None, None)
+
+
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 link: Optional[ResidualLink] = None, branch: Optional[BranchSumLink] = None) -> torch.Tensor:
     """``bn(conv(x), residual)`` for a ``BatchNormAct2d`` ``bn``; fused on gfx950 when possible.
@@ -411,6 +519,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
                 w = w.to(dt)
             if residual is not None and residual.dtype != dt:
                 residual = residual.to(dt)
+    stride, padding = tuple(conv.stride), tuple(conv.padding)
     use = (
         bn.training
         and bn.track_running_stats
@@ -418,8 +527,15 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
         and bn.affine
         and _native.use_native(x, op="conv")
         and _native.use_native(x, op="bn")
-        and _native_conv_ok(x, conv, w)
     )
+    if use and residual is None and link is None and branch is None and _is_stem(conv, x) and w.dtype == x.dtype:
+        # the RGB stem: space-to-depth (stem.hip) + the 64-wide kernels with a 16-element pixel stride
+        _native.count("stem_s2d")
+        _native.count("conv_bn_act")
+        bn._host_batches += 1
+        return _StemConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.momentum),
+                                      float(bn.eps), bool(bn.act))
+    use = use and _native_conv_ok(x, conv, w)
     if not use:
         _native.count("conv_bn_act_fallback")
         return bn(conv(x), residual=residual)
@@ -442,7 +558,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
     # x produced by another fused layer: its BN backward reduce can ride on our dgrad epilogue
     prod = getattr(x.grad_fn, "bnlink", None) if (FUSE_BN_BACKWARD and x.grad_fn is not None) else None
     out = _ConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
-                             tuple(conv.stride), tuple(conv.padding), float(bn.momentum), float(bn.eps), bool(bn.act),
+                             stride, padding, float(bn.momentum), float(bn.eps), bool(bn.act),
                              link_in, link_out, branch, bidx, prod)
     if out.grad_fn is not None:  # (no graph under no_grad: nothing to link)
         if branch is not None:

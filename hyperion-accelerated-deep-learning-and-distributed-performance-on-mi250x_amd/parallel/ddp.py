@@ -22,7 +22,11 @@ MI355X design:
 * after backward, ``param.grad`` (same dtype) or ``param.main_grad`` (fp32 bucket, low-precision
   parameter) points at the bucket slice, so the fused optimizer reads the reduced gradient in
   place (no copy back) and its pointer table stays valid across steps;
-* ``broadcast_buffers`` reproduces the reference's per-forward BN buffer broadcast (K5);
+* ``broadcast_buffers`` reproduces the reference's per-forward BN buffer broadcast (K5); under a
+  segmented hipGraph capture it is an eager hole before the forward, so graphed steps keep it;
+* a segmented capture of the whole step (``train/segments.py``, used by the trainers' captured
+  step) records each bucket's all-reduce and its wait as eager holes at the points where the
+  eager backward issued them: replays overlap RCCL with the rest of the backward for every model;
 * ``defer_allreduce`` (set by ``TrainStep`` for hipGraph replay): backward only packs the buckets
   and ``allreduce_buckets()`` reduces them afterwards — the captured fwd+bwd graph and the
   optimizer graph then hold no RCCL call, and the collectives run eagerly between the two
@@ -41,6 +45,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import streams as _streams
+from ..train import segments as _segments
 from ..ops.conv import flush_wgrad as _flush_wgrad
 from ..utils.nvtx import range_push, range_pop
 from .comm import get_comm
@@ -220,11 +225,23 @@ class DistributedDataParallel(nn.Module):
                 break
             if b.buf.is_cuda:
                 _streams.join(b.buf.device)  # packs issued on the weight-gradient side stream
-            range_push(f"ddp_allreduce_b{b.index}")
-            b.work = self.comm.all_reduce(b.buf, "avg")
-            range_pop()
+            # under a segmented hipGraph capture (train/segments.py) the all-reduce is an eager hole
+            # between two graph segments: every replay re-issues it right where this bucket became
+            # complete, so it overlaps the rest of the captured backward
+            _segments.eager(lambda b=b: self._issue(b))
             b.launched = True
             self._next_launch += 1
+
+    def _issue(self, b: _Bucket) -> None:
+        range_push(f"ddp_allreduce_b{b.index}")
+        b.work = self.comm.all_reduce(b.buf, "avg")
+        range_pop()
+
+    @staticmethod
+    def _wait(b: _Bucket) -> None:
+        if b.work is not None:
+            b.work.wait()  # stream-ordered: the compute stream waits on RCCL, the host does not
+            b.work = None
 
     def _finalize(self) -> None:
         if self.partial_backward:  # more of this step's backward follows: keep the bucket state
@@ -242,9 +259,8 @@ class DistributedDataParallel(nn.Module):
         if not self.defer_allreduce:
             self._launch_ready()
         for b in self._buckets:
-            if b.work is not None:
-                b.work.wait()  # stream-ordered: the compute stream waits on RCCL, the host does not
-                b.work = None
+            if b.launched:
+                _segments.eager(lambda b=b: self._wait(b))
             for p, off in zip(b.params, b.offsets):
                 view = _param_view(b.buf[off : off + p.numel()], p)
                 if view.dtype == p.dtype:
@@ -301,11 +317,20 @@ class DistributedDataParallel(nn.Module):
         finally:
             self._sync = prev
 
+    def sync_buffers(self) -> None:
+        """Rank 0's buffers (BN running statistics) to every rank, in place (K5)."""
+        bufs = [b for b in self.module.buffers() if b.numel() > 0]
+        if bufs:
+            _flat_broadcast(bufs, 0, self.process_group)
+
+    def has_buffers(self) -> bool:
+        return any(b.numel() > 0 for b in self.module.buffers())
+
     def forward(self, *args, **kwargs):
-        if self.world > 1 and self.broadcast_buffers:
-            bufs = [b for b in self.module.buffers() if b.numel() > 0]
-            if bufs:
-                _flat_broadcast(bufs, 0, self.process_group)
+        if self.world > 1 and self.broadcast_buffers and self.has_buffers():
+            # per-forward broadcast (torch DDP's broadcast_buffers=True); an eager hole when the
+            # step is being captured as segments, so replays broadcast before every forward too
+            _segments.eager(self.sync_buffers)
         return self.module(*args, **kwargs)
 
     def state_dict(self, *args, **kwargs):  # keep reference checkpoint keys (model.module.state_dict())

@@ -67,6 +67,9 @@ class RunOptions:
     # GPU: tensor datasets resident in HBM and batched on the device (data/loader.py
     # DeviceTensorLoader) instead of DataLoader workers + per-step H2D copies
     device_data: bool = True
+    # after training, all-gather per-parameter checksums and raise if the data-parallel replicas
+    # differ (parallel/debug.py); the count of compared tensors is returned as "replicas"
+    check_replicas: bool = False
     log: Callable[[str], None] = field(default=print)
 
 
@@ -150,9 +153,8 @@ class _EpochRunner:
         why = ""
         if isinstance(self.model, FullyShardedDataParallel) and not self.model.persistent:
             why = "FSDP step without persistent buffers (storage released / re-allocated per unit)"
-        elif isinstance(self.model, DistributedDataParallel) and not (self.model.bucketed and
-                                                                      not self.model.broadcast_buffers):
-            why = "DDP with per-forward buffer broadcasts"
+        elif isinstance(self.model, DistributedDataParallel) and self.world > 1 and not self.model.bucketed:
+            why = "DDP without gradient buckets"
         elif self.world > 1 and not isinstance(self.model, DistributedDataParallel):
             why = "non-Hyperion data parallel wrapper"
         elif os.environ.get("HYPERION_FAULT"):
@@ -173,12 +175,21 @@ class _EpochRunner:
                 self.global_step += 1
                 return self._captured(inputs)
         inputs = inputs or ()
-        self.opt.zero_grad(set_to_none=True)
+        cap = self._captured
+        if cap is not None:
+            # an eager step beside a captured one (a short last batch): the graphs and the fused
+            # optimizer's pinned table hold the current .grad tensors, so they are zeroed in place and
+            # accumulated into — dropping them (set_to_none) would leave later replays writing freed
+            # blocks
+            self.opt.zero_grad(set_to_none=False)
+        else:
+            self.opt.zero_grad(set_to_none=True)
         with self._autocast():
             loss, extra = loss_fn(*inputs)
         if maybe_inject(self.rank, self.global_step):
             loss = loss * float("nan")
-        self._backward_update(loss)
+        # a captured DDP step left the hooks in deferred mode (they only pack buckets): reduce here
+        self._backward_update(loss, allreduce=cap.eager_allreduce() if cap is not None else None)
         self.global_step += 1
         return loss.detach().float(), extra
 
@@ -215,11 +226,15 @@ class _CapturedStep:
     """One trainer step as hipGraph(s): warm-up on a side stream, then capture.
 
     Single process: ONE graph (zero, forward, backward, unscale/clip, optimizer, scaler update).
-    Hyperion DDP: graph 1 = forward + backward (gradient hooks only pack buckets,
-    ``defer_allreduce``), the bucket all-reduces run eagerly on the comm stream, graph 2 = clip +
-    optimizer — no RCCL call is recorded into a graph (same split as ``train/step.py``).
+    Hyperion DDP (default, ``HYPERION_DDP_CAPTURE=segments``): the whole step as graph segments;
+    each bucket's all-reduce is an eager hole issued where the bucket completed inside the backward
+    (and its wait where the backward ends), and a per-forward buffer broadcast (BN models,
+    ``broadcast_buffers=True``) is a hole before the forward — RCCL overlaps the captured backward
+    for every model.  ``HYPERION_DDP_CAPTURE=split``: graph 1 = forward + backward (hooks only
+    pack, ``defer_allreduce``), eager bucket all-reduces, graph 2 = clip + optimizer.
     Hyperion FSDP (persistent buffers): the whole step as graph segments with every all-gather /
     reduce-scatter / clip all-reduce an eager hole between them (``train/segments.py``).
+    No RCCL call is ever recorded into a graph.
     Inputs are copied into persistent buffers each step; outputs are the captured step's tensors.
     """
 
@@ -235,7 +250,8 @@ class _CapturedStep:
         self.static = [t.clone() if isinstance(t, torch.Tensor) else t for t in inputs]
         m = runner.model
         self.ddp = m if isinstance(m, DistributedDataParallel) and runner.world > 1 else None
-        if self.ddp is not None:
+        self.ddp_segments = self.ddp is not None and os.environ.get("HYPERION_DDP_CAPTURE", "segments") != "split"
+        if self.ddp is not None and not self.ddp_segments:
             self.ddp.defer_allreduce = True
         scaled = runner.scaler is not None and runner.scaler.enabled
         side = torch.cuda.Stream()
@@ -253,8 +269,11 @@ class _CapturedStep:
             runner.opt.zero_grad_in_step = False
         self.g1 = torch.cuda.CUDAGraph()
         self.g2: Optional[torch.cuda.CUDAGraph] = None
+        from ..ops.batchnorm import HostCounterReplay
+
+        counters = HostCounterReplay(m)  # BN num_batches_tracked mirrors: undo the recording pass
         try:
-            if isinstance(m, FullyShardedDataParallel):
+            if isinstance(m, FullyShardedDataParallel) or self.ddp_segments:
                 self.seg = SegmentedGraph()
                 self.out = self.seg.capture(lambda: self._full(zero_in_place=scaled))
             elif self.ddp is None:
@@ -270,6 +289,7 @@ class _CapturedStep:
             flush_pending()
             if zero_flag is not None:
                 runner.opt.zero_grad_in_step = zero_flag
+        self.counters = counters.captured()
         torch.cuda.synchronize()
 
     def _fwd_bwd(self, zero_in_place: bool):
@@ -299,10 +319,17 @@ class _CapturedStep:
 
     def _full(self, zero_in_place: bool):
         out = self._fwd_bwd(zero_in_place)
-        if self.ddp is not None:
+        if self.ddp is not None and self.ddp.defer_allreduce:
             self.ddp.allreduce_buckets()
         self._update()
         return out
+
+    def eager_allreduce(self) -> Optional[Callable[[], None]]:
+        """What an eager step beside this capture must run after its backward: the deferred
+        bucket all-reduce of the split-graph DDP mode (its hooks only pack), else nothing."""
+        if self.ddp is not None and self.ddp.defer_allreduce:
+            return self.ddp.allreduce_buckets
+        return None
 
     def fits(self, inputs: tuple) -> bool:
         return all(not isinstance(st, torch.Tensor) or (isinstance(t, torch.Tensor) and t.shape == st.shape)
@@ -312,6 +339,7 @@ class _CapturedStep:
         for st, t in zip(self.static, inputs):
             if isinstance(st, torch.Tensor) and st.data_ptr() != t.data_ptr():
                 st.copy_(t, non_blocking=True)
+        self.counters.replayed()
         if self.seg is not None:
             self.seg.replay()
             return self.out
@@ -320,6 +348,16 @@ class _CapturedStep:
             self.ddp.allreduce_buckets()
             self.g2.replay()
         return self.out
+
+
+def _replicas(opts: RunOptions, model, world: int) -> Optional[int]:
+    from ..parallel.ddp import DistributedDataParallel
+
+    if not (opts.check_replicas and world > 1 and isinstance(model, DistributedDataParallel)):
+        return None
+    from ..parallel.debug import assert_replicas_in_sync
+
+    return assert_replicas_in_sync(model)
 
 
 def _sync(device):
@@ -387,9 +425,11 @@ def train_language_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: s
             opts.log(f"[language_ddp] epoch {ep + 1}/{epochs} loss {avg:.4f} {dur:.2f}s ({n} steps)")
     ck = _finish(opts, out, run_id, model, opt, scaler, epochs, runner.global_step)
     _manifest(rank, out, run_id, history, batch_size, world, precision)
+    replicas = _replicas(opts, model, world)
     if world > 1:
         cleanup()
-    return {"run_id": run_id, "history": history, "checkpoint": ck}
+    return {"replicas": replicas, "run_id": run_id, "history": history, "checkpoint": ck, "graphed": runner._captured is not None,
+            "graph_reason": runner.graph_reason}
 
 
 # ---------------------------------------------------------------------------------------- CIFAR DDP
@@ -463,9 +503,11 @@ def train_cifar_model_ddp(rank: int, world: int, epochs: int = 3, base_dir: str 
             opts.log(f"[cifar] epoch {ep + 1}/{epochs} loss {loss_avg:.4f} acc {acc:.2f}% {dur:.2f}s")
     ck = _finish(opts, out, run_id, model, opt, scaler, epochs, runner.global_step)
     _manifest(rank, out, run_id, history, batch_size, world, precision)
+    replicas = _replicas(opts, model, world)
     if world > 1:
         cleanup()
-    return {"run_id": run_id, "history": history, "checkpoint": ck}
+    return {"replicas": replicas, "run_id": run_id, "history": history, "checkpoint": ck, "graphed": runner._captured is not None,
+            "graph_reason": runner.graph_reason}
 
 
 # ---------------------------------------------------------------------------------------- LM FSDP
@@ -530,9 +572,11 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
         dist.barrier()
     ck = _finish(opts, out, run_id, model, opt, None, epochs, runner.global_step)
     _manifest(rank, out, run_id, history, batch_size, world, precision)
+    replicas = _replicas(opts, model, world)
     if world > 1:
         cleanup()
-    return {"run_id": run_id, "history": history, "checkpoint": ck}
+    return {"replicas": replicas, "run_id": run_id, "history": history, "checkpoint": ck, "graphed": runner._captured is not None,
+            "graph_reason": runner.graph_reason}
 
 
 def train_gpt2_fsdp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
@@ -654,9 +698,11 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
             ck = save_checkpoint(os.path.join(out, f"{run_id}_{mode}.pt"), model, None, None, epochs,
                                  runner.global_step, mode=opts.ckpt_mode)
     _manifest(rank, out, run_id, history, batch_size, world, precision)
+    replicas = _replicas(opts, model, world)
     if world > 1:
         cleanup()
-    return {"run_id": run_id, "history": history, "checkpoint": ck, "mode": mode}
+    return {"replicas": replicas, "run_id": run_id, "history": history, "checkpoint": ck, "mode": mode,
+            "graphed": runner._captured is not None, "graph_reason": runner.graph_reason}
 
 
 def _save_adapter_from_sd(sd: Dict[str, torch.Tensor], out_dir: str) -> str:

@@ -126,6 +126,7 @@ class SegmentedStep:
         self.warmup = warmup
         self.module = module
         self.seg: Optional[SegmentedGraph] = None
+        self._counters = None
 
     def __call__(self) -> torch.Tensor:
         if self.seg is None:
@@ -138,13 +139,21 @@ class SegmentedStep:
             torch.cuda.synchronize()
             from ..ops.multi_tensor import flush_pending
 
+            from ..ops.batchnorm import HostCounterReplay
+
+            counters = None
             if self.module is not None:
                 for p in self.module.parameters():
                     p.grad = None
+                counters = HostCounterReplay(self.module)
             seg = SegmentedGraph()
             try:
                 seg.capture(self.fn)
             finally:
                 flush_pending()
             self.seg = seg
-        return self.seg.replay()
+            self._counters = counters.captured() if counters is not None else None
+        out = self.seg.replay()
+        if self._counters is not None:
+            self._counters.replayed()  # BN num_batches_tracked mirrors advance once per replayed step
+        return out

@@ -1,0 +1,112 @@
+"""Per-shape roofline of every ResNet-50 (batch 32, bf16, NHWC) convolution: Hyperion's kernels
+against MIOpen (F.conv2d / convolution_backward) and against hipBLASLt on the same GEMM dimensions,
+next to the HBM floor (compulsory bytes / 6 TB/s) and the MFMA floor (FLOP / 2.5 PF).
+
+Each variant is 20 launches captured in one hipGraph (launch overhead amortised), wall / 20.
+
+    python scripts/conv_roofline.py [--out gpurun_out/conv_roofline.json] [--only fwd,dgrad,wgrad]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from hyperion.bench.conv_shapes import resnet50_convs  # noqa: E402
+from hyperion.ops import _native  # noqa: E402
+
+
+def gtime(fn, n=20, reps=5):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        best = min(best, (time.perf_counter() - t0) / n * 1e6)
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/conv_roofline.json")
+    ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--vendor", type=int, default=1)
+    ap.add_argument("--stages", type=int, default=0, help="force the forward/dgrad LDS ring depth (1..4)")
+    ap.add_argument("--tiles", default="", help="bm,bn,splits forced on the native fwd / dgrad (tuning sweeps)")
+    a = ap.parse_args()
+    what = a.only.split(",")
+    bm, bn, sp = (int(v) for v in a.tiles.split(",")) if a.tiles else (-1, -1, -1)
+    C_ = _native.native()
+    if a.stages:
+        C_.conv_set_stages(a.stages, 0)
+    torch.backends.cudnn.benchmark = True
+    rows = []
+    for sh in resnet50_convs(32):
+        N, C, H, K, R, s, p = sh["N"], sh["C"], sh["H"], sh["K"], sh["R"], sh["stride"], sh["pad"]
+        P = (H + 2 * p - R) // s + 1
+        M, Kred = N * P * P, C * R * R
+        gf = 2.0 * M * K * Kred / 1e9
+        x = torch.randn(N, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(K, C, R, R, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+        dy = torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        io = 2 * (x.numel() + w.numel() + dy.numel())
+        r = dict(sh, P=P, M=M, Kred=Kred, gflop=round(gf, 3), hbm_floor_us=round(io / 6.0e6, 2),
+                 mfma_floor_us=round(gf / 2.5, 2))
+        native = C % 64 == 0
+        if "fwd" in what:
+            if native:
+                r["fwd_stats_us"] = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp))
+                r["fwd_us"] = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, False, bm, bn, sp))
+            if a.vendor:
+                r["fwd_miopen_us"] = gtime(lambda: F.conv2d(x, w, None, s, p))
+                A = torch.randn(M, Kred, device="cuda").bfloat16()
+                B = torch.randn(Kred, K, device="cuda").bfloat16()
+                r["fwd_hipblaslt_gemm_us"] = gtime(lambda: torch.matmul(A, B))
+                del A, B
+        if "dgrad" in what:
+            if native and s == 1 and K % 64 == 0:
+                r["dgrad_us"] = gtime(lambda: C_.conv_dgrad(dy, w, p, p, bm, bn, sp))
+            if a.vendor:
+                r["dgrad_miopen_us"] = gtime(lambda: torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False]))
+        if "wgrad" in what:
+            if native:
+                r["wgrad_us"] = gtime(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p))
+            if a.vendor:
+                r["wgrad_miopen_us"] = gtime(lambda: torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False]))
+        for k in list(r):
+            if k.endswith("_us") and isinstance(r[k], float):
+                r[k] = round(r[k], 2)
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+    tot = {}
+    for r in rows:
+        for k, v in r.items():
+            if k.endswith("_us"):
+                tot[k] = round(tot.get(k, 0.0) + v, 1)
+    print(json.dumps({"totals_per_distinct_shape": tot}), flush=True)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump({"rows": rows, "totals": tot}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
