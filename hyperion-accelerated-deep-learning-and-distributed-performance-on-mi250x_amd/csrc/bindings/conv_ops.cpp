@@ -19,7 +19,7 @@ int plan_splits(int M, int K, int nk, int bm, int bn, int64_t splits_req) {
 // [kStatSlots, K] slot partials).  The statistics are ADDED into `sums` ([kStatSlots*2*K] fp64, zeroed).
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t sh, int64_t sw, int64_t ph,
                                  int64_t pw, bool stats, int64_t bm_req, int64_t bn_req, int64_t splits_req,
-                                 const c10::optional<at::Tensor>& sums) {
+                                 const c10::optional<at::Tensor>& sums, int64_t stages) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: 4D tensors");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -49,7 +49,8 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), device_zero_page(x.device()),
                               stats ? acc.data_ptr<double>() : nullptr, stats ? acc.data_ptr<double>() + K : nullptr, N, H,
                               W, C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, splits,
-                              splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream()));
+                              splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f, nullptr, nullptr,
+                              nullptr, 0, 1, 0, 0, (int)stages));
   if (!stats) return {y, at::Tensor(), at::Tensor()};
   return {y, acc.select(1, 0), acc.select(1, 1)};  // [kStatSlots, K] each: .sum(0) = per-channel totals
 }
@@ -186,7 +187,8 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
                       const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_y,
                       const c10::optional<at::Tensor>& bn_w, const c10::optional<at::Tensor>& bn_b,
                       const c10::optional<at::Tensor>& bn_mean, const c10::optional<at::Tensor>& bn_invstd,
-                      int64_t bn_mode, const c10::optional<at::Tensor>& bn_sums) {
+                      int64_t bn_mode, const c10::optional<at::Tensor>& bn_sums, int64_t stride, int64_t Hx,
+                      int64_t Wx, int64_t stages) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -200,7 +202,14 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
   TORCH_CHECK(hyp::conv_fwd_supported(K, C), "conv_dgrad: needs K % 64 == 0 and C % 8 == 0");
   const int dph = R - 1 - (int)ph, dpw = S - 1 - (int)pw;
   TORCH_CHECK(dph >= 0 && dpw >= 0, "conv_dgrad: padding larger than the filter");
-  const int H = P + R - 1 - 2 * (int)ph, W = Q + S - 1 - 2 * (int)pw;
+  TORCH_CHECK(stride == 1 || stride == 2, "conv_dgrad: stride 1 or 2");
+  const bool s2 = stride == 2;
+  // stride 2: dX [N, C, Hx, Wx] with Hx, Wx even and the forward's output size equal to dY's
+  if (s2)
+    TORCH_CHECK(Hx % 2 == 0 && Wx % 2 == 0 && Hx / 2 == P && Wx / 2 == Q && (Hx + 2 * ph - R) / 2 + 1 == P &&
+                    (Wx + 2 * pw - S) / 2 + 1 == Q,
+                "conv_dgrad: stride 2 needs an even dX size whose forward output is dY's (Hx = 2 P)");
+  const int H = s2 ? (int)Hx : P + R - 1 - 2 * (int)ph, W = s2 ? (int)Wx : Q + S - 1 - 2 * (int)pw;
   TORCH_CHECK(H > 0 && W > 0, "conv_dgrad: empty output");
   const at::DeviceGuard guard(dy.device());
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -217,7 +226,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
   if (bn_req > 0) bn = (int)bn_req;
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && !(bm == 64 && bn == 128),
               "conv_dgrad: tiles 64x64, 128x64 or 128x128");
-  const int splits = plan_splits(N * H * W, C, R * S * (K / 64), bm, bn, splits_req);
+  const int splits = s2 ? 1 : plan_splits(N * H * W, C, R * S * (K / 64), bm, bn, splits_req);
   at::Tensor slabs;
   if (splits > 1) slabs = at::empty({splits, (int64_t)N * H * W, C}, dy.options().dtype(at::kFloat));
   const bool add = addend.has_value() && addend->defined();
@@ -253,10 +262,11 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
     bnb.sums = bn_sums->data_ptr<double>();
   }
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
-                              device_zero_page(dy.device()), nullptr, nullptr, N, P, Q, K, C, H, W, R, S, 1, 1,
-                              dph, dpw, bm, bn, 1, splits, splits > 1 ? slabs.data_ptr<float>() : nullptr,
-                              cur_stream(), 1.f, nullptr, (add && (splits == 1 || fuse_bn)) ? addend->data_ptr() : nullptr,
-                              fuse_bn ? &bnb : nullptr));
+                              device_zero_page(dy.device()), nullptr, nullptr, N, P, Q, K, C, s2 ? H / 2 : H,
+                              s2 ? W / 2 : W, R, S, 1, 1, s2 ? (int)ph : dph, s2 ? (int)pw : dpw, bm, bn, 1, splits,
+                              splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f, nullptr,
+                              (add && (splits == 1 || fuse_bn)) ? addend->data_ptr() : nullptr,
+                              fuse_bn ? &bnb : nullptr, 0, s2 ? 2 : 1, s2 ? H : 0, s2 ? W : 0, (int)stages));
   if (add && splits > 1 && !fuse_bn) dx.add_(*addend);  // the plain split-K reduce has no addend input
   return dx;
 }
@@ -641,7 +651,7 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)", pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
         pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1, pybind11::arg("splits") = -1,
-        pybind11::arg("sums") = pybind11::none());
+        pybind11::arg("sums") = pybind11::none(), pybind11::arg("stages") = 0);
   m.def("conv_fwd_affine", &conv_fwd_affine, "eval conv + folded BN affine (+ residual) (+ ReLU), one launch",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
         pybind11::arg("pw"), pybind11::arg("scale"), pybind11::arg("shift"),
@@ -685,7 +695,8 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("bn_x") = pybind11::none(), pybind11::arg("bn_y") = pybind11::none(),
         pybind11::arg("bn_w") = pybind11::none(), pybind11::arg("bn_b") = pybind11::none(),
         pybind11::arg("bn_mean") = pybind11::none(), pybind11::arg("bn_invstd") = pybind11::none(),
-        pybind11::arg("bn_mode") = -1, pybind11::arg("bn_sums") = pybind11::none());
+        pybind11::arg("bn_mode") = -1, pybind11::arg("bn_sums") = pybind11::none(), pybind11::arg("stride") = 1,
+        pybind11::arg("H") = 0, pybind11::arg("W") = 0, pybind11::arg("stages") = 0);
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

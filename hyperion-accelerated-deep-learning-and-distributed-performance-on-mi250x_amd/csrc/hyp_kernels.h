@@ -181,7 +181,11 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
                     const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr,
-                    const struct BnBwdEpilogue* bnb = nullptr, int pix = 0);
+                    const struct BnBwdEpilogue* bnb = nullptr, int pix = 0, int dgrad_stride = 1, int Hx = 0,
+                    int Wx = 0, int nb = 0);
+// dgrad_stride 2 (dgrad only, no split-K / alpha / rank-r epilogue): the stride-2 data gradient as its
+// 4 output-phase sub-convolutions in one launch; (H, W, P, Q) are dY's (H, W) and the phase grid
+// (P, Q) = (Hx / 2, Wx / 2) of dX [N, Hx, Wx, K], (ph, pw) the FORWARD padding, w the original filter.
 // pix (conv_fwd / conv_wgrad): the input's pixel stride in elements when it differs from the
 // 64-multiple reduction slice C (0 = C) — the stem's space-to-depth input (stem.hip): 16-channel
 // pixels read as 64-element runs of 4 adjacent pixels.

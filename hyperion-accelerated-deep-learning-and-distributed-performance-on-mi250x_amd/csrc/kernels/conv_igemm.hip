@@ -49,6 +49,19 @@ __device__ __forceinline__ f32x4 mma<f16_t>(u16x8 a, u16x8 b, f32x4 c) {
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
+template <typename T>
+__device__ __forceinline__ uint32_t pack2(float lo, float hi);
+template <>
+__device__ __forceinline__ uint32_t pack2<bf16_t>(float lo, float hi) { return pack_bf16x2(lo, hi); }
+template <>
+__device__ __forceinline__ uint32_t pack2<f16_t>(float lo, float hi) { return pack_f16x2(lo, hi); }
+
+// floor(x / d) by a host-precomputed 36-bit magic (exact for x < 2^22, d < 2^14): the prologue's
+// per-row (n, p, q) decomposition without integer-division sequences; magic 0 = plain division
+__device__ __forceinline__ int fdiv36(int x, uint64_t magic, int d) {
+  return magic ? (int)(((uint64_t)(uint32_t)x * magic) >> 36) : x / d;
+}
+
 __device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const void*)src, (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0,
                                    0);
@@ -68,6 +81,10 @@ struct ConvArgs {
   int N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw;
   int M;                 // N*P*Q
   int pix;               // input pixel stride in elements (C, or the stem's 16: see hyp_kernels.h)
+  int sd;                // DGRAD only: 2 = stride-2 data gradient by output phase (below), else 1
+  int Hx, Wx;            // sd == 2: dX's spatial size (2P x 2Q); the tile grid is one phase's [N, P, Q]
+  int nb;                // host only: LDS ring depth of this launch (0 = conv_set_stages / default 2)
+  uint64_t mq, mpq;      // 36-bit magic multipliers of Q and P*Q (0: plain division; see fdiv36)
   int group;             // M-tiles per tile-order group (see conv_fwd_group)
   int splits, steps_per_split;  // split-K over the reduction (splits > 1: fp32 partials, no STATS)
   float* part;                  // [splits, M, K] fp32 when splits > 1
@@ -114,10 +131,28 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   if (a.stamps != nullptr) tsa = realtime_stamp();
 
   const int tiles_m = (a.M + BM - 1) / BM, tiles_n = (a.K + BN - 1) / BN, nwg = tiles_m * tiles_n;
-  // split-major logical order: an XCD's contiguous range is tiles of ONE reduction split
-  int bid = mfl::xcd_remap(blockIdx.x, nwg * a.splits);
-  const int split = bid / nwg;
-  bid -= split * nwg;
+  // Stride-2 data gradient (sd2): dX pixel (2i + pa, 2j + pb) only receives taps r ≡ pa + ph,
+  // s ≡ pb + pw (mod 2), from dY pixel (i + (pa + ph - r) / 2, j + (pb + pw - s) / 2) — so each of
+  // the 4 output phases is a small stride-1 conv over dY (1x1, 1x2, 2x1, 2x2 taps for a 3x3
+  // filter, padding 1) and one launch runs all four: the tile grid is one phase's [N, P, Q] x C,
+  // the phase index runs fastest (every XCD gets the same mix of light and heavy phases), and the
+  // epilogue stores each row at its interleaved dX pixel.
+  const bool sd2 = DGRAD && a.sd == 2;
+  int bid, split, phase = 0;
+  if (sd2) {
+    const int lb = mfl::xcd_remap(blockIdx.x, nwg * 4);
+    phase = lb & 3;
+    bid = lb >> 2;
+    split = 0;
+  } else {
+    // split-major logical order: an XCD's contiguous range is tiles of ONE reduction split
+    bid = mfl::xcd_remap(blockIdx.x, nwg * a.splits);
+    split = bid / nwg;
+    bid -= split * nwg;
+  }
+  const int ph_a = phase >> 1, ph_b = phase & 1;
+  const int r0 = sd2 ? ((ph_a + a.ph) & 1) : 0, s0 = sd2 ? ((ph_b + a.pw) & 1) : 0;
+  const int nr = sd2 ? (a.R - r0 + 1) / 2 : a.R, ns = sd2 ? (a.S - s0 + 1) / 2 : a.S;
   const int kGroup = a.group;
   const int group = kGroup * tiles_n;
   const int first_m = (bid / group) * kGroup;
@@ -139,9 +174,9 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     const int chunk = slot ^ swz(row);
     a_ok[i] = m < a.M;
     const int mm = a_ok[i] ? m : 0;
-    const int n = mm / PQ, pq = mm - n * PQ, p = pq / a.Q, q = pq - p * a.Q;
-    a_h0[i] = p * a.sh - a.ph;
-    a_w0[i] = q * a.sw - a.pw;
+    const int n = fdiv36(mm, a.mpq, PQ), pq = mm - n * PQ, p = fdiv36(pq, a.mq, a.Q), q = pq - p * a.Q;
+    a_h0[i] = sd2 ? p + (ph_a + a.ph - r0) / 2 : p * a.sh - a.ph;
+    a_w0[i] = sd2 ? q + (ph_b + a.pw - s0) / 2 : q * a.sw - a.pw;
     a_off[i] = (((int64_t)n * a.H + a_h0[i]) * a.W + a_w0[i]) * a.pix + chunk * 8;
   }
   const int64_t ldw = (int64_t)a.R * a.S * a.C;
@@ -164,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 
   const int cpb = a.C / kBK;  // 64-channel slices per filter tap
   const int kt0 = split * a.steps_per_split;  // this split's reduction steps [kt0, kt0 + nk)
-  const int nk = max(0, min(a.R * a.S * cpb - kt0, a.steps_per_split));
+  const int nk = sd2 ? nr * ns * cpb : max(0, min(a.R * a.S * cpb - kt0, a.steps_per_split));
 
   // reduction position of the NEXT stage to issue, advanced incrementally (stages are issued in
   // order): filter tap (r, s) and channel slice c0 — no per-stage integer divisions
@@ -178,16 +213,18 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   int64_t st_t = kt0;
   auto stage = [&](uint16_t* buf) {
     const int r = st_r, s = st_s, c0 = st_c0;
-    const int64_t tap = ((int64_t)r * a.W + s) * a.pix + c0;
+    const int dh = sd2 ? -r : r, dw = sd2 ? -s : s;  // sd2: (r, s) count the phase's taps
+    const int64_t tap = ((int64_t)dh * a.W + dw) * a.pix + c0;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
-      const int h = a_h0[i] + r, w = a_w0[i] + s;
+      const int h = a_h0[i] + dh, w = a_w0[i] + dw;
       const bool ok = a_ok[i] & ((unsigned)h < (unsigned)a.H) & ((unsigned)w < (unsigned)a.W);
       glds16(ok ? a.in + a_off[i] + tap : zero, buf + (i * 4 + wave) * 8 * kBK);
     }
-    // DGRAD: filter tap (R-1-r, S-1-s) of reduction channels c0 .. c0+63
-    const int64_t kofs = DGRAD ? ((int64_t)c0 * a.R * a.S + (a.R - 1 - r) * a.S + (a.S - 1 - s)) * a.K
-                               : st_t * kBK;
+    // DGRAD: filter tap (R-1-r, S-1-s) of reduction channels c0 .. c0+63 (sd2: tap (r0 + 2r, s0 + 2s))
+    const int64_t kofs =
+        DGRAD ? ((int64_t)c0 * a.R * a.S + (sd2 ? (r0 + 2 * r) * a.S + s0 + 2 * s : (a.R - 1 - r) * a.S + (a.S - 1 - s))) * a.K
+              : st_t * kBK;
 #pragma unroll
     for (int i = 0; i < IB; ++i)
       glds16(b_src[i] ? b_src[i] + kofs : zero, buf + BM * kBK + (i * 4 + wave) * 512);
@@ -195,11 +232,17 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     st_c0 += kBK;
     if (st_c0 == a.C) {
       st_c0 = 0;
-      if (++st_s == a.S) {
+      if (++st_s == ns) {
         st_s = 0;
         ++st_r;
       }
     }
+  };
+  // dX row (in units of K elements) of tile row m: m itself, or (sd2) its interleaved phase pixel
+  auto orow = [&](int m) -> int64_t {
+    if (!sd2) return m;
+    const int n = fdiv36(m, a.mpq, PQ), pq = m - n * PQ, p = fdiv36(pq, a.mq, a.Q), q = pq - p * a.Q;
+    return ((int64_t)n * a.Hx + 2 * p + ph_a) * a.Wx + 2 * q + ph_b;
   };
 
   // per-channel epilogue constants of this thread's store column (the eval-BN affine or the
@@ -211,20 +254,56 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     const int my_k = n0 + (tid % kCpr) * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) asc[e] = ash[e] = 0.f;
+    // (8 channels = two 16-byte loads per array: my_k % 8 == 0 and the [K] fp32 arrays are aligned)
+    auto ld8 = [](const float* p, float (&v)[8]) {
+      const float4 x0 = reinterpret_cast<const float4*>(p)[0], x1 = reinterpret_cast<const float4*>(p)[1];
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    };
     if (!STATS && a.aff_scale != nullptr && my_k < a.K) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        asc[e] = a.aff_scale[my_k + e];
-        ash[e] = a.aff_shift[my_k + e];
-      }
+      ld8(a.aff_scale + my_k, asc);
+      ld8(a.aff_shift + my_k, ash);
     }
     if (STATS && DGRAD && a.bnb.mode == 1 && my_k < a.K) {  // ReluMask<MASKX> arithmetic of bn_act.hip
+      float wv[8], iv[8], bv[8], mv[8];
+      ld8(a.bnb.invstd + my_k, iv);
+      ld8(a.bnb.mean + my_k, mv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wv[e] = 1.f, bv[e] = 0.f;
+      if (a.bnb.w) ld8(a.bnb.w + my_k, wv);
+      if (a.bnb.b) ld8(a.bnb.b + my_k, bv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float sc = (a.bnb.w ? a.bnb.w[my_k + e] : 1.f) * a.bnb.invstd[my_k + e];
+        const float sc = wv[e] * iv[e];
         asc[e] = sc;
-        ash[e] = (a.bnb.b ? a.bnb.b[my_k + e] : 0.f) - a.bnb.mean[my_k + e] * sc;
+        ash[e] = bv[e] - mv[e] * sc;
       }
+    }
+  }
+
+  // Epilogue operand prefetch: the addend / BN-backward x, y chunks this thread will store, issued
+  // BEFORE the K loop so their HBM round trip overlaps the loads and MFMAs of the whole tile
+  // (issued after the loop, the BN-backward epilogue waited ~2 us for x on every workgroup; inside
+  // the store loop, a round trip per iteration: +18 us on a layer1 dgrad).  Older than every stage's
+  // LDS-DMA, they retire with the first counted vmcnt wait.  (Split-K tiles store fp32 partials
+  // instead: no prefetch.)
+  constexpr bool FSTATS = STATS && !DGRAD, BNB = STATS && DGRAD;
+  constexpr int kChunksPerRow = BN / 8;
+  constexpr int kIt = BM * kChunksPerRow / kThreads;
+  uint4 pd[kIt], px[kIt], py[kIt];
+  const bool has_add = !FSTATS && a.addend != nullptr;
+  const bool stores_here = a.splits == 1 || sd2;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int idx = it * kThreads + tid;
+    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
+    const int m = m0 + lr, k = n0 + ch * 8;
+    const bool ok = stores_here && m < a.M && k < a.K;
+    const int64_t off = (ok ? orow(m) : 0) * a.K + k;
+    pd[it] = px[it] = py[it] = uint4{0u, 0u, 0u, 0u};
+    if (has_add && ok) pd[it] = *reinterpret_cast<const uint4*>(a.addend + off);
+    if (BNB && ok) {
+      px[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.x) + off);
+      if (a.bnb.mode == 2) py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
     }
   }
 
@@ -372,7 +451,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
 
-  if (a.splits > 1) {  // split-K: raw fp32 partials (16 lanes = one 64-byte row segment per store)
+  if (a.splits > 1 && !sd2) {  // split-K: raw fp32 partials (16 lanes = one 64-byte row segment per store)
     float* part = a.part + (int64_t)split * a.M * a.K;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -392,52 +471,41 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 
   // ---- epilogue.  acc[i][j][e] is out[m0 + wm*BM/2 + i*16 + c4*4 + e][n0 + wn*BN/2 + j*16 + r16].
   // STATS && !DGRAD: forward BN statistics; STATS && DGRAD: the BN-backward epilogue (a.bnb).
-  constexpr bool FSTATS = STATS && !DGRAD, BNB = STATS && DGRAD;
   // Values are rounded to T once; the BN statistics use the rounded values (what BN will read),
   // and the tile is transposed through LDS so the global stores are whole 16-byte row chunks
   // (a raw accumulator store would be 2-byte scattered writes).
-  // Epilogue operand prefetch: the addend / BN-backward x, y chunks this thread will store,
-  // issued BEFORE the LDS transpose so their memory latency overlaps it (loaded inside the store
-  // loop, every iteration waited a full round trip: +18 us on a layer1 dgrad with the BN epilogue)
-  constexpr int kChunksPerRow = BN / 8;
-  constexpr int kIt = BM * kChunksPerRow / kThreads;
-  uint4 pd[kIt], px[kIt], py[kIt];
-  const bool has_add = !FSTATS && a.addend != nullptr;
-#pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int idx = it * kThreads + tid;
-    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
-    const int m = m0 + lr, k = n0 + ch * 8;
-    const bool ok = m < a.M && k < a.K;
-    const int64_t off = (int64_t)m * a.K + k;
-    pd[it] = px[it] = py[it] = uint4{0u, 0u, 0u, 0u};
-    if (has_add && ok) pd[it] = *reinterpret_cast<const uint4*>(a.addend + off);
-    if (BNB && ok) {
-      px[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.x) + off);
-      if (a.bnb.mode == 2) py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
-    }
-  }
   constexpr int kLd = BN + 8;  // padded LDS row (elements)
   uint16_t* tile = smem;       // [BM][kLd] of T (the K loop ended with a barrier: smem is free)
   float* red = reinterpret_cast<float*>(smem + BM * kLd);  // [2 (wm)][2 (sum, sq)][BN]
   float csum[FN], csq[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) csum[j] = csq[j] = 0.f;
+  // acc -> LDS as 32-bit column pairs: neighbour lanes (r16, r16 ^ 1) hold adjacent columns of the
+  // same 4 rows, so one lane^1 exchange per row pair lets the even lane store rows e, the odd lane
+  // rows e + 1, each as (column 2c, 2c + 1) — half the LDS write instructions of 2-byte stores
+  const bool odd = r16 & 1;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int lr = wm * (BM / 2) + i * 16 + c4 * 4 + e;
-      const bool row_ok = m0 + lr < a.M;
+    for (int j = 0; j < FN; ++j) {
+      const int lc = wn * (BN / 2) + j * 16 + (r16 & ~1);
+      float v[4];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int lc = wn * (BN / 2) + j * 16 + r16;
-        const float v = rnd<T>(acc[i][j][e]);
-        st1<T>(reinterpret_cast<T*>(tile) + lr * kLd + lc, v);
-        if (FSTATS && row_ok) {
-          csum[j] += v;
-          csq[j] += v * v;
+      for (int e = 0; e < 4; ++e) {
+        v[e] = rnd<T>(acc[i][j][e]);
+        if (FSTATS && m0 + wm * (BM / 2) + i * 16 + c4 * 4 + e < a.M) {
+          csum[j] += v[e];
+          csq[j] += v[e] * v[e];
         }
+      }
+#pragma unroll
+      for (int ep = 0; ep < 4; ep += 2) {
+        // lane ^ 1 exchange on the DPP path (quad_perm [1,0,3,2]): no LDS traffic, unlike __shfl_xor
+        const float got = __builtin_bit_cast(
+            float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, odd ? v[ep] : v[ep + 1]), 0xB1, 0xF, 0xF, false));
+        const int lr = wm * (BM / 2) + i * 16 + c4 * 4 + ep + (odd ? 1 : 0);
+        const uint32_t pk = pack2<T>(odd ? got : v[ep], odd ? v[ep + 1] : got);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(tile) + lr * kLd + lc) = pk;
       }
     }
   }
@@ -525,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
         }
         Vec8<T>::store(reinterpret_cast<T*>(&v), o);
       }
-      *reinterpret_cast<uint4*>(a.out + (int64_t)m * a.K + k) = v;
+      *reinterpret_cast<uint4*>(a.out + orow(m) * a.K + k) = v;
     }
   }
   if (BNB) {
@@ -586,7 +654,7 @@ hipError_t launch(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
   // 2 stages: the deeper rings (3/4, counted vmcnt across raw barriers) measured no better on any
   // ResNet-50 layer or Llama projection (profiles/conv_r01, profiles/llama_r01) — at 2-5
   // workgroups per CU the other workgroups already hide the glds latency (guide: "regime-gated")
-  const int nb = g_stages > 0 ? g_stages : 2;
+  const int nb = a.nb > 0 ? a.nb : (g_stages > 0 ? g_stages : 2);
   if (nb == 1) return launch_nb<T, BM, BN, 1>(a, stats, dgrad, st);
   if (nb == 2) return launch_nb<T, BM, BN, 2>(a, stats, dgrad, st);
   if (nb == 3) return launch_nb<T, BM, BN, 3>(a, stats, dgrad, st);
@@ -642,9 +710,13 @@ int conv_fwd_splits(int M, int K, int nk, int bm, int bn) {
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
-                    const SplitkEpilogue* ep, const void* addend, const BnBwdEpilogue* bnb, int pix) {
+                    const SplitkEpilogue* ep, const void* addend, const BnBwdEpilogue* bnb, int pix, int dgrad_stride,
+                    int Hx, int Wx, int nb) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
+  const bool sd2 = dgrad_stride == 2;
+  if (sd2 && (!dgrad || Hx != 2 * P || Wx != 2 * Q || alpha != 1.f || ep != nullptr)) return hipErrorInvalidValue;
+  if (dgrad_stride != 1 && !sd2) return hipErrorInvalidValue;
   if (splits > 1 && part == nullptr) return hipErrorInvalidValue;
   if (addend != nullptr && ((splits > 1 && bnb == nullptr) || psum != nullptr)) return hipErrorInvalidValue;
   if (bnb != nullptr && (!dgrad || bnb->sums == nullptr || bnb->x == nullptr || (bnb->mode == 2 && bnb->y == nullptr) ||
@@ -664,11 +736,25 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   a.kvalid = K;
   a.stamps = g_stamps;
   a.pix = pix > 0 ? pix : C;
+  a.sd = sd2 ? 2 : 1;
+  {
+    auto magic36 = [](int d) -> uint64_t { return ((1ull << 36) + (uint64_t)d - 1) / (uint64_t)d; };
+    const bool exact = M64 < (1 << 22) && (int64_t)P * Q < (1 << 14);
+    a.mq = exact ? magic36(Q) : 0;
+    a.mpq = exact ? magic36(P * Q) : 0;
+  }
+  a.nb = (nb >= 1 && nb <= 4) ? nb : 0;
+  a.Hx = Hx;
+  a.Wx = Wx;
   if (pix > 0 && (dgrad || pix % 8 != 0)) return hipErrorInvalidValue;
   const int nk = R * S * (C / kBK);
   splits = max(1, min(splits, nk));
   a.steps_per_split = (nk + splits - 1) / splits;
   a.splits = (nk + a.steps_per_split - 1) / a.steps_per_split;  // no empty splits
+  if (sd2) {  // one launch over the 4 output phases (the grid's "splits" are the phases), no split-K
+    a.steps_per_split = nk;
+    a.splits = 4;
+  }
   a.part = part;
   a.addend = static_cast<const uint16_t*>(addend);
   if (bnb != nullptr) a.bnb = *bnb;
@@ -676,7 +762,7 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   a.aff_shift = aff ? ep->shift : nullptr;
   a.aff_act = aff ? ep->act : 0;
   if (aff && a.splits == 1) a.addend = static_cast<const uint16_t*>(ep->residual);
-  if (a.splits > 1) {
+  if (a.splits > 1 && !sd2) {
     hipError_t e;
     if (dtype == kBF16) {
       if (bm == 128 && bn == 128) e = launch<bf16_t, 128, 128>(a, false, dgrad, st);

@@ -13,10 +13,11 @@ SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
   add and ReLU folded in (``bn_act.hip``).  No separate statistics read, no finalize launch.
 * backward — the fused BN/ReLU/residual backward (``bn_act.hip``) produces dconv; the data
   gradient of a stride-1 convolution is the same implicit-GEMM kernel in DGRAD mode (the forward
-  filter read flipped and channel-transposed through ds_read_b64_tr_b16, no filter copy); weight
+  filter read flipped and channel-transposed through ds_read_b64_tr_b16, no filter copy); a
+  stride-2 RxS data gradient runs as its 4 output-phase sub-convolutions in ONE DGRAD launch; weight
   gradients run on ``conv_wgrad.hip`` (split-K MFMA over the output pixels); a 1x1 strided data
-  gradient is the same DGRAD GEMM on the output grid plus one scatter(+add) pass; other strided
-  data gradients use the vendor kernels (``aten.convolution_backward``).
+  gradient is the same DGRAD GEMM on the output grid plus one scatter(+add) pass; anything else
+  uses the vendor kernels (``aten.convolution_backward``).
 
 The RGB stem (7x7/s2/p3, C <= 4) is rewritten as space-to-depth + a stride-1 R=4 conv whose
 64-element reduction runs span 4 adjacent 16-channel pixels (``stem.hip``), on the same kernels.  Anything else
@@ -52,6 +53,34 @@ def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d, w: Optional[torch.Tensor] 
         and x.is_contiguous(memory_format=torch.channels_last)
         and w.is_contiguous(memory_format=torch.channels_last)
     )
+
+
+# Tuned launch plans (the MIOpen find-db role): configs/conv_plans_mi355x.json, written by
+# scripts/conv_tune.py on MI355X — per GEMM shape the fastest (tile, split-K, LDS ring depth) of
+# the forward (+ BN statistics) and of the data gradient with the BN-backward epilogue; shapes not
+# in the table use the kernels' own heuristics.  HYPERION_CONV_PLANS=<path> | off.
+_PLANS: Optional[dict] = None
+
+
+def _plan(op: str, M: int, K: int, C: int, R: int, S: int, stride: int):
+    global _PLANS
+    if _PLANS is None:
+        _PLANS = {}
+        path = os.environ.get("HYPERION_CONV_PLANS", "")
+        if path != "off":
+            if not path:
+                path = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                    "configs", "conv_plans_mi355x.json")
+            try:
+                import json
+
+                with open(path) as f:
+                    for pl in json.load(f).get("plans", []):
+                        key = (pl["op"], pl["M"], pl["K"], pl["C"], pl["R"], pl["S"], pl["stride"])
+                        _PLANS[key] = (int(pl["bm"]), int(pl["bn"]), int(pl["splits"]), int(pl["stages"]))
+            except (OSError, ValueError, KeyError):
+                _PLANS = {}
+    return _PLANS.get((op, M, K, C, R, S, stride))
 
 
 FUSE_BN_BACKWARD = True  # dgrad epilogue computes the producing BN layer's backward reduce (A/B switch)
@@ -93,23 +122,31 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
     ``bn``: the producing BN layer's link — when the native kernel runs, it returns dz = dX·mask
     with the BN reduce done (``bn.dz`` is set)."""
     R, S = w.shape[2], w.shape[3]
-    if (tuple(stride) == (1, 1) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0 and padding[0] <= R - 1
+    H, W = x.shape[2], x.shape[3]
+    # stride 2 (ResNet's strided 3x3): the 4 output-phase sub-convolutions in one launch (needs an
+    # even dX whose forward output is dY — true for every ResNet downsampling conv)
+    s2 = (tuple(stride) == (2, 2) and R > 1 and H % 2 == 0 and W % 2 == 0 and dy.shape[2] * 2 == H
+          and dy.shape[3] * 2 == W and (H + 2 * padding[0] - R) // 2 + 1 == dy.shape[2]
+          and (W + 2 * padding[1] - S) // 2 + 1 == dy.shape[3])
+    if ((tuple(stride) == (1, 1) or s2) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0 and padding[0] <= R - 1
             and padding[1] <= S - 1 and _native.use_native(dy, op="dgrad")):
-        # dX = conv(dY, flip(W) with C <-> K), stride 1, padding R-1-p: conv_igemm.hip's DGRAD mode
+        # stride 1: dX = conv(dY, flip(W) with C <-> K), padding R-1-p — conv_igemm.hip's DGRAD mode
         # reads the forward filter flipped and transposed in-kernel (no filter copy)
         dyc = dy.contiguous(memory_format=torch.channels_last)
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
-        _native.count("dgrad")
+        _native.count("dgrad_strided" if s2 else "dgrad")
+        geo = dict(stride=2, H=H, W=W) if s2 else {}
         if bn is not None and not bn.used and bn.yc.dtype == dy.dtype:
             bn.used = True
             _native.count("dgrad_bn_fused")
-            bn.dz = _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend, bn_x=bn.yc,
-                                                bn_y=x if bn.mode == 2 else None, bn_w=bn.bn_w, bn_b=bn.bn_b,
-                                                bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,
-                                                bn_sums=bn.sums)
+            pl = _plan("dgrad_bnb", x.shape[0] * H * W, w.shape[1], w.shape[0], R, S, stride[0]) or (-1, -1, -1, 0)
+            bn.dz = _native.native().conv_dgrad(dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2], addend=addend,
+                                                bn_x=bn.yc, bn_y=x if bn.mode == 2 else None, bn_w=bn.bn_w,
+                                                bn_b=bn.bn_b, bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,
+                                                bn_sums=bn.sums, stages=pl[3], **geo)
             return bn.dz
-        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend)
+        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend, **geo)
     if (R == 1 and S == 1 and tuple(padding) == (0, 0) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0
             and _native.use_native(dy, op="dgrad")):
         # 1x1 stride-s (ResNet downsample): dY·W on the output grid is the stride-1 DGRAD GEMM; one
@@ -255,7 +292,11 @@ class _ConvBNActFn(torch.autograd.Function):
         K = w.shape[0]
         sums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
         ctx.bsums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
-        yc, _, _ = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True, sums=sums)
+        P = (x.shape[2] + 2 * padding[0] - w.shape[2]) // stride[0] + 1
+        Q = (x.shape[3] + 2 * padding[1] - w.shape[3]) // stride[1] + 1
+        pl = _plan("fwd", x.shape[0] * P * Q, K, x.shape[1], w.shape[2], w.shape[3], stride[0]) or (-1, -1, -1, 0)
+        yc, _, _ = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True, pl[0], pl[1], pl[2],
+                              sums=sums, stages=pl[3])
         if residual is not None:
             residual = residual.to(x.dtype).contiguous(memory_format=torch.channels_last)
         out, mean, invstd = C.bn_fwd_sums(yc, residual, sums, bn_w, bn_b, rm, rv, momentum, eps, act)

@@ -18,14 +18,17 @@ import torch  # noqa: E402
 
 from hyperion.ops import _native  # noqa: E402
 
-CASES = [  # N, C, H, K, R, stride, pad, bm, bn, splits
-    (32, 256, 14, 256, 3, 1, 1, -1, -1, -1),
-    (32, 256, 14, 256, 3, 1, 1, 64, 64, 1),
-    (32, 256, 14, 256, 3, 1, 1, 128, 128, 1),
-    (32, 64, 56, 256, 1, 1, 0, -1, -1, -1),
-    (32, 64, 56, 64, 3, 1, 1, -1, -1, -1),
-    (32, 512, 7, 512, 3, 1, 1, -1, -1, -1),
-    (32, 1024, 14, 256, 1, 1, 0, -1, -1, -1),
+CASES = [  # op, N, C, H, K, R, stride, pad, bm, bn, splits
+    ("fwd", 32, 256, 14, 256, 3, 1, 1, -1, -1, -1),
+    ("fwd", 32, 64, 56, 256, 1, 1, 0, -1, -1, -1),
+    ("dgrad", 32, 256, 56, 64, 1, 1, 0, -1, -1, -1),
+    ("dgrad_bnb", 32, 256, 56, 64, 1, 1, 0, -1, -1, -1),
+    ("dgrad", 32, 256, 56, 128, 1, 1, 0, -1, -1, -1),
+    ("dgrad_bnb", 32, 256, 56, 128, 1, 1, 0, -1, -1, -1),
+    ("dgrad_bnb", 32, 256, 56, 128, 1, 1, 0, 64, 64, 1),
+    ("dgrad", 32, 512, 28, 128, 1, 1, 0, -1, -1, -1),
+    ("dgrad_bnb", 32, 512, 28, 128, 1, 1, 0, -1, -1, -1),
+    ("dgrad_bnb", 32, 64, 56, 64, 3, 1, 1, -1, -1, -1),
 ]
 
 
@@ -70,21 +73,34 @@ def main():
     C_ = _native.native()
     rows = []
     buf = torch.zeros(200000 * 6, dtype=torch.int64, device="cuda")
-    for (N, C, H, K, R, s, p, bm, bn, sp) in CASES:
+    for (op, N, C, H, K, R, s, p, bm, bn, sp) in CASES:
         x = torch.randn(N, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         w = (torch.randn(K, C, R, R, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+        P0 = (H + 2 * p - R) // s + 1
+        dy = torch.randn(N, K, P0, P0, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        mean, invstd = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        bs = torch.zeros(_native.STAT_SLOTS * 2 * C, device="cuda", dtype=torch.float64)
+
+        def run():
+            if op == "fwd":
+                return C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp)
+            if op == "dgrad":
+                return C_.conv_dgrad(dy, w, p, p, bm, bn, sp)
+            return C_.conv_dgrad(dy, w, p, p, bm, bn, sp, bn_x=x, bn_mean=mean, bn_invstd=invstd, bn_mode=1,
+                                 bn_sums=bs)
+
         for _ in range(5):
-            C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp)
+            run()
         torch.cuda.synchronize()
         buf.zero_()
         C_.conv_set_stamps(buf)
-        C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp)
+        run()
         torch.cuda.synchronize()
         C_.conv_set_stamps(None)
         st = buf.view(-1, 6).cpu()
         nk = R * R * C // 64
         P = (H + 2 * p - R) // s + 1
-        r = dict(N=N, C=C, H=H, K=K, R=R, stride=s, pad=p, bm=bm, bn=bn, splits=sp, nk=nk, M=N * P * P)
+        r = dict(op=op, N=N, C=C, H=H, K=K, R=R, stride=s, pad=p, bm=bm, bn=bn, splits=sp, nk=nk, M=N * P * P)
         r.update(analyse(st))
         rows.append(r)
         print(json.dumps(r), flush=True)

@@ -1,0 +1,112 @@
+"""Per-shape launch-plan tuning of the native conv kernels (the MIOpen find-db role) on every
+ResNet-50 convolution at a given batch: forward with the BN-statistics epilogue, and the data
+gradient with the producer's BN-backward epilogue (mode 1, the common case in a bottleneck) —
+tile (bm x bn), split-K count and LDS ring depth, each timed as 20 launches in one hipGraph.
+
+Writes the winners to configs/conv_plans_mi355x.json (ops/conv.py looks plans up by GEMM shape)
+and every measurement to gpurun_out/conv_tune.json.
+
+    python scripts/conv_tune.py [--batch 32] [--out configs/conv_plans_mi355x.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from hyperion.bench.conv_shapes import resnet50_convs  # noqa: E402
+from hyperion.ops import _native  # noqa: E402
+from conv_roofline import gtime  # noqa: E402
+
+TILES = [(128, 128), (128, 64), (64, 64)]
+
+
+def configs(nk, strided_dgrad=False):
+    out = []
+    for bm, bn in TILES:
+        for sp in ([1] if strided_dgrad else [1, 2, 3, 4, 6]):
+            if sp > 1 and nk // sp < 2:
+                continue
+            for nb in (1, 2, 3):
+                if nb == 3 and nk // sp < 6:
+                    continue
+                out.append((bm, bn, sp, nb))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--out", default="configs/conv_plans_mi355x.json")
+    ap.add_argument("--raw", default="gpurun_out/conv_tune.json")
+    a = ap.parse_args()
+    C_ = _native.native()
+    plans, raw = [], []
+    for sh in resnet50_convs(a.batch):
+        N, C, H, K, R, s, p = sh["N"], sh["C"], sh["H"], sh["K"], sh["R"], sh["stride"], sh["pad"]
+        if C % 64:
+            continue
+        P = (H + 2 * p - R) // s + 1
+        x = torch.randn(N, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(K, C, R, R, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+        sums = torch.zeros(_native.STAT_SLOTS * 2 * K, device="cuda", dtype=torch.float64)
+        row = dict(sh, P=P)
+        # ---- forward + BN statistics
+        nk = R * R * C // 64
+        fwd = {}
+        for cfg in configs(nk):
+            bm, bn, sp, nb = cfg
+            fwd[cfg] = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp, sums=sums, stages=nb))
+        auto = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True, sums=sums))
+        best = min(fwd, key=fwd.get)
+        row["fwd"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(fwd[best], 2),
+                      "all": {",".join(map(str, k)): round(v, 2) for k, v in fwd.items()}}
+        plans.append({"op": "fwd", "M": N * P * P, "K": K, "C": C, "R": R, "S": R, "stride": s, "pad": p,
+                      "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
+                      "us": round(fwd[best], 2), "auto_us": round(auto, 2)})
+        # ---- data gradient with the producer's BN-backward epilogue (mode 1: BN + ReLU)
+        if K % 64 == 0 and (s == 1 or R > 1):
+            dy = torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+            yc = torch.randn_like(x)
+            mean = torch.zeros(C, device="cuda")
+            invstd = torch.ones(C, device="cuda")
+            bsums = torch.zeros(_native.STAT_SLOTS * 2 * C, device="cuda", dtype=torch.float64)
+            geo = dict(stride=2, H=H, W=H) if s == 2 else {}
+            nkd = R * R * K // 64
+
+            def dg(bm=-1, bn=-1, sp=-1, nb=0):
+                return C_.conv_dgrad(dy, w, p, p, bm, bn, sp, bn_x=yc, bn_mean=mean, bn_invstd=invstd, bn_mode=1,
+                                     bn_sums=bsums, stages=nb, **geo)
+
+            dgr = {}
+            for cfg in configs(nkd, strided_dgrad=s == 2):
+                bm, bn, sp, nb = cfg
+                dgr[cfg] = gtime(lambda: dg(bm, bn, sp, nb))
+            auto = gtime(lambda: dg())
+            best = min(dgr, key=dgr.get)
+            row["dgrad_bnb"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(dgr[best], 2),
+                                "all": {",".join(map(str, k)): round(v, 2) for k, v in dgr.items()}}
+            plans.append({"op": "dgrad_bnb", "M": N * H * H, "K": C, "C": K, "R": R, "S": R, "stride": s, "pad": p,
+                          "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
+                          "us": round(dgr[best], 2), "auto_us": round(auto, 2)})
+        raw.append(row)
+        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb")}),
+              json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "all"} for k, v in row.items()
+                          if k in ("fwd", "dgrad_bnb")}), flush=True)
+    doc = {"device": torch.cuda.get_device_name(), "batch": a.batch,
+           "note": "native conv launch plans by GEMM shape (M = output pixels, K = output channels, C = "
+                   "reduction channels); written by scripts/conv_tune.py",
+           "plans": plans}
+    for path, obj in ((a.out, doc), (a.raw, raw)):
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(obj, f, indent=1)
+    tot_auto = sum(pl["auto_us"] for pl in plans)
+    tot_best = sum(pl["us"] for pl in plans)
+    print(json.dumps({"sum_auto_us": round(tot_auto, 1), "sum_best_us": round(tot_best, 1)}))
+
+
+if __name__ == "__main__":
+    main()

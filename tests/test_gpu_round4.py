@@ -56,3 +56,97 @@ def test_stem_conv_bn_relu_native_matches_fp32(N, H):
     dw = conv_l.weight.grad.float().cpu()
     assert dw.shape == wr.grad.shape
     torch.testing.assert_close(dw, wr.grad, rtol=3e-2, atol=3e-2 * wr.grad.abs().max().item())
+
+
+# ---- stride-2 data gradient as 4 output-phase sub-convolutions in one launch (conv_igemm.hip sd2)
+S2_SHAPES = [  # N, C (dX channels), H (dX), K (dY channels), R, pad
+    (2, 128, 16, 128, 3, 1),
+    (3, 64, 14, 64, 3, 1),
+    (1, 64, 8, 256, 3, 1),
+    (2, 256, 28, 256, 3, 1),
+    (2, 64, 12, 128, 5, 2),
+]
+
+
+@pytest.mark.parametrize("shape", S2_SHAPES)
+@pytest.mark.parametrize("with_add", [False, True])
+def test_strided_dgrad_phases_match_fp32(shape, with_add):
+    from hyperion.ops import _native
+
+    N, C, H, K, R, p = shape
+    torch.manual_seed(0)
+    P = (H + 2 * p - R) // 2 + 1
+    assert 2 * P == H
+    dy = torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device="cuda") / (K * R * R) ** 0.5).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    add = (torch.randn(N, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+           if with_add else None)
+    dx = _native.native().conv_dgrad(dy, w, p, p, addend=add, stride=2, H=H, W=H)
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().cpu(), dy.float().cpu(), stride=2, padding=p)
+    if with_add:
+        ref = ref + add.float().cpu()
+    assert dx.shape == ref.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(dx.float().cpu(), ref, rtol=2e-2, atol=2e-2)
+
+
+def _strided_chain(fuse_bn_backward):
+    from hyperion.ops import _native
+    from hyperion.ops import conv as convmod
+    from hyperion.ops.batchnorm import BatchNormAct2d
+
+    torch.manual_seed(0)
+    _native.reset_counters()
+    prev, convmod.FUSE_BN_BACKWARD = convmod.FUSE_BN_BACKWARD, fuse_bn_backward
+    try:
+        c1 = torch.nn.Conv2d(64, 128, 1, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+        b1 = BatchNormAct2d(128, act=True).cuda()
+        c2 = torch.nn.Conv2d(128, 128, 3, stride=2, padding=1, bias=False).cuda().to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+        b2 = BatchNormAct2d(128, act=True).cuda()
+        x = torch.randn(2, 64, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        out = convmod.conv_bn_act(c2, b2, convmod.conv_bn_act(c1, b1, x))
+        out.backward(torch.randn(out.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(5)).to(
+            out.dtype).contiguous(memory_format=torch.channels_last))
+    finally:
+        convmod.FUSE_BN_BACKWARD = prev
+    return x.grad.float(), c1.weight.grad.float(), c2.weight.grad.float(), _native.counters()
+
+
+def test_strided_conv_bn_act_backward_native_bn_epilogue():
+    """A stride-2 3x3 conv -> BN -> ReLU fed by another fused layer: its data gradient runs the
+    native phase kernel WITH the producer's BN-backward epilogue (no vendor dgrad), and equals the
+    same chain with the epilogue off (separate BN-backward reduce) — the same bf16 math."""
+    gx, g1, g2, cnt = _strided_chain(True)
+    assert cnt.get("dgrad_strided") == 1 and cnt.get("dgrad_bn_fused") == 1 and "dgrad_vendor" not in cnt, cnt
+    rx, r1, r2, cnt0 = _strided_chain(False)
+    assert cnt0.get("dgrad_strided") == 1 and "dgrad_bn_fused" not in cnt0, cnt0
+    for a, b in ((gx, rx), (g1, r1), (g2, r2)):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * b.abs().max().item())
+
+
+def test_strided_conv_bn_act_leaf_input_matches_fp32():
+    """The strided layer alone (leaf input: plain phase dgrad) against fp32 PyTorch."""
+    from hyperion.ops import _native
+    from hyperion.ops.batchnorm import BatchNormAct2d
+    from hyperion.ops.conv import conv_bn_act
+    import torch.nn.functional as F
+
+    torch.manual_seed(0)
+    _native.reset_counters()
+    c2 = torch.nn.Conv2d(128, 256, 3, stride=2, padding=1, bias=False).cuda().to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    b2 = BatchNormAct2d(256, act=False).cuda()
+    x = torch.randn(2, 128, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    out = conv_bn_act(c2, b2, x)
+    g = torch.randn_like(out)
+    out.backward(g)
+    assert _native.counters().get("dgrad_strided") == 1, _native.counters()
+    xr = x.detach().float().cpu().requires_grad_(True)
+    wr = c2.weight.detach().float().cpu().requires_grad_(True)
+    y = F.batch_norm(F.conv2d(xr, wr, stride=2, padding=1), None, None, b2.weight.detach().cpu(),
+                     b2.bias.detach().cpu(), True)
+    y.backward(g.float().cpu())
+    torch.testing.assert_close(x.grad.float().cpu(), xr.grad, rtol=3e-2, atol=3e-2 * xr.grad.abs().max().item())
