@@ -164,9 +164,10 @@ const float* affine_ptr(const c10::optional<at::Tensor>& t) {
 }
 
 // x: [..., d] contiguous; returns (y, s (fused residual stream or undefined), mean, rstd)
+// drop_p > 0 (with a residual and the rng record of ops._native.rng_state): s = residual + dropout(x)
 std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& residual,
                                const c10::optional<at::Tensor>& weight, const c10::optional<at::Tensor>& bias,
-                               double eps, bool rms) {
+                               double eps, bool rms, double drop_p, const c10::optional<at::Tensor>& rng) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.is_contiguous(), "ln_fwd: x must be contiguous");
   const int d = x.size(-1);
@@ -186,17 +187,25 @@ std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tens
   auto mean = at::empty({rows}, fopt);
   auto rstd = at::empty({rows}, fopt);
   const int wt = affine_mode(x, weight, bias, "ln_fwd");
+  hyp::RngState rs{};
+  if (drop_p > 0.0) {
+    TORCH_CHECK(has_res && d <= 2048 && drop_p < 1.0 && rng.has_value() && rng->defined(),
+                "ln_fwd: dropout needs a residual, d <= 2048, p < 1 and an rng record");
+    rs = unpack_rng(*rng);
+  }
   HYP_CHECK_HIP(hyp::layernorm_forward(dtype_code(x), rms ? 1 : 0, x.data_ptr(), has_res ? residual->data_ptr() : nullptr,
                                        has_res ? s.data_ptr() : nullptr, y.data_ptr(), affine_ptr(weight),
                                        affine_ptr(bias), rms ? nullptr : mean.data_ptr<float>(),
-                                       rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream(), wt));
+                                       rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream(), wt, (float)drop_p,
+                                       drop_p > 0.0 ? &rs : nullptr));
   return {y, s, mean, rstd};
 }
 
-// returns (dx, dweight, dbias)
+// returns (dx, dweight, dbias, dxa): dxa = dropout(dx) with the forward's mask when drop_p > 0
 std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, const c10::optional<at::Tensor>& weight,
                                const at::Tensor& mean, const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
-                               bool need_dw, bool need_db, bool rms) {
+                               bool need_dw, bool need_db, bool rms, double drop_p,
+                               const c10::optional<at::Tensor>& rng) {
   const int d = xin.size(-1);
   const int64_t rows = xin.numel() / d;
   at::Tensor g = dy.is_contiguous() ? dy : dy.contiguous();
@@ -219,13 +228,22 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
   }
   at::Tensor dr;
   if (dres.has_value() && dres->defined()) dr = dres->is_contiguous() ? *dres : dres->contiguous();
+  hyp::RngState rs{};
+  at::Tensor dxa;
+  if (drop_p > 0.0) {
+    TORCH_CHECK(d <= 2048 && drop_p < 1.0 && rng.has_value() && rng->defined(),
+                "ln_bwd: dropout needs d <= 2048, p < 1 and the forward's rng record");
+    rs = unpack_rng(*rng);
+    dxa = at::empty_like(xin);
+  }
   HYP_CHECK_HIP(hyp::layernorm_backward(dtype_code(xin), rms ? 1 : 0, g.data_ptr(), xin.data_ptr(),
                                         affine_ptr(weight), rms ? nullptr : mean.data_ptr<float>(),
                                         rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(),
                                         part.data_ptr<float>(), db.defined() ? part.data_ptr<float>() + d : nullptr,
                                         dw.defined() ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr,
-                                        rows, d, P, rpw, cur_stream(), wt));
-  return {dx, need_dw ? dw : at::Tensor(), need_db ? db : at::Tensor()};
+                                        rows, d, P, rpw, cur_stream(), wt, dxa.defined() ? dxa.data_ptr() : nullptr,
+                                        (float)drop_p, drop_p > 0.0 ? &rs : nullptr));
+  return {dx, need_dw ? dw : at::Tensor(), need_db ? db : at::Tensor(), dxa};
 }
 
 }  // namespace
@@ -234,8 +252,13 @@ void register_attn_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, "flash attention forward (MFMA)");
   m.def("attn_bwd", &attn_bwd, "flash attention backward (MFMA)");
   m.def("attn_bwd_rope", &attn_bwd_rope, "flash attention backward with the inverse RoPE fused into dQ / dK");
-  m.def("ln_fwd", &ln_fwd, "LayerNorm/RMSNorm forward (+fused residual add)");
-  m.def("ln_bwd", &ln_bwd, "LayerNorm/RMSNorm backward");
+  m.def("ln_fwd", &ln_fwd, "LayerNorm/RMSNorm forward (+fused residual add, + dropout on x)", pybind11::arg("x"),
+        pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("eps"),
+        pybind11::arg("rms"), pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none());
+  m.def("ln_bwd", &ln_bwd, "LayerNorm/RMSNorm backward (+ the dropped input's gradient)", pybind11::arg("dy"),
+        pybind11::arg("xin"), pybind11::arg("weight"), pybind11::arg("mean"), pybind11::arg("rstd"),
+        pybind11::arg("dres"), pybind11::arg("need_dw"), pybind11::arg("need_db"), pybind11::arg("rms"),
+        pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none());
 }
 
 }  // namespace hypbind

@@ -55,7 +55,8 @@ void check_operand(const at::Tensor& t, const char* name) {
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, c10::optional<at::ScalarType> out_dtype,
                 const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& aux,
                 const c10::optional<at::Tensor>& residual, double alpha, double beta,
-                const c10::optional<at::Tensor>& out, int64_t tile, int64_t splits) {
+                const c10::optional<at::Tensor>& out, int64_t tile, int64_t splits, double drop_p,
+                const c10::optional<at::Tensor>& rng) {
   HYP_CHECK_CUDA_TENSOR(a);
   check_operand(a, "a");
   check_operand(b, "b");
@@ -119,6 +120,12 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, 
     g.R = r.data_ptr();
     g.ldr = (int)r.stride(0);
   }
+  if (drop_p > 0.0) {  // dropout(act(...)) in the epilogue (the FFN's inner dropout)
+    TORCH_CHECK(act != 0 && drop_p < 1.0 && rng.has_value() && rng->defined() && !g.R && c.stride(0) == N,
+                "gemm: dropout needs an activation, p < 1, an rng record, no residual and a dense output");
+    g.drop_p = (float)drop_p;
+    g.drng = unpack_rng(*rng);
+  }
   const int sp = hyp::gemm_tiled_splits(g);
   at::Tensor part;
   if (sp > 1) {
@@ -143,7 +150,8 @@ void register_gemm_ops(pybind11::module& m) {
         pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("act") = 0, pybind11::arg("aux") = pybind11::none(), pybind11::arg("residual") = pybind11::none(),
         pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0, pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("tile") = -1, pybind11::arg("splits") = -1);
+        pybind11::arg("tile") = -1, pybind11::arg("splits") = -1, pybind11::arg("drop_p") = 0.0,
+        pybind11::arg("rng") = pybind11::none());
   m.def("gemm_plan", &gemm_plan, "(tile, splits) the automatic plan picks for an M x N x K GEMM");
   m.def("gemm_f32_nt", &gemm_f32_nt, "C = alpha * A @ B.T, fp32 in, on the fp32-input MFMA", pybind11::arg("a"),
         pybind11::arg("b"), pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("alpha") = 1.0);

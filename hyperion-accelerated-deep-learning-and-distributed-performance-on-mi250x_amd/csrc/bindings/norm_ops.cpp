@@ -115,7 +115,8 @@ at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dty
 // (dy, db): the activation backward (act "relu": z = the saved output; "gelu": z = the pre-activation)
 // with the bias gradient summed in the same pass
 std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z, int64_t act,
-                                       c10::optional<at::ScalarType> db_dtype) {
+                                       c10::optional<at::ScalarType> db_dtype, double drop_p,
+                                       const c10::optional<at::Tensor>& rng) {
   HYP_CHECK_CUDA_TENSOR(dh);
   TORCH_CHECK(dh.is_contiguous() && z.is_contiguous() && dh.sizes() == z.sizes() && dh.scalar_type() == z.scalar_type(),
               "act_bwd_colsum: dh / z contiguous, one shape and dtype");
@@ -128,8 +129,14 @@ std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z
   auto db = at::empty({N}, dh.options().dtype(odt));
   const int P = hyp::colsum_partials(M, (int)N);
   auto part = at::empty({(int64_t)P * N}, dh.options().dtype(at::kFloat));
+  hyp::RngState rs{};
+  if (drop_p > 0.0) {
+    TORCH_CHECK(drop_p < 1.0 && rng.has_value() && rng->defined(), "act_bwd_colsum: dropout needs p < 1 and the rng record");
+    rs = unpack_rng(*rng);
+  }
   HYP_CHECK_HIP(hyp::act_bwd_colsum(dtype_code(dh), (int)act, dh.data_ptr(), z.data_ptr(), dy.data_ptr(), M, (int)N,
-                                    db.data_ptr(), dtype_code(db), part.data_ptr<float>(), P, cur_stream()));
+                                    db.data_ptr(), dtype_code(db), part.data_ptr<float>(), P, cur_stream(),
+                                    (float)drop_p, drop_p > 0.0 ? &rs : nullptr));
   return {dy, db};
 }
 
@@ -202,7 +209,8 @@ void register_norm_ops(pybind11::module& m) {
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());
   m.def("act_bwd_colsum", &act_bwd_colsum, "activation backward + bias gradient in one pass (act 1 relu, 2 gelu)",
-        pybind11::arg("dh"), pybind11::arg("z"), pybind11::arg("act"), pybind11::arg("db_dtype") = pybind11::none());
+        pybind11::arg("dh"), pybind11::arg("z"), pybind11::arg("act"), pybind11::arg("db_dtype") = pybind11::none(),
+        pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none());
   m.def("unscale_mt", &unscale_mt, "multi-tensor unscale + non-finite check");
   m.def("sumsq_mt", &sumsq_mt, "multi-tensor sum of squares");
   m.def("clip_mt", &clip_mt, "multi-tensor clip by global norm (device scalar)");

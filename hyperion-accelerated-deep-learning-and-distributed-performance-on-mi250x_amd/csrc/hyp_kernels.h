@@ -61,12 +61,15 @@ namespace hyp {
 bool layernorm_supported(int d);
 void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave);
 // wt = 1: w / b (and dw / db) are in the activation dtype instead of fp32 (pointers reinterpreted)
+// drop_p > 0 (d <= 2048; forward needs r): s = r + dropout(x) with the dropout.hip mask of *rs; the
+// backward then also writes dxa = dropout(dx), the gradient of the dropped input.
 hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
                              const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
-                             hipStream_t st, int wt = 0);
+                             hipStream_t st, int wt = 0, float drop_p = 0.f, const struct RngState* rs = nullptr);
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
-                              void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt = 0);
+                              void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt = 0,
+                              void* dxa = nullptr, float drop_p = 0.f, const struct RngState* rs = nullptr);
 }  // namespace hyp
 
 namespace hyp {
@@ -158,6 +161,10 @@ struct GemmTiledArgs {
   int act = 0;
   float alpha = 1.f, beta = 0.f;
   int tile = -1, splits = -1;
+  // drop_p > 0 (with act): the stored output is dropout(act(z)) with dropout.hip's mask of drng
+  // (element index row * ldc + col); aux keeps z
+  float drop_p = 0.f;
+  RngState drng{};
 };
 void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits);
 int gemm_tiled_splits(const GemmTiledArgs& a);
@@ -285,8 +292,10 @@ hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);
 // dy = dh·act'(z) (act 1: ReLU with z = output; 2: exact GELU with z = pre-activation) and its column
 // sums into db (out_dtype; null: skip) — the FFN activation backward + bias gradient.
+// drop_p > 0: dh is the gradient of dropout(act(z)) (dropout.hip mask of *rs, element index r*N + c)
 hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, void* dy, int64_t M, int N, void* db,
-                          int out_dtype, float* part, int P, hipStream_t st);
+                          int out_dtype, float* part, int P, hipStream_t st, float drop_p = 0.f,
+                          const RngState* rs = nullptr);
 }  // namespace hyp
 
 namespace hyp {

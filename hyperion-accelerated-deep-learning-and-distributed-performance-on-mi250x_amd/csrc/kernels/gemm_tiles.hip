@@ -175,6 +175,9 @@ struct Epi {
   const void* R;     // residual [M, N] (ldr), output dtype
   float alpha, beta;
   int ldc, ldr, act, bias_dt;
+  uint32_t dthr;     // dropout on the activation output: keep iff rng_u32(key, row * ldc + col) >= dthr
+  float dscale;      // 1 / (1 - p); 0 = no dropout
+  RngState drs;
 };
 
 template <typename OutT>
@@ -243,6 +246,12 @@ __device__ __forceinline__ void epi4(const Epi& e, int row, int col, float (&v)[
     for (int q = 0; q < 4; ++q) {
       const float x = rnd<OutT>(v[q]);  // the activation of the STORED pre-activation (aux)
       v[q] = e.act == 1 ? fmaxf(x, 0.f) : (e.act == 2 ? gelu_erf(x) : gelu_tanh(x));
+    }
+    if (e.dscale != 0.f) {  // dropout(act) as a separate dropout kernel over the stored act would compute it
+      const uint64_t key = rng_key(e.drs);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        v[q] = rng_u32(key, (uint64_t)((int64_t)row * e.ldc + col + q)) >= e.dthr ? rnd<OutT>(v[q]) * e.dscale : 0.f;
     }
   }
   if (e.R != nullptr) {
@@ -556,7 +565,12 @@ hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st) {
   p.B = static_cast<const uint16_t*>(a.B);
   p.zero = static_cast<const uint16_t*>(a.zero);
   p.part = splits > 1 ? a.part : nullptr;
-  p.e = Epi{a.C, a.aux, a.bias, a.R, a.alpha, a.beta, a.ldc, a.ldr, a.act, a.bias_dtype};
+  p.e = Epi{a.C, a.aux, a.bias, a.R, a.alpha, a.beta, a.ldc, a.ldr, a.act, a.bias_dtype, 0u, 0.f, a.drng};
+  if (a.drop_p > 0.f) {
+    if (a.act == 0 || a.R != nullptr || a.drop_p >= 1.f) return hipErrorInvalidValue;
+    p.e.dthr = (uint32_t)fminf(a.drop_p * 4294967296.f, 4294967295.f);  // dropout.hip's threshold
+    p.e.dscale = 1.f / (1.f - a.drop_p);
+  }
   p.M = a.M;
   p.N = a.N;
   p.K = a.K;

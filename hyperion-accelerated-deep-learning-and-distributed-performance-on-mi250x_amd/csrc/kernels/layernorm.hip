@@ -69,14 +69,24 @@ __device__ __forceinline__ void load_affine(const float* p, int wt, int d, int l
   }
 }
 
-template <typename T, int VPL, bool RMS, bool HAS_RES>
+// Dropout on the residual branch (DROP, post-norm transformer layers: s = r + dropout(x)): the keep
+// mask is regenerated from the counter-based hash of dropout.hip (same key, element index row·d +
+// col), so fwd, bwd and an unfused dropout kernel with the same state draw identical masks.
+struct LnDrop {
+  uint32_t thr;  // keep iff rng_u32(key, index) >= thr
+  float scale;   // 1 / (1 - p)
+  RngState rs;
+};
+
+template <typename T, int VPL, bool RMS, bool HAS_RES, bool DROP = false>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_fwd_k(const T* __restrict__ x, const T* __restrict__ r,
                                                                   T* __restrict__ s_out, T* __restrict__ y,
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ b, float* __restrict__ mean_out,
                                                                   float* __restrict__ rstd_out, int64_t rows, int d,
-                                                                  float eps, int rpw, int wt) {
+                                                                  float eps, int rpw, int wt, LnDrop dp = LnDrop{}) {
   const int lane = threadIdx.x & 63;
+  const uint64_t dkey = DROP ? rng_key(dp.rs) : 0;
   const int64_t row0 = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * rpw;
   if (row0 >= rows) return;
   float wv[VPL][8], bv[VPL][8];
@@ -102,6 +112,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_fwd_k(const T* __restr
       if (HAS_RES && c < d) {
         float rv[8];
         cr.unpack(k, rv);
+        if (DROP) {  // the dropped branch in T, as a separate dropout kernel would have stored it
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[k][j] = rng_u32(dkey, (uint64_t)(row * d + c + j)) >= dp.thr ? rnd<T>(v[k][j] * dp.scale) : 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = rnd<T>(v[k][j] + rv[j]);  // stats of the stored stream
         Vec8<T>::store(s_out + row * d + c, v[k]);
@@ -146,15 +161,19 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_fwd_k(const T* __restr
 }
 
 // dx and per-block partial dγ, dβ.  grid.x = ceil(rows / (kWavesPerBlock * rows_per_wave))
-template <typename T, int VPL, bool RMS, bool HAS_DRES>
+// DROP: also dxa = dropout(dx) with the forward's mask — the gradient of the dropped branch (the
+// residual branch gets dx itself): the separate dropout-backward pass over dx disappears.
+template <typename T, int VPL, bool RMS, bool HAS_DRES, bool DROP = false>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restrict__ dy, const T* __restrict__ xin,
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ mean_in,
                                                                   const float* __restrict__ rstd_in,
                                                                   const T* __restrict__ dres, T* __restrict__ dx,
                                                                   float* __restrict__ pdw, float* __restrict__ pdb,
-                                                                  int64_t rows, int d, int rows_per_wave, int wt) {
+                                                                  int64_t rows, int d, int rows_per_wave, int wt,
+                                                                  T* __restrict__ dxa = nullptr, LnDrop dp = LnDrop{}) {
   const int lane = threadIdx.x & 63;
+  const uint64_t dkey = DROP ? rng_key(dp.rs) : 0;
   const int wid = threadIdx.x >> 6;
   float gw[VPL][8], gb[VPL][8], wv[VPL][8];
 #pragma unroll
@@ -217,6 +236,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
           for (int j = 0; j < 8; ++j) o[j] += rv[j];
         }
         Vec8<T>::store(dx + row * d + c, o);
+        if (DROP) {
+          float oa[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            oa[j] = rng_u32(dkey, (uint64_t)(row * d + c + j)) >= dp.thr ? rnd<T>(o[j]) * dp.scale : 0.f;
+          Vec8<T>::store(dxa + row * d + c, oa);
+        }
       }
     }
     if (more) {
@@ -454,7 +480,8 @@ int wide_rows_per_block(int64_t rows) { return (int)((rows + 1023) / 1024); }
 
 template <typename T, bool RMS>
 hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, const float* b, float* mean,
-                           float* rstd, int64_t rows, int d, float eps, hipStream_t st, int wt) {
+                           float* rstd, int64_t rows, int d, float eps, hipStream_t st, int wt, const LnDrop* drop) {
+  if (drop != nullptr && (d > 2048 || r == nullptr)) return hipErrorInvalidValue;
   if (d > 2048) {
     const int rpb = wide_rows_per_block(rows);
     const dim3 grid((unsigned)((rows + rpb - 1) / rpb)), block(kWideThreads);
@@ -474,7 +501,10 @@ hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, c
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
 #define HYP_LN_F(V)                                                                                          \
   case V:                                                                                                    \
-    if (r)                                                                                                   \
+    if (drop)                                                                                                \
+      hipLaunchKernelGGL((ln_fwd_k<T, V, RMS, true, true>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, \
+                         rows, d, eps, rpw, wt, *drop);                                                       \
+    else if (r)                                                                                              \
       hipLaunchKernelGGL((ln_fwd_k<T, V, RMS, true>), grid, block, 0, st, x, r, s, y, w, b, mean, rstd, rows, \
                          d, eps, rpw, wt);                                                                       \
     else                                                                                                     \
@@ -497,7 +527,8 @@ hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, c
 template <typename T, bool RMS>
 hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const float* mean, const float* rstd,
                            const T* dres, T* dx, float* pdw, float* pdb, void* dw, void* db, int64_t rows, int d,
-                           int P, int rows_per_wave, hipStream_t st, int wt, int wdt) {
+                           int P, int rows_per_wave, hipStream_t st, int wt, int wdt, T* dxa, const LnDrop* drop) {
+  if (drop != nullptr && (d > 2048 || dxa == nullptr)) return hipErrorInvalidValue;
   // with a bias: dγ and dβ partials interleave per block row ([P][2d]) and ONE combine writes
   // dw | db (the caller's db must directly follow dw)
   const size_t wbytes = wdt == kF32 ? 4 : 2;
@@ -522,7 +553,13 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
   const size_t lds = 2 * kWavesPerBlock * d * sizeof(float);
 #define HYP_LN_B(V)                                                                                          \
   case V:                                                                                                    \
-    if (dres)                                                                                                \
+    if (drop && dres)                                                                                        \
+      hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, true, true>), grid, block, lds, st, dy, xin, w, mean, rstd, dres, \
+                         dx, pdw, pdb, rows, d, rows_per_wave, wt, dxa, *drop);                               \
+    else if (drop)                                                                                           \
+      hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, false, true>), grid, block, lds, st, dy, xin, w, mean, rstd, dres, \
+                         dx, pdw, pdb, rows, d, rows_per_wave, wt, dxa, *drop);                               \
+    else if (dres)                                                                                           \
       hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, true>), grid, block, lds, st, dy, xin, w, mean, rstd, dres, dx, \
                          pdw, pdb, rows, d, rows_per_wave, wt);                                              \
     else                                                                                                     \
@@ -577,29 +614,48 @@ void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave) {
   if (*P < 1) *P = 1;
 }
 
+namespace {
+LnDrop make_drop(float p, const RngState& rs) {
+  LnDrop dp;
+  dp.thr = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);  // dropout.hip's threshold
+  dp.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  dp.rs = rs;
+  return dp;
+}
+}  // namespace
+
 hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
                              const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
-                             hipStream_t st, int wt) {
+                             hipStream_t st, int wt, float drop_p, const RngState* rs) {
   if (!layernorm_supported(d)) return hipErrorInvalidValue;
+  if (drop_p > 0.f && (rs == nullptr || drop_p >= 1.f)) return hipErrorInvalidValue;
+  const LnDrop dp = drop_p > 0.f ? make_drop(drop_p, *rs) : LnDrop{};
+  const LnDrop* dptr = drop_p > 0.f ? &dp : nullptr;
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (rms)
-      return ln_fwd_dispatch<T, true>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st, wt);
-    return ln_fwd_dispatch<T, false>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st, wt);
+      return ln_fwd_dispatch<T, true>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st, wt,
+                                      dptr);
+    return ln_fwd_dispatch<T, false>((const T*)x, (const T*)r, (T*)s, (T*)y, w, b, mean, rstd, rows, d, eps, st, wt,
+                                     dptr);
   });
   return hipSuccess;
 }
 
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
-                              void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt) {
+                              void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt,
+                              void* dxa, float drop_p, const RngState* rs) {
   const int wdt = wt ? dtype : kF32;  // dγ / dβ in the weight's dtype
   if (!layernorm_supported(d)) return hipErrorInvalidValue;
+  if (drop_p > 0.f && (rs == nullptr || drop_p >= 1.f || dxa == nullptr)) return hipErrorInvalidValue;
+  const LnDrop dp = drop_p > 0.f ? make_drop(drop_p, *rs) : LnDrop{};
+  const LnDrop* dptr = drop_p > 0.f ? &dp : nullptr;
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (rms)
       return ln_bwd_dispatch<T, true>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                      db, rows, d, P, rows_per_wave, st, wt, wdt);
+                                      db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr);
     return ln_bwd_dispatch<T, false>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                     db, rows, d, P, rows_per_wave, st, wt, wdt);
+                                     db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr);
   });
   return hipSuccess;
 }

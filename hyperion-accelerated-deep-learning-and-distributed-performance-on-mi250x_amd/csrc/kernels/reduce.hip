@@ -76,7 +76,11 @@ constexpr int kFinLanes = 16;
 template <typename T, int ACT>
 __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict__ dh, const T* __restrict__ z,
                                                              T* __restrict__ dy, int64_t M, int N,
-                                                             int64_t rows_per_block, float* __restrict__ part) {
+                                                             int64_t rows_per_block, float* __restrict__ part,
+                                                             uint32_t dthr, float dscale, RngState drs) {
+  // dscale != 0: dh is the gradient of dropout(act(z)); the keep mask (dropout.hip's hash) is
+  // regenerated per element and dh scaled in T first, as a separate dropout backward would store it
+  const uint64_t dkey = dscale != 0.f ? rng_key(drs) : 0;
   __shared__ float red[kRowGroups][kColThreads * 8];
   const int ct = threadIdx.x % kColThreads, rg = threadIdx.x / kColThreads;
   const int c0 = (blockIdx.y * kColThreads + ct) * 8;
@@ -87,8 +91,12 @@ __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[u][j] = 0.f;
-  auto one = [&](int64_t r, float (&a)[8], const float (&g)[8], const float (&zz)[8]) {
-    float o[8];
+  auto one = [&](int64_t r, float (&a)[8], const float (&g0)[8], const float (&zz)[8]) {
+    float o[8], g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      g[j] = dscale == 0.f ? g0[j]
+                           : (rng_u32(dkey, (uint64_t)(r * N + c0 + j)) >= dthr ? rnd<T>(g0[j] * dscale) : 0.f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float d;
@@ -224,14 +232,19 @@ hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int
 // dy = dh·act'(z) and db = Σ_rows dy (out_dtype) in two launches (act: 1 ReLU on the output, 2 GELU
 // on the pre-activation).  part: [P, N] fp32 workspace, P = colsum_partials(M, N).
 hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, void* dy, int64_t M, int N, void* db,
-                          int out_dtype, float* part, int P, hipStream_t st) {
+                          int out_dtype, float* part, int P, hipStream_t st, float drop_p,
+                          const RngState* rs) {
   if (N % 8 != 0 || M < 1 || P < 1 || (act != 1 && act != 2) || (dtype != kBF16 && dtype != kF16))
     return hipErrorInvalidValue;
   const int64_t rpb = (M + P - 1) / P;
   const dim3 grid(P, (N + kColThreads * 8 - 1) / (kColThreads * 8));
+  if (drop_p > 0.f && (rs == nullptr || drop_p >= 1.f)) return hipErrorInvalidValue;
+  const uint32_t dthr = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.f, 4294967295.f) : 0u;
+  const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 0.f;
+  const RngState drs = rs != nullptr ? *rs : RngState{};
 #define HYP_ACT_COLSUM(TT, A)                                                                                   \
   hipLaunchKernelGGL((act_bwd_colsum_k<TT, A>), grid, dim3(kThreads), 0, st, static_cast<const TT*>(dh),        \
-                     static_cast<const TT*>(z), static_cast<TT*>(dy), M, N, rpb, part)
+                     static_cast<const TT*>(z), static_cast<TT*>(dy), M, N, rpb, part, dthr, dscale, drs)
   if (dtype == kBF16) {
     if (act == 1) HYP_ACT_COLSUM(bf16_t, 1);
     else HYP_ACT_COLSUM(bf16_t, 2);

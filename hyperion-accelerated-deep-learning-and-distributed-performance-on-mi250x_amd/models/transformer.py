@@ -17,7 +17,8 @@ caller's layout (attention is independent per sequence, so ``batch_first=False``
 the view at the boundary — the reference's two ``permute`` copies per forward disappear).  The
 packed QKV projection output is viewed as ``[B, S, 3, H, Dh]`` and handed straight to the
 flash-attention kernel (``ops.attention.attention_packed``: no split/permute/contiguous), the
-residual add is fused into the LayerNorm kernel (``ops.layernorm``), and the FFN's bias+activation
+residual add AND the residual branch's dropout (``dropout1`` / ``dropout2``) are fused into the
+LayerNorm kernel (``ops.layernorm``), and the FFN's bias+activation
 rides the GEMM epilogue (``ops.linear_act``: ``torch._addmm_activation`` → hipBLASLt epilogue).
 Parameter names match ``nn.TransformerEncoderLayer`` / ``nn.TransformerEncoder`` exactly
 (``self_attn.in_proj_weight`` …, ``layers.N.…``) so reference checkpoints load unchanged.
@@ -108,17 +109,20 @@ class TransformerEncoderLayer(nn.Module):
         self.activation = activation
 
     def _ff(self, x: torch.Tensor) -> torch.Tensor:
-        return self.linear2(self.dropout(self.linear1(x)))
+        # the inner dropout rides linear1's epilogue (forward) and its activation backward
+        return self.linear2(self.linear1(x, dropout_p=self.dropout.p if self.training else 0.0))
 
     def forward(self, x: torch.Tensor, causal: bool = False,
                 key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if self.norm_first:
             x = x + self.dropout1(self.self_attn(self.norm1(x), causal, key_padding_mask))
             return x + self.dropout2(self._ff(self.norm2(x)))
-        a = self.dropout1(self.self_attn(x, causal, key_padding_mask))
-        x = self.norm1(a, residual=x)  # LN(x + attn) in one kernel
-        f = self.dropout2(self._ff(x))
-        return self.norm2(f, residual=x)
+        # LN(x + dropout(branch)) in one kernel each: the residual branches' dropouts ride the norms
+        # (mask regenerated in the LN forward and backward kernels: no dropout launch, no mask tensor)
+        p1 = self.dropout1.p if self.training else 0.0
+        p2 = self.dropout2.p if self.training else 0.0
+        x = self.norm1(self.self_attn(x, causal, key_padding_mask), residual=x, dropout_p=p1)
+        return self.norm2(self._ff(x), residual=x, dropout_p=p2)
 
 
 class TransformerEncoder(nn.Module):

@@ -90,9 +90,11 @@ def _pick(key: Tuple, K: int, native_fn, vendor_fn) -> Optional[Tuple[int, int]]
 
 
 def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: Optional[str] = None,
-          aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+          aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, dropout_p: float = 0.0,
+          rng: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
     """``act(x Wᵀ + bias) (+ residual)`` with ``aux`` = pre-activation, or None when the vendor path
-    should run (the caller keeps its own fallback)."""
+    should run (the caller keeps its own fallback).  ``dropout_p`` (with ``act``): the output is
+    ``dropout(act(...))`` with the mask of the ``rng`` record (the FFN's inner dropout in the epilogue)."""
     if not _ok(x, w) or x.shape[1] % 8 or w.shape[0] % 4:
         return None
     if residual is not None and (residual.dtype != x.dtype or residual.stride(1) != 1 or residual.stride(0) % 4):
@@ -102,10 +104,11 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
         return None
     C = _native.native()
     a = ACTS[act]
-    key = ("nt", x.shape[0], w.shape[0], x.shape[1], a, bias is not None, residual is not None)
+    key = ("nt", x.shape[0], w.shape[0], x.shape[1], a, bias is not None, residual is not None, dropout_p > 0)
 
     def nat(tile=-1, splits=-1):
-        return C.gemm(x, w, bias=bias, act=a, aux=aux, residual=residual, tile=tile, splits=splits)
+        return C.gemm(x, w, bias=bias, act=a, aux=aux, residual=residual, tile=tile, splits=splits,
+                      drop_p=dropout_p, rng=rng)
 
     def ven():
         y = torch.addmm(bias.to(x.dtype), x, w.t()) if bias is not None else x @ w.t()
@@ -113,6 +116,8 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
             y = torch.relu(y)
         elif a >= 2:
             y = torch.nn.functional.gelu(y, approximate="tanh" if a == 3 else "none")
+        if dropout_p > 0:
+            y = C.dropout(y, dropout_p, rng)
         return y + residual if residual is not None else y
 
     c = _pick(key, x.shape[1], nat, ven)

@@ -6,7 +6,11 @@ CustomTransformer ``baseline_performance.ipynb:238-249``) and HF Llama's RMSNorm
 
 ``layer_norm(x, weight, bias, eps, residual=r)`` computes ``LN(x + r)`` in one pass (post-norm:
 ``norm(x + dropout(sublayer(x)))``); ``return_sum=True`` also returns ``x + r`` (pre-norm residual
-stream, Llama).  Modules keep ``nn.LayerNorm`` state-dict keys.
+stream, Llama).  ``dropout_p > 0`` (training, with a residual) fuses the residual branch's dropout:
+``LN(r + dropout(x))`` with the counter-based mask of ``ops.dropout`` regenerated in the kernel, and
+the backward writes the dropped input's gradient ``dropout(ds)`` beside ``ds`` — the two standalone
+dropout passes per norm disappear (SURVEY §2.4 LayerNorm / dropout rows).  Modules keep
+``nn.LayerNorm`` state-dict keys.
 """
 from __future__ import annotations
 
@@ -21,7 +25,9 @@ from . import _native
 _SUPPORTED_D = lambda d: d % 8 == 0 and d <= 4096 and ((d + 511) // 512 <= 4 or (d + 511) // 512 == 8)  # noqa: E731
 
 
-def _ref(x, residual, weight, bias, eps, rms):
+def _ref(x, residual, weight, bias, eps, rms, dropout_p=0.0):
+    if dropout_p > 0.0:
+        x = F.dropout(x, dropout_p, True)
     s = x if residual is None else x + residual
     if rms:
         sf = s.float()
@@ -36,14 +42,18 @@ def _ref(x, residual, weight, bias, eps, rms):
 
 class _LNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum):
+    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum, dropout_p=0.0):
         C = _native.native()
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous().to(x.dtype)
-        y, s, mean, rstd = C.ln_fwd(x, residual, weight, bias, eps, rms)
+        st = _native.rng_state(x.device) if dropout_p > 0.0 else None
+        if st is not None:
+            _native.count("ln_dropout")
+        y, s, mean, rstd = C.ln_fwd(x, residual, weight, bias, eps, rms, dropout_p, st)
         xin = s if residual is not None else x
         ctx.rms = rms
+        ctx.drop = (dropout_p, st)
         ctx.has_res = residual is not None
         ctx.save_for_backward(xin, weight, mean, rstd)
         if return_sum:
@@ -55,13 +65,14 @@ class _LNFn(torch.autograd.Function):
         xin, weight, mean, rstd = ctx.saved_tensors
         need_dw = weight is not None and ctx.needs_input_grad[2]
         need_db = ctx.needs_input_grad[3]
-        dx, dw, db = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms)
+        p, st = ctx.drop
+        dx, dw, db, dxa = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms, p, st)
         return (
-            dx,
+            dxa if p > 0.0 else dx,  # the dropped input's gradient: dropout(ds) with the forward's mask
             dx if ctx.has_res and ctx.needs_input_grad[1] else None,
             dw if need_dw else None,
             db if need_db else None,
-            None, None, None,
+            None, None, None, None,
         )
 
 
@@ -73,7 +84,10 @@ def layer_norm(
     residual: Optional[torch.Tensor] = None,
     rms: bool = False,
     return_sum: bool = False,
+    dropout_p: float = 0.0,
 ) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
+    """``LN(x + residual)`` (or RMSNorm); ``dropout_p``: ``LN(residual + dropout(x))`` — pass it only
+    in training (it is applied whenever > 0)."""
     d = x.shape[-1]
     # the kernels take fp32 affine parameters or parameters in the activation dtype (a model cast
     # wholesale to bf16: FSDP mixed precision, HF-style Llama) — read as such, dγ / dβ returned in it;
@@ -89,24 +103,27 @@ def layer_norm(
         and _SUPPORTED_D(d)
         and all(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in (weight, bias))
         and (residual is None or residual.shape == x.shape)
+        and (dropout_p == 0.0 or (residual is not None and d <= 2048 and dropout_p < 1.0))
     )
     if native:
-        if x.dtype != torch.float32 and torch.is_autocast_enabled():
-            pass  # keep activation dtype; params stay fp32 inside the kernel
-        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum)
-    y, s = _ref(x, residual, weight, bias, eps, rms)
+        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum, float(dropout_p))
+    y, s = _ref(x, residual, weight, bias, eps, rms, dropout_p)
     return (y, s) if return_sum else y
 
 
 class LayerNorm(nn.LayerNorm):
     """``nn.LayerNorm`` (same keys) with an optional fused residual input."""
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:  # type: ignore[override]
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,  # type: ignore[override]
+                dropout_p: float = 0.0) -> torch.Tensor:
+        """``LN(x + residual)``; ``dropout_p`` > 0: ``LN(residual + dropout(x))`` (post-norm branch)."""
         if len(self.normalized_shape) != 1:
+            if dropout_p > 0.0:
+                x = F.dropout(x, dropout_p, True)
             return super().forward(x if residual is None else x + residual)
         if torch.is_autocast_enabled() and x.dtype == torch.float32 and residual is not None:
             residual = residual.float()
-        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual)
+        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual, dropout_p=dropout_p)
 
 
 class RMSNorm(nn.Module):

@@ -28,14 +28,18 @@ from .gemm import mm_nn, mm_nt
 from .linear import bias_grad, linear_wgrad
 
 
-def _act_bwd(dh: torch.Tensor, z: torch.Tensor, act: str, bdt: torch.dtype, need_b: bool):
+def _act_bwd(dh: torch.Tensor, z: torch.Tensor, act: str, bdt: torch.dtype, need_b: bool, drop=(0.0, None)):
     """(dy, db): the activation backward and, when needed, the bias gradient — one native pass
-    (``reduce.hip`` act_bwd_colsum) on gfx950, else autograd's ops."""
+    (``reduce.hip`` act_bwd_colsum) on gfx950, else autograd's ops.  ``drop`` = (p, rng record): dh
+    is the gradient of dropout(act(z)); the mask is regenerated in the same pass."""
+    p, st = drop
     if (z.is_cuda and z.dtype in (torch.bfloat16, torch.float16) and z.shape[-1] % 8 == 0 and z.is_contiguous()
             and _native.use_native(z, op="act_bwd")):
         _native.count("act_bwd_colsum")
-        dy, db = _native.native().act_bwd_colsum(dh.contiguous(), z, 1 if act == "relu" else 2, bdt)
+        dy, db = _native.native().act_bwd_colsum(dh.contiguous(), z, 1 if act == "relu" else 2, bdt, p, st)
         return dy, (db if need_b else None)
+    if p > 0.0:
+        dh = _native.native().dropout(dh.contiguous(), p, st)
     if act == "relu":
         dy = torch.ops.aten.threshold_backward(dh, z, 0)
     else:
@@ -52,65 +56,84 @@ def _cdt(x: torch.Tensor) -> torch.dtype:
     return torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else x.dtype
 
 
+def _drop_state(x: torch.Tensor, p: float):
+    return (p, _native.rng_state(x.device)) if p > 0.0 else (0.0, None)
+
+
 class _LinearReLU(torch.autograd.Function):
+    """``dropout(relu(x Wᵀ + b))`` (p may be 0): bias + ReLU (+ dropout) in the GEMM epilogue; the
+    backward masks with the saved OUTPUT (kept elements: h·scale > 0 ⇔ z > 0; dropped: gradient 0)."""
+
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, p=0.0):
         dt = _cdt(x)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).to(dt)
         wc, bc = w.to(dt), b.to(dt)
-        h = mm_nt(x2, wc, bias=b, act="relu") if x2.is_cuda else None
+        drop = _drop_state(x2, p)
+        h = mm_nt(x2, wc, bias=b, act="relu", dropout_p=drop[0], rng=drop[1]) if x2.is_cuda else None
         if h is None:
             h = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
+            if drop[0] > 0.0:
+                h = _native.native().dropout(h, drop[0], drop[1])
         ctx.save_for_backward(x2, wc, h)
         ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
+        ctx.drop = drop
         return h.view(*shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dh):
         x2, wc, h = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
-        dy, db = _act_bwd(dh.reshape(h.shape).to(h.dtype), h, "relu", bdt, ctx.needs_input_grad[2])
+        dy, db = _act_bwd(dh.reshape(h.shape).to(h.dtype), h, "relu", bdt, ctx.needs_input_grad[2], ctx.drop)
         dx = _dgrad(dy, wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _LinearGELU(torch.autograd.Function):
     """``gelu(x Wᵀ + b)``: bias in the GEMM epilogue, the pre-activation kept for backward."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, p=0.0):
         dt = _cdt(x)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).to(dt)
         wc, bc = w.to(dt), b.to(dt)
+        drop = _drop_state(x2, p)
         y = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=dt) if x2.is_cuda else None
-        h = mm_nt(x2, wc, bias=b, act="gelu", aux=y) if x2.is_cuda else None
+        h = mm_nt(x2, wc, bias=b, act="gelu", aux=y, dropout_p=drop[0], rng=drop[1]) if x2.is_cuda else None
         if h is None:
             y = torch.addmm(bc, x2, wc.t())
             h = F.gelu(y)
+            if drop[0] > 0.0:
+                h = _native.native().dropout(h, drop[0], drop[1])
         ctx.save_for_backward(x2, wc, y)
         ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
+        ctx.drop = drop
         return h.view(*shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dh):
         x2, wc, y = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
-        dy, db = _act_bwd(dh.reshape(y.shape).to(y.dtype), y, "gelu", bdt, ctx.needs_input_grad[2])
+        dy, db = _act_bwd(dh.reshape(y.shape).to(y.dtype), y, "gelu", bdt, ctx.needs_input_grad[2], ctx.drop)
         dx = _dgrad(dy, wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
-    if activation == "relu" and x.is_cuda and b is not None:
-        return _LinearReLU.apply(x, w, b)
-    if activation == "gelu" and x.is_cuda and b is not None:
-        return _LinearGELU.apply(x, w, b)
+def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str,
+               dropout_p: float = 0.0) -> torch.Tensor:
+    """``dropout(act(x Wᵀ + b))`` — pass ``dropout_p`` only in training (applied whenever > 0)."""
+    native_drop = dropout_p == 0.0 or (x.is_cuda and _native.use_native(x, op="dropout") and dropout_p < 1.0)
+    if activation == "relu" and x.is_cuda and b is not None and native_drop:
+        return _LinearReLU.apply(x, w, b, float(dropout_p))
+    if activation == "gelu" and x.is_cuda and b is not None and native_drop:
+        return _LinearGELU.apply(x, w, b, float(dropout_p))
     y = F.linear(x, w, b)
-    return F.gelu(y) if activation == "gelu" else F.relu(y)
+    y = F.gelu(y) if activation == "gelu" else F.relu(y)
+    return F.dropout(y, dropout_p, True) if dropout_p > 0.0 else y
 
 
 class LinearAct(torch.nn.Linear):
@@ -123,5 +146,5 @@ class LinearAct(torch.nn.Linear):
         super().__init__(in_features, out_features, bias=bias, **kw)
         self.activation = activation
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
-        return linear_act(x, self.weight, self.bias, self.activation)
+    def forward(self, x: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:  # type: ignore[override]
+        return linear_act(x, self.weight, self.bias, self.activation, dropout_p)

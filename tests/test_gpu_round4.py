@@ -150,3 +150,117 @@ def test_strided_conv_bn_act_leaf_input_matches_fp32():
                      b2.bias.detach().cpu(), True)
     y.backward(g.float().cpu())
     torch.testing.assert_close(x.grad.float().cpu(), xr.grad, rtol=3e-2, atol=3e-2 * xr.grad.abs().max().item())
+
+
+# ---- dropout fused into LayerNorm (residual branch) and into the FFN's GEMM epilogue / act backward
+def _same_state(fn_fused, fn_unfused):
+    """Run both with the default generator in the same state (the fused op draws one rng record,
+    the unfused composition draws the identical record for its dropout)."""
+    g = torch.cuda.default_generators[torch.cuda.current_device()]
+    st = g.get_state()
+    a = fn_fused()
+    g.set_state(st)
+    b = fn_unfused()
+    return a, b
+
+
+@pytest.mark.parametrize("d", [256, 512, 768])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_layernorm_dropout_fused_matches_unfused(d, dt):
+    from hyperion.ops import _native
+    from hyperion.ops.dropout import dropout
+    from hyperion.ops.layernorm import layer_norm
+
+    torch.manual_seed(0)
+    p = 0.1
+    x0 = torch.randn(4, 37, d, device="cuda").to(dt)
+    r0 = torch.randn(4, 37, d, device="cuda").to(dt)
+    w = (torch.rand(d, device="cuda") + 0.5).requires_grad_(True)
+    b = (torch.randn(d, device="cuda") * 0.1).requires_grad_(True)
+    g = torch.randn(4, 37, d, device="cuda").to(dt)
+
+    def run(fused):
+        x = x0.clone().requires_grad_(True)
+        r = r0.clone().requires_grad_(True)
+        w.grad = b.grad = None
+        if fused:
+            y = layer_norm(x, w, b, 1e-5, residual=r, dropout_p=p)
+        else:
+            y = layer_norm(dropout(x, p), w, b, 1e-5, residual=r)
+        y.backward(g)
+        return y.float(), x.grad.float(), r.grad.float(), w.grad.clone(), b.grad.clone()
+
+    _native.reset_counters()
+    fu, un = _same_state(lambda: run(True), lambda: run(False))
+    assert _native.counters().get("ln_dropout") == 1 and _native.counters().get("dropout") == 1
+    for a, c in zip(fu, un):
+        torch.testing.assert_close(a, c, rtol=1e-2, atol=1e-2)
+    frac = (fu[1] == 0).float().mean().item()  # dropped elements get no gradient
+    assert 0.05 < frac < 0.15, frac
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+@pytest.mark.parametrize("force", ["native", "vendor"])
+def test_linear_act_dropout_fused_matches_unfused(act, force):
+    from hyperion.ops import gemm
+    from hyperion.ops.dropout import dropout
+    from hyperion.ops.linear_act import linear_act
+
+    torch.manual_seed(0)
+    p = 0.1
+    gemm.set_mode(force)
+    try:
+        x0 = torch.randn(512, 256, device="cuda").bfloat16()
+        w = (torch.randn(1024, 256, device="cuda") * 0.05).requires_grad_(True)
+        b = (torch.randn(1024, device="cuda") * 0.1).requires_grad_(True)
+        g = torch.randn(512, 1024, device="cuda").bfloat16()
+
+        def run(fused):
+            x = x0.clone().requires_grad_(True)
+            w.grad = b.grad = None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                if fused:
+                    h = linear_act(x, w, b, act, dropout_p=p)
+                else:
+                    h = dropout(linear_act(x, w, b, act), p)
+            h.backward(g)
+            return h.float(), x.grad.float(), w.grad.clone(), b.grad.clone()
+
+        fu, un = _same_state(lambda: run(True), lambda: run(False))
+    finally:
+        gemm.set_mode("auto")
+    for a, c in zip(fu, un):
+        torch.testing.assert_close(a, c, rtol=2e-2, atol=2e-2 * max(1.0, c.abs().max().item()))
+
+
+def test_fused_dropout_masks_regenerate_under_graph_replay():
+    """A captured post-norm encoder layer (LN + FFN dropouts fused) draws a fresh mask on every
+    replay, and no standalone dropout kernel is left in the layer."""
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    layer = TransformerEncoderLayer(256, 4, 1024, dropout=0.1).cuda().train()
+    x = torch.randn(8, 64, 256, device="cuda")
+    _native.reset_counters()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        layer(x)
+    cnt = _native.counters()
+    assert cnt.get("ln_dropout") == 2 and "dropout" not in cnt, cnt
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.autocast("cuda", dtype=torch.bfloat16):
+        layer(x)
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr), torch.autocast("cuda", dtype=torch.bfloat16):
+        out = layer(x)
+    gr.replay()
+    a = out.clone()
+    gr.replay()
+    b = out.clone()
+    assert not torch.equal(a, b)  # fresh masks per replay
+    layer.eval()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        e1, e2 = layer(x), layer(x)
+    assert torch.equal(e1, e2)  # eval: no dropout
