@@ -176,7 +176,8 @@ def _ensure_pg() -> None:
 
 
 def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps: int = 10, warmup: int = 3,
-                    graph: bool = False, replicate_frozen="auto", persistent=None) -> Dict:
+                    graph: bool = False, replicate_frozen="auto", persistent=None,
+                    collectives_at_world_1: bool = False) -> Dict:
     """One FSDP FULL_SHARD training step exactly as the FSDP trainers run it (C25 / BASELINE config
     4 / C26): Hyperion's FSDP over the native RCCL communicator, bf16 mixed precision (param /
     reduce / buffer), FusedAdamW, global-norm clip 1.0.  ``model``: ``lm256`` (size-based wrap,
@@ -215,7 +216,7 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
         vocab = 50257
     m = FSDP(base, auto_wrap_policy=policy, device_id=dev, mixed_precision=MixedPrecision(bf, bf, bf),
              replicate_frozen=replicate_frozen if model == "llama7b_lora" else False,
-             persistent=True if graph else persistent)
+             persistent=True if graph else persistent, collectives_at_world_1=collectives_at_world_1)
     params = [p for p in m.parameters() if p.requires_grad]
     opt = FusedAdam(params, lr=1e-4, weight_decay=0.01, adamw=True)
     ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=dist.get_rank())
@@ -247,6 +248,8 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
     world = dist.get_world_size()
     tok = batch * (seq if model == "llama7b_lora" else seq - 1)
     return {"model": model, "fsdp": True, "world": world, "graph": graph, "persistent": m.persistent,
+            "persistent_reason": m.persistent_reason, "collectives_at_world_1": collectives_at_world_1,
+            "comm": type(m.comm).__name__,
             "replicate_frozen": m.replicate_frozen,
             "segments": seg.seg.num_segments if seg is not None and seg.seg is not None else 0,
             "batch_per_gpu": batch, "seq": seq, "ms_per_step": t * 1e3,

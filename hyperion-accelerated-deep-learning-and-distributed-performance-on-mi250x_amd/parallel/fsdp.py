@@ -38,6 +38,7 @@ collectives over the 7 xGMI links reach their bus bandwidth.
 """
 from __future__ import annotations
 
+import logging
 import math
 from dataclasses import dataclass
 from typing import Callable, Dict, Iterable, Iterator, List, Optional, Sequence, Set, Tuple, Type
@@ -50,7 +51,9 @@ from ..ops import streams as _streams
 from ..ops.conv import flush_wgrad as _flush_wgrad
 from ..ops.optim import clip_grad_norm_
 from ..train import segments as _seg
-from .comm import get_comm
+from .comm import NativeComm, get_comm
+
+log = logging.getLogger("hyperion.fsdp")
 
 
 # ------------------------------------------------------------------------------------ policies
@@ -145,7 +148,7 @@ class _FlatGroup:
         # resident: a frozen group kept whole on every rank (FSDP(replicate_frozen=...)): never
         # gathered, never freed — the base weights of a LoRA fine-tune fit 288 GB of HBM many times
         # (at world 1 every frozen group is resident: its one shard IS the full tensor — no copy)
-        self.resident = (not trainable) and (fsdp.replicate_frozen or fsdp.world == 1)
+        self.resident = (not trainable) and (fsdp.replicate_frozen or fsdp.identity)
         W, r = (1, 0) if self.resident else (fsdp.world, fsdp.rank)
         # shards of a multiple of 64 elements: every rank's slice of the gathered buffer (and every
         # reduce-scatter output) starts 128-byte aligned for RCCL and the vector kernels
@@ -211,7 +214,7 @@ class _FlatGroup:
         st = self.full.untyped_storage()
         if st.nbytes() != self._full_bytes:
             st.resize_(self._full_bytes)
-        if self.fsdp.world == 1:  # identity gather: one cast-copy of the shard, no staging buffer
+        if self.fsdp.identity:  # world 1: one cast-copy of the shard, no staging buffer
             with torch.no_grad():
                 self.full.data.copy_(self.flat_param.detach())
             self.gathered = True
@@ -289,7 +292,7 @@ class _FlatGroup:
         for i, (o, n) in enumerate(zip(self.offsets, self.numels)):
             if i not in self.grad_ready:  # unused this step: contributes zeros
                 buf[o : o + n].zero_()
-        if self.fsdp.world == 1:
+        if self.fsdp.identity:
             self.rs_out, self.rs_work = buf, None
             return
         # AVG in RCCL; the output lands in a persistent buffer — straight in the fp32 shard
@@ -308,7 +311,7 @@ class _FlatGroup:
             self.rs_work.wait()
             self.rs_work = None
         g = self.rs_out
-        if self.fsdp.world == 1:  # rs_out is the full flat gradient buffer (released below)
+        if self.fsdp.identity:  # rs_out is the full flat gradient buffer (released below)
             g = g[: self.shard_numel]
         with torch.no_grad():
             if self.flat_param.grad is None:
@@ -401,7 +404,11 @@ class FullyShardedDataParallel(nn.Module):
         comm=None,
         replicate_frozen=False,
         persistent=None,
+        collectives_at_world_1: bool = False,
     ):
+        """collectives_at_world_1: on a single rank, still run every gather / reduce-scatter as a
+        collective (the native RCCL communicator on GPU) instead of the identity copies — the
+        multi-GPU transport path, exercised and timed on one device."""
         super().__init__()
         if sharding_strategy not in ("FULL_SHARD", "SHARD_GRAD_OP"):
             raise ValueError("sharding_strategy must be FULL_SHARD or SHARD_GRAD_OP (NO_SHARD = use DDP)")
@@ -413,6 +420,15 @@ class FullyShardedDataParallel(nn.Module):
         if device_id is None:
             device_id = next((p.device for p in module.parameters()), torch.device("cpu"))
         self.device = torch.device(device_id)
+        # identity: world 1 with the collectives elided (a gather is one cast-copy, a reduce-scatter
+        # nothing); collectives_at_world_1 keeps them, over RCCL when a process group exists on GPU
+        self.identity = self.world == 1 and not collectives_at_world_1
+        if (collectives_at_world_1 and self.world == 1 and comm is None and self.device.type == "cuda"
+                and dist.is_available() and dist.is_initialized()):
+            from ..ops import _native
+
+            if _native.available():
+                self._comm = NativeComm(self.device, process_group)
         module.to(self.device)
         self.mp = mixed_precision or MixedPrecision()
         # replicate_frozen: frozen (requires_grad=False) parameters stay whole on every rank in the
@@ -432,13 +448,23 @@ class FullyShardedDataParallel(nn.Module):
         # memory-for-traffic trade 288 GB of HBM affords for the models here, and it makes the step
         # capturable (train/segments.py).  "auto"/None: on GPU when every unit's full parameters +
         # gradients take at most a quarter of the device memory.
+        self.persistent_reason = "requested" if persistent is True else "off"
         if persistent is None or persistent == "auto":
             if self.device.type == "cuda":
                 need = sum(p.numel() for p in module.parameters()) * (
                     torch.finfo(self.mp.param_dtype or torch.float32).bits // 8 + 4)
-                persistent = need <= torch.cuda.get_device_properties(self.device).total_memory // 4
+                cap = torch.cuda.get_device_properties(self.device).total_memory
+                persistent = need <= cap // 4
+                self.persistent_reason = (f"auto: full params + grads {need / 2**30:.2f} GiB "
+                                          f"{'<=' if persistent else '>'} a quarter of {cap / 2**30:.0f} GiB")
+                if persistent and sharding_strategy == "FULL_SHARD":
+                    # FULL_SHARD semantics change (no reshard after forward): say so, once per wrapper
+                    log.warning("FSDP persistent=%s: FULL_SHARD keeps gathered parameters resident between "
+                                "forward and backward (%s); pass persistent=False for reshard-after-forward",
+                                persistent, self.persistent_reason)
             else:
                 persistent = False
+                self.persistent_reason = "auto: not a GPU device"
         self.persistent = bool(persistent)
         self.sharding = sharding_strategy
         self.reshard_after_forward = sharding_strategy == "FULL_SHARD" and not self.persistent

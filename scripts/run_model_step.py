@@ -8,9 +8,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hyperion.bench import models as M  # noqa: E402
 
 which = sys.argv[1]
-if which == "fsdp":  # fsdp <lm256|gpt2_small|llama7b_lora> [graph] [shardbase]
+if which == "fsdp":  # fsdp <lm256|gpt2_small|llama7b_lora> [graph] [shardbase] [coll] [reshard]
     model = sys.argv[2]
-    kw = dict(graph="graph" in sys.argv[3:])
+    kw = dict(graph="graph" in sys.argv[3:], collectives_at_world_1="coll" in sys.argv[3:])
+    if "reshard" in sys.argv[3:]:
+        kw["persistent"] = False
     if "shardbase" in sys.argv[3:]:
         kw["replicate_frozen"] = False
     if model == "gpt2_small":
@@ -36,4 +38,8 @@ elif which == "lm":
     r = M.bench_lm_step(precision="bf16", steps=5, warmup=3)
 else:
     r = M.bench_lm_step(precision="bf16", graph=True, model="gpt2_small", batch=16, steps=10, warmup=3)
+if which in ("gpt2", "lmgraph", "lm", "vit", "vitgraph"):
+    from hyperion.ops import gemm as _gemm
+
+    r["gemm_choices"] = {"x".join(map(str, k)): v for k, v in _gemm.choices().items()}
 print(json.dumps(r), flush=True)

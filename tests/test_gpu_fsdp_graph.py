@@ -27,7 +27,7 @@ def _lm(seed=0):
                                causal=True).cuda()
 
 
-def _fsdp_run(steps, graphed, seed=0, rank=0):
+def _fsdp_run(steps, graphed, seed=0, rank=0, coll=False):
     from hyperion.models.transformer import TransformerEncoderLayer
     from hyperion.ops.optim import FusedAdam
     from hyperion.parallel.fsdp import FSDP, MixedPrecision, transformer_auto_wrap_policy
@@ -35,7 +35,8 @@ def _fsdp_run(steps, graphed, seed=0, rank=0):
 
     bf = torch.bfloat16
     m = FSDP(_lm(seed), auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}),
-             device_id=torch.device("cuda", 0), mixed_precision=MixedPrecision(bf, bf, bf), persistent=True)
+             device_id=torch.device("cuda", 0), mixed_precision=MixedPrecision(bf, bf, bf), persistent=True,
+             collectives_at_world_1=coll)
     opt = FusedAdam(list(m.parameters()), lr=1e-3, weight_decay=0.01, adamw=True)
     g = torch.Generator(device="cuda").manual_seed(7 + rank)
     data = [torch.randint(0, 512, (4, 33), device="cuda", generator=g) for _ in range(steps)]
@@ -69,7 +70,8 @@ def _fsdp_run(steps, graphed, seed=0, rank=0):
         nseg = 0
     torch.cuda.synchronize()
     full = m.full_state_dict(rank0_only=False, offload_to_cpu=True)
-    return {"losses": losses, "params": {k: v.float() for k, v in full.items()}, "segments": nseg}
+    return {"losses": losses, "params": {k: v.float() for k, v in full.items()}, "segments": nseg,
+            "comm": type(m.comm).__name__, "identity": m.identity}
 
 
 def test_fsdp_segmented_capture_matches_eager_one_rank():
@@ -77,6 +79,32 @@ def test_fsdp_segmented_capture_matches_eager_one_rank():
     a = _fsdp_run(4, graphed=True)
     b = _fsdp_run(4, graphed=False)
     assert a["segments"] >= 1
+    for k in b["params"]:
+        torch.testing.assert_close(a["params"][k], b["params"][k], rtol=2e-2, atol=2e-3)
+
+
+def test_fsdp_native_collectives_at_world_1_segmented_matches_eager():
+    """collectives_at_world_1: the gathers / reduce-scatters run over the native RCCL communicator
+    on one GPU (a real collective, not the identity copy) inside the segmented capture, and the
+    captured steps match the eager identity schedule."""
+    import socket
+
+    import torch.distributed as dist
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    os.environ["HYPERION_COMM"] = "native"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        a = _fsdp_run(4, graphed=True, coll=True)
+        b = _fsdp_run(4, graphed=False)
+    finally:
+        dist.destroy_process_group()
+        os.environ["HYPERION_COMM"] = "torch"
+    assert a["comm"] == "NativeComm" and not a["identity"] and b["identity"]
+    assert a["segments"] > 1  # the RCCL collectives are eager holes between captured segments
     for k in b["params"]:
         torch.testing.assert_close(a["params"][k], b["params"][k], rtol=2e-2, atol=2e-3)
 
