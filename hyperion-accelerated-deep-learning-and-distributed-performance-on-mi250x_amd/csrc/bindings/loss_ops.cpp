@@ -8,7 +8,8 @@ namespace {
 // logits [N, V] (row stride ld >= V, unit column stride) is overwritten with dlogits when
 // write_grad.  Returns (loss_rows [N] fp32, lse [N] fp32).
 std::vector<at::Tensor> ce_fwd_bwd(at::Tensor& logits, const at::Tensor& target, const c10::optional<at::Tensor>& scale,
-                                   double scale_mul, int64_t ignore_index, bool write_grad) {
+                                   double scale_mul, int64_t ignore_index, bool write_grad,
+                                   const c10::optional<at::Tensor>& bias) {
   HYP_CHECK_CUDA_TENSOR(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "ce_fwd_bwd: logits must be [N, V] with unit column stride");
   TORCH_CHECK(target.dim() == 1 && target.size(0) == logits.size(0) && target.scalar_type() == at::kLong &&
@@ -18,6 +19,10 @@ std::vector<at::Tensor> ce_fwd_bwd(at::Tensor& logits, const at::Tensor& target,
     TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->device() == logits.device(),
                 "ce_fwd_bwd: scale must be a 1-element fp32 device tensor");
   TORCH_CHECK(logits.size(1) < (int64_t)INT32_MAX, "ce_fwd_bwd: V too large");
+  if (bias.has_value() && bias->defined())
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == logits.size(1) &&
+                    bias->device() == logits.device() && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0,
+                "ce_fwd_bwd: bias must be a contiguous, 16-byte aligned fp32 [V] on the logits device");
   const at::DeviceGuard guard(logits.device());
   auto fopt = logits.options().dtype(at::kFloat);
   auto loss = at::empty({logits.size(0)}, fopt);
@@ -25,7 +30,7 @@ std::vector<at::Tensor> ce_fwd_bwd(at::Tensor& logits, const at::Tensor& target,
   HYP_CHECK_HIP(hyp::cross_entropy_fwd_bwd(dtype_code(logits), logits.data_ptr(), logits.size(0), (int)logits.size(1),
                                            logits.stride(0), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
                                            lse.data_ptr<float>(), ptr_or_null<float>(scale), (float)scale_mul,
-                                           ignore_index, write_grad ? 1 : 0, cur_stream()));
+                                           ignore_index, write_grad ? 1 : 0, cur_stream(), ptr_or_null<float>(bias)));
   return {loss, lse};
 }
 
@@ -65,7 +70,7 @@ void register_loss_ops(pybind11::module& m) {
   m.def("embedding_bwd", &embedding_bwd, "dense embedding gradient (fp32 atomic accumulate + cast)");
   m.def("ce_fwd_bwd", &ce_fwd_bwd, "in-place softmax cross-entropy forward+backward", pybind11::arg("logits"),
         pybind11::arg("target"), pybind11::arg("scale"), pybind11::arg("scale_mul"), pybind11::arg("ignore_index"),
-        pybind11::arg("write_grad"));
+        pybind11::arg("write_grad"), pybind11::arg("bias") = pybind11::none());
 }
 
 }  // namespace hypbind

@@ -110,10 +110,11 @@ namespace hyp {
 // ---- cross_entropy.hip -----------------------------------------------------------------------
 // In-place softmax-CE fwd+bwd over [rows, V] logits with leading dimension ld (elements).
 // loss_rows[r] = lse - z[target] (0 for ignored rows); if write_grad, z <- (softmax - onehot) *
-// (*scale_ptr) * scale_mul (rows with an ignored target get 0).
+// (*scale_ptr) * scale_mul (rows with an ignored target get 0).  bias (fp32 [V], 16-byte aligned,
+// optional): the logits are z + bias (the LM head's bias added here instead of in the GEMM).
 hipError_t cross_entropy_fwd_bwd(int dtype, void* logits, int64_t rows, int V, int64_t ld, const int64_t* target,
                                  float* loss_rows, float* lse, const float* scale_ptr, float scale_mul,
-                                 int64_t ignore_index, int write_grad, hipStream_t st);
+                                 int64_t ignore_index, int write_grad, hipStream_t st, const float* bias = nullptr);
 }  // namespace hyp
 
 namespace hyp {

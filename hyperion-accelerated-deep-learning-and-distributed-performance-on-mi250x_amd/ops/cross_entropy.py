@@ -5,8 +5,20 @@ every LM trainer (``02_development/distributed_utils.py:161,175-177``, ``core_fr
 243-262``, ``mixed_precision.ipynb:121-145``) — the logits GEMM dominates LM compute (≈105 GFLOP
 forward at 4064 tokens) and PyTorch materialises fp32 log-softmax and its gradient.
 
-Hyperion computes the loss AND all three gradients inside the forward, without ever storing the
-[N, V] logits (gfx950, bf16/f16, E % 64 == 0):
+Hyperion computes the loss AND all three gradients inside the forward.  Two schedules (gfx950,
+bf16/f16):
+
+**Materialised** (default while the [N, V] logits take at most HYPERION_CE_MATERIALIZE_MB,
+8 GiB — GPT-2 b16: 206 MB, LM-256 b32: 408 MB of a 288 GB device): the logits GEMM writes bf16
+logits once (hipBLASLt, rows padded to a multiple of 8 classes so every row is 16-byte aligned);
+ce_fwd_bwd (cross_entropy.hip, the register-resident variant: one read + one write per
+logit) adds the bias, takes the loss and overwrites the logits with dz in place; then
+dX = dz W on the tiled MFMA kernel with split-K (ops.gemm.mm_nn on the 64-aligned class
+range, the odd tail as a rank-17 update), dW = dzᵀ X on hipBLASLt and db as column sums.
+Three GEMMs instead of four (no logits recompute): 0.66 vs 1.30 ms for GPT-2-small b16 and
+0.68 vs 1.48 ms for LM-256 b32 (scripts/ce_bench.py, profiles/r04/ce_bench_lm_head.json).
+
+**No-logits** (above that budget; never stores the [N, V] logits, E % 64 == 0):
 
 1. ``linear_ce_lse`` — the logits GEMM on the MFMA implicit-GEMM kernel with a log-sum-exp
    epilogue (``conv_igemm.hip`` EPI 1): every 128 x 64 tile reduces its accumulators to per-row
@@ -40,6 +52,8 @@ DEFAULT_MAX_LOGITS_BYTES = 4 << 30
 # larger chunks keep the dX / dW GEMMs efficient).  HYPERION_CE_CHUNK forces a class count.
 CE_BLOCK_BYTES = int(os.environ.get("HYPERION_CE_BLOCK_MB", "256")) << 20
 CE_CHUNK = int(os.environ.get("HYPERION_CE_CHUNK", "0"))
+# logits budget of the materialised schedule (module docstring); 0 forces the no-logits schedule
+CE_MATERIALIZE_BYTES = int(os.environ.get("HYPERION_CE_MATERIALIZE_MB", "8192")) << 20
 
 
 def _ce_chunk(N: int, V: int, elt: int) -> int:
@@ -82,8 +96,11 @@ class _FusedLinearCE(torch.autograd.Function):
         n_valid = (t != ignore_index).sum().to(torch.float32).clamp_min(1.0)
         scale = (1.0 / n_valid).reshape(1)
         native = _native.use_native(x2, op="ce") and cdt in _native.DTYPE_CODE
-        if native and cdt in (torch.bfloat16, torch.float16) and x2.shape[1] % 64 == 0:
-            return _FusedLinearCE._fused(ctx, x, x2, w, bias, t, ignore_index, scale, n_valid, shape)
+        if native and cdt in (torch.bfloat16, torch.float16) and x2.is_cuda:
+            if N * (-(-V // 8) * 8) * x2.element_size() <= CE_MATERIALIZE_BYTES:
+                return _FusedLinearCE._materialized(ctx, x, x2, w, bias, t, ignore_index, scale, shape)
+            if x2.shape[1] % 64 == 0:
+                return _FusedLinearCE._fused(ctx, x, x2, w, bias, t, ignore_index, scale, n_valid, shape)
         rows = max(1, min(N, max_bytes // max(1, V * x2.element_size())))
         dx = torch.empty_like(x2)
         need_w = ctx.needs_input_grad[1]
@@ -115,6 +132,44 @@ class _FusedLinearCE(torch.autograd.Function):
         ctx.save_for_backward(dx.view(shape), dw if dw is not None else torch.empty(0),
                               db if db is not None else torch.empty(0))
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype, need_w, need_b)
+        return loss
+
+    @staticmethod
+    def _materialized(ctx, x, x2, w, bias, t, ignore_index, scale, shape):
+        """bf16 logits once, CE in place, then the two backward GEMMs on dz (module docstring)."""
+        from .gemm import mm_nn
+
+        C = _native.native()
+        _native.count("linear_ce_materialized")
+        x2 = x2.contiguous()
+        w = w.contiguous()
+        t = t.contiguous()
+        N, V = x2.shape[0], w.shape[0]
+        zb = torch.empty(N, -(-V // 8) * 8, dtype=x2.dtype, device=x2.device)
+        z = zb[:, :V]  # 16-byte aligned rows
+        torch.mm(x2, w.t(), out=z)
+        b32 = None
+        if bias is not None:
+            b32 = bias.detach().float().contiguous()
+            if b32.data_ptr() % 16:
+                b32 = b32.clone()
+        loss_rows, _ = C.ce_fwd_bwd(z, t, scale, 1.0, int(ignore_index), True, b32)  # z <- dz
+        need_w = ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            Vm = V // 64 * 64
+            dx = mm_nn(zb[:, :Vm], w[:Vm]) if Vm > 0 else None
+            if dx is None:
+                dx = torch.mm(z, w)
+            elif Vm < V:
+                dx.addmm_(z[:, Vm:], w[Vm:])  # the odd class tail (rank V - Vm)
+        dw = torch.mm(z.t(), x2) if need_w else None
+        db = C.column_sum(zb, torch.float32)[:V] if need_b else None
+        loss = loss_rows.sum() * scale.reshape(())
+        ctx.save_for_backward(dx.view(shape) if dx is not None else torch.empty(0),
+                              dw if dw is not None else torch.empty(0), db if db is not None else torch.empty(0))
+        ctx.meta = (x.dtype, w.dtype, None if bias is None else bias.dtype, need_w, need_b)
         return loss
 
     @staticmethod

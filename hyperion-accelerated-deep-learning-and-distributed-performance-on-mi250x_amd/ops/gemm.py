@@ -67,7 +67,7 @@ def _time(fn, reps: int = 5) -> float:
 
 def _candidates(K: int):
     for t in (0, 1, 2):
-        for sp in (1, 2, 3, 4, 6, 8):
+        for sp in (1, 2, 3, 4, 6, 8, 12, 16):
             if sp == 1 or K // sp >= 256:
                 yield (t, sp)
 

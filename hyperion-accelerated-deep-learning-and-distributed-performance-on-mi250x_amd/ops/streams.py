@@ -89,3 +89,15 @@ def run_on_side(fn: Callable[[], torch.Tensor], inputs: Iterable[torch.Tensor], 
 def use_side_for(param: torch.Tensor) -> bool:
     """The side stream may produce ``param``'s gradient (it will be stolen, not accumulated)."""
     return enabled() and param.is_cuda and param.grad is None
+
+
+def on_stream(s: Optional["torch.cuda.Stream"]):
+    """Context that makes s current (no-op when s is None or already current).  Autograd
+    hooks run on the engine's thread with the current stream of the node that fired them — for a
+    leaf's AccumulateGrad not necessarily the stream the step runs on — so data-parallel wrappers
+    re-enter the forward's stream before they copy gradients or issue collectives."""
+    import contextlib
+
+    if s is None or s == torch.cuda.current_stream(s.device):
+        return contextlib.nullcontext()
+    return torch.cuda.stream(s)

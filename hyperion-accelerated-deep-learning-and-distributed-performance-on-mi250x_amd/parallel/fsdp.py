@@ -532,7 +532,7 @@ class FullyShardedDataParallel(nn.Module):
             if torch.is_grad_enabled():
                 ins = [t for t in _flatten(args) if isinstance(t, torch.Tensor) and t.requires_grad]
                 if ins:
-                    torch.autograd.graph.register_multi_grad_hook(ins, lambda grads: u.on_input_grads(), mode="all")
+                    torch.autograd.graph.register_multi_grad_hook(ins, lambda grads: self._input_grads(u), mode="all")
             if self._recording and u not in self._fwd_order:
                 self._fwd_order.append(u)
             u.gather()
@@ -557,21 +557,29 @@ class FullyShardedDataParallel(nn.Module):
 
         return hook
 
+    def _on_compute_stream(self):
+        """Run a backward hook's work on the forward's stream (ops.streams.on_stream): a
+        gradient copy or an RCCL issue ordered against another stream would race the backward
+        kernels still writing the gradients (graph warm-up and capture run on side streams)."""
+        return _streams.on_stream(getattr(self, "_compute_stream", None))
+
     def _make_pre_bwd(self, u: _Unit):
         def hook(grad):
-            self._ensure_backward_started()
-            u.gather()
-            if self.backward_prefetch:
-                prv = self._neighbour(u, -1)
-                if prv is not None and not prv.reduced:
-                    prv.gather(async_op=True)
+            with self._on_compute_stream():
+                self._ensure_backward_started()
+                u.gather()
+                if self.backward_prefetch:
+                    prv = self._neighbour(u, -1)
+                    if prv is not None and not prv.reduced:
+                        prv.gather(async_op=True)
 
         return hook
 
     def _make_grad_hook(self, u: _Unit):
         def hook(p):
-            self._ensure_backward_started()
-            u.on_grad(p)
+            with self._on_compute_stream():
+                self._ensure_backward_started()
+                u.on_grad(p)
 
         return hook
 
@@ -589,7 +597,15 @@ class FullyShardedDataParallel(nn.Module):
                 u.start_backward()
             torch.autograd.Variable._execution_engine.queue_callback(self._post_backward)
 
+    def _input_grads(self, u: _Unit) -> None:
+        with self._on_compute_stream():
+            u.on_input_grads()
+
     def _post_backward(self) -> None:
+        with self._on_compute_stream():
+            self._post_backward_body()
+
+    def _post_backward_body(self) -> None:
         for u in self.units:
             u.finish()
             for g in u.groups:
@@ -609,6 +625,9 @@ class FullyShardedDataParallel(nn.Module):
 
     # -- forward ----------------------------------------------------------------------------
     def _root_pre(self) -> None:
+        # the stream the step's compute runs on: backward hooks issue their copies and collectives
+        # on it (see _on_compute_stream)
+        self._compute_stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         self.root_unit.gather()
         if self.forward_prefetch and not self._recording and self._fwd_order:
             self._fwd_order[0].gather(async_op=True)

@@ -43,6 +43,7 @@ def test_fused_linear_ce_no_logits_path(chunk, monkeypatch):
     from hyperion.ops import _native
 
     monkeypatch.setattr(hce, "CE_CHUNK", chunk)
+    monkeypatch.setattr(hce, "CE_MATERIALIZE_BYTES", 0)
     torch.manual_seed(0)
     N, E, V, pad = 4064, 256, 50257, 50256
     x = (torch.randn(N, E, device="cuda") * 0.5).bfloat16().requires_grad_(True)
@@ -66,6 +67,61 @@ def test_fused_linear_ce_no_logits_path(chunk, monkeypatch):
     torch.testing.assert_close(loss.float(), ref, rtol=2e-2, atol=2e-2)
     for got, want in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
         assert (got.float() - want).norm() <= 3e-2 * want.norm() + 1e-6
+
+
+@pytest.mark.parametrize("N,E,with_bias", [(4064, 256, True), (2032, 768, True), (300, 128, False)])
+def test_fused_linear_ce_materialized_path(N, E, with_bias):
+    """The default bf16 schedule: bf16 logits (rows padded to 8 classes), register-resident
+    in-place CE with the bias added in the kernel, dX on the tiled split-K GEMM + odd-tail update,
+    dW on hipBLASLt — against the fp32 reference (LM-256 / GPT-2 head shapes, V = 50257)."""
+    import hyperion.ops.cross_entropy as hce
+    from hyperion.ops import _native
+
+    torch.manual_seed(0)
+    V, pad = 50257, 50256
+    x = (torch.randn(N, E, device="cuda") * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(V, E, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    b = (torch.randn(V, device="cuda") * 0.1).bfloat16().requires_grad_(True) if with_bias else None
+    t = torch.randint(0, V, (N,), device="cuda")
+    t[::9] = pad
+    _native.reset_counters()
+    loss = hce.fused_linear_cross_entropy(x, w, b, t, ignore_index=pad)
+    (loss * 0.5).backward()  # a non-unit incoming gradient
+    assert _native.counters().get("linear_ce_materialized") == 1
+    leaves = (x, w) + ((b,) if with_bias else ())
+    refs = [a.detach().float().requires_grad_(True) for a in leaves]
+    ref = F.cross_entropy(F.linear(refs[0], refs[1], refs[2] if with_bias else None), t, ignore_index=pad)
+    (ref * 0.5).backward()
+    torch.testing.assert_close(loss.float(), ref, rtol=2e-2, atol=2e-2)
+    for got, want in zip(leaves, refs):
+        assert (got.grad.float() - want.grad).norm() <= 3e-2 * want.grad.norm() + 1e-6
+
+
+@pytest.mark.parametrize("ld_pad", [0, 7, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_ce_kernel_bias_and_row_layouts(ld_pad, dtype):
+    """ce_fwd_bwd with an fp32 bias on aligned rows (register-resident kernel) and on odd row
+    strides (two-pass kernel) equals the fp32 softmax-CE of z + b and its gradient."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    torch.manual_seed(3)
+    N, V = 67, 5003
+    buf = (torch.randn(N, V + ld_pad, device="cuda") * 3).to(dtype)
+    z = buf[:, :V]
+    bias = torch.randn(V, device="cuda")
+    t = torch.randint(0, V, (N,), device="cuda")
+    t[5] = -100
+    scale = torch.full((1,), 1.0 / N, device="cuda")
+    zr = (z.float() + bias).requires_grad_(True)
+    ref = F.cross_entropy(zr, t, ignore_index=-100, reduction="sum") / N
+    ref.backward()
+    lse_ref = torch.logsumexp(zr.detach(), 1)
+    loss_rows, lse = C.ce_fwd_bwd(z, t, scale, 1.0, -100, True, bias)
+    torch.testing.assert_close(loss_rows.sum() / N, ref, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(lse, lse_ref, rtol=1e-4, atol=1e-4)
+    tol = dict(rtol=1e-3, atol=1e-6) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-4)
+    torch.testing.assert_close(z.float(), zr.grad, **tol)
 
 
 def test_fused_linear_ce_chunked_equals_unchunked():
