@@ -177,7 +177,7 @@ def _ensure_pg() -> None:
 
 def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps: int = 10, warmup: int = 3,
                     graph: bool = False, replicate_frozen="auto", persistent=None,
-                    collectives_at_world_1: bool = False) -> Dict:
+                    collectives_at_world_1: bool = False, loss_curve: bool = False, lr: float = 1e-4) -> Dict:
     """One FSDP FULL_SHARD training step exactly as the FSDP trainers run it (C25 / BASELINE config
     4 / C26): Hyperion's FSDP over the native RCCL communicator, bf16 mixed precision (param /
     reduce / buffer), FusedAdamW, global-norm clip 1.0.  ``model``: ``lm256`` (size-based wrap,
@@ -196,14 +196,15 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(0)
     bf = torch.bfloat16
-    if model == "llama7b_lora":
+    if model in ("llama7b_lora", "llama7b_full"):
         from ..models.llama import LlamaConfig, LlamaDecoderLayer, LlamaForCausalLM
         from ..models.lora import apply_lora
 
         cfg = LlamaConfig.llama2_7b()
         with torch.device(dev):
             base = LlamaForCausalLM(cfg).to(bf)
-        apply_lora(base)
+        if model == "llama7b_lora":
+            apply_lora(base)
         policy = transformer_auto_wrap_policy({LlamaDecoderLayer})
         vocab = cfg.vocab_size
     else:
@@ -218,13 +219,13 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
              replicate_frozen=replicate_frozen if model == "llama7b_lora" else False,
              persistent=True if graph else persistent, collectives_at_world_1=collectives_at_world_1)
     params = [p for p in m.parameters() if p.requires_grad]
-    opt = FusedAdam(params, lr=1e-4, weight_decay=0.01, adamw=True)
+    opt = FusedAdam(params, lr=lr, weight_decay=0.01, adamw=True)
     ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=dist.get_rank())
     ids = (ds.input_ids % vocab).to(dev)
 
     def step():
         opt.zero_grad(set_to_none=True)
-        if model == "llama7b_lora":
+        if model.startswith("llama7b"):
             loss = m(ids, labels=ids).loss
         else:
             # FSDP's MixedPrecision already holds the gathered parameters in bf16: no autocast (its
@@ -241,12 +242,21 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
 
         seg = SegmentedStep(step, warmup=2, module=m)
     torch.cuda.reset_peak_memory_stats()
-    t = _timeit(seg if seg is not None else step, steps, warmup)
-    final_loss = float((seg if seg is not None else step)())  # one more step: the timed schedule trains
+    run = seg if seg is not None else step
+    curve = []
+
+    def timed():
+        out = run()
+        if loss_curve:
+            curve.append(out.detach().clone().reshape(()))  # (a graphed step returns one static tensor)
+        return out
+
+    t = _timeit(timed if loss_curve else run, steps, warmup)
+    final_loss = float(run())  # one more step: the timed schedule trains
     if not math.isfinite(final_loss):
         raise RuntimeError(f"bench_fsdp_step({model}, graph={graph}): non-finite loss {final_loss}")
     world = dist.get_world_size()
-    tok = batch * (seq if model == "llama7b_lora" else seq - 1)
+    tok = batch * (seq if model.startswith("llama7b") else seq - 1)
     return {"model": model, "fsdp": True, "world": world, "graph": graph, "persistent": m.persistent,
             "persistent_reason": m.persistent_reason, "collectives_at_world_1": collectives_at_world_1,
             "comm": type(m.comm).__name__,
@@ -255,4 +265,5 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
             "batch_per_gpu": batch, "seq": seq, "ms_per_step": t * 1e3,
             "samples_per_s": world * batch / t, "tokens_per_s": world * tok / t,
             "trainable_params": sum(p.numel() for p in params), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20,
-            "final_loss": final_loss}
+            "final_loss": final_loss,
+            **({"loss_curve": [round(v, 4) for v in torch.stack(curve[warmup:]).tolist()]} if loss_curve else {})}

@@ -87,15 +87,19 @@ hyp::RngState unpack_rng(const at::Tensor& t) {
 namespace {
 
 // out = dropout(x) with the state's mask (mode 0), or the scaled keep mask keep/(1-p) shaped like x
-at::Tensor dropout_apply(const at::Tensor& x, double p, const at::Tensor& state, bool mask) {
+at::Tensor dropout_apply(const at::Tensor& x, double p, const c10::optional<at::Tensor>& state, bool mask,
+                         int64_t act) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.is_contiguous(), "dropout: contiguous input");
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout: 0 <= p < 1");
+  TORCH_CHECK(act == 0 || (act == 2 && !mask), "dropout: act is 0 (none) or 2 (exact GELU before the dropout)");
+  TORCH_CHECK(p == 0.0 || (state.has_value() && state->defined()), "dropout: p > 0 needs an rng state");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "dropout: 16-byte aligned input");
   const at::DeviceGuard guard(x.device());
   auto out = at::empty_like(x);
-  HYP_CHECK_HIP(hyp::dropout_apply(dtype_code(x), mask ? 1 : 0, x.data_ptr(), out.data_ptr(), x.numel(), (float)p,
-                                   unpack_rng(state), cur_stream()));
+  const hyp::RngState rs = (state.has_value() && state->defined()) ? unpack_rng(*state) : hyp::RngState{};
+  HYP_CHECK_HIP(hyp::dropout_apply(dtype_code(x), mask ? 1 : (act == 2 ? 2 : 0), x.data_ptr(), out.data_ptr(),
+                                   x.numel(), (float)p, rs, cur_stream()));
   return out;
 }
 
@@ -105,7 +109,8 @@ void register_rng_ops(pybind11::module& m) {
   m.def("rng_state", &rng_state, "graph-safe philox (seed, offset) record from torch's default HIP generator",
         pybind11::arg("device"), pybind11::arg("increment"));
   m.def("dropout", &dropout_apply, "counter-based dropout (mask regenerated from the rng state; mask=True: keep/(1-p))",
-        pybind11::arg("x"), pybind11::arg("p"), pybind11::arg("state"), pybind11::arg("mask") = false);
+        pybind11::arg("x"), pybind11::arg("p"), pybind11::arg("state"), pybind11::arg("mask") = false,
+        pybind11::arg("act") = 0);
 }
 
 }  // namespace hypbind

@@ -245,9 +245,51 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     return ((int64_t)n * a.Hx + 2 * p + ph_a) * a.Wx + 2 * q + ph_b;
   };
 
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // NB-deep ring: stage t+NB-1 is issued right after the barrier that retires stage t-1's buffer
+  // (NB == 1: stage 0 is issued here too, ahead of the epilogue loads below)
+#pragma unroll
+  for (int i = 0; i < (NB > 1 ? NB - 1 : 1); ++i)
+    if (i < nk) stage(smem + i * kBuf);
+  // Epilogue operand prefetch: the addend / BN-backward x, y chunks this thread will store, issued
+  // BEFORE the K loop so their HBM round trip overlaps the loads and MFMAs of the whole tile
+  // (issued after the loop, the BN-backward epilogue waited ~2 us for x on every workgroup; inside
+  // the store loop, a round trip per iteration: +18 us on a layer1 dgrad).  Issued right after the
+  // first stages (which the K loop needs first) and ahead of the epilogue constants; a counted
+  // stage wait that sees them behind stage 0 only over-waits.  (Split-K tiles store fp32 partials
+  // instead: no prefetch.)
+  constexpr bool FSTATS = STATS && !DGRAD, BNB = STATS && DGRAD;
+  constexpr int kChunksPerRow = BN / 8;
+  constexpr int kIt = BM * kChunksPerRow / kThreads;
+  uint4 pd[kIt], px[kIt], py[kIt];
+  const bool has_add = !FSTATS && a.addend != nullptr;
+  const bool stores_here = a.splits == 1 || sd2;
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int idx = it * kThreads + tid;
+    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
+    const int m = m0 + lr, k = n0 + ch * 8;
+    const bool ok = stores_here && m < a.M && k < a.K;
+    const int64_t off = (ok ? orow(m) : 0) * a.K + k;
+    pd[it] = px[it] = py[it] = uint4{0u, 0u, 0u, 0u};
+    if (has_add && ok) pd[it] = *reinterpret_cast<const uint4*>(a.addend + off);
+    if (BNB && ok) {
+      px[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.x) + off);
+      if (a.bnb.mode == 2) py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
+    }
+  }
+
   // per-channel epilogue constants of this thread's store column (the eval-BN affine or the
   // BN-backward ReLU-mask scale/shift), loaded before the main loop so the epilogue never waits
-  // on them (loaded there, they cost a full memory round trip per tile)
+  // on them (loaded there, they cost a full memory round trip per tile) — but AFTER the first
+  // stages are issued: the BN-backward scale/shift arithmetic consumes its loads at once, and
+  // ahead of the stage issue that vmcnt(0) serialised a whole HBM round trip (~2 us per
+  // workgroup) in front of the K loop; here it overlaps the stages' own latency
   float asc[8], ash[8];
   {
     constexpr int kCpr = BN / 8;
@@ -280,51 +322,16 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
 
-  // Epilogue operand prefetch: the addend / BN-backward x, y chunks this thread will store, issued
-  // BEFORE the K loop so their HBM round trip overlaps the loads and MFMAs of the whole tile
-  // (issued after the loop, the BN-backward epilogue waited ~2 us for x on every workgroup; inside
-  // the store loop, a round trip per iteration: +18 us on a layer1 dgrad).  Older than every stage's
-  // LDS-DMA, they retire with the first counted vmcnt wait.  (Split-K tiles store fp32 partials
-  // instead: no prefetch.)
-  constexpr bool FSTATS = STATS && !DGRAD, BNB = STATS && DGRAD;
-  constexpr int kChunksPerRow = BN / 8;
-  constexpr int kIt = BM * kChunksPerRow / kThreads;
-  uint4 pd[kIt], px[kIt], py[kIt];
-  const bool has_add = !FSTATS && a.addend != nullptr;
-  const bool stores_here = a.splits == 1 || sd2;
-#pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int idx = it * kThreads + tid;
-    const int lr = idx / kChunksPerRow, ch = idx - lr * kChunksPerRow;
-    const int m = m0 + lr, k = n0 + ch * 8;
-    const bool ok = stores_here && m < a.M && k < a.K;
-    const int64_t off = (ok ? orow(m) : 0) * a.K + k;
-    pd[it] = px[it] = py[it] = uint4{0u, 0u, 0u, 0u};
-    if (has_add && ok) pd[it] = *reinterpret_cast<const uint4*>(a.addend + off);
-    if (BNB && ok) {
-      px[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.x) + off);
-      if (a.bnb.mode == 2) py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
-    }
-  }
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // NB-deep ring: stage t+NB-1 is issued right after the barrier that retires stage t-1's buffer
-#pragma unroll
-  for (int i = 0; i < NB - 1; ++i)
-    if (i < nk) stage(smem + i * kBuf);
   const int r16 = lane & 15, c4 = lane >> 4;
   if (a.stamps != nullptr) tsb = realtime_stamp();
   for (int t = 0; t < nk; ++t) {
     if (NB == 1) {
       // single buffer (short reductions: LDS for more resident workgroups instead of a ring):
       // wait until every wave has read stage t-1, refill, wait for the DMA, publish
-      if (t > 0) mfl::barrier_keep_vm();
-      stage(smem);
+      if (t > 0) {
+        mfl::barrier_keep_vm();
+        stage(smem);
+      }
       mfl::wait_vmcnt<0>();
       mfl::barrier_keep_vm();
     } else {

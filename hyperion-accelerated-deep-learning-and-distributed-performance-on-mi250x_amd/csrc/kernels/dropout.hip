@@ -16,7 +16,12 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// MODE 0: y = keep ? x*scale : 0 ; MODE 1: y = keep ? scale : 0 (the scaled mask in T, x unused)
+__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+
+// MODE 0: y = keep ? x*scale : 0 ; MODE 1: y = keep ? scale : 0 (the scaled mask in T, x unused);
+// MODE 2: y = keep ? gelu(x)*scale : 0 (exact erf GELU: the activation + dropout of an FFN whose
+// GEMM ran on the vendor library with a bias epilogue — one pass over the pre-activation instead
+// of torch's GELU kernel and a separate dropout pass)
 template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads) void dropout_k(const T* __restrict__ x, T* __restrict__ y, int64_t n,
                                                       uint32_t thr, float scale, RngState rs) {
@@ -26,17 +31,20 @@ __global__ __launch_bounds__(kThreads) void dropout_k(const T* __restrict__ x, T
   for (int64_t i = i0; i < n; i += stride) {
     if (i + 8 <= n) {
       float v[8];
-      if (MODE == 0) Vec8<T>::load(x + i, v);
+      if (MODE != 1) Vec8<T>::load(x + i, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const bool keep = rng_u32(key, (uint64_t)(i + e)) >= thr;
-        v[e] = MODE == 0 ? (keep ? v[e] * scale : 0.f) : (keep ? scale : 0.f);
+        const bool keep = thr == 0u || rng_u32(key, (uint64_t)(i + e)) >= thr;
+        if (MODE == 2) v[e] = gelu_erf(v[e]);
+        v[e] = MODE != 1 ? (keep ? v[e] * scale : 0.f) : (keep ? scale : 0.f);
       }
       Vec8<T>::store(y + i, v);
     } else {
       for (int64_t j = i; j < n; ++j) {
-        const bool keep = rng_u32(key, (uint64_t)j) >= thr;
-        st1<T>(y + j, MODE == 0 ? (keep ? ld1<T>(x + j) * scale : 0.f) : (keep ? scale : 0.f));
+        const bool keep = thr == 0u || rng_u32(key, (uint64_t)j) >= thr;
+        float xv = MODE != 1 ? ld1<T>(x + j) : 0.f;
+        if (MODE == 2) xv = gelu_erf(xv);
+        st1<T>(y + j, MODE != 1 ? (keep ? xv * scale : 0.f) : (keep ? scale : 0.f));
       }
     }
   }
@@ -57,13 +65,17 @@ hipError_t launch(const void* x, void* y, int64_t n, float p, const RngState& rs
 }  // namespace
 
 // mode 0: out = dropout(x) (the same call with the same state is its own backward on dy);
-// mode 1: out = the scaled keep mask (keep / (1 - p)).  x / out contiguous (16-byte aligned for the vector body).
+// mode 1: out = the scaled keep mask (keep / (1 - p)); mode 2: out = dropout(gelu(x)) (p may be 0).
+// x / out contiguous (16-byte aligned for the vector body).
 hipError_t dropout_apply(int dtype, int mode, const void* x, void* out, int64_t n, float p, const RngState& rs,
                          hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (dtype == kBF16) return mode ? launch<bf16_t, 1>(x, out, n, p, rs, st) : launch<bf16_t, 0>(x, out, n, p, rs, st);
-  if (dtype == kF16) return mode ? launch<f16_t, 1>(x, out, n, p, rs, st) : launch<f16_t, 0>(x, out, n, p, rs, st);
-  return mode ? launch<float, 1>(x, out, n, p, rs, st) : launch<float, 0>(x, out, n, p, rs, st);
+  if (mode < 0 || mode > 2) return hipErrorInvalidValue;
+  HYP_DISPATCH_FLOAT(dtype, T, {
+    return mode == 0 ? launch<T, 0>(x, out, n, p, rs, st)
+                     : mode == 1 ? launch<T, 1>(x, out, n, p, rs, st) : launch<T, 2>(x, out, n, p, rs, st);
+  });
+  return hipErrorInvalidValue;
 }
 
 }  // namespace hyp

@@ -112,10 +112,12 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
 
     def ven():
         y = torch.addmm(bias.to(x.dtype), x, w.t()) if bias is not None else x @ w.t()
+        if a == 2:  # what the vendor fallback of linear_act runs: GELU + dropout in one native pass
+            return C.dropout(y, dropout_p, rng, act=2) + (residual if residual is not None else 0)
         if a == 1:
             y = torch.relu(y)
-        elif a >= 2:
-            y = torch.nn.functional.gelu(y, approximate="tanh" if a == 3 else "none")
+        elif a == 3:
+            y = torch.nn.functional.gelu(y, approximate="tanh")
         if dropout_p > 0:
             y = C.dropout(y, dropout_p, rng)
         return y + residual if residual is not None else y

@@ -9,7 +9,8 @@ tensor — but it has no autograd formula.  ``linear_act`` wraps it:
   so the pre-activation is never stored;
 * GELU: backward needs the pre-activation: the tiled MFMA kernel (``ops.gemm``) writes BOTH
   ``z = x Wᵀ + b`` (aux output) and ``gelu(z)`` from one epilogue; on the vendor path the forward
-  keeps ``z`` (bias epilogue) and applies GELU as a second pass;
+  keeps ``z`` (bias epilogue) and applies GELU and the inner dropout as ONE native pass
+  (``dropout.hip`` mode 2);
 * large-token GEMMs (forward, ``dy W``, ``dyᵀ x``) run on the tiled MFMA kernel where it beats the
   vendor GEMM for the shape (``ops.gemm`` routing);
 * backward: the activation backward and the bias gradient are ONE native pass
@@ -105,9 +106,12 @@ class _LinearGELU(torch.autograd.Function):
         h = mm_nt(x2, wc, bias=b, act="gelu", aux=y, dropout_p=drop[0], rng=drop[1]) if x2.is_cuda else None
         if h is None:
             y = torch.addmm(bc, x2, wc.t())
-            h = F.gelu(y)
-            if drop[0] > 0.0:
-                h = _native.native().dropout(h, drop[0], drop[1])
+            if y.is_cuda and y.dtype in (torch.bfloat16, torch.float16) and _native.use_native(y, op="act_dropout"):
+                h = _native.native().dropout(y, drop[0], drop[1], act=2)  # GELU + dropout: one pass
+            else:
+                h = F.gelu(y)
+                if drop[0] > 0.0:
+                    h = _native.native().dropout(h, drop[0], drop[1])
         ctx.save_for_backward(x2, wc, y)
         ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
         ctx.drop = drop

@@ -172,15 +172,16 @@ class _FlatGroup:
         self.gathered = True
         self.gather_work = None
         # persistent all-gather source in the compute dtype: cast ONCE per optimizer step (the
-        # forward gather), reused by the backward re-gather; None when the shard already has it
+        # forward gather), reused by the backward re-gather; None when the shard already has it or
+        # at world 1 without collectives (the gather is then one cast-copy straight into the buffer)
         self._send_buf = (torch.empty(self.shard_numel, dtype=self.cdtype, device=dev)
-                          if self.flat_param.dtype != self.cdtype else None)
+                          if self.flat_param.dtype != self.cdtype and not fsdp.identity else None)
         self.send_valid = False
         self.rs_work = None
         self.rs_out: Optional[torch.Tensor] = None
         # persistent reduce-scatter output / fp32 shard gradient (no per-step allocation or .to())
         self._rs_buf = (torch.empty(self.shard_numel, dtype=self.rdtype, device=dev)
-                        if trainable and self.rdtype != torch.float32 else None)
+                        if trainable and self.rdtype != torch.float32 and not fsdp.identity else None)
         self._grad_shard = torch.empty(self.shard_numel, dtype=torch.float32, device=dev) if trainable else None
         self.grad_ready: Set[int] = set()
         self._pending: List[Tuple[int, torch.Tensor]] = []  # (param index, grad) not yet in full_grad

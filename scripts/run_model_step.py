@@ -17,9 +17,12 @@ if which == "fsdp":  # fsdp <lm256|gpt2_small|llama7b_lora> [graph] [shardbase] 
         kw["replicate_frozen"] = False
     if model == "gpt2_small":
         kw["batch"] = 16
-    if model == "llama7b_lora":
+    if model.startswith("llama7b"):
         kw["batch"] = 1
-    r = M.bench_fsdp_step(model, steps=10, warmup=3, **kw)
+    if "curve" in sys.argv[3:]:
+        kw["loss_curve"] = True
+    steps = 50 if model == "llama7b_full" else 10
+    r = M.bench_fsdp_step(model, steps=steps, warmup=3, **kw)
 elif which == "vit":
     r = M.bench_vit_step(checkpointing=False, steps=5, warmup=3)
 elif which == "vitgraph":

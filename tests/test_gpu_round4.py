@@ -264,3 +264,23 @@ def test_fused_dropout_masks_regenerate_under_graph_replay():
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         e1, e2 = layer(x), layer(x)
     assert torch.equal(e1, e2)  # eval: no dropout
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gelu_dropout_one_pass_matches_fp32(p, dt):
+    """dropout.hip mode 2 (the vendor-GEMM FFN path: exact-erf GELU + dropout in one pass) against
+    fp32 GELU times the same call's scaled keep mask; odd element count exercises the scalar tail."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    torch.manual_seed(0)
+    z = (torch.randn(1001, 77, device="cuda") * 3).to(dt)
+    st = _native.rng_state(z.device) if p > 0 else None
+    h = C.dropout(z, p, st, act=2)
+    keep = C.dropout(torch.ones_like(z), p, st, mask=True).float() if p > 0 else 1.0
+    ref = torch.nn.functional.gelu(z.float()) * keep
+    torch.testing.assert_close(h.float(), ref, rtol=1e-2, atol=1e-2)
+    if p > 0:  # (GELU itself is exactly 0 below about -5.5 in fp32: count the mask, not h)
+        frac = float((keep == 0).float().mean())
+        assert abs(frac - p) < 0.02
