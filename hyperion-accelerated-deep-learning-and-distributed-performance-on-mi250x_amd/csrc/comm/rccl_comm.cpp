@@ -32,6 +32,7 @@
 #include "comm/watchdog.h"
 
 #include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
 
 #include "bindings/common.h"
 #include "bindings/registry.h"
@@ -60,12 +61,15 @@ ncclDataType_t nccl_dtype(const at::Tensor& t) {
   }
 }
 
+// "avg" is issued as ncclSum followed by a 1/world scale on the comm stream (scale_avg below), never
+// as ncclAvg: the torch-bundled RCCL 2.26.6 leaves the last 4-16 elements of some reduce-scatter
+// outputs unwritten under ncclAvg (bf16 132480 / 131392 / 133568 elements, fp32 16704 / 17024 /
+// ..., single rank — scripts/rccl_avg_check.py), which corrupted the tail of FSDP flat gradients.
 ncclRedOp_t nccl_op(const std::string& op) {
-  if (op == "sum") return ncclSum;
+  if (op == "sum" || op == "avg") return ncclSum;
   if (op == "max") return ncclMax;
   if (op == "min") return ncclMin;
   if (op == "prod") return ncclProd;
-  if (op == "avg") return ncclAvg;
   TORCH_CHECK(false, "hyperion RCCL: unknown reduce op ", op);
 }
 
@@ -194,12 +198,20 @@ class RcclComm {
   int world() const { return world_; }
   int64_t stream_handle() const { return reinterpret_cast<int64_t>(stream_); }
 
+  // the 1/world of an "avg" (see nccl_op), on the comm stream before the completion event
+  void scale_avg(at::Tensor& t, const std::string& op) {
+    if (op != "avg" || world_ == 1) return;
+    const c10::hip::HIPStreamGuard sg(stream_obj_);
+    t.mul_(1.0 / world_);
+  }
+
   std::shared_ptr<Work> all_reduce(at::Tensor& t, const std::string& op) {
     check(t);
     std::lock_guard<std::recursive_mutex> g(mu_);
     begin({t});
     settle(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_, stream_),
            "all_reduce");
+    scale_avg(t, op);
     return end("all_reduce", t.numel() * t.element_size());
   }
 
@@ -214,6 +226,7 @@ class RcclComm {
       HYP_CHECK_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_, stream_));
     }
     settle(ncclGroupEnd(), "all_reduce_coalesced");
+    for (auto& t : ts) scale_avg(t, op);
     return end("all_reduce_coalesced", bytes);
   }
 
@@ -225,6 +238,7 @@ class RcclComm {
     begin({out, in});
     settle(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(out), nccl_op(op), comm_, stream_),
            "reduce_scatter");
+    scale_avg(out, op);
     return end("reduce_scatter", in.numel() * in.element_size());
   }
 

@@ -42,6 +42,22 @@ class _Done:
         return True
 
 
+class _ScaleAfter:
+    """A SUM collective's work handle whose wait() also divides the result by the world size (the
+    "avg" of a reduction, in the caller's stream order after the collective)."""
+
+    def __init__(self, work, t: torch.Tensor, world: int):
+        self.work, self.t, self.world = work, t, world
+
+    def wait(self):
+        self.work.wait()
+        self.t.div_(self.world)
+        return True
+
+    def is_completed(self):
+        return self.work.is_completed()
+
+
 class TorchComm:
     backend = "torch"
 
@@ -53,11 +69,8 @@ class TorchComm:
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         if self.world == 1:
             return _Done()
-        if op == "avg" and dist.get_backend(self.group) == "gloo":
-            w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            w.wait()
-            t.div_(self.world)
-            return _Done()
+        if op == "avg":  # SUM + 1/world: never ReduceOp.AVG (RCCL's ncclAvg drops output tails, rccl_comm.cpp)
+            return _ScaleAfter(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), t, self.world)
         return dist.all_reduce(t, op=_OPS[op], group=self.group, async_op=True)
 
     def all_reduce_coalesced(self, ts: List[torch.Tensor], op: str = "sum"):
@@ -68,6 +81,9 @@ class TorchComm:
         if self.world == 1:
             out.copy_(inp)
             return _Done()
+        if op == "avg":
+            w = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            return _ScaleAfter(w, out, self.world)
         return dist.reduce_scatter_tensor(out, inp, op=_OPS[op], group=self.group, async_op=True)
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):

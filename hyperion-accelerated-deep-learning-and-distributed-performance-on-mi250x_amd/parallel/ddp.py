@@ -187,12 +187,10 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------------ hooks
     def _grad_ready(self, p: nn.Parameter) -> None:
+        # (runs on the stream autograd gives the parameter's AccumulateGrad: the stream of the
+        # forward op that consumed it — where the gradient was produced)
         if not self._sync or p.grad is None:
             return
-        with _streams.on_stream(getattr(self, "_compute_stream", None)):
-            self._grad_ready_body(p)
-
-    def _grad_ready_body(self, p: nn.Parameter) -> None:
         _flush_wgrad()  # a deferred weight-gradient reduce may still owe this gradient its values
         if not self._callback_queued:
             self._callback_queued = True
@@ -248,10 +246,6 @@ class DistributedDataParallel(nn.Module):
             b.work = None
 
     def _finalize(self) -> None:
-        with _streams.on_stream(getattr(self, "_compute_stream", None)):
-            self._finalize_body()
-
-    def _finalize_body(self) -> None:
         if self.partial_backward:  # more of this step's backward follows: keep the bucket state
             self._callback_queued = False
             return
@@ -335,9 +329,6 @@ class DistributedDataParallel(nn.Module):
         return any(b.numel() > 0 for b in self.module.buffers())
 
     def forward(self, *args, **kwargs):
-        # the step's stream: the gradient hooks pack and issue on it (ops.streams.on_stream)
-        dev = self._buckets[0].buf.device if self._buckets else None
-        self._compute_stream = torch.cuda.current_stream(dev) if dev is not None and dev.type == "cuda" else None
         if self.world > 1 and self.broadcast_buffers and self.has_buffers():
             # per-forward broadcast (torch DDP's broadcast_buffers=True); an eager hole when the
             # step is being captured as segments, so replays broadcast before every forward too

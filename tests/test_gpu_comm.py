@@ -49,6 +49,25 @@ def test_native_comm_collectives_world1(pg):
     c.destroy()
 
 
+@pytest.mark.parametrize("dt,n", [(torch.bfloat16, 132480), (torch.bfloat16, 131392), (torch.bfloat16, 133568),
+                                  (torch.float32, 16704), (torch.float32, 17024)])
+def test_native_comm_avg_writes_every_element(pg, dt, n):
+    """"avg" reductions run as SUM + 1/world on the comm stream: RCCL's own ncclAvg (torch-bundled
+    2.26.6) left the last 4-16 outputs of these reduce-scatter sizes unwritten (an FSDP unit's
+    flat gradient tail — its last LayerNorm bias — came back stale)."""
+    from hyperion.parallel.comm import NativeComm
+
+    c = NativeComm(torch.device("cuda", 0))
+    x = torch.randn(n, device="cuda").to(dt)
+    out = torch.full((n,), 7.0, device="cuda", dtype=dt)
+    c.reduce_scatter(out, x, "avg").wait()
+    torch.testing.assert_close(out, x, rtol=0, atol=0)
+    y = x.clone()
+    c.all_reduce(y, "avg").wait()
+    torch.testing.assert_close(y, x, rtol=0, atol=0)
+    c.destroy()
+
+
 def test_native_comm_orders_against_compute_stream(pg):
     # a producer kernel on the current stream, then the collective on the comm stream, then a
     # consumer: the result must see the producer's data and the consumer must see the collective
