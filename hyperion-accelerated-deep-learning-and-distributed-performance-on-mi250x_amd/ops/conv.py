@@ -146,7 +146,9 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
                                                 bn_b=bn.bn_b, bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,
                                                 bn_sums=bn.sums, stages=pl[3], **geo)
             return bn.dz
-        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], addend=addend, **geo)
+        pl = _plan("dgrad", x.shape[0] * H * W, w.shape[1], w.shape[0], R, S, stride[0]) or (-1, -1, -1, 0)
+        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2], addend=addend,
+                                           stages=pl[3], **geo)
     if (R == 1 and S == 1 and tuple(padding) == (0, 0) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0
             and _native.use_native(dy, op="dgrad")):
         # 1x1 stride-s (ResNet downsample): dY·W on the output grid is the stride-1 DGRAD GEMM; one
@@ -154,7 +156,9 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         # ran a zero-fill kernel, its own dgrad, and autograd a separate add)
         Cn = _native.native()
         _native.count("dgrad_strided1x1")
-        comp = Cn.conv_dgrad(dy.contiguous(memory_format=torch.channels_last), w, 0, 0)
+        pl = _plan("dgrad", dy.shape[0] * dy.shape[2] * dy.shape[3], w.shape[1], w.shape[0], 1, 1, 1) or (-1, -1, -1, 0)
+        comp = Cn.conv_dgrad(dy.contiguous(memory_format=torch.channels_last), w, 0, 0, pl[0], pl[1], pl[2],
+                             stages=pl[3])
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
         return Cn.upsample_add(comp, addend, x.shape[2], x.shape[3], stride[0], stride[1])
@@ -266,7 +270,9 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         dyc = dy.contiguous(memory_format=torch.channels_last)
         _native.count("wgrad")
         defer = _can_defer(w_param)
-        dw = _native.native().conv_wgrad(dyc, x, R, S, stride[0], stride[1], padding[0], padding[1], defer=defer)
+        pl = _plan("wgrad", dy.shape[0] * P * Q, dy.shape[1], x.shape[1], R, S, stride[0]) or (-1, -1, -1, 0)
+        dw = _native.native().conv_wgrad(dyc, x, R, S, stride[0], stride[1], padding[0], padding[1], pl[0], pl[1],
+                                         pl[2], defer=defer)
         if defer:
             _defer_state["pending"] = True
         return dw

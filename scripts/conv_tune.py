@@ -1,7 +1,8 @@
 """Per-shape launch-plan tuning of the native conv kernels (the MIOpen find-db role) on every
-ResNet-50 convolution at a given batch: forward with the BN-statistics epilogue, and the data
-gradient with the producer's BN-backward epilogue (mode 1, the common case in a bottleneck) —
-tile (bm x bn), split-K count and LDS ring depth, each timed as 20 launches in one hipGraph.
+ResNet-50 convolution at a given batch: forward with the BN-statistics epilogue, the data
+gradient with the producer's BN-backward epilogue (mode 1, the common case in a bottleneck) and
+without it (the block-input convs), and the weight gradient — tile (bm x bn), split-K count and
+(fwd / dgrad) LDS ring depth, each timed as 20 launches in one hipGraph.
 
 Writes the winners to configs/conv_plans_mi355x.json (ops/conv.py looks plans up by GEMM shape)
 and every measurement to gpurun_out/conv_tune.json.
@@ -91,10 +92,47 @@ def main():
             plans.append({"op": "dgrad_bnb", "M": N * H * H, "K": C, "C": K, "R": R, "S": R, "stride": s, "pad": p,
                           "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
                           "us": round(dgr[best], 2), "auto_us": round(auto, 2)})
+        # ---- plain data gradient (block-input convs: no BN epilogue); 1x1 stride-2 runs on the output grid
+        if K % 64 == 0 and (s == 1 or R > 1 or (R == 1 and p == 0)):
+            s1x1 = R == 1 and s == 2
+            dy = torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+            geo = dict(stride=2, H=H, W=H) if (s == 2 and R > 1) else {}
+            nkd = R * R * K // 64
+            pd = {}
+            for cfg in configs(nkd, strided_dgrad=s == 2 and R > 1):
+                bm, bn, sp, nb = cfg
+                pd[cfg] = gtime(lambda: C_.conv_dgrad(dy, w, p, p, bm, bn, sp, stages=nb, **geo))
+            auto = gtime(lambda: C_.conv_dgrad(dy, w, p, p, **geo))
+            best = min(pd, key=pd.get)
+            row["dgrad"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(pd[best], 2)}
+            Mg = N * P * P if s1x1 else N * H * H
+            plans.append({"op": "dgrad", "M": Mg, "K": C, "C": K, "R": R, "S": R, "stride": 1 if s1x1 else s,
+                          "pad": p, "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
+                          "us": round(pd[best], 2), "auto_us": round(auto, 2)})
+        # ---- weight gradient: tiles x pixel splits (the deferred reduce is off while timing)
+        if C % 64 == 0 and K % 8 == 0:
+            dy = torch.randn(N, K, P, P, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+            wg = {}
+            for bm in (64, 128):
+                for bn in (64, 128):
+                    if C % bn or (bm == 128 and K < 128):
+                        continue
+                    for sp in (-1, 8, 16, 32, 64, 96, 128):
+                        try:
+                            wg[(bm, bn, sp, 0)] = gtime(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p, bm, bn, sp))
+                        except RuntimeError:
+                            pass
+            auto = gtime(lambda: C_.conv_wgrad(dy, x, R, R, s, s, p, p))
+            best = min(wg, key=wg.get)
+            row["wgrad"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(wg[best], 2)}
+            if wg[best] < auto:
+                plans.append({"op": "wgrad", "M": N * P * P, "K": K, "C": C, "R": R, "S": R, "stride": s, "pad": p,
+                              "bm": best[0], "bn": best[1], "splits": best[2], "stages": 0,
+                              "us": round(wg[best], 2), "auto_us": round(auto, 2)})
         raw.append(row)
-        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb")}),
+        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb", "dgrad", "wgrad")}),
               json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "all"} for k, v in row.items()
-                          if k in ("fwd", "dgrad_bnb")}), flush=True)
+                          if k in ("fwd", "dgrad_bnb", "dgrad", "wgrad")}), flush=True)
     doc = {"device": torch.cuda.get_device_name(), "batch": a.batch,
            "note": "native conv launch plans by GEMM shape (M = output pixels, K = output channels, C = "
                    "reduction channels); written by scripts/conv_tune.py",
@@ -103,9 +141,10 @@ def main():
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         with open(path, "w") as f:
             json.dump(obj, f, indent=1)
-    tot_auto = sum(pl["auto_us"] for pl in plans)
-    tot_best = sum(pl["us"] for pl in plans)
-    print(json.dumps({"sum_auto_us": round(tot_auto, 1), "sum_best_us": round(tot_best, 1)}))
+    for op in ("fwd", "dgrad_bnb", "dgrad", "wgrad"):
+        ps = [pl for pl in plans if pl["op"] == op]
+        print(json.dumps({"op": op, "n": len(ps), "sum_auto_us": round(sum(pl["auto_us"] for pl in ps), 1),
+                          "sum_best_us": round(sum(pl["us"] for pl in ps), 1)}))
 
 
 if __name__ == "__main__":

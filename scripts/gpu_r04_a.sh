@@ -16,6 +16,6 @@ for r in json.load(open(f"gpurun_out/r04/timeline_{sys.argv[1]}.json")):
     print(r["op"], r["C"], r["H"], r["K"], r["R"], "span", r["span_us"], "pro", r["prologue_us_med"], "loop", r["loop_us_med"], "epi", r["epilogue_us_med"], "conc", r["max_concurrent_per_cu"])
 PY
 if [ "${TUNE:-0}" = "1" ]; then
-  timeout -k 10 600 python -u scripts/conv_tune.py --out gpurun_out/r04/conv_plans_$tag.json --raw gpurun_out/r04/conv_tune_raw_$tag.json > gpurun_out/r04/conv_tune_$tag.log 2>&1
+  timeout -k 10 1000 python -u scripts/conv_tune.py --out gpurun_out/r04/conv_plans_$tag.json --raw gpurun_out/r04/conv_tune_raw_$tag.json > gpurun_out/r04/conv_tune_$tag.log 2>&1
   echo tune rc=$?; tail -1 gpurun_out/r04/conv_tune_$tag.log
 fi
