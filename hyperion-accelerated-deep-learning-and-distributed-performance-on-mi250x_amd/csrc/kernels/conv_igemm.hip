@@ -116,7 +116,9 @@ __device__ __forceinline__ unsigned long long realtime_stamp() {
 //   (tr_row_to_k) and read transposed with ds_read_b64_tr_b16 — no flipped/transposed filter copy.
 // EPI 0: the stores above; 1: linear-CE log-sum-exp partials (no output tensor); 2: linear-CE
 // softmax gradient written in place of the logits (see linear_ce)
-template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, int EPI = 0>
+// LEAN (BN-backward epilogue only): mode 0/1 without an addend — no y / addend prefetch registers
+// (64x64: 119 -> 104 VGPR+AGPR, 128x64: 191 -> 158, one more resident wave per SIMD there)
+template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, int EPI = 0, bool LEAN = false>
 __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (wave tile BM/2 x BN/2)
   constexpr int IA = BM / 32, IB = BN / 32;  // glds instructions per wave per slice
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int kChunksPerRow = BN / 8;
   constexpr int kIt = BM * kChunksPerRow / kThreads;
   uint4 pd[kIt], px[kIt], py[kIt];
-  const bool has_add = !FSTATS && a.addend != nullptr;
+  const bool has_add = !FSTATS && !LEAN && a.addend != nullptr;
   const bool stores_here = a.splits == 1 || sd2;
 #pragma unroll
   for (int it = 0; it < kIt; ++it) {
@@ -280,7 +282,8 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     if (has_add && ok) pd[it] = *reinterpret_cast<const uint4*>(a.addend + off);
     if (BNB && ok) {
       px[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.x) + off);
-      if (a.bnb.mode == 2) py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
+      if (!LEAN && a.bnb.mode == 2)
+        py[it] = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.bnb.y) + off);
     }
   }
 
@@ -560,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       uint4 v = *reinterpret_cast<const uint4*>(tile + lr * kLd + ch * 8);
       if (BNB) {
         // dz = round(round(acc) + addend) * mask; Σdz, Σdz·x over the stored (rounded) values
-        float o[8], xv[8], yv[8];
+        float o[8], xv[8], yv[8] = {};
         Vec8<T>::load(reinterpret_cast<const T*>(&v), o);
         if (has_add) {
           float d[8];
@@ -569,10 +572,11 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
           for (int e = 0; e < 8; ++e) o[e] = rnd<T>(o[e] + d[e]);
         }
         Vec8<T>::load(reinterpret_cast<const T*>(&px[it]), xv);
-        Vec8<T>::load(reinterpret_cast<const T*>(&py[it]), yv);
+        if (!LEAN) Vec8<T>::load(reinterpret_cast<const T*>(&py[it]), yv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const bool keep = a.bnb.mode == 0 || (a.bnb.mode == 1 ? fmaf(xv[e], asc[e], ash[e]) > 0.f : yv[e] > 0.f);
+          const bool keep =
+              a.bnb.mode == 0 || ((LEAN || a.bnb.mode == 1) ? fmaf(xv[e], asc[e], ash[e]) > 0.f : yv[e] > 0.f);
           o[e] = keep ? o[e] : 0.f;
           bs[e] += o[e];
           bq[e] += o[e] * xv[e];
@@ -642,7 +646,9 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 template <typename T, int BM, int BN, int NB>
 hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.K + BN - 1) / BN) * a.splits;
-  if (dgrad && stats)
+  if (dgrad && stats && a.bnb.mode <= 1 && a.addend == nullptr)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, true, NB, 0, true>), dim3(tiles), dim3(kThreads), 0, st, a);
+  else if (dgrad && stats)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   else if (dgrad)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);

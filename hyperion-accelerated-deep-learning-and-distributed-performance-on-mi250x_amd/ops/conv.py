@@ -140,7 +140,9 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         if bn is not None and not bn.used and bn.yc.dtype == dy.dtype:
             bn.used = True
             _native.count("dgrad_bn_fused")
-            pl = _plan("dgrad_bnb", x.shape[0] * H * W, w.shape[1], w.shape[0], R, S, stride[0]) or (-1, -1, -1, 0)
+            # (mode 2 or an addend: the full-register kernel variant, tuned under its own key)
+            op = "dgrad_bnb2" if (bn.mode == 2 or addend is not None) else "dgrad_bnb"
+            pl = _plan(op, x.shape[0] * H * W, w.shape[1], w.shape[0], R, S, stride[0]) or (-1, -1, -1, 0)
             bn.dz = _native.native().conv_dgrad(dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2], addend=addend,
                                                 bn_x=bn.yc, bn_y=x if bn.mode == 2 else None, bn_w=bn.bn_w,
                                                 bn_b=bn.bn_b, bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,

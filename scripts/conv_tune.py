@@ -92,6 +92,25 @@ def main():
             plans.append({"op": "dgrad_bnb", "M": N * H * H, "K": C, "C": K, "R": R, "S": R, "stride": s, "pad": p,
                           "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
                           "us": round(dgr[best], 2), "auto_us": round(auto, 2)})
+            # the full-register variant: producer BN + residual + ReLU (mode 2: y read) with the
+            # shortcut-gradient addend (a block's first conv) — its own plan key ("dgrad_bnb2")
+            yy = torch.relu(torch.randn_like(x))
+            add = torch.randn_like(x)
+
+            def dg2(bm=-1, bn=-1, sp=-1, nb=0):
+                return C_.conv_dgrad(dy, w, p, p, bm, bn, sp, addend=add, bn_x=yc, bn_y=yy, bn_mean=mean,
+                                     bn_invstd=invstd, bn_mode=2, bn_sums=bsums, stages=nb, **geo)
+
+            dg2r = {}
+            for cfg in configs(nkd, strided_dgrad=s == 2):
+                bm, bn, sp, nb = cfg
+                dg2r[cfg] = gtime(lambda: dg2(bm, bn, sp, nb))
+            auto = gtime(lambda: dg2())
+            best = min(dg2r, key=dg2r.get)
+            row["dgrad_bnb2"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(dg2r[best], 2)}
+            plans.append({"op": "dgrad_bnb2", "M": N * H * H, "K": C, "C": K, "R": R, "S": R, "stride": s, "pad": p,
+                          "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
+                          "us": round(dg2r[best], 2), "auto_us": round(auto, 2)})
         # ---- plain data gradient (block-input convs: no BN epilogue); 1x1 stride-2 runs on the output grid
         if K % 64 == 0 and (s == 1 or R > 1 or (R == 1 and p == 0)):
             s1x1 = R == 1 and s == 2
@@ -130,9 +149,9 @@ def main():
                               "bm": best[0], "bn": best[1], "splits": best[2], "stages": 0,
                               "us": round(wg[best], 2), "auto_us": round(auto, 2)})
         raw.append(row)
-        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb", "dgrad", "wgrad")}),
+        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad")}),
               json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "all"} for k, v in row.items()
-                          if k in ("fwd", "dgrad_bnb", "dgrad", "wgrad")}), flush=True)
+                          if k in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad")}), flush=True)
     doc = {"device": torch.cuda.get_device_name(), "batch": a.batch,
            "note": "native conv launch plans by GEMM shape (M = output pixels, K = output channels, C = "
                    "reduction channels); written by scripts/conv_tune.py",
@@ -141,7 +160,7 @@ def main():
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         with open(path, "w") as f:
             json.dump(obj, f, indent=1)
-    for op in ("fwd", "dgrad_bnb", "dgrad", "wgrad"):
+    for op in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad"):
         ps = [pl for pl in plans if pl["op"] == op]
         print(json.dumps({"op": op, "n": len(ps), "sum_auto_us": round(sum(pl["auto_us"] for pl in ps), 1),
                           "sum_best_us": round(sum(pl["us"] for pl in ps), 1)}))
