@@ -19,7 +19,9 @@ import torch  # noqa: E402
 
 from hyperion.bench.conv_shapes import resnet50_convs  # noqa: E402
 from hyperion.ops import _native  # noqa: E402
-from conv_roofline import gtime  # noqa: E402
+from conv_roofline import gtime as _gtime_warm, gtime_cold  # noqa: E402
+
+gtime = gtime_cold  # plans are chosen on HBM-cold operands (--warm: repeat-loop timing)
 
 TILES = [(128, 128), (128, 64), (64, 64)]
 
@@ -42,7 +44,11 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default="configs/conv_plans_mi355x.json")
     ap.add_argument("--raw", default="gpurun_out/conv_tune.json")
+    ap.add_argument("--warm", action="store_true", help="time repeat loops (operands cache-resident)")
     a = ap.parse_args()
+    global gtime
+    if a.warm:
+        gtime = _gtime_warm
     C_ = _native.native()
     plans, raw = [], []
     for sh in resnet50_convs(a.batch):
