@@ -48,6 +48,8 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--channels-last", type=int, default=1)
+    ap.add_argument("--loss", default="torch", choices=["torch", "fused"],
+                    help="MSE loss: torch's ops or Hyperion's one-pass kernel (ops.losses)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--smi", type=int, default=0, help="sample amd-smi power / clocks during the timed steps")
     return ap.parse_args(argv)
@@ -91,7 +93,10 @@ def main(argv=None) -> int:
         model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                     comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
     opt = FusedAdam(model.parameters(), lr=1e-3, zero_grad_in_step=True)
-    loss_fn = nn.MSELoss()
+    # the reference's nn.MSELoss (mean) — Hyperion's fused forward+gradient pass on gfx950
+    from hyperion.ops.losses import MSELoss
+
+    loss_fn = MSELoss() if (args.kernels != "torch" and args.loss == "fused") else nn.MSELoss()
 
     B = args.batch
     x = torch.rand(B, 3, args.image, args.image, device=dev).to(memory_format=mf)

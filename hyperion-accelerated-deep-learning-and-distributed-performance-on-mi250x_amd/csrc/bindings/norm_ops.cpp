@@ -206,6 +206,17 @@ void register_norm_ops(pybind11::module& m) {
         pybind11::arg("sums") = pybind11::none());
   m.def("bn_bwd_dx", &bn_bwd_dx, "BN backward dx pass from a pre-masked dz and its complete sums");
   m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
+  m.def("mse_fwd_bwd", [](const at::Tensor& x, const at::Tensor& t) {
+    HYP_CHECK_CUDA_TENSOR(x);
+    TORCH_CHECK(x.is_contiguous() && t.is_contiguous() && t.scalar_type() == at::kFloat && x.numel() == t.numel() &&
+                    t.device() == x.device(), "mse_fwd_bwd: contiguous x and fp32 target of the same size");
+    const at::DeviceGuard guard(x.device());
+    auto loss = at::empty({}, x.options().dtype(at::kFloat));
+    auto g = at::empty_like(x);
+    HYP_CHECK_HIP(hyp::mse_fwd_bwd(dtype_code(x), x.data_ptr(), t.data_ptr<float>(), x.numel(), loss.data_ptr<float>(),
+                                   g.data_ptr(), cur_stream()));
+    return std::vector<at::Tensor>{loss, g};
+  }, "mean-squared error and its gradient 2(x - t)/n in one pass", pybind11::arg("x"), pybind11::arg("target"));
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());
   m.def("act_bwd_colsum", &act_bwd_colsum, "activation backward + bias gradient in one pass (act 1 relu, 2 gelu)",

@@ -288,6 +288,8 @@ namespace hyp {
 // Column sums of a row-major [M, N] matrix (bias gradients): P partial rows (colsum_partials) in
 // `part` [P, N] fp32, then combined into out[N] (out_dtype).  N % 8 == 0, 16-byte aligned x.
 int colsum_partials(int64_t M, int N);
+// loss = mean((x - t)^2) (fp32 scalar) and g = 2 (x - t) / n in x's dtype; one block (small n)
+hipError_t mse_fwd_bwd(int dtype, const void* x, const float* t, int64_t n, float* loss, void* g, hipStream_t st);
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,
                       hipStream_t st);
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);

@@ -13,6 +13,7 @@ residual add and ReLU folded in; fused backward).  Module attribute names (``con
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type, Union
 
 import torch
@@ -23,6 +24,7 @@ from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import branch_sum_link, conv_bn_act, residual_link
+from ..ops.linear import Linear
 
 
 def _downsample(ds: nn.Sequential, x: torch.Tensor, branch=None) -> torch.Tensor:
@@ -104,7 +106,10 @@ class ResNet(nn.Module):
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
         self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
         self.avgpool = AdaptiveAvgPool2d((1, 1))
-        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        # (Hyperion's Linear measured slower here: 3 native launches for the [32, 2048] x 1000 head
+        # vs hipBLASLt's one — HYPERION_RESNET_FC=native opts in)
+        fc_cls = Linear if os.environ.get("HYPERION_RESNET_FC", "torch") == "native" else nn.Linear
+        self.fc = fc_cls(512 * block.expansion, num_classes)
 
         for m in self.modules():
             if isinstance(m, nn.Conv2d):

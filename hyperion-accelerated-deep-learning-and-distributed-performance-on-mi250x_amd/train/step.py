@@ -110,6 +110,12 @@ class TrainStep:
             return None
         return st
 
+    def _loss_in(self, out: torch.Tensor) -> torch.Tensor:
+        """The logits as the loss takes them: fp32, unless the loss fuses the cast itself."""
+        if out.dtype == torch.float32 or getattr(self.loss_fn, "accepts_low_precision", False):
+            return out
+        return out.float()
+
     def _fwd_bwd_top(self, x: torch.Tensor, y: torch.Tensor, stages, zero_in_place: bool = False):
         """Forward through both stages, backward through the top one only."""
         if zero_in_place:
@@ -119,7 +125,7 @@ class TrainStep:
             h = stages[0](x)
             h2 = h.detach().requires_grad_(True)
             out = stages[1](h2)
-            loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
+            loss = self.loss_fn(self._loss_in(out), y)
         ddp.partial_backward = True
         try:
             loss.backward()
@@ -150,7 +156,7 @@ class TrainStep:
         dev = x.device
         with autocast_ctx(dev, self.amp_dtype):
             out = self.model(x)
-            loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
+            loss = self.loss_fn(self._loss_in(out), y)
         loss.backward()
         return loss.detach()
 
@@ -160,7 +166,7 @@ class TrainStep:
                 self.opt.zero_grad(set_to_none=False)
             with autocast_ctx(x.device, self.amp_dtype):
                 out = self.model(x)
-                loss = self.loss_fn(out.float() if out.dtype != torch.float32 else out, y)
+                loss = self.loss_fn(self._loss_in(out), y)
             self.scaler.scale(loss).backward()
             self.scaler.step(self.opt)
             self.scaler.update()

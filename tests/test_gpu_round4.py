@@ -284,3 +284,23 @@ def test_gelu_dropout_one_pass_matches_fp32(p, dt):
     if p > 0:  # (GELU itself is exactly 0 below about -5.5 in fp32: count the mask, not h)
         frac = float((keep == 0).float().mean())
         assert abs(frac - p) < 0.02
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_fused_mse_loss_matches_fp32(dt):
+    """ops.losses.MSELoss (one native pass: mean + gradient 2(x - t)/n) vs nn.MSELoss in fp32."""
+    from hyperion.ops import _native
+    from hyperion.ops.losses import MSELoss
+
+    torch.manual_seed(0)
+    x = torch.randn(32, 1000, device="cuda").to(dt).requires_grad_(True)
+    t = torch.rand(32, 1000, device="cuda")
+    _native.reset_counters()
+    loss = MSELoss()(x, t)
+    (loss * 3.0).backward()
+    assert _native.counters().get("mse_fused") == 1
+    xr = x.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.mse_loss(xr, t)
+    (ref * 3.0).backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-6)
