@@ -26,7 +26,7 @@ def _timeit(step, steps: int, warmup: int) -> float:
 
 def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", steps: int = 20, warmup: int = 5,
                   model: str = "lm256", causal: bool = False, graph: bool = False,
-                  compute_copies: Optional[bool] = None) -> Dict:
+                  compute_copies: Optional[bool] = None, ddp_world1: bool = False, one_graph: bool = False) -> Dict:
     """SimpleTransformerLM (C14) training step as in train_language_model_ddp (single GPU).
     ``compute_copies`` (default for bf16): the parameters live in bf16 with fp32 masters inside
     FusedAdam (train.amp.cast_for_compute, as the ViT bench) instead of fp32 parameters cast by
@@ -45,6 +45,7 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
         from ..train.amp import cast_for_compute
 
         cast_for_compute(m, dt)
+    dpm = _ddp_world1(m) if ddp_world1 else None
     opt = FusedAdam(m.parameters(), lr=2e-4, weight_decay=0.01, adamw=True, zero_grad_in_step=graph)
     scaler = LossScaler(enabled=precision == "fp16", device=dev)
     ids = SyntheticWikiText2(n=batch, seq_len=seq, seed=0).input_ids.to(dev)
@@ -63,19 +64,17 @@ def bench_lm_step(batch: int = 32, seq: int = 128, precision: str = "fp16", step
             opt.step()
         return loss.detach()
 
-    from ..train.step import GraphedClosure
-
-    step = GraphedClosure(body, warmup=2, module=m) if graph else body
+    step = _graphed(body, m, dpm, one_graph) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
     return {"model": model, "batch": batch, "seq": seq, "precision": precision, "graph": graph,
-            "compute_copies": copies, "ms_per_step": t * 1e3,
+            "compute_copies": copies, "ms_per_step": t * 1e3, **_ddp_info(dpm), "one_graph": one_graph,
             "samples_per_s": batch / t, "tokens_per_s": batch * (seq - 1) / t,
             "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
 
 def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool = True, steps: int = 20,
-                   warmup: int = 5, graph: bool = False) -> Dict:
+                   warmup: int = 5, graph: bool = False, ddp_world1: bool = False, one_graph: bool = False) -> Dict:
     """ViT-B/16 bf16 + activation checkpointing (BASELINE.json config 3), MSE/Adam like C6.
     ``graph``: the whole step captured once as a hipGraph and replayed."""
     from ..models.vit import vit_b_16
@@ -88,6 +87,7 @@ def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool
     dt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(precision)
     if dt is not None:
         cast_for_compute(m, dt)
+    dpm = _ddp_world1(m) if ddp_world1 else None
     opt = FusedAdam(m.parameters(), lr=1e-3, zero_grad_in_step=graph)
     x = torch.rand(batch, 3, 224, 224, device=dev).contiguous(memory_format=torch.channels_last)
     x = x.to(dt) if dt is not None else x
@@ -100,13 +100,11 @@ def bench_vit_step(batch: int = 32, precision: str = "bf16", checkpointing: bool
         opt.step()
         return loss.detach()
 
-    from ..train.step import GraphedClosure
-
-    step = GraphedClosure(body, warmup=2, module=m) if graph else body
+    step = _graphed(body, m, dpm, one_graph) if graph else body
     torch.cuda.reset_peak_memory_stats()
     t = _timeit(step, steps, warmup)
     return {"model": "vit_b_16", "batch": batch, "precision": precision, "checkpointing": checkpointing,
-            "graph": graph, "ms_per_step": t * 1e3, "samples_per_s": batch / t,
+            "graph": graph, "ms_per_step": t * 1e3, "samples_per_s": batch / t, **_ddp_info(dpm),
             "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
 
@@ -152,6 +150,36 @@ def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmu
             "ms_per_step": t * 1e3, "samples_per_s": batch / t, "tokens_per_s": batch * seq / t,
             "trainable_params": trainable_parameters(m), "peak_mem_mb": torch.cuda.max_memory_allocated() / 2**20}
 
+
+
+
+def _ddp_world1(m):
+    """m's parameters under Hyperion DDP on one GPU: buckets on, native RCCL communicator."""
+    from ..parallel import DDP
+    from ..parallel.comm import NativeComm
+
+    _ensure_pg()
+    dev = next(m.parameters()).device
+    return DDP(m, buckets_at_world_1=True, comm=NativeComm(dev), broadcast_buffers=False)
+
+
+def _graphed(body, m, dpm, one_graph: bool = False):
+    """The step as one hipGraph — or, under DDP, as graph segments with the bucket all-reduces as
+    eager holes (train/segments.py: the trainers' capture of a data-parallel step).  one_graph:
+    DDP too as ONE graph, the native RCCL all-reduces recorded into it (stream fork / join)."""
+    if dpm is not None and not one_graph:
+        from ..train.segments import SegmentedStep
+
+        return SegmentedStep(body, warmup=2, module=m)
+    from ..train.step import GraphedClosure
+
+    return GraphedClosure(body, warmup=2, module=m)
+
+
+def _ddp_info(dpm) -> Dict:
+    if dpm is None:
+        return {}
+    return {"ddp_world1": True, "comm": type(dpm.comm).__name__, "buckets": len(dpm.bucket_sizes())}
 
 
 

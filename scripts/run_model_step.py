@@ -35,6 +35,14 @@ elif which == "llamagraph":
     r = M.bench_llama_lora_step(steps=5, warmup=3, graph=True)
 elif which == "llamagraph20":
     r = M.bench_llama_lora_step(steps=20, warmup=3, graph=True)
+elif which == "lmddp1":  # LM-256 graphed under DDP(buckets_at_world_1, NativeComm)
+    r = M.bench_lm_step(precision="bf16", graph=True, steps=20, warmup=5, ddp_world1=True)
+elif which == "lmddp1g":  # ... as ONE graph with the RCCL all-reduces captured
+    r = M.bench_lm_step(precision="bf16", graph=True, steps=20, warmup=5, ddp_world1=True, one_graph=True)
+elif which == "vitddp1g":
+    r = M.bench_vit_step(checkpointing=False, steps=20, warmup=5, graph=True, ddp_world1=True, one_graph=True)
+elif which == "vitddp1":
+    r = M.bench_vit_step(checkpointing=False, steps=20, warmup=5, graph=True, ddp_world1=True)
 elif which == "lmgraph":
     r = M.bench_lm_step(precision="bf16", graph=True, steps=20, warmup=5)
 elif which == "lm":
