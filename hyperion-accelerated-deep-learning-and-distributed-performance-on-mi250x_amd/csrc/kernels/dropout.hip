@@ -23,8 +23,8 @@ __device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.f + er
 // GEMM ran on the vendor library with a bias epilogue — one pass over the pre-activation instead
 // of torch's GELU kernel and a separate dropout pass)
 template <typename T, int MODE>
-__global__ __launch_bounds__(kThreads) void dropout_k(const T* __restrict__ x, T* __restrict__ y, int64_t n,
-                                                      uint32_t thr, float scale, RngState rs) {
+__device__ __forceinline__ void dropout_body(const T* __restrict__ x, T* __restrict__ y, int64_t n, uint32_t thr,
+                                             float scale, const RngState& rs) {
   const uint64_t key = rng_key(rs);
   const int64_t i0 = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 8;
   const int64_t stride = (int64_t)gridDim.x * kThreads * 8;
@@ -51,14 +51,31 @@ __global__ __launch_bounds__(kThreads) void dropout_k(const T* __restrict__ x, T
 }
 
 template <typename T, int MODE>
+__global__ __launch_bounds__(kThreads) void dropout_k(const T* __restrict__ x, T* __restrict__ y, int64_t n,
+                                                      uint32_t thr, float scale, RngState rs) {
+  dropout_body<T, MODE>(x, y, n, thr, scale, rs);
+}
+
+// mode 2 under its own name: an FFN's activation (+ its dropout), not a standalone dropout pass
+template <typename T>
+__global__ __launch_bounds__(kThreads) void gelu_dropout_k(const T* __restrict__ x, T* __restrict__ y, int64_t n,
+                                                           uint32_t thr, float scale, RngState rs) {
+  dropout_body<T, 2>(x, y, n, thr, scale, rs);
+}
+
+template <typename T, int MODE>
 hipError_t launch(const void* x, void* y, int64_t n, float p, const RngState& rs, hipStream_t st) {
   const uint32_t thr = (uint32_t)fminf(p * 4294967296.f, 4294967295.f);
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   int64_t blocks = (n + kThreads * 8 - 1) / (kThreads * 8);
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((dropout_k<T, MODE>), dim3((unsigned)blocks), dim3(kThreads), 0, st, static_cast<const T*>(x),
-                     static_cast<T*>(y), n, thr, scale, rs);
+  if (MODE == 2)
+    hipLaunchKernelGGL((gelu_dropout_k<T>), dim3((unsigned)blocks), dim3(kThreads), 0, st, static_cast<const T*>(x),
+                       static_cast<T*>(y), n, thr, scale, rs);
+  else
+    hipLaunchKernelGGL((dropout_k<T, MODE>), dim3((unsigned)blocks), dim3(kThreads), 0, st, static_cast<const T*>(x),
+                       static_cast<T*>(y), n, thr, scale, rs);
   return hipGetLastError();
 }
 

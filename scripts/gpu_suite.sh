@@ -1,0 +1,79 @@
+#!/bin/bash
+# One-GPU measurement suite (run through gpurun or on any MI355X box); every step has its own time
+# limit and a failing step ends the run.  Output under gpurun_out/suite/<stage>/.
+#
+#   bash scripts/gpu_suite.sh tests [pytest files ...]   GPU tests (default: every tests/test_gpu_*.py)
+#   bash scripts/gpu_suite.sh bench                      ResNet-50 bench.py, 50 timed steps
+#   bash scripts/gpu_suite.sh trace                      rocprofv3 kernel trace of the bench step (+ step table)
+#   bash scripts/gpu_suite.sh tune                       conv launch-plan tuning (HBM-cold) + A/B bench kept vs new
+#   bash scripts/gpu_suite.sh timeline                   per-workgroup conv timelines (diagnostic stamps)
+#   bash scripts/gpu_suite.sh models                     LM-256 / GPT-2 / ViT graphed steps (+ DDP at world 1)
+#   bash scripts/gpu_suite.sh fsdp                       FSDP steps: LM-256 / GPT-2 graphed, GPT-2 reshard, Llama-7B full
+#   bash scripts/gpu_suite.sh lmhead                     LM-head + CE schedules, GEMM epilogue probe
+#   bash scripts/gpu_suite.sh rccl                       RCCL reduce-scatter / all-reduce tail check
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+stage=${1:-bench}
+shift || true
+out=gpurun_out/suite/$stage
+mkdir -p "$out"
+
+json_ms() { grep -o '"ms_per_step": [0-9.]*' "$1" | head -1; }
+
+case $stage in
+tests)
+  files=${*:-tests/test_gpu_*.py}
+  timeout -k 10 1500 python -u -m pytest -x -q --timeout 300 --timeout-method thread $files > "$out/pytest.log" 2>&1
+  rc=$?; tail -3 "$out/pytest.log"; exit $rc
+  ;;
+bench)
+  timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 > "$out/bench.json" 2> "$out/bench.err" || exit 1
+  json_ms "$out/bench.json"
+  ;;
+trace)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$out/prof" -o run -- \
+    python3 bench.py --steps 10 --warmup 5 > "$out/bench.json" 2> "$out/bench.err" || exit 1
+  f=$(ls "$out"/prof/*/run_kernel_trace.csv 2>/dev/null || ls "$out"/prof/run_kernel_trace.csv) || exit 1
+  python3 scripts/step_trace.py "$f" --step -2 --out "$out/step.txt" > /dev/null && \
+  python3 scripts/kstats.py "$f" > "$out/kstats.txt" 2>&1 || exit 1
+  grep -E "step -2" "$out/step.txt"; head -20 "$out/kstats.txt" | cut -c1-160
+  ;;
+tune)
+  timeout -k 10 1000 python -u scripts/conv_tune.py --out "$out/conv_plans.json" --raw "$out/conv_tune_raw.json" \
+    > "$out/conv_tune.log" 2>&1 || exit 1
+  tail -5 "$out/conv_tune.log"
+  timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 > "$out/bench_kept.json" 2>/dev/null && \
+  HYPERION_CONV_PLANS=$PWD/$out/conv_plans.json timeout -k 10 300 python -u bench.py --steps 50 --warmup 10 \
+    > "$out/bench_new.json" 2>/dev/null || exit 1
+  echo kept $(json_ms "$out/bench_kept.json"); echo new $(json_ms "$out/bench_new.json")
+  ;;
+timeline)
+  timeout -k 10 200 python -u scripts/conv_timeline.py --out "$out/timeline.json" > "$out/timeline.log" 2>&1 || exit 1
+  tail -12 "$out/timeline.log" | cut -c1-200
+  ;;
+models)
+  for w in ${WL:-lmgraph gpt2 vitgraph lmddp1g vitddp1g}; do
+    timeout -k 10 300 python -u scripts/run_model_step.py $w > "$out/$w.json" 2> "$out/$w.err" || { tail -5 "$out/$w.err"; exit 1; }
+    echo $w $(json_ms "$out/$w.json")
+  done
+  ;;
+fsdp)
+  for cfg in "lm256 graph" "gpt2_small graph" "gpt2_small reshard" "gpt2_small graph coll" "llama7b_full curve"; do
+    timeout -k 10 400 python -u scripts/run_model_step.py fsdp $cfg >> "$out/fsdp_steps.jsonl" 2>> "$out/fsdp_steps.err" || exit 1
+  done
+  grep "^{" "$out/fsdp_steps.jsonl" | cut -c1-260
+  ;;
+lmhead)
+  timeout -k 10 300 python -u scripts/ce_bench.py --out "$out/ce_bench.json" > "$out/ce_bench.log" 2>&1 && \
+  timeout -k 10 300 python -u scripts/gemm_probe.py --out "$out/gemm_probe.json" > "$out/gemm_probe.log" 2>&1 || exit 1
+  grep -v amdgpu.ids "$out/ce_bench.log" | cut -c1-300
+  ;;
+rccl)
+  timeout -k 10 200 python -u scripts/rccl_avg_check.py > "$out/rccl.log" 2>&1 || exit 1
+  grep -E "^bad|^rs" "$out/rccl.log"
+  ;;
+*)
+  echo "unknown stage $stage"; exit 2
+  ;;
+esac
