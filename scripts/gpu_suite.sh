@@ -10,6 +10,7 @@
 #   bash scripts/gpu_suite.sh models                     LM-256 / GPT-2 / ViT graphed steps (+ DDP at world 1)
 #   bash scripts/gpu_suite.sh fsdp                       FSDP steps: LM-256 / GPT-2 graphed, GPT-2 reshard, Llama-7B full
 #   bash scripts/gpu_suite.sh lmhead                     LM-head + CE schedules, GEMM epilogue probe
+#   bash scripts/gpu_suite.sh baseline                   reference-methodology model benchmarks + fused-vs-eager
 #   bash scripts/gpu_suite.sh rccl                       RCCL reduce-scatter / all-reduce tail check
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -68,6 +69,13 @@ lmhead)
   timeout -k 10 300 python -u scripts/ce_bench.py --out "$out/ce_bench.json" > "$out/ce_bench.log" 2>&1 && \
   timeout -k 10 300 python -u scripts/gemm_probe.py --out "$out/gemm_probe.json" > "$out/gemm_probe.log" 2>&1 || exit 1
   grep -v amdgpu.ids "$out/ce_bench.log" | cut -c1-300
+  ;;
+baseline)
+  # the reference-methodology ResNet / CNN benchmark (fp32, torch and Hyperion kernels; bf16) and the
+  # fused-vs-eager inference study
+  PYTHONPATH=$PWD timeout -k 10 900 python -u -m hyperion.cli.bench_models --out "$out" --only baseline,fusion \
+    > "$out/bench_models.log" 2>&1 || { tail -20 "$out/bench_models.log"; exit 1; }
+  ls "$out"; tail -5 "$out/bench_models.log"
   ;;
 rccl)
   timeout -k 10 200 python -u scripts/rccl_avg_check.py > "$out/rccl.log" 2>&1 || exit 1
