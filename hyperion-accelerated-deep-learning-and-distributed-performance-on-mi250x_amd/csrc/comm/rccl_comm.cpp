@@ -324,6 +324,9 @@ class RcclComm {
 
   // comm stream waits for the producer stream; tensors are marked in use by the comm stream
   void begin(std::vector<at::Tensor> ts) {
+    // (under mu_: the watchdog may have aborted the communicator since the unlocked check())
+    if (wd_ && wd_->failed()) raise_comm_failure(wd_->error());
+    TORCH_CHECK(comm_ != nullptr, "hyperion RCCL communicator is destroyed");
     const at::DeviceGuard g(at::Device(at::kCUDA, device_));
     auto cur = c10::hip::getCurrentHIPStream(device_);
     hipEvent_t ready;

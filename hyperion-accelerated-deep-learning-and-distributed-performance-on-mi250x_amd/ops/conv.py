@@ -251,6 +251,10 @@ def _can_defer(w_param: Optional[torch.Tensor]) -> bool:
     if not (DEFER_WGRAD_REDUCE and w_param is not None and w_param.grad is None and not _streams.enabled()
             and not torch.is_grad_enabled()):
         return False
+    # a tensor hook on the weight sees dw before AccumulateGrad (and before any flush): its values
+    # must be final, so no deferral.  (Post-accumulate hooks — DDP / FSDP — call flush_wgrad first.)
+    if getattr(w_param, "_backward_hooks", None):
+        return False
     if not _defer_state["queued"]:
         try:
             torch.autograd.Variable._execution_engine.queue_callback(flush_wgrad)

@@ -304,3 +304,19 @@ def test_fused_mse_loss_matches_fp32(dt):
     (ref * 3.0).backward()
     torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-6)
+
+
+def test_weight_hook_sees_reduced_wgrad():
+    """A tensor hook on a conv weight receives the final weight gradient: the split-K wgrad reduce
+    is not deferred past it (ops/conv.py _can_defer), so the hooked value equals .grad."""
+    from hyperion.models.resnet import resnet18
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    seen = {}
+    w = m.layer1[0].conv1.weight
+    w.register_hook(lambda g: seen.__setitem__("g", g.detach().clone()))
+    x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    m(x).float().square().mean().backward()
+    torch.cuda.synchronize()
+    assert "g" in seen and torch.equal(seen["g"], w.grad)
