@@ -11,6 +11,7 @@
 #   bash scripts/gpu_suite.sh fsdp                       FSDP steps: LM-256 / GPT-2 graphed, GPT-2 reshard, Llama-7B full
 #   bash scripts/gpu_suite.sh lmhead                     LM-head + CE schedules, GEMM epilogue probe
 #   bash scripts/gpu_suite.sh baseline                   reference-methodology model benchmarks + fused-vs-eager
+#   bash scripts/gpu_suite.sh pmc                        PMC counter passes over ResNet-50 steps -> per-kernel table
 #   bash scripts/gpu_suite.sh rccl                       RCCL reduce-scatter / all-reduce tail check
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -76,6 +77,24 @@ baseline)
   PYTHONPATH=$PWD timeout -k 10 900 python -u -m hyperion.cli.bench_models --out "$out" --only baseline,fusion \
     > "$out/bench_models.log" 2>&1 || { tail -20 "$out/bench_models.log"; exit 1; }
   ls "$out"; tail -5 "$out/bench_models.log"
+  ;;
+pmc)
+  # counter passes (one run each, no tracing) over eager ResNet-50 bench steps -> per-kernel table
+  P1="SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_VALU_MFMA_BUSY_CYCLES,SQ_BUSY_CYCLES,SQ_INSTS_VALU_MFMA_MOPS_BF16,SQ_LDS_BANK_CONFLICT,GRBM_GUI_ACTIVE"
+  P2="SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_MFMA,SQ_WAVES,SQ_INST_LEVEL_VMEM,SQ_WAIT_INST_LDS,GRBM_GUI_ACTIVE"
+  P3="TCC_HIT_sum,TCC_MISS_sum,GRBM_GUI_ACTIVE"
+  P4="FETCH_SIZE,GRBM_GUI_ACTIVE"
+  P5="WRITE_SIZE,GRBM_GUI_ACTIVE"
+  i=0
+  for pass in "$P1" "$P2" "$P3" "$P4" "$P5"; do
+    i=$((i+1))
+    timeout -s KILL 150 rocprofv3 --pmc $pass --output-format csv -d "$PWD/$out/resnet50_P$i" -o run -- \
+      python3 bench.py --graph 0 --steps 3 --warmup 2 > "$out/pass_$i.log" 2>&1 || { echo "pass $i failed"; tail -3 "$out/pass_$i.log"; exit 1; }
+    f=$(ls "$out"/resnet50_P$i/*/run_counter_collection.csv 2>/dev/null | head -1)
+    [ -n "$f" ] && cp "$f" "$out/resnet50_P$i/run_counter_collection.csv"
+  done
+  python3 scripts/pmc_summary.py "$out" --out "$out/pmc_table.md" > /dev/null || exit 1
+  head -30 "$out/pmc_table.md" | cut -c1-260
   ;;
 rccl)
   timeout -k 10 200 python -u scripts/rccl_avg_check.py > "$out/rccl.log" 2>&1 || exit 1

@@ -14,6 +14,8 @@ combined across passes:
   HBM wr GB/s = WRITE_SIZE (KiB) / time
   L2 hit %    = TCC_HIT / (TCC_HIT + TCC_MISS)
   LDS conflict = SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS  (extra cycles per LDS instruction)
+  waves/CU    = SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8 * 256 CUs)  (mean resident waves per CU)
+  wait %      = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES  (wave-cycles stalled waiting on any instruction)
 """
 import argparse
 import csv
@@ -70,8 +72,8 @@ def main():
             m.update({kk: v for kk, v in c.items() if not kk.startswith("_")})
             m["_us_list"] = us
             m["_n"] = c["_n"]
-    lines = ["| target | kernel | dispatches | us/dispatch | MfmaUtil % | MFMA TF/s | HBM rd GB/s | HBM wr GB/s | L2 hit % | LDS confl/inst |",
-             "|---|---|---|---|---|---|---|---|---|---|"]
+    lines = ["| target | kernel | dispatches | us/dispatch | MfmaUtil % | MFMA TF/s | HBM rd GB/s | HBM wr GB/s | L2 hit % | LDS confl/inst | waves/CU | wait % |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for (t, k), c in sorted(merged.items()):
         us = min(c["_us_list"])  # the SQ pass perturbs timing least
         def g(name):
@@ -82,8 +84,11 @@ def main():
         wr = g("WRITE_SIZE") * 1024 / (us * 1e-6) / 1e9 if g("WRITE_SIZE") is not None else None
         hit = 100 * g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")) if g("TCC_HIT_sum") is not None and (g("TCC_HIT_sum") + g("TCC_MISS_sum")) > 0 else None
         lds = g("SQ_LDS_BANK_CONFLICT") / g("SQ_INSTS_LDS") if g("SQ_INSTS_LDS") else None
+        occ = g("SQ_WAVE_CYCLES") / (g("GRBM_GUI_ACTIVE") / 8 * 256) if g("SQ_WAVE_CYCLES") and g("GRBM_GUI_ACTIVE") else None
+        wait = 100 * g("SQ_WAIT_INST_ANY") / g("SQ_WAVE_CYCLES") if g("SQ_WAIT_INST_ANY") and g("SQ_WAVE_CYCLES") else None
         f = lambda v, p=1: "-" if v is None else f"{v:.{p}f}"  # noqa: E731
-        lines.append(f"| {t} | `{k}` | {c['_n']} | {us:.1f} | {f(util)} | {f(tf, 0)} | {f(rd, 0)} | {f(wr, 0)} | {f(hit)} | {f(lds, 2)} |")
+        lines.append(f"| {t} | `{k}` | {c['_n']} | {us:.1f} | {f(util)} | {f(tf, 0)} | {f(rd, 0)} | {f(wr, 0)} | {f(hit)} | "
+                     f"{f(lds, 2)} | {f(occ)} | {f(wait)} |")
     txt = "\n".join(lines)
     print(txt)
     if a.out:
