@@ -84,6 +84,7 @@ struct ConvArgs {
   int sd;                // DGRAD only: 2 = stride-2 data gradient by output phase (below), else 1
   int Hx, Wx;            // sd == 2: dX's spatial size (2P x 2Q); the tile grid is one phase's [N, P, Q]
   int nb;                // host only: LDS ring depth of this launch (0 = conv_set_stages / default 2)
+  int direct;            // host only: forward + statistics with the DIRECT store epilogue (see conv_fwd_k)
   uint64_t mq, mpq;      // 36-bit magic multipliers of Q and P*Q (0: plain division; see fdiv36)
   int group;             // M-tiles per tile-order group (see conv_fwd_group)
   int splits, steps_per_split;  // split-K over the reduction (splits > 1: fp32 partials, no STATS)
@@ -99,7 +100,8 @@ struct ConvArgs {
 };
 
 // Diagnostic per-workgroup timeline: s_memrealtime (100 MHz, chip-wide) at entry, before and
-// after the K loop and at the end, plus HW_ID / XCC_ID — 6 words per workgroup.  Never on in
+// after the K loop and at the end, plus HW_ID / XCC_ID, then (EPI 0 stores) after the epilogue's
+// LDS transpose and after its store loop — 8 words per workgroup.  Never on in
 // timed runs (the stamp's lgkmcnt(0) forbids overlaps); read its SHARES, not its length.
 __device__ __forceinline__ unsigned long long realtime_stamp() {
   unsigned long long t;
@@ -118,7 +120,12 @@ __device__ __forceinline__ unsigned long long realtime_stamp() {
 // softmax gradient written in place of the logits (see linear_ce)
 // LEAN (BN-backward epilogue only): mode 0/1 without an addend — no y / addend prefetch registers
 // (64x64: 119 -> 104 VGPR+AGPR, 128x64: 191 -> 158, one more resident wave per SIMD there)
-template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, int EPI = 0, bool LEAN = false>
+// DIRECT (forward + BN statistics only, no addend / affine): the epilogue stores the lane-pair
+// packed accumulators straight to global memory (32-byte row segments per 8 lanes) instead of
+// transposing the tile through LDS into 16-byte row chunks — no LDS round trip or barrier before
+// the stores (the transpose was ~2 us of a 1x1 forward tile's ~6 us)
+template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, int EPI = 0, bool LEAN = false,
+          bool DIRECT = false>
 __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (wave tile BM/2 x BN/2)
   constexpr int IA = BM / 32, IB = BN / 32;  // glds instructions per wave per slice
@@ -363,22 +370,27 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   __syncthreads();  // the epilogue reuses the ring
   if (a.stamps != nullptr) tsc = realtime_stamp();
   // (the end stamp is written when the kernel returns, on every epilogue path)
+  unsigned long long tsd = 0, tse = 0;
   struct StampEnd {
     const ConvArgs& a;
     unsigned long long s0, s1, s2;
+    const unsigned long long& s4;
+    const unsigned long long& s5;
     __device__ ~StampEnd() {
       if (a.stamps != nullptr && threadIdx.x == 0) {
         const unsigned long long s3 = realtime_stamp();
-        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 6;
+        unsigned long long* o = a.stamps + (size_t)blockIdx.x * 8;
         o[0] = s0;
         o[1] = s1;
         o[2] = s2;
         o[3] = s3;
         o[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
         o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        o[6] = s4;
+        o[7] = s5;
       }
     }
-  } stamp_end{a, tsa, tsb, tsc};
+  } stamp_end{a, tsa, tsb, tsc, tsd, tse};
 
   if (EPI != 0) {
     // ---- fused linear + cross-entropy.  Class n0 + n of this tile is vocabulary index
@@ -515,7 +527,12 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
             float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, odd ? v[ep] : v[ep + 1]), 0xB1, 0xF, 0xF, false));
         const int lr = wm * (BM / 2) + i * 16 + c4 * 4 + ep + (odd ? 1 : 0);
         const uint32_t pk = pack2<T>(odd ? got : v[ep], odd ? v[ep + 1] : got);
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(tile) + lr * kLd + lc) = pk;
+        if (DIRECT) {
+          if (m0 + lr < a.M && n0 + lc < a.K)
+            *reinterpret_cast<uint32_t*>(a.out + (int64_t)(m0 + lr) * a.K + n0 + lc) = pk;
+        } else {
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<T*>(tile) + lr * kLd + lc) = pk;
+        }
       }
     }
   }
@@ -538,6 +555,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
   __syncthreads();
+  if (a.stamps != nullptr) tsd = realtime_stamp();
   // one no-return f64 atomic per channel per tile, issued BEFORE the tile's stores so their
   // ~1 us memory-side latency overlaps the store phase instead of extending the workgroup's drain
   if (FSTATS && tid < BN) {
@@ -548,6 +566,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       unsafeAtomicAdd(a.psq + slot + k, (double)(red[1 * BN + tid] + red[3 * BN + tid]));
     }
   }
+  if (DIRECT) return;  // (stored above; the statistics atomics are issued)
   // BNB: every thread keeps ONE 8-channel chunk column (kThreads % kChunksPerRow == 0) across its rows
   float bs[8], bq[8];
   if (BNB) {
@@ -607,6 +626,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       *reinterpret_cast<uint4*>(a.out + orow(m) * a.K + k) = v;
     }
   }
+  if (a.stamps != nullptr) tse = realtime_stamp();
   if (BNB) {
     // column sums: the lanes of a wave that share a chunk column (lane % kChunksPerRow) by xor
     // shuffles, then the 4 waves through LDS in fixed order
@@ -652,6 +672,9 @@ hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) 
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   else if (dgrad)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
+  else if (stats && a.direct)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, false, NB, 0, false, true>), dim3(tiles), dim3(kThreads), 0, st,
+                       a);
   else if (stats)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, false, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   else
@@ -756,6 +779,9 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
     a.mq = exact ? magic36(Q) : 0;
     a.mpq = exact ? magic36(P * Q) : 0;
   }
+  // nb: LDS ring depth 1..4 (0 = automatic); + 16: the DIRECT store epilogue (forward + statistics)
+  a.direct = (nb & 16) && psum != nullptr && !dgrad && addend == nullptr && !aff ? 1 : 0;
+  nb &= 15;
   a.nb = (nb >= 1 && nb <= 4) ? nb : 0;
   a.Hx = Hx;
   a.Wx = Wx;

@@ -1,5 +1,6 @@
 """Per-workgroup timeline of one conv_fwd launch (diagnostic stamps, csrc/kernels/conv_igemm.hip):
-entry / before K loop / after K loop / end in s_memrealtime ticks (100 MHz) plus HW_ID / XCC_ID.
+entry / before K loop / after K loop / end in s_memrealtime ticks (100 MHz) plus HW_ID / XCC_ID, and
+inside the epilogue: after the LDS transpose and after the store loop (8 words per workgroup).
 
 Prints, per configuration, the kernel span, the per-workgroup phase medians (prologue, K loop,
 epilogue), how many workgroups ran concurrently per CU, and how long a K step takes.  The stamp's
@@ -42,6 +43,11 @@ def analyse(st):
     pro = (s[:, 1] - s[:, 0]).tolist()
     loop = (s[:, 2] - s[:, 1]).tolist()
     epi = (s[:, 3] - s[:, 2]).tolist()
+    sd = (st[:, 6:8] - t0).double() * 10.0 / 1000.0
+    has = st[:, 6] != 0
+    transp = (sd[has, 0] - s[has, 2]).tolist()
+    stores = (sd[has, 1] - sd[has, 0]).tolist()
+    tail = (s[has, 3] - sd[has, 1]).tolist()
     tot = (s[:, 3] - s[:, 0]).tolist()
     # concurrency per CU: max overlapping [start, end) intervals among workgroups on one CU
     per_cu = {}
@@ -60,6 +66,9 @@ def analyse(st):
     return {
         "wgs": int(st.shape[0]), "cus_used": len(per_cu), "span_us": round(float(s[:, 3].max()), 2),
         "prologue_us_med": round(med(pro), 2), "loop_us_med": round(med(loop), 2), "epilogue_us_med": round(med(epi), 2),
+        "epi_transpose_us_med": round(med(transp), 2) if transp else None,
+        "epi_stores_us_med": round(med(stores), 2) if stores else None,
+        "epi_tail_us_med": round(med(tail), 2) if tail else None,
         "wg_total_us_med": round(med(tot), 2), "wg_total_us_max": round(max(tot), 2),
         "max_concurrent_per_cu": max(conc), "median_concurrent_per_cu": med(conc),
         "last_start_us": round(starts[-1], 2), "start_p50_us": round(starts[len(starts) // 2], 2),
@@ -72,7 +81,7 @@ def main():
     a = ap.parse_args()
     C_ = _native.native()
     rows = []
-    buf = torch.zeros(200000 * 6, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(200000 * 8, dtype=torch.int64, device="cuda")
     for (op, N, C, H, K, R, s, p, bm, bn, sp) in CASES:
         x = torch.randn(N, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         w = (torch.randn(K, C, R, R, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
@@ -97,7 +106,7 @@ def main():
         run()
         torch.cuda.synchronize()
         C_.conv_set_stamps(None)
-        st = buf.view(-1, 6).cpu()
+        st = buf.view(-1, 8).cpu()
         nk = R * R * C // 64
         P = (H + 2 * p - R) // s + 1
         r = dict(op=op, N=N, C=C, H=H, K=K, R=R, stride=s, pad=p, bm=bm, bn=bn, splits=sp, nk=nk, M=N * P * P)

@@ -63,8 +63,8 @@ def main():
         # ---- forward + BN statistics
         nk = R * R * C // 64
         fwd = {}
-        for cfg in configs(nk):
-            bm, bn, sp, nb = cfg
+        for cfg in configs(nk) + [(bm, bn, 1, nb + 16) for (bm, bn, sp, nb) in configs(nk) if sp == 1]:
+            bm, bn, sp, nb = cfg  # (nb + 16: the DIRECT store epilogue)
             fwd[cfg] = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True, bm, bn, sp, sums=sums, stages=nb))
         auto = gtime(lambda: C_.conv_fwd(x, w, s, s, p, p, True, sums=sums))
         best = min(fwd, key=fwd.get)

@@ -310,9 +310,11 @@ def test_weight_hook_sees_reduced_wgrad():
     """A tensor hook on a conv weight receives the final weight gradient: the split-K wgrad reduce
     is not deferred past it (ops/conv.py _can_defer), so the hooked value equals .grad."""
     from hyperion.models.resnet import resnet18
+    from hyperion.train.amp import cast_for_compute
 
     torch.manual_seed(0)
-    m = resnet18(num_classes=10).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
     seen = {}
     w = m.layer1[0].conv1.weight
     w.register_hook(lambda g: seen.__setitem__("g", g.detach().clone()))
@@ -320,3 +322,29 @@ def test_weight_hook_sees_reduced_wgrad():
     m(x).float().square().mean().backward()
     torch.cuda.synchronize()
     assert "g" in seen and torch.equal(seen["g"], w.grad)
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 28, 256, 1, 1, 0), (8, 128, 14, 128, 3, 1, 1), (4, 256, 14, 512, 1, 2, 0),
+                                   (3, 64, 9, 64, 3, 1, 1)])
+@pytest.mark.parametrize("tile", [(64, 64), (128, 64), (128, 128)])
+def test_conv_fwd_direct_store_epilogue_bitwise(shape, tile):
+    """The DIRECT forward epilogue (accumulator lane pairs stored straight to global, stages + 16)
+    writes the same output and BN-statistics sums as the LDS-transposed store epilogue, bit for bit
+    (same rounding, same summation order), including partial edge tiles."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    N, Cin, H, K, R, s, p = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, Cin, R, R, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for stages in (2, 18):
+        sums = torch.zeros(_native.STAT_SLOTS * 2 * K, device="cuda", dtype=torch.float64)
+        y = C.conv_fwd(x, w, s, s, p, p, True, tile[0], tile[1], 1, sums=sums, stages=stages)[0]
+        outs.append((y.clone(), sums.clone()))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-12, atol=1e-9)  # f64 atomics: order may vary
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), stride=s, padding=p)
+    torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2)
