@@ -19,7 +19,11 @@ int plan_splits(int M, int K, int nk, int bm, int bn, int64_t splits_req) {
 // [kStatSlots, K] slot partials).  The statistics are ADDED into `sums` ([kStatSlots*2*K] fp64, zeroed).
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t sh, int64_t sw, int64_t ph,
                                  int64_t pw, bool stats, int64_t bm_req, int64_t bn_req, int64_t splits_req,
-                                 const c10::optional<at::Tensor>& sums, int64_t stages) {
+                                 const c10::optional<at::Tensor>& sums, int64_t stages,
+                                 const c10::optional<at::Tensor>& xf_sums, const c10::optional<at::Tensor>& xf_w,
+                                 const c10::optional<at::Tensor>& xf_b, const c10::optional<at::Tensor>& xf_rm,
+                                 const c10::optional<at::Tensor>& xf_rv, double xf_momentum, double xf_eps,
+                                 const c10::optional<at::Tensor>& xf_out, const c10::optional<at::Tensor>& xf_stats) {
   HYP_CHECK_CUDA_TENSOR(x);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: 4D tensors");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -46,11 +50,49 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   at::Tensor acc, slabs;
   if (stats) acc = stats_sums(sums, K, x);
   if (splits > 1) slabs = at::empty({splits, M, K}, x.options().dtype(at::kFloat));
+  // xf_sums: x is the RAW output of a conv whose training BN (+ ReLU) this conv applies to its input
+  // as it reads it (hyp_kernels.h ConvInXform); xf_stats [2, C] fp32 receives save_mean / invstd,
+  // xf_out (optional, x's shape) the transformed activation
+  hyp::ConvInXform xf;
+  const bool has_xf = xf_sums.has_value() && xf_sums->defined();
+  if (has_xf) {
+    TORCH_CHECK(xf_sums->scalar_type() == at::kDouble && xf_sums->is_contiguous() &&
+                    xf_sums->numel() == 2 * C * hyp::kStatSlots && xf_sums->device() == x.device(),
+                "conv_fwd: xf_sums must be a contiguous fp64 [kStatSlots * 2 * C] tensor on x's device");
+    TORCH_CHECK(xf_stats.has_value() && xf_stats->scalar_type() == at::kFloat && xf_stats->is_contiguous() &&
+                    xf_stats->numel() == 2 * C,
+                "conv_fwd: xf_stats must be a contiguous fp32 [2, C] tensor");
+    TORCH_CHECK(C <= hyp::kXfMaxC, "conv_fwd: input transform supports at most ", hyp::kXfMaxC, " channels");
+    auto chk = [&](const c10::optional<at::Tensor>& t, const char* nm) -> float* {
+      if (!t.has_value() || !t->defined()) return nullptr;
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, "conv_fwd: ", nm,
+                  " must be a contiguous fp32 [C] tensor");
+      return t->data_ptr<float>();
+    };
+    xf.sums = xf_sums->data_ptr<double>();
+    xf.weight = chk(xf_w, "xf_w");
+    xf.bias = chk(xf_b, "xf_b");
+    xf.running_mean = chk(xf_rm, "xf_rm");
+    xf.running_var = chk(xf_rv, "xf_rv");
+    TORCH_CHECK((xf.running_mean == nullptr) == (xf.running_var == nullptr), "conv_fwd: xf_rm and xf_rv together");
+    xf.momentum = (float)xf_momentum;
+    xf.eps = (float)xf_eps;
+    xf.save_mean = xf_stats->data_ptr<float>();
+    xf.save_invstd = xf_stats->data_ptr<float>() + C;
+    if (xf_out.has_value() && xf_out->defined()) {
+      TORCH_CHECK(xf_out->sizes() == x.sizes() && xf_out->scalar_type() == x.scalar_type() &&
+                      xf_out->is_contiguous(at::MemoryFormat::ChannelsLast) && !xf_out->is_same(x),
+                  "conv_fwd: xf_out must be a separate channels-last tensor shaped like x");
+      TORCH_CHECK(sh == 1 && sw == 1 && 2 * ph == R - 1 && 2 * pw == S - 1,
+                  "conv_fwd: xf_out needs stride 1 and 'same' padding (the centre tap covers every pixel)");
+      xf.out = xf_out->data_ptr();
+    }
+  }
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), device_zero_page(x.device()),
                               stats ? acc.data_ptr<double>() : nullptr, stats ? acc.data_ptr<double>() + K : nullptr, N, H,
                               W, C, K, P, Q, R, S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, 0, splits,
                               splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f, nullptr, nullptr,
-                              nullptr, 0, 1, 0, 0, (int)stages));
+                              nullptr, 0, 1, 0, 0, (int)stages, has_xf ? &xf : nullptr));
   if (!stats) return {y, at::Tensor(), at::Tensor()};
   return {y, acc.select(1, 0), acc.select(1, 1)};  // [kStatSlots, K] each: .sum(0) = per-channel totals
 }
@@ -651,7 +693,14 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_fwd", &conv_fwd, "NHWC implicit-GEMM conv on MFMA (+ BN statistics partials)", pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
         pybind11::arg("stats"), pybind11::arg("bm") = -1, pybind11::arg("bn") = -1, pybind11::arg("splits") = -1,
-        pybind11::arg("sums") = pybind11::none(), pybind11::arg("stages") = 0);
+        pybind11::arg("sums") = pybind11::none(), pybind11::arg("stages") = 0,
+        pybind11::arg("xf_sums") = pybind11::none(), pybind11::arg("xf_w") = pybind11::none(),
+        pybind11::arg("xf_b") = pybind11::none(), pybind11::arg("xf_rm") = pybind11::none(),
+        pybind11::arg("xf_rv") = pybind11::none(), pybind11::arg("xf_momentum") = 0.1,
+        pybind11::arg("xf_eps") = 1e-5, pybind11::arg("xf_out") = pybind11::none(),
+        pybind11::arg("xf_stats") = pybind11::none());
+  m.def("conv_set_xf_debug", [](int64_t bits) { hyp::conv_set_xf_debug((int)bits); },
+        "diagnostic: disable parts of the fused input transform (1 transform, 2 finalize, 4 side store)");
   m.def("conv_fwd_affine", &conv_fwd_affine, "eval conv + folded BN affine (+ residual) (+ ReLU), one launch",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
         pybind11::arg("pw"), pybind11::arg("scale"), pybind11::arg("shift"),

@@ -179,18 +179,39 @@ namespace hyp {
 // stats come from the split-K reduce.
 bool conv_fwd_supported(int C, int K);
 void conv_set_stages(int nb);        // LDS pipeline depth 2..4 (0 = automatic); tuning only
+void conv_set_xf_debug(int bits);    // XF diagnostics: 1 skip the transform, 2 the finalize, 4 the side store
 void conv_wgrad_set_stages(int nb);
 void conv_fwd_tile(int M, int K, int* bm, int* bn);
 // addend (optional, splits == 1, no stats): out [M, K] += addend after rounding (fused residual grad).
 // dgrad != 0: stride-1 data gradient; "in" is dY [N,H,W,C], "w" the ORIGINAL filter [C][R][S][K]
 // (read flipped and transposed in-kernel), (ph, pw) the dgrad padding R-1-p.
 // bnb (dgrad only): the BatchNorm-backward epilogue above (any split count).
+// Training BatchNorm + ReLU of the conv's INPUT, applied as its A operand is read (forward only):
+// the conv reads the producer's raw conv output x and computes with relu(x * scale + shift),
+// scale / shift finalized inline from the producer's statistics sums (bn_fin.h arithmetic; the
+// workgroup with blockIdx 0 also writes save_mean / save_invstd and the running statistics).
+// out (optional): the transformed activation [N, H, W, C] is stored there as a side output —
+// by the workgroups of the first output-channel tile, at the filter's centre tap, which covers
+// every input pixel exactly once when stride == 1 and the padding is (R-1)/2, (S-1)/2.
+struct ConvInXform {
+  const double* sums = nullptr;  // [kStatSlots][2][C] Σx, Σx² of the producer
+  const float* weight = nullptr;
+  const float* bias = nullptr;
+  float* running_mean = nullptr;
+  float* running_var = nullptr;
+  float momentum = 0.1f, eps = 1e-5f;
+  float* save_mean = nullptr;
+  float* save_invstd = nullptr;
+  void* out = nullptr;
+};
+constexpr int kXfMaxC = 512;  // input channels of a transformed conv (the scale / shift table in LDS)
+
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
                     const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr,
                     const struct BnBwdEpilogue* bnb = nullptr, int pix = 0, int dgrad_stride = 1, int Hx = 0,
-                    int Wx = 0, int nb = 0);
+                    int Wx = 0, int nb = 0, const ConvInXform* xf = nullptr);
 // dgrad_stride 2 (dgrad only, no split-K / alpha / rank-r epilogue): the stride-2 data gradient as its
 // 4 output-phase sub-convolutions in one launch; (H, W, P, Q) are dY's (H, W) and the phase grid
 // (P, Q) = (Hx / 2, Wx / 2) of dX [N, Hx, Wx, K], (ph, pw) the FORWARD padding, w the original filter.

@@ -26,6 +26,7 @@
 //                      (M <= 2048: one register-resident launch does all of it)
 #include "hyp_common.h"
 #include "hyp_kernels.h"
+#include "bn_fin.h"
 
 namespace hyp {
 namespace {
@@ -95,49 +96,6 @@ bool stats_geom(int64_t M, int C, BnGeom& g) {
   g.rows_per_block = (M + P - 1) / P;
   g.P = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
   return true;
-}
-
-// ---------------------------------------------------------------- inline finalize
-struct FwdFin {
-  const double* sums;  // [kStatSlots][2][C]: Σx, Σx²
-  const float* weight;
-  const float* bias;
-  float* running_mean;
-  float* running_var;
-  float momentum, eps;
-  float* save_mean;
-  float* save_invstd;
-  double invM;    // 1 / M
-  double unbias;  // M / (M - 1): the running variance is unbiased
-};
-
-// scale / shift of channel c (the arithmetic the backward's ReluMask repeats bit for bit: invstd
-// and mean rounded to float, scale = w*invstd, shift = b - mean*scale).  `writer`: also store
-// save_mean / save_invstd and update the running statistics.
-__device__ __forceinline__ void fwd_const1(const FwdFin& f, int C, int c, bool writer, float& sc, float& sh) {
-  double a = 0.0, b2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < kStatSlots; ++k) {  // fixed order
-    a += f.sums[(int64_t)k * 2 * C + c];
-    b2 += f.sums[(int64_t)k * 2 * C + C + c];
-  }
-  const double mean = a * f.invM;
-  double var = b2 * f.invM - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-  const float w = f.weight ? f.weight[c] : 1.f;
-  const float b = f.bias ? f.bias[c] : 0.f;
-  const float s = w * invstd;
-  sc = s;
-  sh = b - (float)mean * s;
-  if (writer) {
-    f.save_mean[c] = (float)mean;
-    f.save_invstd[c] = invstd;
-    if (f.running_mean != nullptr) {
-      f.running_mean[c] = (float)((1.0 - f.momentum) * f.running_mean[c] + f.momentum * mean);
-      f.running_var[c] = (float)((1.0 - f.momentum) * f.running_var[c] + f.momentum * var * f.unbias);
-    }
-  }
 }
 
 struct BwdFin {

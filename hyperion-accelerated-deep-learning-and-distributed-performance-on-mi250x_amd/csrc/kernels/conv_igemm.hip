@@ -23,6 +23,7 @@
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 #include "mfma_lds.h"
+#include "bn_fin.h"
 
 namespace hyp {
 namespace {
@@ -97,7 +98,39 @@ struct ConvArgs {
   int kvalid;                   // B rows that exist (< K only for a padded linear-CE vocabulary chunk)
   CeEpilogue ce;                // EPI 1 / 2: fused linear + cross-entropy (see linear_ce)
   unsigned long long* stamps;   // diagnostic timeline (conv_set_stamps), null in normal runs
+  // XF: the input BatchNorm + ReLU applied to the A operand (hyp_kernels.h ConvInXform)
+  FwdFin xfin;                  // the producer's statistics -> scale / shift (bn_fin.h)
+  uint16_t* xf_out;             // side output relu(x * scale + shift) [N, H, W, C], or null
+  int xf_on;
+  int xf_dbg;                   // diagnostic (conv_set_xf_debug): 1 no transform, 2 no finalize, 4 no side store
 };
+
+// relu(v * scale + shift) of 8 consecutive channels, rounded to T: the fp32 FMAs as packed pairs
+// (v_pk_fma_f32), then the ReLU on the rounded 16-bit pairs as a signed-integer max with 0
+// (v_pk_max_i16: a negative bf16 / f16 is a negative int16, -0 included) — the same values as the
+// standalone apply's round(max(fma, 0)) for every finite input (a NaN stays NaN here)
+typedef float xf_f2 __attribute__((ext_vector_type(2)));
+typedef short xf_s2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ u16x8 xf_apply(u16x8 v, const xf_f2 (&sc)[4], const xf_f2 (&sh)[4]) {
+  const uint4 w = __builtin_bit_cast(uint4, v);
+  const uint32_t wi[4] = {w.x, w.y, w.z, w.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    xf_f2 f;
+    if constexpr (sizeof(T) == 2 && __is_same(T, bf16_t)) {
+      f = xf_f2{__uint_as_float(wi[q] << 16), __uint_as_float(wi[q] & 0xffff0000u)};
+    } else {
+      f = xf_f2{f16_lo(wi[q]), f16_hi(wi[q])};
+    }
+    f = __builtin_elementwise_fma(f, sc[q], sh[q]);
+    const uint32_t pk = __is_same(T, bf16_t) ? pack_bf16x2(f.x, f.y) : pack_f16x2(f.x, f.y);
+    const xf_s2 r = __builtin_elementwise_max(__builtin_bit_cast(xf_s2, pk), xf_s2{0, 0});
+    o[q] = __builtin_bit_cast(uint32_t, r);
+  }
+  return __builtin_bit_cast(u16x8, (uint4){o[0], o[1], o[2], o[3]});
+}
 
 // Diagnostic per-workgroup timeline: s_memrealtime (100 MHz, chip-wide) at entry, before and
 // after the K loop and at the end, plus HW_ID / XCC_ID, then (EPI 0 stores) after the epilogue's
@@ -120,12 +153,18 @@ __device__ __forceinline__ unsigned long long realtime_stamp() {
 // softmax gradient written in place of the logits (see linear_ce)
 // LEAN (BN-backward epilogue only): mode 0/1 without an addend — no y / addend prefetch registers
 // (64x64: 119 -> 104 VGPR+AGPR, 128x64: 191 -> 158, one more resident wave per SIMD there)
+// XF (forward only): the A operand is the producer's raw conv output, transformed at fragment-read
+// time into relu(x * scale + shift) — the training BatchNorm apply + ReLU of the previous layer
+// fused into this conv (no standalone apply pass: one launch and one read + write of the
+// activation fewer).  scale / shift are finalized per workgroup from the producer's statistics
+// sums into an LDS table; the first output-channel tile's workgroups also store the transformed
+// activation (the backward's saved input) at the centre tap.
 // DIRECT (forward + BN statistics only, no addend / affine): the epilogue stores the lane-pair
 // packed accumulators straight to global memory (32-byte row segments per 8 lanes) instead of
 // transposing the tile through LDS into 16-byte row chunks — no LDS round trip or barrier before
 // the stores (the transpose was ~2 us of a 1x1 forward tile's ~6 us)
 template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, int EPI = 0, bool LEAN = false,
-          bool DIRECT = false>
+          bool DIRECT = false, bool XF = false>
 __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
   constexpr int FM = BM / 32, FN = BN / 32;  // 16x16 fragments per wave (wave tile BM/2 x BN/2)
   constexpr int IA = BM / 32, IB = BN / 32;  // glds instructions per wave per slice
@@ -260,11 +299,39 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // XF: channel tid's statistics loads go out ahead of the first stages (their arithmetic runs
+  // after the stage issue, so the two round trips overlap); channels >= 256 (C = 512) after
+  __shared__ float xtab[XF ? 2 * kXfMaxC : 1];  // [scale | shift] of the input channels
+  double xsa[kStatSlots], xsq[kStatSlots];
+  float xw = 0.f, xb = 0.f;
+  if constexpr (XF) {
+    if (tid < a.C && !(a.xf_dbg & 2)) fwd_const_load(a.xfin, a.C, tid, xsa, xsq, xw, xb);
+  }
+  __builtin_amdgcn_sched_barrier(0);
   // NB-deep ring: stage t+NB-1 is issued right after the barrier that retires stage t-1's buffer
   // (NB == 1: stage 0 is issued here too, ahead of the epilogue loads below)
 #pragma unroll
   for (int i = 0; i < (NB > 1 ? NB - 1 : 1); ++i)
     if (i < nk) stage(smem + i * kBuf);
+  __builtin_amdgcn_sched_barrier(0);
+  // XF: the consumed stage's filter tap / channel slice, advanced per K step
+  int cs_r = 0, cs_s = 0, cs_c0 = 0;
+  bool xside = false;
+  if constexpr (XF) {
+    const bool writer = blockIdx.x == 0;
+    if (a.xf_dbg & 2) {
+      for (int c = tid; c < a.C; c += kThreads) xtab[c] = 1.f, xtab[kXfMaxC + c] = 0.f;
+    } else {
+      if (tid < a.C) fwd_const_from(a.xfin, tid, xsa, xsq, xw, xb, writer, xtab[tid], xtab[kXfMaxC + tid]);
+      for (int c = tid + kThreads; c < a.C; c += kThreads) fwd_const1(a.xfin, a.C, c, writer, xtab[c], xtab[kXfMaxC + c]);
+    }
+    mfl::barrier_keep_vm();  // the table is read before the K loop's first barrier (xf_pass)
+    const int rs = kt0 / cpb;
+    cs_c0 = (kt0 - rs * cpb) * kBK;
+    cs_r = rs / a.S;
+    cs_s = rs - cs_r * a.S;
+    xside = a.xf_out != nullptr && tn == 0 && !(a.xf_dbg & 4);
+  }
   // Epilogue operand prefetch: the addend / BN-backward x, y chunks this thread will store, issued
   // BEFORE the K loop so their HBM round trip overlaps the loads and MFMAs of the whole tile
   // (issued after the loop, the BN-backward epilogue waited ~2 us for x on every workgroup; inside
@@ -332,6 +399,47 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
     }
   }
 
+  // XF: every thread transforms, in place, the A chunks its own LDS-DMA wrote (row
+  // (i*4 + wave)*8 + lane/8, physical 16-byte slot lane%8 = logical chunk slot ^ swz(row)) once its
+  // own loads have landed and BEFORE the barrier that publishes the stage: each element is
+  // transformed once, the K loop's fragment reads and MFMAs stay as they are.  Padding taps and
+  // rows past M read the zero page and stay zero.
+  auto xf_pass = [&](uint16_t* buf) {
+    if (a.xf_dbg & 1) return;
+    const bool center = xside && cs_r == a.ph && cs_s == a.pw;
+    // the thread's logical chunk is the same in all IA rows (swz = (row >> 1) & 7, rows 32 apart)
+    const int cb = cs_c0 + ((slot ^ swz(wave * 8 + (lane >> 3))) << 3);
+    xf_f2 sc[4], sh[4];
+    {
+      const float4* ps = reinterpret_cast<const float4*>(xtab + cb);
+      const float4* pt = reinterpret_cast<const float4*>(xtab + kXfMaxC + cb);
+      const float4 s0 = ps[0], s1 = ps[1], t0 = pt[0], t1 = pt[1];
+      sc[0] = xf_f2{s0.x, s0.y}; sc[1] = xf_f2{s0.z, s0.w}; sc[2] = xf_f2{s1.x, s1.y}; sc[3] = xf_f2{s1.z, s1.w};
+      sh[0] = xf_f2{t0.x, t0.y}; sh[1] = xf_f2{t0.z, t0.w}; sh[2] = xf_f2{t1.x, t1.y}; sh[3] = xf_f2{t1.z, t1.w};
+    }
+    u16x8 v[IA];
+    bool ok[IA];
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {  // every read first (no write can alias a later read)
+      const int h = a_h0[i] + cs_r, w = a_w0[i] + cs_s;
+      ok[i] = a_ok[i] & ((unsigned)h < (unsigned)a.H) & ((unsigned)w < (unsigned)a.W);
+      v[i] = *reinterpret_cast<const u16x8*>(buf + (i * 4 + wave) * 8 * kBK + lane * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      if (ok[i]) {  // padding taps / rows past M read the zero page and stay zero
+        v[i] = xf_apply<T>(v[i], sc, sh);
+        *reinterpret_cast<u16x8*>(buf + (i * 4 + wave) * 8 * kBK + lane * 8) = v[i];
+      }
+    }
+    if (center) {  // centre tap: this row's input pixel is its output pixel (stride 1, "same" padding)
+#pragma unroll
+      for (int i = 0; i < IA; ++i)
+        if (ok[i])
+          *reinterpret_cast<u16x8*>(a.xf_out + (int64_t)(m0 + (i * 4 + wave) * 8 + (lane >> 3)) * a.C + cb) = v[i];
+    }
+  };
+
   const int r16 = lane & 15, c4 = lane >> 4;
   if (a.stamps != nullptr) tsb = realtime_stamp();
   for (int t = 0; t < nk; ++t) {
@@ -343,9 +451,11 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
         stage(smem);
       }
       mfl::wait_vmcnt<0>();
+      if constexpr (XF) xf_pass(smem);
       mfl::barrier_keep_vm();
     } else {
       mfl::wait_stage<IA + IB, NB>(min(NB - 2, nk - 1 - t));
+      if constexpr (XF) xf_pass(smem + (t % NB) * kBuf);
       mfl::barrier_keep_vm();  // stage t visible to all waves; every wave is done with buffer (t-1) % NB
       if (t + NB - 1 < nk) stage(smem + ((t + NB - 1) % NB) * kBuf);
     }
@@ -365,6 +475,16 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mma<T>(fa[i], fb[j], acc[i][j]);
+    }
+    if constexpr (XF) {  // the next consumed stage's tap / channel slice
+      cs_c0 += kBK;
+      if (cs_c0 == a.C) {
+        cs_c0 = 0;
+        if (++cs_s == a.S) {
+          cs_s = 0;
+          ++cs_r;
+        }
+      }
     }
   }
   __syncthreads();  // the epilogue reuses the ring
@@ -666,7 +786,13 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_k(const ConvArgs a) {
 template <typename T, int BM, int BN, int NB>
 hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.K + BN - 1) / BN) * a.splits;
-  if (dgrad && stats && a.bnb.mode <= 1 && a.addend == nullptr)
+  if (a.xf_on && stats)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, false, NB, 0, false, false, true>), dim3(tiles), dim3(kThreads), 0,
+                       st, a);
+  else if (a.xf_on)
+    hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, false, NB, 0, false, false, true>), dim3(tiles), dim3(kThreads), 0,
+                       st, a);
+  else if (dgrad && stats && a.bnb.mode <= 1 && a.addend == nullptr)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, true, NB, 0, true>), dim3(tiles), dim3(kThreads), 0, st, a);
   else if (dgrad && stats)
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, true, true, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
@@ -683,6 +809,7 @@ hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) 
 }
 
 int g_stages = 0;  // 0 = automatic (conv_set_stages, for tuning sweeps)
+int g_xf_dbg = 0;  // conv_set_xf_debug (diagnostics only)
 unsigned long long* g_stamps = nullptr;  // diagnostic timeline buffer (conv_set_stamps)
 
 template <typename T, int BM, int BN>
@@ -730,6 +857,8 @@ void conv_set_stamps(void* buf) { g_stamps = static_cast<unsigned long long*>(bu
 
 void conv_set_stages(int nb) { g_stages = (nb >= 1 && nb <= 4) ? nb : 0; }
 
+void conv_set_xf_debug(int bits) { g_xf_dbg = bits & 7; }
+
 // Below ~2 workgroups per CU a conv runs latency-bound on its long reduction (ResNet-50 layer4
 // 3x3: 200 tiles x 72 K-steps, 55 us).  Split the reduction until ~768 workgroups run, keeping
 // >= 6 K-steps per split.  The reduce launch costs ~5 us, so at 300-480 tiles only long
@@ -747,7 +876,7 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha,
                     const SplitkEpilogue* ep, const void* addend, const BnBwdEpilogue* bnb, int pix, int dgrad_stride,
-                    int Hx, int Wx, int nb) {
+                    int Hx, int Wx, int nb, const ConvInXform* xf) {
   if (!conv_fwd_supported(C, K) || dtype == kF32) return hipErrorInvalidValue;
   if (dgrad && (psum != nullptr || sh != 1 || sw != 1)) return hipErrorInvalidValue;
   const bool sd2 = dgrad_stride == 2;
@@ -766,6 +895,11 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
     return hipErrorInvalidValue;
   const int64_t M64 = (int64_t)N * P * Q;
   if (M64 <= 0 || M64 > INT32_MAX) return hipErrorInvalidValue;
+  if (xf != nullptr &&
+      (dgrad || C > kXfMaxC || pix > 0 || xf->sums == nullptr || xf->save_mean == nullptr || xf->save_invstd == nullptr ||
+       addend != nullptr || aff || alpha != 1.f || ep != nullptr || (int64_t)N * H * W < 2 ||
+       (xf->out != nullptr && (sh != 1 || sw != 1 || P != H || Q != W || 2 * ph != R - 1 || 2 * pw != S - 1))))
+    return hipErrorInvalidValue;
   ConvArgs a{static_cast<const uint16_t*>(in), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(out),
              static_cast<const uint16_t*>(zero), psum, psq, N, H, W, C, K, P, Q, R, S, sh, sw, ph, pw, (int)M64};
   a.group = conv_fwd_group(a.M, K, R * S, bm, bn);
@@ -780,7 +914,16 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
     a.mpq = exact ? magic36(P * Q) : 0;
   }
   // nb: LDS ring depth 1..4 (0 = automatic); + 16: the DIRECT store epilogue (forward + statistics)
-  a.direct = (nb & 16) && psum != nullptr && !dgrad && addend == nullptr && !aff ? 1 : 0;
+  a.direct = (nb & 16) && psum != nullptr && !dgrad && addend == nullptr && !aff && xf == nullptr ? 1 : 0;
+  a.xf_on = xf != nullptr ? 1 : 0;
+  a.xf_dbg = g_xf_dbg;
+  a.xf_out = nullptr;
+  if (xf != nullptr) {
+    const double Mi = (double)N * H * W;  // the producer's rows (this conv's input pixels)
+    a.xfin = FwdFin{xf->sums, xf->weight, xf->bias, xf->running_mean, xf->running_var, xf->momentum, xf->eps,
+                    xf->save_mean, xf->save_invstd, 1.0 / Mi, Mi / (Mi - 1.0)};
+    a.xf_out = static_cast<uint16_t*>(xf->out);
+  }
   nb &= 15;
   a.nb = (nb >= 1 && nb <= 4) ? nb : 0;
   a.Hx = Hx;

@@ -23,7 +23,7 @@ from ..ops import _native
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import branch_sum_link, conv_bn_act, residual_link
+from ..ops.conv import branch_sum_link, conv_bn_act, residual_link, xf_consumer_ok
 from ..ops.linear import Linear
 
 
@@ -58,7 +58,8 @@ class BasicBlock(nn.Module):
         branch = branch_sum_link(x) if self.downsample is not None else None
         identity = x if self.downsample is None else _downsample(self.downsample, x, branch)
         link = residual_link(x) if self.downsample is None else None
-        out = conv_bn_act(self.conv1, self.bn1, x, link=link, branch=branch)
+        # bn1 + ReLU applied by conv2's operand read (no apply pass) where conv2 can take it
+        out = conv_bn_act(self.conv1, self.bn1, x, link=link, branch=branch, defer=xf_consumer_ok(self.conv2))
         return conv_bn_act(self.conv2, self.bn2, out, residual=identity, link=link)
 
 
@@ -83,8 +84,9 @@ class Bottleneck(nn.Module):
         branch = branch_sum_link(x) if self.downsample is not None else None
         identity = x if self.downsample is None else _downsample(self.downsample, x, branch)
         link = residual_link(x) if self.downsample is None else None
-        out = conv_bn_act(self.conv1, self.bn1, x, link=link, branch=branch)
-        out = conv_bn_act(self.conv2, self.bn2, out)
+        # bn1 / bn2 + ReLU applied by the next conv's operand read (no apply passes) where it can
+        out = conv_bn_act(self.conv1, self.bn1, x, link=link, branch=branch, defer=xf_consumer_ok(self.conv2))
+        out = conv_bn_act(self.conv2, self.bn2, out, defer=xf_consumer_ok(self.conv3))
         return conv_bn_act(self.conv3, self.bn3, out, residual=identity, link=link)
 
 

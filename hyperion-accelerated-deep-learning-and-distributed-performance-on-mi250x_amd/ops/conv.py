@@ -11,6 +11,13 @@ SURVEY §2.4 "Convolution + BatchNorm + ReLU", hard part #1 in §7.4).
   per-channel Σy, Σy² of its (rounded) outputs into a zeroed accumulator in the epilogue (float
   atomics); BN then runs ONE apply launch that finalizes the statistics inline, with the residual
   add and ReLU folded in (``bn_act.hip``).  No separate statistics read, no finalize launch.
+  ``defer=True`` (a ``conv → BN → ReLU`` whose output feeds a stride-1 "same"-padded conv, i.e.
+  every bottleneck's conv1 → conv2 → conv3 chain): no apply launch at all — the CONSUMING conv
+  reads the raw conv output and applies BN + ReLU to its A operand as it reads it (the kernel's
+  XF mode), storing the activation the backward needs as a side output (SURVEY §2.4 "BN-apply
+  + ReLU stage in the next conv's prologue").  Opt-in (``HYPERION_CONV_XF=1x1|all``): measured
+  on MI355X it does not beat the apply pass — the latency-bound conv kernels pay the transform on
+  every K step's critical path, a 3x3 once per tap (README "Measured non-wins", profiles/r04/xf).
 * backward — the fused BN/ReLU/residual backward (``bn_act.hip``) produces dconv; the data
   gradient of a stride-1 convolution is the same implicit-GEMM kernel in DGRAD mode (the forward
   filter read flipped and channel-transposed through ds_read_b64_tr_b16, no filter copy); a
@@ -37,13 +44,15 @@ from . import _native
 from . import streams as _streams
 
 
-def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d, w: Optional[torch.Tensor] = None) -> bool:
+def _native_conv_ok(x: torch.Tensor, conv: nn.Conv2d, w: Optional[torch.Tensor] = None,
+                    wdt: Optional[torch.dtype] = None) -> bool:
+    """``wdt``: the dtype the weight will have at the call (autocast casts it), default its own."""
     w = conv.weight if w is None else w
     return (
         x.is_cuda
         and x.dim() == 4
         and x.dtype in (torch.bfloat16, torch.float16)
-        and w.dtype == x.dtype
+        and (w.dtype if wdt is None else wdt) == x.dtype
         and conv.groups == 1
         and tuple(conv.dilation) == (1, 1)
         and conv.bias is None
@@ -172,6 +181,69 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
 
 FUSE_SHORTCUT_GRAD = True  # models create ResidualLinks only when set (A/B switch for tests)
 
+# BN apply + ReLU fused into the consuming conv's operand read (conv_igemm.hip XF); A/B switch
+# HYPERION_CONV_XF: "0" off, "1x1" only 1x1 consumers (each element transformed once), "all" every
+# stride-1 consumer (a 3x3 re-transforms every element per tap)
+_XF_MODE = os.environ.get("HYPERION_CONV_XF", "0")
+FUSE_BN_APPLY = _XF_MODE in ("1", "all", "1x1")
+XF_ONLY_1X1 = _XF_MODE == "1x1"
+# launch plan of a fused consumer with >= 256 output channels (measured best, scripts/xf_bench.py);
+# None: the plain conv's plan
+XF_TILE = (128, 128, 1, 2)
+
+
+class PendingBN:
+    """A deferred ``relu(BN(y))``: the producer stored the raw conv output ``yc`` and its statistics
+    sums; ``out`` (the activation autograd knows) and ``stats`` (save_mean / save_invstd) are
+    allocated but written only by the consumer — the XF conv, or :func:`materialize` when the
+    consumer cannot fuse.  Reached as ``out.grad_fn.bnpend``."""
+
+    __slots__ = ("yc", "sums", "bn_w", "bn_b", "rm", "rv", "momentum", "eps", "stats", "out", "done")
+
+    def __init__(self, yc, sums, bn_w, bn_b, rm, rv, momentum, eps, stats, out):
+        self.yc, self.sums, self.bn_w, self.bn_b, self.rm, self.rv = yc, sums, bn_w, bn_b, rm, rv
+        self.momentum, self.eps, self.stats, self.out = momentum, eps, stats, out
+        self.done = False
+
+    def release(self) -> None:
+        # consumed: drop the tensors (``out`` would otherwise keep a ctx -> output -> grad_fn cycle)
+        self.done = True
+        self.yc = self.sums = self.bn_w = self.bn_b = self.rm = self.rv = self.stats = self.out = None
+
+
+def pending_of(x: torch.Tensor) -> Optional[PendingBN]:
+    p = getattr(x.grad_fn, "bnpend", None) if x.grad_fn is not None else None
+    if p is None or p.done:
+        return None
+    if p.out.data_ptr() != x.data_ptr() or p.out.shape != x.shape:
+        materialize(p)  # a view of the deferred output reached a consumer: apply the BN for real
+        return None
+    return p
+
+
+def materialize(p: PendingBN) -> None:
+    """Run a deferred BN apply as the standalone pass (the consumer is not an XF conv)."""
+    if p.done:
+        return
+    _native.count("bn_apply_materialized")
+    out, mean, invstd = _native.native().bn_fwd_sums(p.yc, None, p.sums, p.bn_w, p.bn_b, p.rm, p.rv, p.momentum,
+                                                     p.eps, True)
+    # (.data: filling the allocated-but-unwritten tensors is not a modification autograd must see —
+    # the producer saved the stats views for its backward)
+    p.out.data.copy_(out)
+    p.stats.data[0].copy_(mean)
+    p.stats.data[1].copy_(invstd)
+    p.release()
+
+
+def xf_consumer_ok(conv: nn.Conv2d) -> bool:
+    """Can ``conv`` consume a deferred BN + ReLU (stride 1, "same" padding, <= 512 input channels)?"""
+    R, S = conv.kernel_size
+    return (FUSE_BN_APPLY and not isinstance(conv.padding, str) and tuple(conv.stride) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and conv.groups == 1 and conv.bias is None
+            and tuple(conv.padding) == ((R - 1) // 2, (S - 1) // 2) and R % 2 == 1 and S % 2 == 1
+            and conv.in_channels % 64 == 0 and conv.in_channels <= 512 and (R == 1 or not XF_ONLY_1X1))
+
 
 def residual_link(x: torch.Tensor) -> Optional["ResidualLink"]:
     return ResidualLink(x) if FUSE_SHORTCUT_GRAD else None
@@ -296,7 +368,7 @@ def _will_run(ref) -> bool:
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bn_w, bn_b, rm, rv, residual, stride, padding, momentum, eps, act, link_in, link_out,
-                branch, bidx, prod):
+                branch, bidx, prod, xin=None, defer=False):
         C = _native.native()
         # BN statistics: the conv epilogue ADDS Σy, Σy² into a zeroed [2, K] slice of the forward's
         # arena; the apply finalizes inline.  The backward's Σdz, Σdz·x slice is reserved now so
@@ -307,11 +379,32 @@ class _ConvBNActFn(torch.autograd.Function):
         P = (x.shape[2] + 2 * padding[0] - w.shape[2]) // stride[0] + 1
         Q = (x.shape[3] + 2 * padding[1] - w.shape[3]) // stride[1] + 1
         pl = _plan("fwd", x.shape[0] * P * Q, K, x.shape[1], w.shape[2], w.shape[3], stride[0]) or (-1, -1, -1, 0)
-        yc, _, _ = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True, pl[0], pl[1], pl[2],
-                              sums=sums, stages=pl[3])
+        if xin is not None:
+            # x is the deferred activation of the producing layer: read its raw conv output, apply
+            # that layer's BN + ReLU on the operand path, and fill x (and its BN stats) on the way.
+            # Tile: 128x128 / 2 stages where the output has >= 256 channels (measured best for the
+            # fused 1x1 consumers, scripts/xf_bench.py), else the plain conv's plan
+            if XF_TILE is not None and K >= 256 and K % 128 == 0:
+                pl = XF_TILE
+            _native.count("conv_xf")
+            yc, _, _ = C.conv_fwd(xin.yc, w, stride[0], stride[1], padding[0], padding[1], True, pl[0], pl[1], pl[2],
+                                  sums=sums, stages=pl[3], xf_sums=xin.sums, xf_w=xin.bn_w, xf_b=xin.bn_b,
+                                  xf_rm=xin.rm, xf_rv=xin.rv, xf_momentum=xin.momentum, xf_eps=xin.eps, xf_out=x,
+                                  xf_stats=xin.stats)
+            xin.release()
+        else:
+            yc, _, _ = C.conv_fwd(x, w, stride[0], stride[1], padding[0], padding[1], True, pl[0], pl[1], pl[2],
+                                  sums=sums, stages=pl[3])
         if residual is not None:
             residual = residual.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        out, mean, invstd = C.bn_fwd_sums(yc, residual, sums, bn_w, bn_b, rm, rv, momentum, eps, act)
+        if defer:
+            # no apply pass: the consumer conv applies BN + ReLU as it reads yc (PendingBN)
+            out = torch.empty_like(yc)
+            stats = torch.empty(2, K, device=yc.device, dtype=torch.float32)
+            mean, invstd = stats[0], stats[1]
+            ctx.bnpend = PendingBN(yc, sums, bn_w, bn_b, rm, rv, momentum, eps, stats, out)
+        else:
+            out, mean, invstd = C.bn_fwd_sums(yc, residual, sums, bn_w, bn_b, rm, rv, momentum, eps, act)
         # without a residual the backward recomputes the ReLU mask from yc (no need to keep `out`)
         ctx.save_for_backward(x, w, yc, out if (act and residual is not None) else None, bn_w, bn_b, mean, invstd)
         ctx.cfg = (stride, padding, act, residual is not None)
@@ -371,7 +464,24 @@ class _ConvBNActFn(torch.autograd.Function):
         if dw is None and ctx.needs_input_grad[1]:
             dw = _wgrad(dyc, x, w, stride, padding, w_param=ctx.w_param)
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,
-                dres, None, None, None, None, None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None, None, None, None, None, None)
+
+
+def _xf_fusable(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual, link, branch) -> bool:
+    """Will conv_bn_act take the native fused path for (conv, bn, x) with an XF-capable geometry
+    (so a pending BN on x is applied by this conv's operand read)?"""
+    wdt = conv.weight.dtype
+    if x.is_cuda and torch.is_autocast_enabled(x.device.type):
+        wdt = torch.get_autocast_dtype(x.device.type)  # conv_bn_act casts the weight (and x) to it
+        if wdt != x.dtype:
+            return False
+    if not (xf_consumer_ok(conv) and bn.training and bn.track_running_stats and bn.momentum is not None
+            and bn.affine and x.is_cuda and x.dtype == torch.bfloat16 and wdt == x.dtype
+            and _native.use_native(x, op="conv") and _native.use_native(x, op="bn")):
+        return False
+    if (link is not None and x is link.src) or (branch is not None and x is branch.src):
+        return False  # a block input is never a deferred activation
+    return _native_conv_ok(x, conv, conv.weight, wdt=wdt) and not _is_stem(conv, x)
 
 
 def _eval_affine(bn: nn.Module, device):
@@ -544,13 +654,21 @@ class _StemConvBNActFn(torch.autograd.Function):
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                link: Optional[ResidualLink] = None, branch: Optional[BranchSumLink] = None) -> torch.Tensor:
+                link: Optional[ResidualLink] = None, branch: Optional[BranchSumLink] = None,
+                defer: bool = False) -> torch.Tensor:
     """``bn(conv(x), residual)`` for a ``BatchNormAct2d`` ``bn``; fused on gfx950 when possible.
 
     ``link``: a ``ResidualLink`` whose ``src`` is the block input — pass it to the block's FIRST
     conv (``x is link.src``) and to its LAST (``residual is link.src``) to fuse the shortcut
     gradient into the first conv's data gradient.  ``branch``: a ``BranchSumLink`` on the block
-    input, passed to the downsample conv and the first conv (sums their data gradients in-kernel)."""
+    input, passed to the downsample conv and the first conv (sums their data gradients in-kernel).
+    ``defer``: the output feeds a conv for which :func:`xf_consumer_ok` holds, called next through
+    this function — BN + ReLU are then applied by that conv's operand read (no apply pass); any
+    other consumer must see the output materialized (this function does it for its own input)."""
+    pend = pending_of(x)
+    if pend is not None and not _xf_fusable(conv, bn, x, residual, link, branch):
+        materialize(pend)
+        pend = None
     if not bn.training:
         out = _conv_bn_eval(conv, bn, x, residual)
         if out is not None:
@@ -610,9 +728,11 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
             branch = None
     # x produced by another fused layer: its BN backward reduce can ride on our dgrad epilogue
     prod = getattr(x.grad_fn, "bnlink", None) if (FUSE_BN_BACKWARD and x.grad_fn is not None) else None
+    defer = (defer and FUSE_BN_APPLY and bool(bn.act) and residual is None and torch.is_grad_enabled()
+             and x.dtype == torch.bfloat16 and w.dtype == x.dtype and bn.num_features <= 512)
     out = _ConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
                              stride, padding, float(bn.momentum), float(bn.eps), bool(bn.act),
-                             link_in, link_out, branch, bidx, prod)
+                             link_in, link_out, branch, bidx, prod, pend, defer)
     if out.grad_fn is not None:  # (no graph under no_grad: nothing to link)
         if branch is not None:
             branch.nodes[bidx] = weakref.ref(out.grad_fn)
