@@ -33,6 +33,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.attention import attention_packed
+from ..ops.conv import residual_link
 from ..ops.dropout import Dropout
 from ..ops.layernorm import LayerNorm
 from ..ops.linear import Linear, linear
@@ -66,9 +67,10 @@ class MultiheadSelfAttention(nn.Module):
         x: torch.Tensor,
         causal: bool = False,
         key_padding_mask: Optional[torch.Tensor] = None,
+        link=None,
     ) -> torch.Tensor:
         B, S, E = x.shape
-        qkv = linear(x, self.in_proj_weight, self.in_proj_bias).view(B, S, 3, self.num_heads, self.head_dim)
+        qkv = linear(x, self.in_proj_weight, self.in_proj_bias, link=link).view(B, S, 3, self.num_heads, self.head_dim)
         p = self.dropout if self.training else 0.0
         o = attention_packed(qkv, causal=causal, dropout_p=p, key_padding_mask=key_padding_mask)
         return self.out_proj(o.reshape(B, S, E))
@@ -108,9 +110,9 @@ class TransformerEncoderLayer(nn.Module):
         self.dropout2 = Dropout(dropout)
         self.activation = activation
 
-    def _ff(self, x: torch.Tensor) -> torch.Tensor:
+    def _ff(self, x: torch.Tensor, link=None) -> torch.Tensor:
         # the inner dropout rides linear1's epilogue (forward) and its activation backward
-        return self.linear2(self.linear1(x, dropout_p=self.dropout.p if self.training else 0.0))
+        return self.linear2(self.linear1(x, dropout_p=self.dropout.p if self.training else 0.0, link=link))
 
     def forward(self, x: torch.Tensor, causal: bool = False,
                 key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -119,10 +121,15 @@ class TransformerEncoderLayer(nn.Module):
             return x + self.dropout2(self._ff(self.norm2(x)))
         # LN(x + dropout(branch)) in one kernel each: the residual branches' dropouts ride the norms
         # (mask regenerated in the LN forward and backward kernels: no dropout launch, no mask tensor)
+        # The layer input feeds the QKV GEMM and norm1's residual (then norm1's output feeds linear1 and
+        # norm2's residual): each norm's backward parks the residual gradient in a ResidualLink and
+        # the GEMM's data gradient adds it in its epilogue — no autograd add of the two gradients
         p1 = self.dropout1.p if self.training else 0.0
         p2 = self.dropout2.p if self.training else 0.0
-        x = self.norm1(self.self_attn(x, causal, key_padding_mask), residual=x, dropout_p=p1)
-        return self.norm2(self._ff(x), residual=x, dropout_p=p2)
+        link = residual_link(x) if torch.is_grad_enabled() else None
+        x = self.norm1(self.self_attn(x, causal, key_padding_mask, link=link), residual=x, dropout_p=p1, link=link)
+        link = residual_link(x) if torch.is_grad_enabled() else None
+        return self.norm2(self._ff(x, link=link), residual=x, dropout_p=p2, link=link)
 
 
 class TransformerEncoder(nn.Module):

@@ -179,7 +179,7 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
     return dx if addend is None else dx + addend
 
 
-FUSE_SHORTCUT_GRAD = True  # models create ResidualLinks only when set (A/B switch for tests)
+FUSE_SHORTCUT_GRAD = os.environ.get("HYPERION_RESIDUAL_LINK", "1") == "1"  # models create ResidualLinks only when set (A/B)
 
 # BN apply + ReLU fused into the consuming conv's operand read (conv_igemm.hip XF); A/B switch
 # HYPERION_CONV_XF: "0" off, "1x1" only 1x1 consumers (each element transformed once), "all" every

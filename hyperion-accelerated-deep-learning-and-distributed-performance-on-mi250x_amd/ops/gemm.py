@@ -129,17 +129,22 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
     return nat(*c)
 
 
-def mm_nn(dy: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
-    """``dy W`` (dy [M, N], W [N, K]) or None (vendor)."""
+def mm_nn(dy: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """``dy W`` (dy [M, N], W [N, K]) ``(+ residual)`` (added in the epilogue: a data gradient that
+    also receives a residual branch's gradient) or None (vendor)."""
     if not _ok(dy, w) or w.shape[1] % 4 or dy.shape[1] % 8:
         return None
+    if residual is not None and (residual.dtype != dy.dtype or residual.stride(1) != 1 or residual.stride(0) % 4):
+        return None
     C = _native.native()
-    key = ("nn", dy.shape[0], w.shape[1], dy.shape[1])
-    c = _pick(key, dy.shape[1], lambda t=-1, sp=-1: C.gemm(dy, w, b_tr=True, tile=t, splits=sp), lambda: dy @ w)
+    key = ("nn", dy.shape[0], w.shape[1], dy.shape[1]) + (("res",) if residual is not None else ())
+    ven = (lambda: dy @ w) if residual is None else (lambda: torch.addmm(residual, dy, w))
+    c = _pick(key, dy.shape[1], lambda t=-1, sp=-1: C.gemm(dy, w, b_tr=True, residual=residual, tile=t, splits=sp),
+              ven)
     if c is None:
         return None
     _native.count("gemm_nn")
-    return C.gemm(dy, w, b_tr=True, tile=c[0], splits=c[1])
+    return C.gemm(dy, w, b_tr=True, residual=residual, tile=c[0], splits=c[1])
 
 
 def mm_tn(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None, beta: float = 0.0,

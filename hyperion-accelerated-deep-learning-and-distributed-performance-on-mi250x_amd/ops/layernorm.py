@@ -40,9 +40,14 @@ def _ref(x, residual, weight, bias, eps, rms, dropout_p=0.0):
     return y, s
 
 
+def _will_run(ref) -> bool:
+    node = ref() if ref is not None else None
+    return node is not None and torch._C._will_engine_execute_node(node)
+
+
 class _LNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum, dropout_p=0.0):
+    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum, dropout_p=0.0, link=None):
         C = _native.native()
         x = x.contiguous()
         if residual is not None:
@@ -55,6 +60,7 @@ class _LNFn(torch.autograd.Function):
         ctx.rms = rms
         ctx.drop = (dropout_p, st)
         ctx.has_res = residual is not None
+        ctx.link = link
         ctx.save_for_backward(xin, weight, mean, rstd)
         if return_sum:
             return y, (s if residual is not None else x)
@@ -67,12 +73,18 @@ class _LNFn(torch.autograd.Function):
         need_db = ctx.needs_input_grad[3]
         p, st = ctx.drop
         dx, dw, db, dxa = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms, p, st)
+        dres = dx if ctx.has_res and ctx.needs_input_grad[1] else None
+        link = ctx.link
+        if dres is not None and link is not None and link.armed and _will_run(link.first_node):
+            # the residual input's other consumer (the block's first GEMM) adds it in its data-gradient
+            # epilogue: no separate add of the two gradients of the block input
+            link.dres, dres = dres, None
         return (
             dxa if p > 0.0 else dx,  # the dropped input's gradient: dropout(ds) with the forward's mask
-            dx if ctx.has_res and ctx.needs_input_grad[1] else None,
+            dres,
             dw if need_dw else None,
             db if need_db else None,
-            None, None, None, None,
+            None, None, None, None, None,
         )
 
 
@@ -85,6 +97,7 @@ def layer_norm(
     rms: bool = False,
     return_sum: bool = False,
     dropout_p: float = 0.0,
+    link=None,
 ) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
     """``LN(x + residual)`` (or RMSNorm); ``dropout_p``: ``LN(residual + dropout(x))`` — pass it only
     in training (it is applied whenever > 0)."""
@@ -106,7 +119,9 @@ def layer_norm(
         and (dropout_p == 0.0 or (residual is not None and d <= 2048 and dropout_p < 1.0))
     )
     if native:
-        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum, float(dropout_p))
+        if link is not None and residual is not link.src:
+            link = None
+        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum, float(dropout_p), link)
     y, s = _ref(x, residual, weight, bias, eps, rms, dropout_p)
     return (y, s) if return_sum else y
 
@@ -115,7 +130,7 @@ class LayerNorm(nn.LayerNorm):
     """``nn.LayerNorm`` (same keys) with an optional fused residual input."""
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,  # type: ignore[override]
-                dropout_p: float = 0.0) -> torch.Tensor:
+                dropout_p: float = 0.0, link=None) -> torch.Tensor:
         """``LN(x + residual)``; ``dropout_p`` > 0: ``LN(residual + dropout(x))`` (post-norm branch)."""
         if len(self.normalized_shape) != 1:
             if dropout_p > 0.0:
@@ -123,7 +138,7 @@ class LayerNorm(nn.LayerNorm):
             return super().forward(x if residual is None else x + residual)
         if torch.is_autocast_enabled() and x.dtype == torch.float32 and residual is not None:
             residual = residual.float()
-        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual, dropout_p=dropout_p)
+        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual, dropout_p=dropout_p, link=link)
 
 
 class RMSNorm(nn.Module):

@@ -20,6 +20,7 @@ else the tiled kernel (or the vendor GEMM).
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -52,12 +53,36 @@ def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return y if y is not None else F.linear(x2, w)
 
 
-def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``dy2 @ w`` (the data gradient of ``linear_fwd``)."""
+def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor, addend: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``dy2 @ w`` (the data gradient of ``linear_fwd``) ``+ addend`` (2D, in the GEMM epilogue —
+    a residual branch's gradient of the same input; ``ResidualLink``)."""
     if dy2.is_cuda and _bwd_ok(dy2, w):
-        return _native.native().linear_nn(dy2.contiguous(), w)
-    dx = mm_nn(dy2, w) if dy2.is_cuda else None
-    return dx if dx is not None else dy2 @ w
+        dx = _native.native().linear_nn(dy2.contiguous(), w)
+        return dx if addend is None else dx + addend
+    if addend is not None:
+        addend = addend.to(dy2.dtype)
+    dx = mm_nn(dy2, w, residual=addend) if dy2.is_cuda else None
+    if dx is not None:
+        return dx
+    return dy2 @ w if addend is None else torch.addmm(addend, dy2, w)
+
+
+def arm_link(link, x: torch.Tensor):
+    """``link`` (an ``ops.conv.ResidualLink`` on a residual-block input) if ``x`` is its source: the
+    op consuming x will add the residual branch's parked gradient into its data gradient."""
+    if link is not None and x is link.src and torch.is_grad_enabled():
+        link.armed = True
+        return link
+    return None
+
+
+def take_link_grad(link, shape) -> Optional[torch.Tensor]:
+    """The parked residual gradient for this op's data gradient (2D), consumed."""
+    if link is None or link.dres is None:
+        return None
+    d, link.dres = link.dres, None
+    _native.count("residual_grad_fused")
+    return d.reshape(-1, shape[-1])
 
 
 # Weight gradients whose output is small (out x in <= WGRAD_NATIVE_MAX elements) run on the
@@ -93,7 +118,7 @@ def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, link=None):
         x2 = x.reshape(-1, x.shape[-1])
         y = None
         if b is not None and not _fwd_ok(x2, w):
@@ -108,22 +133,25 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.bdt = b.dtype if b is not None else None
         ctx.xshape = x.shape
+        ctx.link = link
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).to(w.dtype)
-        dx = linear_dgrad(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        add = take_link_grad(ctx.link, ctx.xshape)
+        dx = linear_dgrad(dy2, w, add).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy2.contiguous(), x2.contiguous()).to(w.dtype) if ctx.needs_input_grad[1] else None
         db = bias_grad(dy2.contiguous(), ctx.bdt) if (ctx.has_b and ctx.needs_input_grad[2]) else None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, link=None) -> torch.Tensor:
     """``F.linear`` with the weight-streaming kernels on gfx950 (same math, same grads).  Under
     autocast, x and w are cast to the autocast dtype first (differentiable casts, like torch's own
-    autocast of ``F.linear``), so the native kernels serve the AMP trainers too."""
+    autocast of ``F.linear``), so the native kernels serve the AMP trainers too.  ``link``: a
+    ``ResidualLink`` on x (see :func:`arm_link`)."""
     if not (x.is_cuda and _native.use_native(x, op="linear")):
         return F.linear(x, w, b)
     if torch.is_autocast_enabled(x.device.type):
@@ -131,12 +159,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
         if dt not in (torch.bfloat16, torch.float16):
             return F.linear(x, w, b)
         with torch.autocast(x.device.type, enabled=False):
-            return _LinearFn.apply(x.to(dt), w.to(dt), b)
-    return _LinearFn.apply(x, w, b)
+            return _LinearFn.apply(x.to(dt), w.to(dt), b)  # (a cast copy: the link stays unarmed)
+    link = arm_link(link, x)
+    y = _LinearFn.apply(x, w, b, link)
+    if link is not None and y.grad_fn is not None:
+        link.first_node = weakref.ref(y.grad_fn)
+    return y
 
 
 class Linear(nn.Linear):
     """``nn.Linear`` (same parameters and state-dict keys) routed through :func:`linear`."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return linear(x, self.weight, self.bias)
+    def forward(self, x: torch.Tensor, link=None) -> torch.Tensor:  # type: ignore[override]
+        return linear(x, self.weight, self.bias, link=link)

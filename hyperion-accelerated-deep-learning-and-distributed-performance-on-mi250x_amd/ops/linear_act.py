@@ -26,7 +26,9 @@ import torch.nn.functional as F
 
 from . import _native
 from .gemm import mm_nn, mm_nt
-from .linear import bias_grad, linear_wgrad
+import weakref
+
+from .linear import arm_link, bias_grad, linear_wgrad, take_link_grad
 
 
 def _act_bwd(dh: torch.Tensor, z: torch.Tensor, act: str, bdt: torch.dtype, need_b: bool, drop=(0.0, None)):
@@ -48,9 +50,13 @@ def _act_bwd(dh: torch.Tensor, z: torch.Tensor, act: str, bdt: torch.dtype, need
     return dy, (bias_grad(dy, bdt) if need_b else None)
 
 
-def _dgrad(dy: torch.Tensor, wc: torch.Tensor) -> torch.Tensor:
-    dx = mm_nn(dy, wc) if dy.is_cuda else None
-    return dx if dx is not None else dy @ wc
+def _dgrad(dy: torch.Tensor, wc: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if add is not None:
+        add = add.to(dy.dtype)
+    dx = mm_nn(dy, wc, residual=add) if dy.is_cuda else None
+    if dx is not None:
+        return dx
+    return dy @ wc if add is None else torch.addmm(add, dy, wc)
 
 
 def _cdt(x: torch.Tensor) -> torch.dtype:
@@ -66,12 +72,13 @@ class _LinearReLU(torch.autograd.Function):
     backward masks with the saved OUTPUT (kept elements: h·scale > 0 ⇔ z > 0; dropped: gradient 0)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, p=0.0):
+    def forward(ctx, x, w, b, p=0.0, link=None):
         dt = _cdt(x)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).to(dt)
         wc, bc = w.to(dt), b.to(dt)
         drop = _drop_state(x2, p)
+        ctx.link = link
         h = mm_nt(x2, wc, bias=b, act="relu", dropout_p=drop[0], rng=drop[1]) if x2.is_cuda else None
         if h is None:
             h = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
@@ -87,21 +94,23 @@ class _LinearReLU(torch.autograd.Function):
         x2, wc, h = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
         dy, db = _act_bwd(dh.reshape(h.shape).to(h.dtype), h, "relu", bdt, ctx.needs_input_grad[2], ctx.drop)
-        dx = _dgrad(dy, wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
+        add = take_link_grad(ctx.link, shape)
+        dx = _dgrad(dy, wc, add).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class _LinearGELU(torch.autograd.Function):
     """``gelu(x Wᵀ + b)``: bias in the GEMM epilogue, the pre-activation kept for backward."""
 
     @staticmethod
-    def forward(ctx, x, w, b, p=0.0):
+    def forward(ctx, x, w, b, p=0.0, link=None):
         dt = _cdt(x)
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).to(dt)
         wc, bc = w.to(dt), b.to(dt)
         drop = _drop_state(x2, p)
+        ctx.link = link
         y = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=dt) if x2.is_cuda else None
         h = mm_nt(x2, wc, bias=b, act="gelu", aux=y, dropout_p=drop[0], rng=drop[1]) if x2.is_cuda else None
         if h is None:
@@ -122,19 +131,28 @@ class _LinearGELU(torch.autograd.Function):
         x2, wc, y = ctx.saved_tensors
         xdt, wdt, bdt, shape = ctx.meta
         dy, db = _act_bwd(dh.reshape(y.shape).to(y.dtype), y, "gelu", bdt, ctx.needs_input_grad[2], ctx.drop)
-        dx = _dgrad(dy, wc).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
+        add = take_link_grad(ctx.link, shape)
+        dx = _dgrad(dy, wc, add).view(shape).to(xdt) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy, x2.contiguous()).to(wdt) if ctx.needs_input_grad[1] else None
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str,
-               dropout_p: float = 0.0) -> torch.Tensor:
-    """``dropout(act(x Wᵀ + b))`` — pass ``dropout_p`` only in training (applied whenever > 0)."""
+               dropout_p: float = 0.0, link=None) -> torch.Tensor:
+    """``dropout(act(x Wᵀ + b))`` — pass ``dropout_p`` only in training (applied whenever > 0).
+    ``link``: a ``ResidualLink`` on x (its parked residual gradient rides the data-gradient GEMM)."""
     native_drop = dropout_p == 0.0 or (x.is_cuda and _native.use_native(x, op="dropout") and dropout_p < 1.0)
+    fn = None
     if activation == "relu" and x.is_cuda and b is not None and native_drop:
-        return _LinearReLU.apply(x, w, b, float(dropout_p))
+        fn = _LinearReLU
     if activation == "gelu" and x.is_cuda and b is not None and native_drop:
-        return _LinearGELU.apply(x, w, b, float(dropout_p))
+        fn = _LinearGELU
+    if fn is not None:
+        link = arm_link(link, x)
+        y = fn.apply(x, w, b, float(dropout_p), link)
+        if link is not None and y.grad_fn is not None:
+            link.first_node = weakref.ref(y.grad_fn)
+        return y
     y = F.linear(x, w, b)
     y = F.gelu(y) if activation == "gelu" else F.relu(y)
     return F.dropout(y, dropout_p, True) if dropout_p > 0.0 else y
@@ -150,5 +168,5 @@ class LinearAct(torch.nn.Linear):
         super().__init__(in_features, out_features, bias=bias, **kw)
         self.activation = activation
 
-    def forward(self, x: torch.Tensor, dropout_p: float = 0.0) -> torch.Tensor:  # type: ignore[override]
-        return linear_act(x, self.weight, self.bias, self.activation, dropout_p)
+    def forward(self, x: torch.Tensor, dropout_p: float = 0.0, link=None) -> torch.Tensor:  # type: ignore[override]
+        return linear_act(x, self.weight, self.bias, self.activation, dropout_p, link=link)

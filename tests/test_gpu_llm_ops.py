@@ -280,3 +280,37 @@ def test_native_dropout_fresh_mask_per_graph_replay():
     torch.cuda.synchronize()
     assert not torch.equal(m1, out)
     assert abs((out != 0).float().mean().item() - 0.5) < 0.02
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_post_norm_layer_residual_grad_rides_the_gemm(monkeypatch, p):
+    """Post-norm encoder layer: each norm's residual gradient is added in the epilogue of the data
+    gradient GEMM of the layer input's other consumer (QKV, linear1) instead of an autograd add —
+    same gradients as the unlinked layer (ops/linear.py arm_link / take_link_grad)."""
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.ops import _native
+    from hyperion.ops import conv as conv_mod
+
+    torch.manual_seed(0)
+    layer = TransformerEncoderLayer(256, 4, 1024, dropout=p, activation="gelu").cuda().bfloat16()
+    x0 = torch.randn(4, 64, 256, device="cuda").bfloat16()
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(conv_mod, "FUSE_SHORTCUT_GRAD", fuse)
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        _native.reset_counters()
+        torch.manual_seed(1)
+        _native.rng_state(x.device)  # (same dropout stream for both runs)
+        y = layer(x, causal=True)
+        (y.float() * torch.linspace(-1, 1, 256, device="cuda")).sum().backward()
+        torch.cuda.synchronize()
+        res.append((y.detach().clone(), x.grad.clone(), {n: q.grad.clone() for n, q in layer.named_parameters()},
+                    dict(_native.counters())))
+    assert res[1][3].get("residual_grad_fused") == 2 and not res[0][3].get("residual_grad_fused")
+    if p == 0.0:
+        assert torch.equal(res[0][0], res[1][0])
+        torch.testing.assert_close(res[1][1].float(), res[0][1].float(), rtol=2e-2, atol=2e-2)
+        for n in res[0][2]:  # (the attention backward's atomics make both runs differ at bf16 level)
+            a, b = res[1][2][n].float(), res[0][2][n].float()
+            assert float((a - b).norm() / (b.norm() + 1e-12)) < 1e-2, n
