@@ -1,4 +1,5 @@
 // Torch bindings: fused BatchNorm(+res)(+ReLU), multi-tensor optimizer kernels, STREAM kernels.
+#include <atomic>
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
@@ -95,6 +96,16 @@ std::vector<at::Tensor> bn_bwd_dx(const at::Tensor& dz, const at::Tensor& x, con
 }
 
 // ---- column sums (bias gradients) ---------------------------------------------------------------
+// ticket slots of the one-launch column sums: a ring over device_counters' second half (each call
+// takes the next `n` slots; its kernel resets them) — launches 512 calls apart never overlap
+int* colsum_tickets(const at::Device& dev, int n) {
+  static std::atomic<int> next{0};
+  constexpr int kBase = 8192, kSpan = 8192;
+  const int step = (n + 15) & ~15;
+  int at = next.fetch_add(step) % kSpan;
+  if (at + step > kSpan) at = 0;
+  return device_counters(dev) + kBase + at;
+}
 // x: [..., N] contiguous -> Σ over all leading dims, [N] in out_dtype (default x's dtype)
 at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dtype) {
   HYP_CHECK_CUDA_TENSOR(x);
@@ -105,10 +116,12 @@ at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dty
   const at::DeviceGuard guard(x.device());
   const auto odt = out_dtype.value_or(x.scalar_type());
   auto out = at::empty({N}, x.options().dtype(odt));
-  const int P = hyp::colsum_partials(M, (int)N);
+  const bool fused = hyp::colsum_fused_max_p() > 0;
+  const int P = fused ? hyp::colsum_partials_fused(M, (int)N) : hyp::colsum_partials(M, (int)N);
   auto part = at::empty({(int64_t)P * N}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::column_sum(dtype_code(x), x.data_ptr(), M, (int)N, out.data_ptr(), dtype_code(out),
-                                part.data_ptr<float>(), P, cur_stream()));
+                                part.data_ptr<float>(), P, cur_stream(),
+                                fused ? colsum_tickets(x.device(), (int)((N + 511) / 512)) : nullptr));
   return out;
 }
 
@@ -127,7 +140,8 @@ std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z
   auto dy = at::empty_like(dh);
   const auto odt = db_dtype.value_or(dh.scalar_type());
   auto db = at::empty({N}, dh.options().dtype(odt));
-  const int P = hyp::colsum_partials(M, (int)N);
+  const bool fused = hyp::colsum_fused_max_p() > 0;
+  const int P = fused ? hyp::colsum_partials_fused(M, (int)N) : hyp::colsum_partials(M, (int)N);
   auto part = at::empty({(int64_t)P * N}, dh.options().dtype(at::kFloat));
   hyp::RngState rs{};
   if (drop_p > 0.0) {
@@ -136,7 +150,8 @@ std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z
   }
   HYP_CHECK_HIP(hyp::act_bwd_colsum(dtype_code(dh), (int)act, dh.data_ptr(), z.data_ptr(), dy.data_ptr(), M, (int)N,
                                     db.data_ptr(), dtype_code(db), part.data_ptr<float>(), P, cur_stream(),
-                                    (float)drop_p, drop_p > 0.0 ? &rs : nullptr));
+                                    (float)drop_p, drop_p > 0.0 ? &rs : nullptr,
+                                    fused ? colsum_tickets(dh.device(), (int)((N + 511) / 512)) : nullptr));
   return {dy, db};
 }
 
@@ -217,6 +232,8 @@ void register_norm_ops(pybind11::module& m) {
                                    g.data_ptr(), cur_stream()));
     return std::vector<at::Tensor>{loss, g};
   }, "mean-squared error and its gradient 2(x - t)/n in one pass", pybind11::arg("x"), pybind11::arg("target"));
+  m.def("colsum_set_fused", [](int64_t max_p) { hyp::colsum_set_fused((int)max_p); },
+        "column sums: partial-row cap of the one-launch last-arriver combine (0 = two launches, the default)");
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());
   m.def("act_bwd_colsum", &act_bwd_colsum, "activation backward + bias gradient in one pass (act 1 relu, 2 gelu)",

@@ -309,17 +309,23 @@ namespace hyp {
 // Column sums of a row-major [M, N] matrix (bias gradients): P partial rows (colsum_partials) in
 // `part` [P, N] fp32, then combined into out[N] (out_dtype).  N % 8 == 0, 16-byte aligned x.
 int colsum_partials(int64_t M, int N);
+// the partial count of the one-launch (last-arriver) combine, and its cap (0 = two launches)
+int colsum_partials_fused(int64_t M, int N);
+void colsum_set_fused(int max_p);
+int colsum_fused_max_p();
 // loss = mean((x - t)^2) (fp32 scalar) and g = 2 (x - t) / n in x's dtype; one block (small n)
 hipError_t mse_fwd_bwd(int dtype, const void* x, const float* t, int64_t n, float* loss, void* g, hipStream_t st);
+// tickets (non-null): ceil(N / 512) zeroed int32 slots — the combine runs in the same launch (the
+// last-arriving block of each column slab; the slots are reset to zero on exit)
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,
-                      hipStream_t st);
+                      hipStream_t st, int* tickets = nullptr);
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);
 // dy = dh·act'(z) (act 1: ReLU with z = output; 2: exact GELU with z = pre-activation) and its column
 // sums into db (out_dtype; null: skip) — the FFN activation backward + bias gradient.
 // drop_p > 0: dh is the gradient of dropout(act(z)) (dropout.hip mask of *rs, element index r*N + c)
 hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, void* dy, int64_t M, int N, void* db,
                           int out_dtype, float* part, int P, hipStream_t st, float drop_p = 0.f,
-                          const RngState* rs = nullptr);
+                          const RngState* rs = nullptr, int* tickets = nullptr);
 }  // namespace hyp
 
 namespace hyp {

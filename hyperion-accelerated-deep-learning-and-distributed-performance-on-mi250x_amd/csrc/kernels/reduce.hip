@@ -21,9 +21,65 @@ constexpr int kThreads = 256;
 constexpr int kColThreads = 64;  // threads across columns (x 8 columns each = 512 columns per block)
 constexpr int kRowGroups = kThreads / kColThreads;
 
+// Last-arriver combine (no second launch): every block of column slab blockIdx.y publishes its
+// partial row (agent-scope release: the L2 write-back that makes it visible to the other XCDs),
+// counts in on the slab's ticket, and the LAST block (acquire) sums the slab's P partial rows in a
+// fixed order — 2 row lanes x 4 independent accumulators per column quad, then lane 0 + lane 1 —
+// so the result does not depend on which block arrived last (deterministic), writes out[] and
+// resets the ticket for the next launch / graph replay.  The partial count is capped
+// (colsum_partials_fused) so that one block reads at most 64 x 512 floats.
+__device__ __forceinline__ void colsum_last_block(const float* part, int N, int* ticket, void* out, int odt,
+                                                  float* red /* >= 2 * 512 floats of LDS */) {
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const int P = gridDim.x;
+  const int q = threadIdx.x & 127, lane = threadIdx.x >> 7;
+  const int c = blockIdx.y * kColThreads * 8 + q * 4;
+  float4 a[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < N) {  // N % 8 == 0: a quad never straddles the edge
+    int p = lane;
+    for (; p + 6 < P; p += 8) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)(p + 2 * u) * N + c);
+        a[u].x += v.x; a[u].y += v.y; a[u].z += v.z; a[u].w += v.w;
+      }
+    }
+    for (; p < P; p += 2) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)p * N + c);
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
+  }
+  const float4 s = make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
+                               (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
+  __syncthreads();  // red is the caller's partial-row scratch
+  reinterpret_cast<float4*>(red)[lane * 128 + q] = s;
+  __syncthreads();
+  if (lane == 0 && c < N) {
+    const float4 o = reinterpret_cast<const float4*>(red)[q];
+    const float4 t = reinterpret_cast<const float4*>(red)[128 + q];
+    const float r[4] = {o.x + t.x, o.y + t.y, o.z + t.z, o.w + t.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (odt == kF32) static_cast<float*>(out)[c + e] = r[e];
+      else if (odt == kBF16) st1<bf16_t>(static_cast<bf16_t*>(out) + c + e, r[e]);
+      else st1<f16_t>(static_cast<f16_t*>(out) + c + e, r[e]);
+    }
+  }
+  if (threadIdx.x == 0) *ticket = 0;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void colsum_partial_k(const T* __restrict__ x, int64_t M, int N,
-                                                             int64_t rows_per_block, float* __restrict__ part) {
+                                                             int64_t rows_per_block, float* __restrict__ part,
+                                                             int* tickets, void* out, int odt) {
   __shared__ float red[kRowGroups][kColThreads * 8];
   const int ct = threadIdx.x % kColThreads, rg = threadIdx.x / kColThreads;
   const int c0 = (blockIdx.y * kColThreads + ct) * 8;
@@ -59,6 +115,7 @@ __global__ __launch_bounds__(kThreads) void colsum_partial_k(const T* __restrict
     const int c = blockIdx.y * kColThreads * 8 + i;
     if (c < N) part[(int64_t)blockIdx.x * N + c] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
+  if (tickets != nullptr) colsum_last_block(part, N, tickets + blockIdx.y, out, odt, &red[0][0]);
 }
 
 // out[c] = Σ_p part[p][c].  One block = 64 columns (16 float4 column quads) x 16 row lanes, every
@@ -77,7 +134,8 @@ template <typename T, int ACT>
 __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict__ dh, const T* __restrict__ z,
                                                              T* __restrict__ dy, int64_t M, int N,
                                                              int64_t rows_per_block, float* __restrict__ part,
-                                                             uint32_t dthr, float dscale, RngState drs) {
+                                                             uint32_t dthr, float dscale, RngState drs,
+                                                             int* tickets, void* out, int odt) {
   // dscale != 0: dh is the gradient of dropout(act(z)); the keep mask (dropout.hip's hash) is
   // regenerated per element and dh scaled in T first, as a separate dropout backward would store it
   const uint64_t dkey = dscale != 0.f ? rng_key(drs) : 0;
@@ -138,6 +196,7 @@ __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict
     const int c = blockIdx.y * kColThreads * 8 + i;
     if (c < N) part[(int64_t)blockIdx.x * N + c] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
+  if (tickets != nullptr) colsum_last_block(part, N, tickets + blockIdx.y, out, odt, &red[0][0]);
 }
 
 template <typename O>
@@ -194,6 +253,17 @@ int colsum_partials(int64_t M, int N) {
   return (int)P;
 }
 
+int g_colsum_fused_max_p = 0;  // colsum_set_fused (0: the two-launch path — measured faster, see README)
+
+int colsum_partials_fused(int64_t M, int N) {
+  const int P = colsum_partials(M, N);
+  return g_colsum_fused_max_p > 0 && P > g_colsum_fused_max_p ? g_colsum_fused_max_p : P;
+}
+
+void colsum_set_fused(int max_p) { g_colsum_fused_max_p = max_p < 0 ? 0 : (max_p > 256 ? 256 : max_p); }
+
+int colsum_fused_max_p() { return g_colsum_fused_max_p; }
+
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st) {
   if (N % 4 != 0 || P < 1) return hipErrorInvalidValue;
   const dim3 grid((N + 63) / 64);
@@ -209,42 +279,48 @@ hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dt
 }
 
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,
-                      hipStream_t st) {
+                      hipStream_t st, int* tickets) {
   if (N % 8 != 0 || M < 1 || P < 1) return hipErrorInvalidValue;
+  if (tickets != nullptr && out_dtype != kF32 && out_dtype != kBF16 && out_dtype != kF16) return hipErrorInvalidValue;
   const int64_t rpb = (M + P - 1) / P;
-  const dim3 grid(P, (N + kColThreads * 8 - 1) / (kColThreads * 8));
+  const int Pe = (int)((M + rpb - 1) / rpb);  // blocks that own rows (= the partial rows written)
+  const dim3 grid(Pe, (N + kColThreads * 8 - 1) / (kColThreads * 8));
   if (dtype == kBF16)
     hipLaunchKernelGGL(colsum_partial_k<bf16_t>, grid, dim3(kThreads), 0, st, static_cast<const bf16_t*>(x), M, N,
-                       rpb, part);
+                       rpb, part, tickets, out, out_dtype);
   else if (dtype == kF16)
     hipLaunchKernelGGL(colsum_partial_k<f16_t>, grid, dim3(kThreads), 0, st, static_cast<const f16_t*>(x), M, N, rpb,
-                       part);
+                       part, tickets, out, out_dtype);
   else if (dtype == kF32)
     hipLaunchKernelGGL(colsum_partial_k<float>, grid, dim3(kThreads), 0, st, static_cast<const float*>(x), M, N, rpb,
-                       part);
+                       part, tickets, out, out_dtype);
   else
     return hipErrorInvalidValue;
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return colsum_combine(part, P, N, out, out_dtype, st);
+  if (e != hipSuccess || tickets != nullptr) return e;
+  return colsum_combine(part, Pe, N, out, out_dtype, st);
 }
 
 // dy = dh·act'(z) and db = Σ_rows dy (out_dtype) in two launches (act: 1 ReLU on the output, 2 GELU
 // on the pre-activation).  part: [P, N] fp32 workspace, P = colsum_partials(M, N).
 hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, void* dy, int64_t M, int N, void* db,
                           int out_dtype, float* part, int P, hipStream_t st, float drop_p,
-                          const RngState* rs) {
+                          const RngState* rs, int* tickets) {
   if (N % 8 != 0 || M < 1 || P < 1 || (act != 1 && act != 2) || (dtype != kBF16 && dtype != kF16))
     return hipErrorInvalidValue;
+  if (db == nullptr) tickets = nullptr;
+  if (tickets != nullptr && out_dtype != kF32 && out_dtype != kBF16 && out_dtype != kF16) return hipErrorInvalidValue;
   const int64_t rpb = (M + P - 1) / P;
-  const dim3 grid(P, (N + kColThreads * 8 - 1) / (kColThreads * 8));
+  const int Pe = (int)((M + rpb - 1) / rpb);
+  const dim3 grid(Pe, (N + kColThreads * 8 - 1) / (kColThreads * 8));
   if (drop_p > 0.f && (rs == nullptr || drop_p >= 1.f)) return hipErrorInvalidValue;
   const uint32_t dthr = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.f, 4294967295.f) : 0u;
   const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 0.f;
   const RngState drs = rs != nullptr ? *rs : RngState{};
 #define HYP_ACT_COLSUM(TT, A)                                                                                   \
   hipLaunchKernelGGL((act_bwd_colsum_k<TT, A>), grid, dim3(kThreads), 0, st, static_cast<const TT*>(dh),        \
-                     static_cast<const TT*>(z), static_cast<TT*>(dy), M, N, rpb, part, dthr, dscale, drs)
+                     static_cast<const TT*>(z), static_cast<TT*>(dy), M, N, rpb, part, dthr, dscale, drs, tickets, \
+                     db, out_dtype)
   if (dtype == kBF16) {
     if (act == 1) HYP_ACT_COLSUM(bf16_t, 1);
     else HYP_ACT_COLSUM(bf16_t, 2);
@@ -254,8 +330,8 @@ hipError_t act_bwd_colsum(int dtype, int act, const void* dh, const void* z, voi
   }
 #undef HYP_ACT_COLSUM
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess || db == nullptr) return e;
-  return colsum_combine(part, P, N, db, out_dtype, st);
+  if (e != hipSuccess || db == nullptr || tickets != nullptr) return e;
+  return colsum_combine(part, Pe, N, db, out_dtype, st);
 }
 
 // ---- mean-squared error, forward + gradient in one pass ------------------------------------
