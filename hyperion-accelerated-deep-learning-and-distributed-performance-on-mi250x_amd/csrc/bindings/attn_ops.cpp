@@ -205,7 +205,7 @@ std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tens
 std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, const c10::optional<at::Tensor>& weight,
                                const at::Tensor& mean, const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
                                bool need_dw, bool need_db, bool rms, double drop_p,
-                               const c10::optional<at::Tensor>& rng) {
+                               const c10::optional<at::Tensor>& rng, bool branch_sum) {
   const int d = xin.size(-1);
   const int64_t rows = xin.numel() / d;
   at::Tensor g = dy.is_contiguous() ? dy : dy.contiguous();
@@ -214,12 +214,18 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
   int P = 1, rpw = 1;
   hyp::layernorm_bwd_geom(rows, d, &P, &rpw);
   auto fopt = xin.options().dtype(at::kFloat);
-  auto part = at::empty({2 * (int64_t)P * d}, fopt);
+  branch_sum = branch_sum && d <= 2048;
+  auto part = at::empty({(branch_sum ? 3 : 2) * (int64_t)P * d}, fopt);
   const int wt = affine_mode(xin, weight, c10::nullopt, "ln_bwd");
   auto wopt = wt ? xin.options() : fopt;  // dγ / dβ in the weight's dtype
   // LayerNorm: dγ and dβ come out of one combine pass into one [2, d] buffer (both computed)
-  at::Tensor dw, db, dwdb;
-  if (!rms && (need_dw || need_db)) {
+  at::Tensor dw, db, dwdb, dbs;
+  if (branch_sum) {  // [dγ | dβ | Σ branch gradient] (RMS: [dγ | Σ]) from one combine
+    dwdb = at::empty({rms ? 2 : 3, d}, wopt);
+    dw = dwdb[0];
+    if (!rms) db = dwdb[1];
+    dbs = dwdb[rms ? 1 : 2];
+  } else if (!rms && (need_dw || need_db)) {
     dwdb = at::empty({2, d}, wopt);
     dw = dwdb[0];
     db = dwdb[1];
@@ -242,8 +248,9 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
                                         part.data_ptr<float>(), db.defined() ? part.data_ptr<float>() + d : nullptr,
                                         dw.defined() ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr,
                                         rows, d, P, rpw, cur_stream(), wt, dxa.defined() ? dxa.data_ptr() : nullptr,
-                                        (float)drop_p, drop_p > 0.0 ? &rs : nullptr));
-  return {dx, need_dw ? dw : at::Tensor(), need_db ? db : at::Tensor(), dxa};
+                                        (float)drop_p, drop_p > 0.0 ? &rs : nullptr,
+                                        dbs.defined() ? dbs.data_ptr() : nullptr));
+  return {dx, need_dw ? dw : at::Tensor(), need_db ? db : at::Tensor(), dxa, dbs};
 }
 
 }  // namespace
@@ -258,7 +265,8 @@ void register_attn_ops(pybind11::module& m) {
   m.def("ln_bwd", &ln_bwd, "LayerNorm/RMSNorm backward (+ the dropped input's gradient)", pybind11::arg("dy"),
         pybind11::arg("xin"), pybind11::arg("weight"), pybind11::arg("mean"), pybind11::arg("rstd"),
         pybind11::arg("dres"), pybind11::arg("need_dw"), pybind11::arg("need_db"), pybind11::arg("rms"),
-        pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none());
+        pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none(),
+        pybind11::arg("branch_sum") = false);
 }
 
 }  // namespace hypbind

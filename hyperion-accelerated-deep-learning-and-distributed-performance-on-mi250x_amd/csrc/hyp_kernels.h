@@ -69,7 +69,11 @@ hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, v
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
                               void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt = 0,
-                              void* dxa = nullptr, float drop_p = 0.f, const struct RngState* rs = nullptr);
+                              void* dxa = nullptr, float drop_p = 0.f, const struct RngState* rs = nullptr,
+                              void* dbs = nullptr);
+// dbs (d <= 2048): also Σ_rows of the branch gradient as stored (dxa when dropping, else dx), in the
+// weight dtype, at dw + d (no bias) or dw + 2d (with db) — the bias gradient of the linear layer
+// that produced the norm's input, combined in the same launch as dγ / dβ
 }  // namespace hyp
 
 namespace hyp {

@@ -163,7 +163,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_fwd_k(const T* __restr
 // dx and per-block partial dγ, dβ.  grid.x = ceil(rows / (kWavesPerBlock * rows_per_wave))
 // DROP: also dxa = dropout(dx) with the forward's mask — the gradient of the dropped branch (the
 // residual branch gets dx itself): the separate dropout-backward pass over dx disappears.
-template <typename T, int VPL, bool RMS, bool HAS_DRES, bool DROP = false>
+// BSUM: also the column sums of the branch gradient as stored (dxa, or dx) — the bias gradient of
+// the linear layer whose output is this norm's input (ops/layernorm.py BiasGradLink): a third
+// partial segment [P][.. | d] combined in the same launch as dγ / dβ (no column-sum passes).
+template <typename T, int VPL, bool RMS, bool HAS_DRES, bool DROP = false, bool BSUM = false>
 __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restrict__ dy, const T* __restrict__ xin,
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ mean_in,
@@ -171,15 +174,22 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
                                                                   const T* __restrict__ dres, T* __restrict__ dx,
                                                                   float* __restrict__ pdw, float* __restrict__ pdb,
                                                                   int64_t rows, int d, int rows_per_wave, int wt,
-                                                                  T* __restrict__ dxa = nullptr, LnDrop dp = LnDrop{}) {
+                                                                  T* __restrict__ dxa = nullptr, LnDrop dp = LnDrop{},
+                                                                  int bs_off = 0) {
   const int lane = threadIdx.x & 63;
   const uint64_t dkey = DROP ? rng_key(dp.rs) : 0;
   const int wid = threadIdx.x >> 6;
-  float gw[VPL][8], gb[VPL][8], wv[VPL][8];
+  float gw[VPL][8], gb[VPL][8], wv[VPL][8], gs[BSUM ? VPL : 1][8];
 #pragma unroll
   for (int k = 0; k < VPL; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) gw[k][j] = gb[k][j] = 0.f;
+  if constexpr (BSUM) {
+#pragma unroll
+    for (int k = 0; k < VPL; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gs[k][j] = 0.f;
+  }
   load_affine<T, VPL>(w, wt, d, lane, wv, 1.f);
 
   const int64_t row_begin = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * rows_per_wave;
@@ -242,6 +252,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
           for (int j = 0; j < 8; ++j)
             oa[j] = rng_u32(dkey, (uint64_t)(row * d + c + j)) >= dp.thr ? rnd<T>(o[j]) * dp.scale : 0.f;
           Vec8<T>::store(dxa + row * d + c, oa);
+          if constexpr (BSUM) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gs[k][j] += rnd<T>(oa[j]);  // the stored (rounded) values
+          }
+        } else if constexpr (BSUM) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gs[k][j] += rnd<T>(o[j]);
         }
       }
     }
@@ -255,6 +272,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sw = smem;
   float* sb = smem + kWavesPerBlock * d;
+  float* ss = smem + 2 * kWavesPerBlock * d;  // BSUM
 #pragma unroll
   for (int k = 0; k < VPL; ++k) {
     const int c = (k * 64 + lane) * 8;
@@ -263,21 +281,25 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void ln_bwd_k(const T* __restr
       for (int j = 0; j < 8; ++j) {
         sw[wid * d + c + j] = gw[k][j];
         sb[wid * d + c + j] = gb[k][j];
+        if constexpr (BSUM) ss[wid * d + c + j] = gs[k][j];
       }
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < d; c += 64 * kWavesPerBlock) {
-    float a = 0.f, bb = 0.f;
+    float a = 0.f, bb = 0.f, sa = 0.f;
 #pragma unroll
     for (int q = 0; q < kWavesPerBlock; ++q) {
       a += sw[q * d + c];
       bb += sb[q * d + c];
+      if constexpr (BSUM) sa += ss[q * d + c];
     }
-    // partial rows [P][d] (dγ only) or [P][2d] (dγ | dβ: one combine pass for both)
-    const int64_t ps = pdb ? 2 * (int64_t)d : d;
+    // partial rows [P][d] (dγ only) or [P][2d] (dγ | dβ: one combine pass for both), + d (BSUM:
+    // the branch-gradient sums at column bs_off)
+    const int64_t ps = (pdb ? 2 * (int64_t)d : d) + (BSUM ? d : 0);
     pdw[(int64_t)blockIdx.x * ps + c] = a;
     if (pdb) pdb[(int64_t)blockIdx.x * ps + c] = bb;
+    if constexpr (BSUM) pdw[(int64_t)blockIdx.x * ps + bs_off + c] = sa;
   }
 }
 
@@ -527,8 +549,49 @@ hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, c
 template <typename T, bool RMS>
 hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const float* mean, const float* rstd,
                            const T* dres, T* dx, float* pdw, float* pdb, void* dw, void* db, int64_t rows, int d,
-                           int P, int rows_per_wave, hipStream_t st, int wt, int wdt, T* dxa, const LnDrop* drop) {
+                           int P, int rows_per_wave, hipStream_t st, int wt, int wdt, T* dxa, const LnDrop* drop,
+                           void* dbs) {
   if (drop != nullptr && (d > 2048 || dxa == nullptr)) return hipErrorInvalidValue;
+  if (dbs != nullptr) {  // the branch-gradient sums follow dw (| db) in the combined output
+    const size_t wb = wdt == kF32 ? 4 : 2;
+    if (d > 2048 || dw == nullptr ||
+        static_cast<char*>(dbs) != static_cast<char*>(dw) + (size_t)(pdb != nullptr ? 2 : 1) * d * wb)
+      return hipErrorInvalidValue;
+    if (pdb != nullptr) pdb = pdw + d;
+    const int bs_off = pdb != nullptr ? 2 * d : d;
+    const int vpl = (d + 511) / 512;
+    const dim3 grid(P), block(64 * kWavesPerBlock);
+    const size_t lds = 3 * kWavesPerBlock * d * sizeof(float);
+    const LnDrop dp0 = drop != nullptr ? *drop : LnDrop{};
+#define HYP_LN_BS(V)                                                                                           \
+  case V:                                                                                                      \
+    if (drop && dres)                                                                                          \
+      hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, true, true, true>), grid, block, lds, st, dy, xin, w, mean, rstd, \
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave, wt, dxa, dp0, bs_off);                    \
+    else if (drop)                                                                                             \
+      hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, false, true, true>), grid, block, lds, st, dy, xin, w, mean, rstd, \
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave, wt, dxa, dp0, bs_off);                    \
+    else if (dres)                                                                                             \
+      hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, true, false, true>), grid, block, lds, st, dy, xin, w, mean, rstd, \
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave, wt, dxa, dp0, bs_off);                    \
+    else                                                                                                       \
+      hipLaunchKernelGGL((ln_bwd_k<T, V, RMS, false, false, true>), grid, block, lds, st, dy, xin, w, mean, rstd, \
+                         dres, dx, pdw, pdb, rows, d, rows_per_wave, wt, dxa, dp0, bs_off);                    \
+    break;
+    switch (vpl) {
+      HYP_LN_BS(1)
+      HYP_LN_BS(2)
+      HYP_LN_BS(3)
+      HYP_LN_BS(4)
+      HYP_LN_BS(8)
+      default:
+        return hipErrorInvalidValue;
+    }
+#undef HYP_LN_BS
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = colsum_combine(pdw, P, bs_off + d, dw, wdt, st);
+    return e;
+  }
   // with a bias: dγ and dβ partials interleave per block row ([P][2d]) and ONE combine writes
   // dw | db (the caller's db must directly follow dw)
   const size_t wbytes = wdt == kF32 ? 4 : 2;
@@ -644,7 +707,7 @@ hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, v
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
                               void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt,
-                              void* dxa, float drop_p, const RngState* rs) {
+                              void* dxa, float drop_p, const RngState* rs, void* dbs) {
   const int wdt = wt ? dtype : kF32;  // dγ / dβ in the weight's dtype
   if (!layernorm_supported(d)) return hipErrorInvalidValue;
   if (drop_p > 0.f && (rs == nullptr || drop_p >= 1.f || dxa == nullptr)) return hipErrorInvalidValue;
@@ -653,9 +716,9 @@ hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xi
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (rms)
       return ln_bwd_dispatch<T, true>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                      db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr);
+                                      db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr, dbs);
     return ln_bwd_dispatch<T, false>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                     db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr);
+                                     db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr, dbs);
   });
   return hipSuccess;
 }

@@ -35,7 +35,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops.attention import attention_packed
 from ..ops.conv import residual_link
 from ..ops.dropout import Dropout
-from ..ops.layernorm import LayerNorm
+from ..ops.layernorm import LayerNorm, bias_grad_link
 from ..ops.linear import Linear, linear
 from ..ops.linear_act import LinearAct, linear_act
 
@@ -68,12 +68,13 @@ class MultiheadSelfAttention(nn.Module):
         causal: bool = False,
         key_padding_mask: Optional[torch.Tensor] = None,
         link=None,
+        blink=None,
     ) -> torch.Tensor:
         B, S, E = x.shape
         qkv = linear(x, self.in_proj_weight, self.in_proj_bias, link=link).view(B, S, 3, self.num_heads, self.head_dim)
         p = self.dropout if self.training else 0.0
         o = attention_packed(qkv, causal=causal, dropout_p=p, key_padding_mask=key_padding_mask)
-        return self.out_proj(o.reshape(B, S, E))
+        return self.out_proj(o.reshape(B, S, E), blink=blink)
 
 
 def _ffn_up(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], activation: str) -> torch.Tensor:
@@ -110,9 +111,10 @@ class TransformerEncoderLayer(nn.Module):
         self.dropout2 = Dropout(dropout)
         self.activation = activation
 
-    def _ff(self, x: torch.Tensor, link=None) -> torch.Tensor:
+    def _ff(self, x: torch.Tensor, link=None, blink=None) -> torch.Tensor:
         # the inner dropout rides linear1's epilogue (forward) and its activation backward
-        return self.linear2(self.linear1(x, dropout_p=self.dropout.p if self.training else 0.0, link=link))
+        return self.linear2(self.linear1(x, dropout_p=self.dropout.p if self.training else 0.0, link=link),
+                            blink=blink)
 
     def forward(self, x: torch.Tensor, causal: bool = False,
                 key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -126,10 +128,14 @@ class TransformerEncoderLayer(nn.Module):
         # the GEMM's data gradient adds it in its epilogue — no autograd add of the two gradients
         p1 = self.dropout1.p if self.training else 0.0
         p2 = self.dropout2.p if self.training else 0.0
+        # and out_proj's / linear2's bias gradients come from the norm backward's column sums (BiasGradLink)
         link = residual_link(x) if torch.is_grad_enabled() else None
-        x = self.norm1(self.self_attn(x, causal, key_padding_mask, link=link), residual=x, dropout_p=p1, link=link)
+        bl = bias_grad_link()
+        x = self.norm1(self.self_attn(x, causal, key_padding_mask, link=link, blink=bl), residual=x, dropout_p=p1,
+                       link=link, blink=bl)
         link = residual_link(x) if torch.is_grad_enabled() else None
-        return self.norm2(self._ff(x, link=link), residual=x, dropout_p=p2, link=link)
+        bl = bias_grad_link()
+        return self.norm2(self._ff(x, link=link, blink=bl), residual=x, dropout_p=p2, link=link, blink=bl)
 
 
 class TransformerEncoder(nn.Module):

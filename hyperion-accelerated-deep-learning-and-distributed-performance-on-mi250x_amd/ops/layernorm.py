@@ -40,6 +40,35 @@ def _ref(x, residual, weight, bias, eps, rms, dropout_p=0.0):
     return y, s
 
 
+class BiasGradLink:
+    """Hands a norm's branch gradient column sums to the linear layer that produced its input.
+
+    The linear's output is the norm's ``x`` (its only consumer), so the linear's bias gradient is
+    Σ_rows of the gradient the norm's backward returns for x — the LayerNorm backward kernel sums
+    it while storing it (``layernorm.hip`` BSUM, combined with dγ / dβ in one launch) and parks it
+    here; the linear's backward uses it when the gradient it receives IS that tensor (else it sums
+    dy itself).  ``armed`` is set by the linear (it has a bias and ran the native path)."""
+
+    __slots__ = ("armed", "db", "g")
+
+    def __init__(self):
+        self.armed = False
+        self.db = None
+        self.g = None
+
+    def take(self, dy: torch.Tensor) -> Optional[torch.Tensor]:
+        db, g = self.db, self.g
+        self.db = self.g = None
+        return db if (db is not None and g is dy) else None
+
+
+def bias_grad_link() -> Optional[BiasGradLink]:
+    return BiasGradLink() if (FUSE_BIAS_GRAD and torch.is_grad_enabled()) else None
+
+
+FUSE_BIAS_GRAD = True  # A/B switch (tests)
+
+
 def _will_run(ref) -> bool:
     node = ref() if ref is not None else None
     return node is not None and torch._C._will_engine_execute_node(node)
@@ -47,7 +76,7 @@ def _will_run(ref) -> bool:
 
 class _LNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum, dropout_p=0.0, link=None):
+    def forward(ctx, x, residual, weight, bias, eps, rms, return_sum, dropout_p=0.0, link=None, blink=None):
         C = _native.native()
         x = x.contiguous()
         if residual is not None:
@@ -61,6 +90,7 @@ class _LNFn(torch.autograd.Function):
         ctx.drop = (dropout_p, st)
         ctx.has_res = residual is not None
         ctx.link = link
+        ctx.blink = blink
         ctx.save_for_backward(xin, weight, mean, rstd)
         if return_sum:
             return y, (s if residual is not None else x)
@@ -72,7 +102,12 @@ class _LNFn(torch.autograd.Function):
         need_dw = weight is not None and ctx.needs_input_grad[2]
         need_db = ctx.needs_input_grad[3]
         p, st = ctx.drop
-        dx, dw, db, dxa = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms, p, st)
+        blink = ctx.blink
+        bsum = blink is not None and blink.armed and ctx.needs_input_grad[0]
+        dx, dw, db, dxa, dbs = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms, p,
+                                                       st, bsum)
+        if bsum and dbs is not None:
+            blink.db, blink.g = dbs, (dxa if p > 0.0 else dx)
         dres = dx if ctx.has_res and ctx.needs_input_grad[1] else None
         link = ctx.link
         if dres is not None and link is not None and link.armed and _will_run(link.first_node):
@@ -84,7 +119,7 @@ class _LNFn(torch.autograd.Function):
             dres,
             dw if need_dw else None,
             db if need_db else None,
-            None, None, None, None, None,
+            None, None, None, None, None, None,
         )
 
 
@@ -98,6 +133,7 @@ def layer_norm(
     return_sum: bool = False,
     dropout_p: float = 0.0,
     link=None,
+    blink=None,
 ) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
     """``LN(x + residual)`` (or RMSNorm); ``dropout_p``: ``LN(residual + dropout(x))`` — pass it only
     in training (it is applied whenever > 0)."""
@@ -121,7 +157,7 @@ def layer_norm(
     if native:
         if link is not None and residual is not link.src:
             link = None
-        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum, float(dropout_p), link)
+        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum, float(dropout_p), link, blink)
     y, s = _ref(x, residual, weight, bias, eps, rms, dropout_p)
     return (y, s) if return_sum else y
 
@@ -130,7 +166,7 @@ class LayerNorm(nn.LayerNorm):
     """``nn.LayerNorm`` (same keys) with an optional fused residual input."""
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,  # type: ignore[override]
-                dropout_p: float = 0.0, link=None) -> torch.Tensor:
+                dropout_p: float = 0.0, link=None, blink=None) -> torch.Tensor:
         """``LN(x + residual)``; ``dropout_p`` > 0: ``LN(residual + dropout(x))`` (post-norm branch)."""
         if len(self.normalized_shape) != 1:
             if dropout_p > 0.0:
@@ -138,7 +174,8 @@ class LayerNorm(nn.LayerNorm):
             return super().forward(x if residual is None else x + residual)
         if torch.is_autocast_enabled() and x.dtype == torch.float32 and residual is not None:
             residual = residual.float()
-        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual, dropout_p=dropout_p, link=link)
+        return layer_norm(x, self.weight, self.bias, self.eps, residual=residual, dropout_p=dropout_p, link=link,
+                          blink=blink)
 
 
 class RMSNorm(nn.Module):

@@ -118,7 +118,7 @@ def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, link=None):
+    def forward(ctx, x, w, b, link=None, blink=None):
         x2 = x.reshape(-1, x.shape[-1])
         y = None
         if b is not None and not _fwd_ok(x2, w):
@@ -134,6 +134,9 @@ class _LinearFn(torch.autograd.Function):
         ctx.bdt = b.dtype if b is not None else None
         ctx.xshape = x.shape
         ctx.link = link
+        ctx.blink = blink
+        if blink is not None and b is not None:
+            blink.armed = True  # the consuming norm's backward will sum our output's gradient
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -143,11 +146,21 @@ class _LinearFn(torch.autograd.Function):
         add = take_link_grad(ctx.link, ctx.xshape)
         dx = linear_dgrad(dy2, w, add).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = linear_wgrad(dy2.contiguous(), x2.contiguous()).to(w.dtype) if ctx.needs_input_grad[1] else None
-        db = bias_grad(dy2.contiguous(), ctx.bdt) if (ctx.has_b and ctx.needs_input_grad[2]) else None
-        return dx, dw, db, None
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = ctx.blink.take(dy) if ctx.blink is not None else None
+            if db is not None:
+                _native.count("bias_grad_from_norm")
+                db = db.to(ctx.bdt)
+            else:
+                db = bias_grad(dy2.contiguous(), ctx.bdt)
+        elif ctx.blink is not None:
+            ctx.blink.take(dy)
+        return dx, dw, db, None, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, link=None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, link=None,
+           blink=None) -> torch.Tensor:
     """``F.linear`` with the weight-streaming kernels on gfx950 (same math, same grads).  Under
     autocast, x and w are cast to the autocast dtype first (differentiable casts, like torch's own
     autocast of ``F.linear``), so the native kernels serve the AMP trainers too.  ``link``: a
@@ -161,7 +174,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, l
         with torch.autocast(x.device.type, enabled=False):
             return _LinearFn.apply(x.to(dt), w.to(dt), b)  # (a cast copy: the link stays unarmed)
     link = arm_link(link, x)
-    y = _LinearFn.apply(x, w, b, link)
+    y = _LinearFn.apply(x, w, b, link, blink)
     if link is not None and y.grad_fn is not None:
         link.first_node = weakref.ref(y.grad_fn)
     return y
@@ -170,5 +183,5 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, l
 class Linear(nn.Linear):
     """``nn.Linear`` (same parameters and state-dict keys) routed through :func:`linear`."""
 
-    def forward(self, x: torch.Tensor, link=None) -> torch.Tensor:  # type: ignore[override]
-        return linear(x, self.weight, self.bias, link=link)
+    def forward(self, x: torch.Tensor, link=None, blink=None) -> torch.Tensor:  # type: ignore[override]
+        return linear(x, self.weight, self.bias, link=link, blink=blink)

@@ -314,3 +314,31 @@ def test_post_norm_layer_residual_grad_rides_the_gemm(monkeypatch, p):
         for n in res[0][2]:  # (the attention backward's atomics make both runs differ at bf16 level)
             a, b = res[1][2][n].float(), res[0][2][n].float()
             assert float((a - b).norm() / (b.norm() + 1e-12)) < 1e-2, n
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_post_norm_layer_bias_grads_from_norm_backward(monkeypatch, p):
+    """out_proj's and linear2's bias gradients come from the LayerNorm backward kernel's column sums
+    of the branch gradient (BiasGradLink, layernorm.hip BSUM) — equal to summing dy separately."""
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.ops import _native
+    from hyperion.ops import layernorm as ln_mod
+
+    torch.manual_seed(0)
+    layer = TransformerEncoderLayer(256, 4, 1024, dropout=p, activation="gelu").cuda().bfloat16()
+    x0 = torch.randn(4, 64, 256, device="cuda").bfloat16()
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(ln_mod, "FUSE_BIAS_GRAD", fuse)
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        _native.reset_counters()
+        torch.cuda.manual_seed(123)  # the same dropout masks in both runs
+        y = layer(x, causal=True)
+        (y.float() * torch.linspace(-1, 1, 256, device="cuda")).sum().backward()
+        torch.cuda.synchronize()
+        res.append(({n: q.grad.clone() for n, q in layer.named_parameters()}, dict(_native.counters())))
+    assert res[1][1].get("bias_grad_from_norm") == 2 and not res[0][1].get("bias_grad_from_norm")
+    for n in ("self_attn.out_proj.bias", "linear2.bias"):
+        a, b = res[1][0][n].float(), res[0][0][n].float()
+        assert float((a - b).norm() / (b.norm() + 1e-12)) < 2e-2, n
