@@ -28,7 +28,7 @@ from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.dropout import Dropout
-from ..ops.layernorm import LayerNorm, layer_norm
+from ..ops.layernorm import LayerNorm, bias_grad_link, layer_norm
 from ..ops.linear import Linear
 from ..ops.linear_act import LinearAct
 from .transformer import MultiheadSelfAttention, _ffn_up
@@ -45,8 +45,8 @@ class MLPBlock(nn.Sequential):
             nn.init.xavier_uniform_(m.weight)
             nn.init.normal_(m.bias, std=1e-6)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
-        return self[4](self[3](self[2](self[0](x))))
+    def forward(self, x: torch.Tensor, blink=None) -> torch.Tensor:  # type: ignore[override]
+        return self[4](self[3](self[2](self[0](x)), blink=blink))
 
 
 class EncoderBlock(nn.Module):
@@ -60,20 +60,25 @@ class EncoderBlock(nn.Module):
         self.ln_2 = LayerNorm(hidden_dim, eps=1e-6)
         self.mlp = MLPBlock(hidden_dim, mlp_dim, dropout)
 
-    def forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:  # type: ignore[override]
+    def forward(self, delta: Optional[torch.Tensor], stream: torch.Tensor, blink_in=None,
+                blink_out=None) -> Tuple[torch.Tensor, torch.Tensor]:  # type: ignore[override]
         """One block on the residual stream.
 
         Input ``stream + delta`` is the block input (``delta`` = previous block's MLP output, not yet
         added).  Returns ``(mlp_out, new_stream)`` with ``new_stream + mlp_out`` = block output.
+        ``blink_in`` / ``blink_out``: BiasGradLinks of the previous / this block's fc2 (its bias
+        gradient is the column sum the next LayerNorm backward takes of its input gradient); the
+        attention out_proj's bias gradient comes from ln_2's backward the same way.
         """
         if delta is None:
             h, s = self.ln_1(stream), stream
         else:
             h, s = layer_norm(delta, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps, residual=stream,
-                              return_sum=True)
-        a = self.dropout(self.self_attention(h))
-        h2, s2 = layer_norm(a, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps, residual=s, return_sum=True)
-        return self.mlp(h2), s2
+                              return_sum=True, blink=blink_in)
+        bl = bias_grad_link()
+        a = self.dropout(self.self_attention(h, blink=bl))
+        h2, s2 = layer_norm(a, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps, residual=s, return_sum=True, blink=bl)
+        return self.mlp(h2, blink=blink_out), s2
 
     def block(self, x: torch.Tensor) -> torch.Tensor:
         """Plain form: x -> block output."""
@@ -107,10 +112,12 @@ class Encoder(nn.Module):
                 else:
                     d, s = checkpoint(blk, d, s, use_reentrant=False)
             else:
-                d, s = blk(d, s)
+                bl_prev = bl if d is not None else None
+                bl = bias_grad_link()
+                d, s = blk(d, s, blink_in=bl_prev, blink_out=bl)
         if d is None:
             return self.ln(s)
-        return self.ln(d, residual=s)
+        return self.ln(d, residual=s, blink=None if ckpt else bl)
 
 
 class VisionTransformer(nn.Module):

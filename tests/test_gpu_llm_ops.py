@@ -342,3 +342,31 @@ def test_post_norm_layer_bias_grads_from_norm_backward(monkeypatch, p):
     for n in ("self_attn.out_proj.bias", "linear2.bias"):
         a, b = res[1][0][n].float(), res[0][0][n].float()
         assert float((a - b).norm() / (b.norm() + 1e-12)) < 2e-2, n
+
+
+@pytest.mark.parametrize("ckpt", [False, True])
+def test_vit_bias_grads_from_norm_backward(monkeypatch, ckpt):
+    """ViT pre-norm blocks: out_proj (via ln_2) and fc2 (via the next block's ln_1 / the final ln)
+    bias gradients from the LayerNorm backward's column sums — same gradients as summing dy."""
+    from hyperion.models.vit import VisionTransformer
+    from hyperion.ops import _native
+    from hyperion.ops import layernorm as ln_mod
+
+    torch.manual_seed(0)
+    m = VisionTransformer(64, 16, 3, 4, 256, 512, num_classes=10, use_checkpoint=ckpt).cuda().bfloat16()
+    x0 = torch.randn(4, 3, 64, 64, device="cuda").bfloat16()
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(ln_mod, "FUSE_BIAS_GRAD", fuse)
+        m.zero_grad(set_to_none=True)
+        _native.reset_counters()
+        m(x0).float().square().mean().backward()
+        torch.cuda.synchronize()
+        res.append(({n: q.grad.clone() for n, q in m.named_parameters() if q.grad is not None},
+                    dict(_native.counters())))
+    if not ckpt:
+        assert res[1][1].get("bias_grad_from_norm") == 6, res[1][1]
+    assert not res[0][1].get("bias_grad_from_norm")
+    for n in res[0][0]:
+        a, b = res[1][0][n].float(), res[0][0][n].float()
+        assert float((a - b).norm() / (b.norm() + 1e-12)) < 2e-2, n
