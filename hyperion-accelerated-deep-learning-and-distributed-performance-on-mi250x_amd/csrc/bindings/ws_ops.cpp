@@ -288,6 +288,8 @@ void register_ws_ops(pybind11::module& m) {
         "nn"_a = false, "alpha"_a = 1.0, "addend"_a = pybind11::none(), "beta"_a = 1.0, "mf"_a = 0, "kr"_a = 0,
         "G"_a = 0, "nf"_a = 0);
   m.def("ws_plan", &ws_plan_py, "(mf, kr, G, nf, S, MFtot) of the automatic plan");
+  m.def("ws_set_depth", [](int64_t d) { hyp::ws_set_depth((int)d); },
+        "weight-streaming GEMM: k-steps in flight per wave (4 default, 8 where the slices allow)");
   m.def("ws_epilogue", &ws_epilogue_py, "fused slab epilogue (0 plain, 1 LoRA up + RoPE, 2 SwiGLU, 3 SwiGLU bwd, 4 LoRA dgrad)",
         "part"_a, "S"_a, "MFtot"_a, "M"_a, "N"_a, "epi"_a, "out"_a, "out2"_a = pybind11::none(),
         "aux"_a = pybind11::none(), "t"_a = pybind11::none(), "lw"_a = std::vector<at::Tensor>{}, "segw"_a = 0,

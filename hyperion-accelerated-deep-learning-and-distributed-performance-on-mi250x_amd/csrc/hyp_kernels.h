@@ -374,6 +374,7 @@ namespace hyp {
 // nn = false: y = x Wᵀ (W [N, K]); nn = true: y = x W (W [K, N]).  Writes fp32 partial slabs
 // [S][MB*mf][N/16][64][4] (fragment order; sb = 1: bf16 elements); ws_reduce sums them (+ epilogue) into [M, N].
 bool ws_supported(int M, int N, int K, bool nn);
+void ws_set_depth(int d);  // weight-streaming GEMM: k-steps in flight per wave (4 default, or 8)
 void ws_plan(int M, int N, int K, bool nn, int* mf, int* kr, int* G, int* nf);
 hipError_t ws_gemm(int dtype, bool nn, const void* x, int64_t ldx, const void* w, int64_t ldw, float* part,
                    const void* zero, int M, int N, int K, int mf, int kr, int G, int nf, hipStream_t st, int sb = 0);

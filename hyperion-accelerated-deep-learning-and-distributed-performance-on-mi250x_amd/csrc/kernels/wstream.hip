@@ -244,9 +244,10 @@ __global__ __launch_bounds__(WAVES * 64) void ws_gemm_k(const WsArgs a) {
   }
 }
 
-template <typename T, int MF, int NF, bool NN>
-hipError_t launch_gemm(const WsArgs& a, int grid, hipStream_t st) {
-  constexpr int D = 4;
+int g_ws_depth = 4;  // k-steps in flight per wave (ws_set_depth): 4, or 8 where the slices allow it
+
+template <typename T, int MF, int NF, bool NN, int D>
+hipError_t launch_gemm_d(const WsArgs& a, int grid, hipStream_t st) {
   // two waves per SIMD where the registers allow it (NT with <= 2 fragments per chunk)
   constexpr int WAVES = (!NN && MF * NF <= 16) ? 8 : 4;
   const size_t lds = (size_t)MF * 16 * a.krp * 2;
@@ -260,6 +261,15 @@ hipError_t launch_gemm(const WsArgs& a, int grid, hipStream_t st) {
   }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(WAVES * 64), lds, st, a);
   return hipGetLastError();
+}
+
+// D = 8 (twice the weight bytes in flight per wave) needs every slice's k-steps to fill whole rings
+template <typename T, int MF, int NF, bool NN>
+hipError_t launch_gemm(const WsArgs& a, int grid, hipStream_t st) {
+  if constexpr (MF == 8) {
+    if (g_ws_depth == 8 && a.kr % 256 == 0 && (a.K % a.kr) % 256 == 0) return launch_gemm_d<T, MF, NF, NN, 8>(a, grid, st);
+  }
+  return launch_gemm_d<T, MF, NF, NN, 4>(a, grid, st);
 }
 
 // ---- slab reduction: out[m, n] = alpha * Σ_s part[s] (+ beta * addend) (+ rank-r term) ---------------
@@ -614,6 +624,8 @@ __global__ __launch_bounds__(256) void ws_epi_k(const WsEpi a) {
 }
 
 }  // namespace
+
+void ws_set_depth(int d) { g_ws_depth = d == 8 ? 8 : 4; }
 
 bool ws_supported(int M, int N, int K, bool nn) {
   if (M < 1 || K < 128 || K % 128 != 0) return false;
