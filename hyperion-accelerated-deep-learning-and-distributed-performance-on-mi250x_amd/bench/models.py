@@ -7,6 +7,7 @@ samples/s, tokens/s, ms/step and peak memory.  Used by ``cli/bench_models`` and 
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Dict, Optional
 
@@ -154,13 +155,16 @@ def bench_llama_lora_step(batch: int = 1, seq: int = 128, steps: int = 10, warmu
 
 
 def _ddp_world1(m):
-    """m's parameters under Hyperion DDP on one GPU: buckets on, native RCCL communicator."""
+    """m's parameters under Hyperion DDP on one GPU: buckets on, native RCCL communicator.
+    HYPERION_DDP_COMM_DTYPE=param reduces in the parameters' dtype (torch DDP's semantics: the
+    gradients then live in their bucket slots, no pack copies); default fp32 buckets."""
     from ..parallel import DDP
     from ..parallel.comm import NativeComm
 
     _ensure_pg()
     dev = next(m.parameters()).device
-    return DDP(m, buckets_at_world_1=True, comm=NativeComm(dev), broadcast_buffers=False)
+    kw = {"comm_dtype": None} if os.environ.get("HYPERION_DDP_COMM_DTYPE") == "param" else {}
+    return DDP(m, buckets_at_world_1=True, comm=NativeComm(dev), broadcast_buffers=False, **kw)
 
 
 def _graphed(body, m, dpm, one_graph: bool = False):
