@@ -219,18 +219,94 @@ at::Tensor linear_ce_grad(const at::Tensor& x, const at::Tensor& w, const c10::o
   return dz;
 }
 
+// Deferred weight-gradient reduce (per device): the split-K reduce of the last conv_wgrad(defer=True)
+// waits here and rides on the next conv_wgrad launch as extra workgroups; conv_wgrad_flush() runs
+// it standalone.  The partials tensor and the OUTPUT's storage are held until the kernel that uses
+// them is queued (stream order protects the reuse of their memory after that).  The output is held
+// by storage, not as a tensor: an extra tensor reference would stop AccumulateGrad from stealing
+// the gradient (it would clone the not-yet-reduced values instead).
+struct PendingWgrad {
+  at::Tensor part;
+  c10::Storage out_storage;
+  void* out = nullptr;
+  int out_dtype = 0;
+  int64_t n = 0;
+  int splits = 0;
+  float alpha = 1.f;
+  hipStream_t stream = nullptr;
+};
+// leaked on purpose: no tensor destructor may run after the HIP runtime is torn down at exit
+PendingWgrad* const g_pending_wgrad = new PendingWgrad[64];
+
+bool conv_wgrad_flush_dev(int dev) {
+  PendingWgrad& p = g_pending_wgrad[dev];
+  if (!p.part.defined()) return false;
+  PendingWgrad q = std::move(p);
+  p = PendingWgrad{};
+  HYP_CHECK_HIP(hyp::splitk_reduce(q.out_dtype, q.part.data_ptr<float>(), q.out, q.n, q.splits, q.stream, q.alpha));
+  return true;
+}
+
+bool conv_wgrad_flush() {
+  bool any = false;
+  for (int d = 0; d < 64; ++d) any |= conv_wgrad_flush_dev(d);
+  return any;
+}
+
+// The pending reduce of this device's stream, taken out to ride on the next weight-gradient launch
+// (another stream's pending reduce is flushed instead: no chaining across streams).
+hyp::WgradPendingReduce take_pending_wgrad(int dev, hipStream_t stream, PendingWgrad& taken) {
+  PendingWgrad& pend = g_pending_wgrad[dev];
+  if (pend.part.defined() && pend.stream != stream) conv_wgrad_flush_dev(dev);
+  hyp::WgradPendingReduce pr{};
+  if (pend.part.defined()) {
+    taken = std::move(pend);
+    pend = PendingWgrad{};
+    pr.part = taken.part.data_ptr<float>();
+    pr.out = taken.out;
+    pr.n = taken.n;
+    pr.splits = taken.splits;
+    pr.alpha = taken.alpha;
+    pr.dtype = taken.out_dtype;
+  }
+  return pr;
+}
+
+void park_pending_wgrad(int dev, const at::Tensor& part, const at::Tensor& dw, int splits, float alpha,
+                        hipStream_t stream) {
+  PendingWgrad& pend = g_pending_wgrad[dev];
+  pend.part = part;
+  pend.out_storage = dw.storage();
+  pend.out = dw.data_ptr();
+  pend.out_dtype = dtype_code(dw);
+  pend.n = dw.numel();
+  pend.splits = splits;
+  pend.alpha = alpha;
+  pend.stream = stream;
+}
+
 // Stride-1 data gradient: dy [N,K,P,Q] channels-last, w [K,C,R,S] channels-last (the forward
 // filter, NOT flipped) -> dx [N,C,H,W] channels-last with H = P + R - 1 - 2 ph.
 // bn_mode >= 0: BN-backward epilogue for the BN layer whose OUTPUT is dx's tensor (hyp::BnBwdEpilogue):
 // bn_x its input [N,C,H,W], bn_y its output (mode 2), bn_w/bn_b/bn_mean/bn_invstd (mode 1), bn_sums
 // a zeroed fp64 [kStatSlots*2*C] accumulator; the result is then dz = dx · mask.
-at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
-                      int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend,
-                      const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_y,
-                      const c10::optional<at::Tensor>& bn_w, const c10::optional<at::Tensor>& bn_b,
-                      const c10::optional<at::Tensor>& bn_mean, const c10::optional<at::Tensor>& bn_invstd,
-                      int64_t bn_mode, const c10::optional<at::Tensor>& bn_sums, int64_t stride, int64_t Hx,
-                      int64_t Wx, int64_t stages) {
+// The weight gradient that may ride in the data gradient's launch (conv_dual.hip)
+struct WgradReq {
+  const at::Tensor* x = nullptr;  // the conv's input [N, C, H, W] channels-last
+  int64_t R = 1, S = 1, sh = 1, sw = 1, ph = 0, pw = 0;
+  int64_t splits = -1;            // <= 0: conv_wgrad_plan's (64 x 64 tiles)
+  bool defer = false;
+  int64_t order = 0;
+  at::Tensor dw;                  // out
+};
+
+at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
+                           int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend,
+                           const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_y,
+                           const c10::optional<at::Tensor>& bn_w, const c10::optional<at::Tensor>& bn_b,
+                           const c10::optional<at::Tensor>& bn_mean, const c10::optional<at::Tensor>& bn_invstd,
+                           int64_t bn_mode, const c10::optional<at::Tensor>& bn_sums, int64_t stride, int64_t Hx,
+                           int64_t Wx, int64_t stages, WgradReq* wg) {
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(dy.dim() == 4 && w.dim() == 4, "conv_dgrad: 4D tensors");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -303,14 +379,90 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int
     bnb.mode = (int)bn_mode;
     bnb.sums = bn_sums->data_ptr<double>();
   }
+  // the weight gradient of the same conv, from the same dY, in the same launch
+  hyp::DualWgrad dual;
+  PendingWgrad taken;  // (holds the taken pending reduce's partials until the launch is queued)
+  at::Tensor wpart;
+  const int dev = dy.device().index() < 0 ? 0 : dy.device().index();
+  if (wg != nullptr) {
+    const at::Tensor& x = *wg->x;
+    TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.scalar_type() == dy.scalar_type() &&
+                    x.size(0) == N,
+                "conv_dgrad_wgrad: x must be a channels-last [N, C, H, W] tensor of dY's dtype");
+    const int Cx = x.size(1), Hi = x.size(2), Wi = x.size(3);
+    TORCH_CHECK(P == (Hi + 2 * wg->ph - wg->R) / wg->sh + 1 && Q == (Wi + 2 * wg->pw - wg->S) / wg->sw + 1,
+                "conv_dgrad_wgrad: dY spatial shape vs x");
+    TORCH_CHECK(hyp::conv_wgrad_supported(Cx, K), "conv_dgrad_wgrad: needs C % 64 == 0 and K % 8 == 0");
+    int wbm, wbn, wsplits, per;
+    hyp::conv_wgrad_plan(N * P * Q, K, Cx, (int)wg->R, (int)wg->S, &wbm, &wbn, &wsplits, &per);
+    if (wg->splits > 0) {
+      const int steps = (N * P * Q + 63) / 64;
+      per = (steps + (int)wg->splits - 1) / (int)wg->splits;
+      wsplits = (steps + per - 1) / per;
+    }
+    wg->dw = at::empty({K, Cx, wg->R, wg->S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    if (wsplits > 1) wpart = at::empty({(int64_t)wsplits * K * wg->R * wg->S * Cx}, x.options().dtype(at::kFloat));
+    dual.dy = dy.data_ptr();
+    dual.x = x.data_ptr();
+    dual.dw = wg->dw.data_ptr();
+    dual.partials = wsplits > 1 ? wpart.data_ptr<float>() : nullptr;
+    dual.N = N, dual.H = Hi, dual.W = Wi, dual.C = Cx, dual.K = K, dual.P = P, dual.Q = Q;
+    dual.R = (int)wg->R, dual.S = (int)wg->S, dual.sh = (int)wg->sh, dual.sw = (int)wg->sw;
+    dual.ph = (int)wg->ph, dual.pw = (int)wg->pw;
+    dual.splits = wsplits, dual.steps_per_split = per;
+    dual.defer_reduce = wg->defer && wsplits > 1;
+    dual.order = (int)wg->order;
+  }
+  hyp::WgradPendingReduce pr{};
+  if (wg != nullptr) {
+    pr = take_pending_wgrad(dev, cur_stream(), taken);
+    dual.pending = pr.part != nullptr ? &pr : nullptr;
+  }
   HYP_CHECK_HIP(hyp::conv_fwd(dtype_code(dy), dy.data_ptr(), w.data_ptr(), dx.data_ptr(),
                               device_zero_page(dy.device()), nullptr, nullptr, N, P, Q, K, C, s2 ? H / 2 : H,
                               s2 ? W / 2 : W, R, S, 1, 1, s2 ? (int)ph : dph, s2 ? (int)pw : dpw, bm, bn, 1, splits,
                               splits > 1 ? slabs.data_ptr<float>() : nullptr, cur_stream(), 1.f, nullptr,
                               (add && (splits == 1 || fuse_bn)) ? addend->data_ptr() : nullptr,
-                              fuse_bn ? &bnb : nullptr, 0, s2 ? 2 : 1, s2 ? H : 0, s2 ? W : 0, (int)stages));
+                              fuse_bn ? &bnb : nullptr, 0, s2 ? 2 : 1, s2 ? H : 0, s2 ? W : 0, (int)stages, nullptr,
+                              wg != nullptr ? &dual : nullptr));
+  if (wg != nullptr && dual.defer_reduce) park_pending_wgrad(dev, wpart, wg->dw, dual.splits, 1.f, cur_stream());
   if (add && splits > 1 && !fuse_bn) dx.add_(*addend);  // the plain split-K reduce has no addend input
   return dx;
+}
+
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
+                      int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend,
+                      const c10::optional<at::Tensor>& bn_x, const c10::optional<at::Tensor>& bn_y,
+                      const c10::optional<at::Tensor>& bn_w, const c10::optional<at::Tensor>& bn_b,
+                      const c10::optional<at::Tensor>& bn_mean, const c10::optional<at::Tensor>& bn_invstd,
+                      int64_t bn_mode, const c10::optional<at::Tensor>& bn_sums, int64_t stride, int64_t Hx,
+                      int64_t Wx, int64_t stages) {
+  return conv_dgrad_impl(dy, w, ph, pw, bm_req, bn_req, splits_req, addend, bn_x, bn_y, bn_w, bn_b, bn_mean,
+                         bn_invstd, bn_mode, bn_sums, stride, Hx, Wx, stages, nullptr);
+}
+
+// conv_dgrad + the same conv's weight gradient dW = dYᵀ·X (x, R, S, stride, padding: the FORWARD conv's)
+// in one launch (conv_dual.hip) -> [dx, dw].  wg_splits <= 0: conv_wgrad_plan's pixel split;
+// wg_defer: leave dW's split-K reduce pending (conv_wgrad(defer=True) semantics).
+std::vector<at::Tensor> conv_dgrad_wgrad(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw,
+                                         int64_t bm_req, int64_t bn_req, int64_t splits_req,
+                                         const c10::optional<at::Tensor>& addend, const c10::optional<at::Tensor>& bn_x,
+                                         const c10::optional<at::Tensor>& bn_y, const c10::optional<at::Tensor>& bn_w,
+                                         const c10::optional<at::Tensor>& bn_b,
+                                         const c10::optional<at::Tensor>& bn_mean,
+                                         const c10::optional<at::Tensor>& bn_invstd, int64_t bn_mode,
+                                         const c10::optional<at::Tensor>& bn_sums, int64_t stride, int64_t Hx,
+                                         int64_t Wx, int64_t stages, const at::Tensor& wg_x, int64_t wg_R, int64_t wg_S,
+                                         int64_t wg_sh, int64_t wg_sw, int64_t wg_ph, int64_t wg_pw, int64_t wg_splits,
+                                         bool wg_defer, int64_t order) {
+  HYP_CHECK_CUDA_TENSOR(wg_x);
+  WgradReq wg;
+  wg.x = &wg_x;
+  wg.R = wg_R, wg.S = wg_S, wg.sh = wg_sh, wg.sw = wg_sw, wg.ph = wg_ph, wg.pw = wg_pw;
+  wg.splits = wg_splits, wg.defer = wg_defer, wg.order = order;
+  at::Tensor dx = conv_dgrad_impl(dy, w, ph, pw, bm_req, bn_req, splits_req, addend, bn_x, bn_y, bn_w, bn_b, bn_mean,
+                                  bn_invstd, bn_mode, bn_sums, stride, Hx, Wx, stages, &wg);
+  return {dx, wg.dw};
 }
 
 // ---- skinny GEMMs (weight-streaming regime: few hundred tokens x large frozen weights) ----------
@@ -413,40 +565,6 @@ at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_r
   return dx;
 }
 
-// Deferred weight-gradient reduce (per device): the split-K reduce of the last conv_wgrad(defer=True)
-// waits here and rides on the next conv_wgrad launch as extra workgroups; conv_wgrad_flush() runs
-// it standalone.  The partials tensor and the OUTPUT's storage are held until the kernel that uses
-// them is queued (stream order protects the reuse of their memory after that).  The output is held
-// by storage, not as a tensor: an extra tensor reference would stop AccumulateGrad from stealing
-// the gradient (it would clone the not-yet-reduced values instead).
-struct PendingWgrad {
-  at::Tensor part;
-  c10::Storage out_storage;
-  void* out = nullptr;
-  int out_dtype = 0;
-  int64_t n = 0;
-  int splits = 0;
-  float alpha = 1.f;
-  hipStream_t stream = nullptr;
-};
-// leaked on purpose: no tensor destructor may run after the HIP runtime is torn down at exit
-PendingWgrad* const g_pending_wgrad = new PendingWgrad[64];
-
-bool conv_wgrad_flush_dev(int dev) {
-  PendingWgrad& p = g_pending_wgrad[dev];
-  if (!p.part.defined()) return false;
-  PendingWgrad q = std::move(p);
-  p = PendingWgrad{};
-  HYP_CHECK_HIP(hyp::splitk_reduce(q.out_dtype, q.part.data_ptr<float>(), q.out, q.n, q.splits, q.stream, q.alpha));
-  return true;
-}
-
-bool conv_wgrad_flush() {
-  bool any = false;
-  for (int d = 0; d < 64; ++d) any |= conv_wgrad_flush_dev(d);
-  return any;
-}
-
 // dy [N,K,P,Q] channels-last, x [N,C,H,W] channels-last -> dW [K,C,R,S] channels-last (x's dtype)
 // bm / bn / splits < 0: automatic plan (conv_wgrad_plan); explicit values are for tuning sweeps.
 // defer: leave this gradient's split-K reduce pending (see PendingWgrad); the values of the
@@ -479,36 +597,15 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int6
   at::Tensor part;
   if (splits > 1) part = at::empty({(int64_t)splits * K * R * S * C}, x.options().dtype(at::kFloat));
   const int dev = x.device().index() < 0 ? 0 : x.device().index();
-  PendingWgrad& pend = g_pending_wgrad[dev];
   hipStream_t stream = cur_stream();
-  if (pend.part.defined() && pend.stream != stream) conv_wgrad_flush_dev(dev);  // other stream: no chaining
-  hyp::WgradPendingReduce pr{};
   PendingWgrad taken;
-  if (pend.part.defined()) {
-    taken = std::move(pend);
-    pend = PendingWgrad{};
-    pr.part = taken.part.data_ptr<float>();
-    pr.out = taken.out;
-    pr.n = taken.n;
-    pr.splits = taken.splits;
-    pr.alpha = taken.alpha;
-    pr.dtype = taken.out_dtype;
-  }
+  const hyp::WgradPendingReduce pr = take_pending_wgrad(dev, stream, taken);
   const bool defer_now = defer && splits > 1;
   HYP_CHECK_HIP(hyp::conv_wgrad(dtype_code(x), dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                                 splits > 1 ? part.data_ptr<float>() : nullptr, device_zero_page(x.device()), N, H,
                                 W, C, K, P, Q, (int)R, (int)S, (int)sh, (int)sw, (int)ph, (int)pw, bm, bn, splits, per,
                                 stream, (float)alpha, pr.part != nullptr ? &pr : nullptr, defer_now));
-  if (defer_now) {
-    pend.part = part;
-    pend.out_storage = dw.storage();
-    pend.out = dw.data_ptr();
-    pend.out_dtype = dtype_code(dw);
-    pend.n = (int64_t)K * R * S * C;
-    pend.splits = splits;
-    pend.alpha = (float)alpha;
-    pend.stream = stream;
-  }
+  if (defer_now) park_pending_wgrad(dev, part, dw, splits, (float)alpha, stream);
   return dw;
 }
 
@@ -746,6 +843,20 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("bn_mean") = pybind11::none(), pybind11::arg("bn_invstd") = pybind11::none(),
         pybind11::arg("bn_mode") = -1, pybind11::arg("bn_sums") = pybind11::none(), pybind11::arg("stride") = 1,
         pybind11::arg("H") = 0, pybind11::arg("W") = 0, pybind11::arg("stages") = 0);
+  m.def("conv_dgrad_wgrad", &conv_dgrad_wgrad,
+        "conv_dgrad + the same conv's weight gradient in ONE launch (conv_dual.hip) -> [dx, dw]", pybind11::arg("dy"),
+        pybind11::arg("w"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
+        pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("addend") = pybind11::none(),
+        pybind11::arg("bn_x") = pybind11::none(), pybind11::arg("bn_y") = pybind11::none(),
+        pybind11::arg("bn_w") = pybind11::none(), pybind11::arg("bn_b") = pybind11::none(),
+        pybind11::arg("bn_mean") = pybind11::none(), pybind11::arg("bn_invstd") = pybind11::none(),
+        pybind11::arg("bn_mode") = -1, pybind11::arg("bn_sums") = pybind11::none(), pybind11::arg("stride") = 1,
+        pybind11::arg("H") = 0, pybind11::arg("W") = 0, pybind11::arg("stages") = 0, pybind11::arg("wg_x"),
+        pybind11::arg("wg_R"), pybind11::arg("wg_S"), pybind11::arg("wg_sh"), pybind11::arg("wg_sw"),
+        pybind11::arg("wg_ph"), pybind11::arg("wg_pw"), pybind11::arg("wg_splits") = -1,
+        pybind11::arg("wg_defer") = false, pybind11::arg("order") = 0);
+  m.def("conv_dual_set_order", [](int64_t o) { hyp::conv_dual_set_order((int)o); },
+        "A/B: grid order of conv_dgrad_wgrad launches (-1 per call, 0 interleaved, 1 data gradient first)");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,

@@ -200,10 +200,14 @@ class RcclComm {
 
   // the 1/world of an "avg" (see nccl_op), on the comm stream before the completion event
   void scale_avg(at::Tensor& t, const std::string& op) {
-    if (op != "avg" || world_ == 1) return;
+    const int div = avg_div_ > 0 ? avg_div_ : world_;
+    if (op != "avg" || div == 1) return;
     const c10::hip::HIPStreamGuard sg(stream_obj_);
-    t.mul_(1.0 / world_);
+    t.mul_(1.0 / div);
   }
+  // tests only: the divisor "avg" applies (0 = the world size), so a one-GPU run drives the
+  // world > 1 branch of scale_avg (a 2-rank RCCL communicator needs two GPUs)
+  void set_avg_divisor(int d) { avg_div_ = d; }
 
   std::shared_ptr<Work> all_reduce(at::Tensor& t, const std::string& op) {
     check(t);
@@ -387,6 +391,7 @@ class RcclComm {
   c10::hip::HIPStream stream_obj_ = c10::hip::getDefaultHIPStream();
   hipStream_t stream_ = nullptr;
   int rank_, world_, device_;
+  int avg_div_ = 0;
   double timeout_s_;
   bool exit_on_fail_ = false;
   int64_t seq_ = 0;
@@ -498,6 +503,7 @@ void register_comm(pybind11::module& m) {
       .def("all_to_all", &RcclComm::all_to_all, py::arg("out"), py::arg("inp"))
       .def("barrier", &RcclComm::barrier)
       .def("async_error", &RcclComm::async_error)
+      .def("set_avg_divisor", &RcclComm::set_avg_divisor, "tests: the divisor of 'avg' (0 = world size)")
       .def("abort", &RcclComm::abort)
       .def("destroy", &RcclComm::destroy);
   py::class_<WatchdogSim>(m, "WatchdogSim", "CPU harness for the communicator watchdog (tests)")

@@ -210,12 +210,13 @@ struct ConvInXform {
 };
 constexpr int kXfMaxC = 512;  // input channels of a transformed conv (the scale / shift table in LDS)
 
+struct DualWgrad;
 hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const void* zero, double* psum, double* psq,
                     int N, int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
                     int bm, int bn, int dgrad, int splits, float* part, hipStream_t st, float alpha = 1.f,
                     const struct SplitkEpilogue* ep = nullptr, const void* addend = nullptr,
                     const struct BnBwdEpilogue* bnb = nullptr, int pix = 0, int dgrad_stride = 1, int Hx = 0,
-                    int Wx = 0, int nb = 0, const ConvInXform* xf = nullptr);
+                    int Wx = 0, int nb = 0, const ConvInXform* xf = nullptr, const DualWgrad* dual = nullptr);
 // dgrad_stride 2 (dgrad only, no split-K / alpha / rank-r epilogue): the stride-2 data gradient as its
 // 4 output-phase sub-convolutions in one launch; (H, W, P, Q) are dY's (H, W) and the phase grid
 // (P, Q) = (Hx / 2, Wx / 2) of dX [N, Hx, Wx, K], (ph, pw) the FORWARD padding, w the original filter.
@@ -306,6 +307,29 @@ hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float*
                       int H, int W, int C, int K, int P, int Q, int R, int S, int sh, int sw, int ph, int pw, int bm,
                       int bn, int splits, int steps_per_split, hipStream_t st, float alpha,
                       const WgradPendingReduce* pending = nullptr, bool defer_reduce = false, int pix = 0);
+// ---- conv_dual.hip ---------------------------------------------------------------------------
+// A stride-1 / stride-2 data gradient and a weight gradient of the SAME backward step in ONE launch
+// (horizontal fusion): both consume dY, neither consumes the other, and the ResNet backward runs
+// them as ~50 latency-bound pairs.  The weight gradient runs 64 x 64 tiles (split-K over pixels,
+// its reduce deferred or run by the pending-reduce workgroups as with conv_wgrad).
+struct WgradArgs;
+struct DualWgrad {
+  const void* dy = nullptr;   // [N, P, Q, K] the weight gradient's output gradient (usually the dgrad's dY)
+  const void* x = nullptr;    // [N, H, W, C] the conv's input
+  void* dw = nullptr;         // [K, R, S, C] in dtype
+  float* partials = nullptr;  // [splits, K, R*S*C] when splits > 1
+  int N = 0, H = 0, W = 0, C = 0, K = 0, P = 0, Q = 0, R = 0, S = 0, sh = 1, sw = 1, ph = 0, pw = 0;
+  int splits = 0, steps_per_split = 0;  // from conv_wgrad_plan (64 x 64 tiles)
+  const WgradPendingReduce* pending = nullptr;  // an earlier weight gradient's deferred reduce
+  bool defer_reduce = false;                    // leave THIS gradient's reduce pending
+  int order = 0;  // 0: the two gradients' workgroups interleaved in 8-wide groups; 1: dgrad first
+};
+// Fill a WgradArgs for a 64 x 64-tile weight gradient (the checks of conv_wgrad); no launch.
+hipError_t conv_wgrad_prepare(WgradArgs* a, int dtype, const DualWgrad& d, const void* zero);
+// conv_fwd(..., dual): the data gradient's launch carries the weight gradient `dual` (bf16, a data
+// gradient without split-K); any other case launches the two separately (same results).
+// A/B: -1 = each DualWgrad's own order, 0 interleaved, 1 data gradient first
+void conv_dual_set_order(int order);
 }  // namespace hyp
 
 namespace hyp {

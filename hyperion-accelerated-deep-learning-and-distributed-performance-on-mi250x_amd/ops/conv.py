@@ -125,11 +125,71 @@ class BNGradLink:
         self.used = False
 
 
+# The layer's weight gradient in the data gradient's launch (csrc/kernels/conv_dual.hip): both read
+# dY, neither reads the other — one launch per layer instead of two, and the two gradients' latency-
+# bound workgroups overlap (skipping every weight gradient outright: 4.79 -> 3.81 ms per ResNet-50
+# step, profiles/r05).  HYPERION_CONV_DUAL: "0" off (separate launches), "1" the two gradients'
+# workgroups interleaved, "2" data-gradient workgroups first (default).  Same box, ResNet-50 step:
+# separate 4.79 ms, interleaved 4.83-4.87 (other box), data gradient first 4.67 (profiles/r05/dual_ab.txt).
+_DUAL = os.environ.get("HYPERION_CONV_DUAL", "2")
+
+
+class WgradRequest:
+    """The weight gradient ``_dgrad`` may compute in its own launch: the conv's input ``x`` and
+    geometry; ``dw`` is set when it did (else the caller runs :func:`_wgrad`)."""
+
+    __slots__ = ("x", "R", "S", "stride", "padding", "w_param", "dw")
+
+    def __init__(self, x, w, stride, padding, w_param):
+        self.x, self.R, self.S = x, w.shape[2], w.shape[3]
+        self.stride, self.padding, self.w_param = tuple(stride), tuple(padding), w_param
+        self.dw = None
+
+
+def _wgrad_native_ok(dy: torch.Tensor, x: torch.Tensor) -> bool:
+    P, Q = dy.shape[2], dy.shape[3]
+    return (x.shape[1] % 64 == 0 and dy.shape[1] % 8 == 0 and P * Q < (1 << 14) and dy.shape[0] * P * Q < (1 << 22)
+            and _native.use_native(x, op="wgrad"))
+
+
+def wgrad_request(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
+                  w_param: Optional[torch.Tensor] = None) -> Optional[WgradRequest]:
+    """A request for :func:`_dgrad` when the fused launch applies (bf16 channels-last operands of one
+    dtype, the native weight-gradient envelope), else None."""
+    if _DUAL == "0" or _streams.enabled():
+        return None
+    if not (dy.dtype == torch.bfloat16 and x.dtype == dy.dtype and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and _wgrad_native_ok(dy, x)):
+        return None
+    return WgradRequest(x, w, stride, padding, w_param)
+
+
+def _dual_call(Cn, wg: Optional[WgradRequest], dyc: torch.Tensor, w: torch.Tensor, ph: int, pw: int, bm: int,
+               bn: int, splits: int, **kw) -> torch.Tensor:
+    """conv_dgrad, or conv_dgrad_wgrad with ``wg``'s weight gradient in the same launch (sets wg.dw)."""
+    if wg is None:
+        return Cn.conv_dgrad(dyc, w, ph, pw, bm, bn, splits, **kw)
+    defer = _can_defer(wg.w_param)
+    pl = _plan("wgrad_dual", dyc.shape[0] * dyc.shape[2] * dyc.shape[3], dyc.shape[1], wg.x.shape[1], wg.R, wg.S,
+               wg.stride[0])
+    _native.count("wgrad")
+    _native.count("wgrad_dual")
+    dx, wg.dw = Cn.conv_dgrad_wgrad(dyc, w, ph, pw, bm, bn, splits, wg_x=wg.x, wg_R=wg.R, wg_S=wg.S,
+                                    wg_sh=wg.stride[0], wg_sw=wg.stride[1], wg_ph=wg.padding[0], wg_pw=wg.padding[1],
+                                    wg_splits=pl[2] if pl is not None else -1, wg_defer=defer,
+                                    order=1 if _DUAL == "2" else 0, **kw)
+    if defer:
+        _defer_state["pending"] = True
+    return dx
+
+
 def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
-           addend: Optional[torch.Tensor] = None, bn: Optional[BNGradLink] = None) -> torch.Tensor:
+           addend: Optional[torch.Tensor] = None, bn: Optional[BNGradLink] = None,
+           wg: Optional[WgradRequest] = None) -> torch.Tensor:
     """dX (+ addend: the identity-shortcut gradient of a residual block, fused into the store).
     ``bn``: the producing BN layer's link — when the native kernel runs, it returns dz = dX·mask
-    with the BN reduce done (``bn.dz`` is set)."""
+    with the BN reduce done (``bn.dz`` is set).  ``wg``: this conv's weight gradient, computed in
+    the same launch when the native kernel runs (``wg.dw`` is set)."""
     R, S = w.shape[2], w.shape[3]
     H, W = x.shape[2], x.shape[3]
     # stride 2 (ResNet's strided 3x3): the 4 output-phase sub-convolutions in one launch (needs an
@@ -152,14 +212,14 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
             # (mode 2 or an addend: the full-register kernel variant, tuned under its own key)
             op = "dgrad_bnb2" if (bn.mode == 2 or addend is not None) else "dgrad_bnb"
             pl = _plan(op, x.shape[0] * H * W, w.shape[1], w.shape[0], R, S, stride[0]) or (-1, -1, -1, 0)
-            bn.dz = _native.native().conv_dgrad(dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2], addend=addend,
-                                                bn_x=bn.yc, bn_y=x if bn.mode == 2 else None, bn_w=bn.bn_w,
-                                                bn_b=bn.bn_b, bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,
-                                                bn_sums=bn.sums, stages=pl[3], **geo)
+            bn.dz = _dual_call(_native.native(), wg, dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2],
+                               addend=addend, bn_x=bn.yc, bn_y=x if bn.mode == 2 else None, bn_w=bn.bn_w,
+                               bn_b=bn.bn_b, bn_mean=bn.mean, bn_invstd=bn.invstd, bn_mode=bn.mode,
+                               bn_sums=bn.sums, stages=pl[3], **geo)
             return bn.dz
         pl = _plan("dgrad", x.shape[0] * H * W, w.shape[1], w.shape[0], R, S, stride[0]) or (-1, -1, -1, 0)
-        return _native.native().conv_dgrad(dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2], addend=addend,
-                                           stages=pl[3], **geo)
+        return _dual_call(_native.native(), wg, dyc, w, padding[0], padding[1], pl[0], pl[1], pl[2], addend=addend,
+                          stages=pl[3], **geo)
     if (R == 1 and S == 1 and tuple(padding) == (0, 0) and dy.shape[1] % 64 == 0 and w.shape[1] % 8 == 0
             and _native.use_native(dy, op="dgrad")):
         # 1x1 stride-s (ResNet downsample): dY·W on the output grid is the stride-1 DGRAD GEMM; one
@@ -168,8 +228,8 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
         Cn = _native.native()
         _native.count("dgrad_strided1x1")
         pl = _plan("dgrad", dy.shape[0] * dy.shape[2] * dy.shape[3], w.shape[1], w.shape[0], 1, 1, 1) or (-1, -1, -1, 0)
-        comp = Cn.conv_dgrad(dy.contiguous(memory_format=torch.channels_last), w, 0, 0, pl[0], pl[1], pl[2],
-                             stages=pl[3])
+        comp = _dual_call(Cn, wg, dy.contiguous(memory_format=torch.channels_last), w, 0, 0, pl[0], pl[1], pl[2],
+                          stages=pl[3])
         if addend is not None:
             addend = addend.to(dy.dtype).contiguous(memory_format=torch.channels_last)
         return Cn.upsample_add(comp, addend, x.shape[2], x.shape[3], stride[0], stride[1])
@@ -343,8 +403,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding,
     # (hipBLASLt on the 1x1 case dYᵀ·X runs a 10⁵-long reduction without split-K: 10x slower.)
     R, S = w.shape[2], w.shape[3]
     P, Q = dy.shape[2], dy.shape[3]
-    if (x.shape[1] % 64 == 0 and dy.shape[1] % 8 == 0 and P * Q < (1 << 14) and dy.shape[0] * P * Q < (1 << 22)
-            and _native.use_native(x, op="wgrad")):
+    if _wgrad_native_ok(dy, x):
         dyc = dy.contiguous(memory_format=torch.channels_last)
         _native.count("wgrad")
         defer = _can_defer(w_param)
@@ -447,20 +506,26 @@ class _ConvBNActFn(torch.autograd.Function):
             dw = _streams.run_on_side(lambda: _wgrad(dyc, x, w, stride, padding), [dyc, x], dyc.device)
         dx = None
         prod = ctx.prod
+        # this layer's weight gradient rides in the data gradient's launch when both are native
+        wg = (wgrad_request(dyc, x, w, stride, padding, ctx.w_param)
+              if dw is None and ctx.needs_input_grad[1] and ctx.needs_input_grad[0] else None)
         if ctx.needs_input_grad[0]:
             if branch is not None and branch.users == 2 and _will_run(branch.nodes[1 - bidx]):
                 pend, branch.pending = branch.pending, None
                 if pend is not None and pend[0] == bidx:
                     pend = None  # our own dX from an abandoned pass (its partner never ran): stale
                 if pend is None:  # first of the block input's two consumers: park dX for the second
-                    branch.pending = (bidx, _dgrad(dyc, x, w, stride, padding, addend=add))
+                    branch.pending = (bidx, _dgrad(dyc, x, w, stride, padding, addend=add, wg=wg))
                 else:  # the second computes the whole gradient of x: it can run the BN epilogue
                     other = pend[1]
-                    dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add, bn=prod)
+                    dx = _dgrad(dyc, x, w, stride, padding, addend=other if add is None else other + add, bn=prod,
+                                wg=wg)
             else:
                 # the whole gradient of x unless another op consumes x outside our links (then the
                 # producer sees a summed gradient and takes its full path)
-                dx = _dgrad(dyc, x, w, stride, padding, addend=add, bn=prod)
+                dx = _dgrad(dyc, x, w, stride, padding, addend=add, bn=prod, wg=wg)
+        if dw is None and wg is not None and wg.dw is not None:
+            dw = wg.dw
         if dw is None and ctx.needs_input_grad[1]:
             dw = _wgrad(dyc, x, w, stride, padding, w_param=ctx.w_param)
         return (dx, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None, None, None,

@@ -155,6 +155,12 @@ class _EpochRunner:
             why = "FSDP step without persistent buffers (storage released / re-allocated per unit)"
         elif isinstance(self.model, DistributedDataParallel) and self.world > 1 and not self.model.bucketed:
             why = "DDP without gradient buckets"
+        elif (isinstance(self.model, DistributedDataParallel) and self.world > 1 and self.model.broadcast_buffers
+              and os.environ.get("HYPERION_DDP_CAPTURE", "segments") == "split"):
+            # the split capture records fwd+bwd as ONE plain graph: the per-forward buffer broadcast
+            # would be recorded into it (an RCCL call inside a graph) — only the segmented capture
+            # turns it into an eager hole
+            why = "split DDP capture with broadcast_buffers=True (per-forward buffer broadcast)"
         elif self.world > 1 and not isinstance(self.model, DistributedDataParallel):
             why = "non-Hyperion data parallel wrapper"
         elif os.environ.get("HYPERION_FAULT"):

@@ -68,6 +68,35 @@ def test_native_comm_avg_writes_every_element(pg, dt, n):
     c.destroy()
 
 
+@pytest.mark.parametrize("div", [2, 8])
+def test_native_comm_avg_scale_path_world_gt_1(pg, div):
+    """The world > 1 branch of RcclComm::scale_avg (SUM, then x 1/world on the comm stream before
+    the completion event) on one GPU: the divisor is forced to ``div`` while RCCL reduces over one
+    rank, so the result must be exactly x / div — and visible to the compute stream after wait()
+    without any host synchronisation (a consumer kernel reads it at once)."""
+    from hyperion.parallel.comm import NativeComm
+
+    c = NativeComm(torch.device("cuda", 0))
+    c._c.set_avg_divisor(div)
+    x = torch.randn(1 << 20, device="cuda")
+    y = x.clone()
+    c.all_reduce(y, "avg").wait()
+    got = y * 1.0  # compute-stream consumer right after the wait
+    torch.testing.assert_close(got, x / div, rtol=0, atol=0)
+    out = torch.full((4099,), 3.0, device="cuda", dtype=torch.bfloat16)
+    xb = torch.randn(4099, device="cuda").to(torch.bfloat16)
+    c.reduce_scatter(out, xb, "avg").wait()
+    torch.testing.assert_close(out, xb * (1.0 / div), rtol=0, atol=0)
+    ts = [torch.ones(10, device="cuda"), torch.full((7,), 2.0, device="cuda")]
+    c.all_reduce_coalesced(ts, "avg").wait()
+    torch.testing.assert_close(ts[1], torch.full((7,), 2.0 / div, device="cuda"))
+    y2 = x.clone()
+    c.all_reduce(y2, "sum").wait()  # "sum" is never scaled
+    torch.testing.assert_close(y2, x, rtol=0, atol=0)
+    c._c.set_avg_divisor(0)
+    c.destroy()
+
+
 def test_native_comm_orders_against_compute_stream(pg):
     # a producer kernel on the current stream, then the collective on the comm stream, then a
     # consumer: the result must see the producer's data and the consumer must see the collective

@@ -17,6 +17,7 @@ import pytest
 import torch
 
 from dist_utils import run_world
+from parity import assert_losses_match, assert_update_parity, snapshot
 
 pytestmark = pytest.mark.gpu
 
@@ -138,22 +139,25 @@ def _two_rank_graph(rank, world, steps):
     res = {}
     for mode in ("graph", "split_step"):
         ddp = DDP(_make(seed=rank), bucket_cap_mb=2.0, first_bucket_mb=0.5, broadcast_buffers=False)
+        before = snapshot(ddp.module.named_parameters())
         opt = FusedAdam(ddp.parameters(), lr=1e-3, zero_grad_in_step=True)
+        losses = []
         if mode == "graph":
             st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=True, warmup_iters=1)
-            st(xs[0], ys[0])  # warm-up step + capture + replay: steps 0 (twice: warm-up, replay)
+            losses.append(float(st(xs[0], ys[0])))  # warm-up step + capture + replay: step 0 twice
             for i in range(1, steps):
-                st(xs[i], ys[i])
+                losses.append(float(st(xs[i], ys[i])))
             graphs = st.graph3 is not None
         else:
             ddp.defer_allreduce = True
             st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=False)
             st.split_step(xs[0], ys[0])  # mirror the warm-up step
             for i in range(steps):
-                st.split_step(xs[i], ys[i])
+                losses.append(float(st.split_step(xs[i], ys[i])))
             graphs = None
         torch.cuda.synchronize()
-        res[mode] = {"params": [p.detach().float().cpu() for p in ddp.module.parameters()], "graph3": graphs}
+        res[mode] = {"params": [p.detach().float().cpu() for p in ddp.module.parameters()], "graph3": graphs,
+                     "before": before, "after": snapshot(ddp.module.named_parameters()), "losses": losses}
     return res
 
 
@@ -162,5 +166,8 @@ def test_two_rank_gloo_three_graph_step_replicas_identical():
     assert res[0]["graph"]["graph3"] and res[1]["graph"]["graph3"]
     for a, b in zip(res[0]["graph"]["params"], res[1]["graph"]["params"]):
         assert torch.equal(a, b)  # replicas bit-identical after captured steps
-    for a, b in zip(res[0]["graph"]["params"], res[0]["split_step"]["params"]):
-        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-3)  # same schedule, eager
+    for r in (0, 1):  # same schedule, eager: per-step losses and the parameter UPDATE (tests/parity.py)
+        g, e = res[r]["graph"], res[r]["split_step"]
+        assert all(torch.equal(g["before"][k], e["before"][k]) for k in g["before"])
+        assert_losses_match(g["losses"], e["losses"], rtol=1e-2, what=f"rank {r}")
+        assert_update_parity(e["before"], g["after"], e["after"], rel=2e-2, what=f"rank {r}")

@@ -25,6 +25,7 @@ import pytest
 import torch
 
 from dist_utils import run_world
+from parity import assert_losses_match, assert_update_parity, snapshot
 
 pytestmark = pytest.mark.gpu
 
@@ -83,6 +84,7 @@ def _ddp_steps(rank, world, steps, graphed):
     data = [(torch.randn(8, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last),
              torch.randint(0, 10, (8,), device="cuda", generator=g)) for _ in range(steps)]
     img, lbl = data[0][0].clone(), data[0][1].clone()
+    before = snapshot(m.module.named_parameters())
 
     def body():
         opt.zero_grad(set_to_none=False)
@@ -95,6 +97,7 @@ def _ddp_steps(rank, world, steps, graphed):
 
     body()  # gradients exist from here on (zeroed in place in every step)
     nseg = 0
+    losses = []
     if graphed:
         st = SegmentedStep(body, warmup=1, module=m)
         for i in range(steps):
@@ -102,7 +105,7 @@ def _ddp_steps(rank, world, steps, graphed):
             lbl.copy_(data[i][1])
             if i == 0:
                 body()
-            st()
+            losses.append(float(st()))
         nseg = st.seg.num_segments
     else:
         for i in range(steps):
@@ -111,10 +114,11 @@ def _ddp_steps(rank, world, steps, graphed):
             if i == 0:
                 body()
                 body()  # SegmentedStep: one warm-up call + the capture pass are steps too
-            body()
+            losses.append(float(body()))
     torch.cuda.synchronize()
     return {"state": {k: v.detach().float().cpu() for k, v in m.module.state_dict().items()},
-            "params": {k for k, _ in m.module.named_parameters()}, "segments": nseg}
+            "params": {k for k, _ in m.module.named_parameters()}, "segments": nseg, "losses": losses,
+            "before": before, "after": snapshot(m.module.named_parameters())}
 
 
 def test_ddp_segmented_capture_matches_eager_two_ranks():
@@ -124,4 +128,10 @@ def test_ddp_segmented_capture_matches_eager_two_ranks():
     for k, v in g[0]["state"].items():
         if k in g[0]["params"]:  # parameters: identical replicas (BN running stats are per-rank after
             assert torch.equal(v, g[1]["state"][k]), k  # the last forward, as with torch DDP)
-        torch.testing.assert_close(v, e[0]["state"][k], rtol=2e-2, atol=5e-3)  # (Adam amplifies last-bit noise)
+        else:  # BN running statistics
+            torch.testing.assert_close(v, e[0]["state"][k], rtol=2e-2, atol=5e-3)
+    for r in (0, 1):
+        # the per-step losses and the parameter UPDATE from the same start (tests/parity.py: a
+        # skipped optimizer step or a stale gradient fails this; the parameters alone would pass)
+        assert_losses_match(g[r]["losses"], e[r]["losses"], rtol=1e-2, what=f"rank {r}")
+        assert_update_parity(e[r]["before"], g[r]["after"], e[r]["after"], rel=2e-2, what=f"rank {r}")
