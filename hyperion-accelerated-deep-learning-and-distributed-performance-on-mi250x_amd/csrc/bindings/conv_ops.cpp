@@ -294,11 +294,55 @@ void park_pending_wgrad(int dev, const at::Tensor& part, const at::Tensor& dw, i
 struct WgradReq {
   const at::Tensor* x = nullptr;  // the conv's input [N, C, H, W] channels-last
   int64_t R = 1, S = 1, sh = 1, sw = 1, ph = 0, pw = 0;
+  int64_t bm = 64, bn = 64;       // weight-gradient tile
   int64_t splits = -1;            // <= 0: conv_wgrad_plan's (64 x 64 tiles)
   bool defer = false;
   int64_t order = 0;
-  at::Tensor dw;                  // out
+  at::Tensor dw;                  // out (given: written in place — a gradient handed to autograd earlier)
 };
+
+// Validate the request against dY [N, K, P, Q] and fill the kernel-side description (allocates dW and
+// the split-K partials)
+void fill_dual(hyp::DualWgrad& dual, WgradReq& wg, const at::Tensor& dy, at::Tensor& wpart, const char* who) {
+  const int N = dy.size(0), K = dy.size(1), P = dy.size(2), Q = dy.size(3);
+  const at::Tensor& x = *wg.x;
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.scalar_type() == dy.scalar_type() &&
+                  x.size(0) == N && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              who, ": x and dY must be channels-last [N, C, H, W] / [N, K, P, Q] tensors of one dtype");
+  const int Cx = x.size(1), Hi = x.size(2), Wi = x.size(3);
+  TORCH_CHECK(P == (Hi + 2 * wg.ph - wg.R) / wg.sh + 1 && Q == (Wi + 2 * wg.pw - wg.S) / wg.sw + 1, who,
+              ": dY spatial shape vs x");
+  TORCH_CHECK(hyp::conv_wgrad_supported(Cx, K), who, ": needs C % 64 == 0 and K % 8 == 0");
+  TORCH_CHECK((wg.bm == 64 || wg.bm == 128) && (wg.bn == 64 || wg.bn == 128) && Cx % wg.bn == 0, who,
+              ": weight-gradient tile 64 / 128 each (bn | C)");
+  int wbm, wbn, wsplits, per;
+  hyp::conv_wgrad_plan(N * P * Q, K, Cx, (int)wg.R, (int)wg.S, &wbm, &wbn, &wsplits, &per);
+  if (wg.splits > 0) {
+    const int steps = (N * P * Q + 63) / 64;
+    per = (steps + (int)wg.splits - 1) / (int)wg.splits;
+    wsplits = (steps + per - 1) / per;
+  }
+  if (wg.dw.defined()) {
+    TORCH_CHECK(wg.dw.dim() == 4 && wg.dw.size(0) == K && wg.dw.size(1) == Cx && wg.dw.size(2) == wg.R &&
+                    wg.dw.size(3) == wg.S && wg.dw.scalar_type() == x.scalar_type() &&
+                    wg.dw.is_contiguous(at::MemoryFormat::ChannelsLast) && wg.dw.device() == x.device(),
+                who, ": out must be a channels-last [K, C, R, S] tensor of x's dtype");
+  } else {
+    wg.dw = at::empty({K, Cx, wg.R, wg.S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  if (wsplits > 1) wpart = at::empty({(int64_t)wsplits * K * wg.R * wg.S * Cx}, x.options().dtype(at::kFloat));
+  dual.dy = dy.data_ptr();
+  dual.x = x.data_ptr();
+  dual.dw = wg.dw.data_ptr();
+  dual.partials = wsplits > 1 ? wpart.data_ptr<float>() : nullptr;
+  dual.N = N, dual.H = Hi, dual.W = Wi, dual.C = Cx, dual.K = K, dual.P = P, dual.Q = Q;
+  dual.R = (int)wg.R, dual.S = (int)wg.S, dual.sh = (int)wg.sh, dual.sw = (int)wg.sw;
+  dual.ph = (int)wg.ph, dual.pw = (int)wg.pw;
+  dual.bm = (int)wg.bm, dual.bn = (int)wg.bn;
+  dual.splits = wsplits, dual.steps_per_split = per;
+  dual.defer_reduce = wg.defer && wsplits > 1;
+  dual.order = (int)wg.order;
+}
 
 at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw, int64_t bm_req,
                            int64_t bn_req, int64_t splits_req, const c10::optional<at::Tensor>& addend,
@@ -384,35 +428,7 @@ at::Tensor conv_dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t ph
   PendingWgrad taken;  // (holds the taken pending reduce's partials until the launch is queued)
   at::Tensor wpart;
   const int dev = dy.device().index() < 0 ? 0 : dy.device().index();
-  if (wg != nullptr) {
-    const at::Tensor& x = *wg->x;
-    TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.scalar_type() == dy.scalar_type() &&
-                    x.size(0) == N,
-                "conv_dgrad_wgrad: x must be a channels-last [N, C, H, W] tensor of dY's dtype");
-    const int Cx = x.size(1), Hi = x.size(2), Wi = x.size(3);
-    TORCH_CHECK(P == (Hi + 2 * wg->ph - wg->R) / wg->sh + 1 && Q == (Wi + 2 * wg->pw - wg->S) / wg->sw + 1,
-                "conv_dgrad_wgrad: dY spatial shape vs x");
-    TORCH_CHECK(hyp::conv_wgrad_supported(Cx, K), "conv_dgrad_wgrad: needs C % 64 == 0 and K % 8 == 0");
-    int wbm, wbn, wsplits, per;
-    hyp::conv_wgrad_plan(N * P * Q, K, Cx, (int)wg->R, (int)wg->S, &wbm, &wbn, &wsplits, &per);
-    if (wg->splits > 0) {
-      const int steps = (N * P * Q + 63) / 64;
-      per = (steps + (int)wg->splits - 1) / (int)wg->splits;
-      wsplits = (steps + per - 1) / per;
-    }
-    wg->dw = at::empty({K, Cx, wg->R, wg->S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-    if (wsplits > 1) wpart = at::empty({(int64_t)wsplits * K * wg->R * wg->S * Cx}, x.options().dtype(at::kFloat));
-    dual.dy = dy.data_ptr();
-    dual.x = x.data_ptr();
-    dual.dw = wg->dw.data_ptr();
-    dual.partials = wsplits > 1 ? wpart.data_ptr<float>() : nullptr;
-    dual.N = N, dual.H = Hi, dual.W = Wi, dual.C = Cx, dual.K = K, dual.P = P, dual.Q = Q;
-    dual.R = (int)wg->R, dual.S = (int)wg->S, dual.sh = (int)wg->sh, dual.sw = (int)wg->sw;
-    dual.ph = (int)wg->ph, dual.pw = (int)wg->pw;
-    dual.splits = wsplits, dual.steps_per_split = per;
-    dual.defer_reduce = wg->defer && wsplits > 1;
-    dual.order = (int)wg->order;
-  }
+  if (wg != nullptr) fill_dual(dual, *wg, dy, wpart, "conv_dgrad_wgrad");
   hyp::WgradPendingReduce pr{};
   if (wg != nullptr) {
     pr = take_pending_wgrad(dev, cur_stream(), taken);
@@ -463,6 +479,63 @@ std::vector<at::Tensor> conv_dgrad_wgrad(const at::Tensor& dy, const at::Tensor&
   at::Tensor dx = conv_dgrad_impl(dy, w, ph, pw, bm_req, bn_req, splits_req, addend, bn_x, bn_y, bn_w, bn_b, bn_mean,
                                   bn_invstd, bn_mode, bn_sums, stride, Hx, Wx, stages, &wg);
   return {dx, wg.dw};
+}
+
+// bn_bwd_dx (norm_ops.cpp) + the weight gradient of the conv ABOVE this BN layer (its dY wg_dy, input
+// wg_x, forward geometry) in one launch (bn_wgrad.hip) -> [dx, dweight, dbias, dw].  wg_defer:
+// leave dW's split-K reduce pending (conv_wgrad(defer=True) semantics); an earlier pending reduce
+// rides on this launch.
+std::vector<at::Tensor> bn_bwd_dx_wgrad(const at::Tensor& dz, const at::Tensor& x,
+                                        const c10::optional<at::Tensor>& weight, const at::Tensor& save_mean,
+                                        const at::Tensor& save_invstd, bool training, const at::Tensor& sums,
+                                        const at::Tensor& wg_dy, const at::Tensor& wg_x, int64_t wg_R, int64_t wg_S,
+                                        int64_t wg_sh, int64_t wg_sw, int64_t wg_ph, int64_t wg_pw, int64_t wg_bm,
+                                        int64_t wg_bn, int64_t wg_splits, bool wg_defer,
+                                        const c10::optional<at::Tensor>& wg_out) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  HYP_CHECK_CUDA_TENSOR(wg_x);
+  HYP_CHECK_CUDA_TENSOR(wg_dy);
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(x.dim() == 4 && dz.sizes() == x.sizes() && dz.scalar_type() == x.scalar_type() &&
+                  dz.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_bwd_dx_wgrad: dz and x of one shape / dtype, channels-last");
+  TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.is_contiguous() && sums.numel() == 2 * C * hyp::kStatSlots,
+              "bn_bwd_dx_wgrad: sums must be an fp64 [kStatSlots * 2 * C] tensor");
+  TORCH_CHECK(save_mean.numel() == C && save_invstd.numel() == C, "bn_bwd_dx_wgrad: mean / invstd of C channels");
+  const at::DeviceGuard guard(x.device());
+  WgradReq wg;
+  wg.x = &wg_x;
+  wg.R = wg_R, wg.S = wg_S, wg.sh = wg_sh, wg.sw = wg_sw, wg.ph = wg_ph, wg.pw = wg_pw;
+  wg.bm = wg_bm, wg.bn = wg_bn, wg.splits = wg_splits, wg.defer = wg_defer;
+  if (wg_out.has_value() && wg_out->defined()) wg.dw = *wg_out;
+  hyp::DualWgrad dual;
+  at::Tensor wpart;
+  fill_dual(dual, wg, wg_dy, wpart, "bn_bwd_dx_wgrad");
+  auto dx = at::empty_like(x);
+  auto dwb = at::empty({2, C}, x.options().dtype(at::kFloat));
+  const int dev = x.device().index() < 0 ? 0 : x.device().index();
+  PendingWgrad taken;
+  hyp::WgradPendingReduce pr = take_pending_wgrad(dev, cur_stream(), taken);
+  dual.pending = pr.part != nullptr ? &pr : nullptr;
+  hipError_t e = hyp::bn_backward_dx_wgrad(dtype_code(x), dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C,
+                                           ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
+                                           save_invstd.data_ptr<float>(), training ? 1 : 0, sums.data_ptr<double>(),
+                                           dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, dual,
+                                           device_zero_page(x.device()), cur_stream());
+  if (e == hipErrorNotSupported) {  // (f16) the two launches
+    HYP_CHECK_HIP(hyp::bn_backward_dx(dtype_code(x), dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C,
+                                      ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
+                                      save_invstd.data_ptr<float>(), training ? 1 : 0, sums.data_ptr<double>(),
+                                      dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, cur_stream()));
+    e = hyp::conv_wgrad(dtype_code(x), dual.dy, dual.x, dual.dw, dual.partials, device_zero_page(x.device()), dual.N,
+                        dual.H, dual.W, dual.C, dual.K, dual.P, dual.Q, dual.R, dual.S, dual.sh, dual.sw, dual.ph,
+                        dual.pw, dual.bm, dual.bn, dual.splits, dual.steps_per_split, cur_stream(), 1.f,
+                        dual.pending, dual.defer_reduce);
+  }
+  HYP_CHECK_HIP(e);
+  if (dual.defer_reduce) park_pending_wgrad(dev, wpart, wg.dw, dual.splits, 1.f, cur_stream());
+  return {dx, dwb[0], dwb[1], wg.dw};
 }
 
 // ---- skinny GEMMs (weight-streaming regime: few hundred tokens x large frozen weights) ----------
@@ -570,7 +643,8 @@ at::Tensor linear_nn(const at::Tensor& dy, const at::Tensor& w, int64_t splits_r
 // defer: leave this gradient's split-K reduce pending (see PendingWgrad); the values of the
 // returned tensor are final only after the next conv_wgrad launch or conv_wgrad_flush().
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int64_t S, int64_t sh, int64_t sw,
-                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_, double alpha, bool defer) {
+                      int64_t ph, int64_t pw, int64_t bm_, int64_t bn_, int64_t splits_, double alpha, bool defer,
+                      const c10::optional<at::Tensor>& out) {
   HYP_CHECK_CUDA_TENSOR(x);
   HYP_CHECK_CUDA_TENSOR(dy);
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "conv_wgrad: 4D tensors");
@@ -584,7 +658,16 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t R, int6
   TORCH_CHECK(P == (H + 2 * ph - R) / sh + 1 && Q == (W + 2 * pw - S) / sw + 1, "conv_wgrad: dy spatial shape");
   TORCH_CHECK(hyp::conv_wgrad_supported(C, K), "conv_wgrad: needs C % 64 == 0 and K % 8 == 0");
   const at::DeviceGuard guard(x.device());
-  auto dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor dw;
+  if (out.has_value() && out->defined()) {  // (a gradient handed to autograd before it was computed)
+    dw = *out;
+    TORCH_CHECK(dw.dim() == 4 && dw.size(0) == K && dw.size(1) == C && dw.size(2) == R && dw.size(3) == S &&
+                    dw.scalar_type() == x.scalar_type() && dw.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dw.device() == x.device(),
+                "conv_wgrad: out must be a channels-last [K, C, R, S] tensor of x's dtype");
+  } else {
+    dw = at::empty({K, C, R, S}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
   int bm, bn, splits, per;
   hyp::conv_wgrad_plan(N * P * Q, K, C, (int)R, (int)S, &bm, &bn, &splits, &per);
   if (bm_ > 0) bm = (int)bm_;
@@ -855,13 +938,22 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("wg_R"), pybind11::arg("wg_S"), pybind11::arg("wg_sh"), pybind11::arg("wg_sw"),
         pybind11::arg("wg_ph"), pybind11::arg("wg_pw"), pybind11::arg("wg_splits") = -1,
         pybind11::arg("wg_defer") = false, pybind11::arg("order") = 0);
+  m.def("bn_bwd_dx_wgrad", &bn_bwd_dx_wgrad,
+        "BN backward dx pass + the weight gradient of the conv above it in ONE launch (bn_wgrad.hip) -> "
+        "[dx, dweight, dbias, dw]",
+        pybind11::arg("dz"), pybind11::arg("x"), pybind11::arg("weight"), pybind11::arg("save_mean"),
+        pybind11::arg("save_invstd"), pybind11::arg("training"), pybind11::arg("sums"), pybind11::arg("wg_dy"),
+        pybind11::arg("wg_x"), pybind11::arg("wg_R"), pybind11::arg("wg_S"), pybind11::arg("wg_sh"),
+        pybind11::arg("wg_sw"), pybind11::arg("wg_ph"), pybind11::arg("wg_pw"), pybind11::arg("wg_bm") = 64,
+        pybind11::arg("wg_bn") = 64, pybind11::arg("wg_splits") = -1, pybind11::arg("wg_defer") = false,
+        pybind11::arg("wg_out") = pybind11::none());
   m.def("conv_dual_set_order", [](int64_t o) { hyp::conv_dual_set_order((int)o); },
         "A/B: grid order of conv_dgrad_wgrad launches (-1 per call, 0 interleaved, 1 data gradient first)");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("R"), pybind11::arg("S"), pybind11::arg("sh"),
         pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"), pybind11::arg("bm") = -1,
         pybind11::arg("bn") = -1, pybind11::arg("splits") = -1, pybind11::arg("alpha") = 1.0,
-        pybind11::arg("defer") = false);
+        pybind11::arg("defer") = false, pybind11::arg("out") = pybind11::none());
   m.def("conv_wgrad_flush", &conv_wgrad_flush,
         "run a deferred weight-gradient split-K reduce now (returns whether one was pending)");
   m.def("bn_fwd_sums", &bn_fwd_sums, "BN apply (inline finalize) from conv-epilogue statistics sums");

@@ -97,14 +97,23 @@ std::vector<at::Tensor> bn_bwd_dx(const at::Tensor& dz, const at::Tensor& x, con
 
 // ---- column sums (bias gradients) ---------------------------------------------------------------
 // ticket slots of the one-launch column sums: a ring over device_counters' second half (each call
-// takes the next `n` slots; its kernel resets them) — launches 512 calls apart never overlap
+// takes the next `n` slots; its kernel resets them) — launches 512 calls apart never overlap.  A
+// captured launch keeps its slot on every replay while eager calls cycle the ring, so under stream
+// capture the callers take the two-launch path instead (colsum_fused_ok).  (Unsigned 64-bit
+// counter: never wraps negative)
 int* colsum_tickets(const at::Device& dev, int n) {
-  static std::atomic<int> next{0};
-  constexpr int kBase = 8192, kSpan = 8192;
-  const int step = (n + 15) & ~15;
-  int at = next.fetch_add(step) % kSpan;
+  static std::atomic<uint64_t> next{0};
+  constexpr uint64_t kBase = 8192, kSpan = 8192;
+  const uint64_t step = (uint64_t)((n + 15) & ~15);
+  uint64_t at = next.fetch_add(step) % kSpan;
   if (at + step > kSpan) at = 0;
   return device_counters(dev) + kBase + at;
+}
+
+bool colsum_fused_ok() {
+  if (hyp::colsum_fused_max_p() <= 0) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(cur_stream(), &st) == hipSuccess && st == hipStreamCaptureStatusNone;
 }
 // x: [..., N] contiguous -> Σ over all leading dims, [N] in out_dtype (default x's dtype)
 at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dtype) {
@@ -116,7 +125,7 @@ at::Tensor column_sum(const at::Tensor& x, c10::optional<at::ScalarType> out_dty
   const at::DeviceGuard guard(x.device());
   const auto odt = out_dtype.value_or(x.scalar_type());
   auto out = at::empty({N}, x.options().dtype(odt));
-  const bool fused = hyp::colsum_fused_max_p() > 0;
+  const bool fused = colsum_fused_ok();
   const int P = fused ? hyp::colsum_partials_fused(M, (int)N) : hyp::colsum_partials(M, (int)N);
   auto part = at::empty({(int64_t)P * N}, x.options().dtype(at::kFloat));
   HYP_CHECK_HIP(hyp::column_sum(dtype_code(x), x.data_ptr(), M, (int)N, out.data_ptr(), dtype_code(out),
@@ -140,7 +149,7 @@ std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z
   auto dy = at::empty_like(dh);
   const auto odt = db_dtype.value_or(dh.scalar_type());
   auto db = at::empty({N}, dh.options().dtype(odt));
-  const bool fused = hyp::colsum_fused_max_p() > 0;
+  const bool fused = colsum_fused_ok();
   const int P = fused ? hyp::colsum_partials_fused(M, (int)N) : hyp::colsum_partials(M, (int)N);
   auto part = at::empty({(int64_t)P * N}, dh.options().dtype(at::kFloat));
   hyp::RngState rs{};

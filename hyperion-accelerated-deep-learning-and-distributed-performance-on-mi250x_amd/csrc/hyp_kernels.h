@@ -319,17 +319,26 @@ struct DualWgrad {
   void* dw = nullptr;         // [K, R, S, C] in dtype
   float* partials = nullptr;  // [splits, K, R*S*C] when splits > 1
   int N = 0, H = 0, W = 0, C = 0, K = 0, P = 0, Q = 0, R = 0, S = 0, sh = 1, sw = 1, ph = 0, pw = 0;
-  int splits = 0, steps_per_split = 0;  // from conv_wgrad_plan (64 x 64 tiles)
+  int bm = 64, bn = 64;                  // weight-gradient tile (bn_wgrad.hip: 64 / 128 each; conv_dual: 64)
+  int splits = 0, steps_per_split = 0;  // pixel split (conv_wgrad_plan's rule)
   const WgradPendingReduce* pending = nullptr;  // an earlier weight gradient's deferred reduce
   bool defer_reduce = false;                    // leave THIS gradient's reduce pending
   int order = 0;  // 0: the two gradients' workgroups interleaved in 8-wide groups; 1: dgrad first
 };
-// Fill a WgradArgs for a 64 x 64-tile weight gradient (the checks of conv_wgrad); no launch.
+// Fill a WgradArgs for the weight gradient d (the checks of conv_wgrad); no launch.
 hipError_t conv_wgrad_prepare(WgradArgs* a, int dtype, const DualWgrad& d, const void* zero);
 // conv_fwd(..., dual): the data gradient's launch carries the weight gradient `dual` (bf16, a data
 // gradient without split-K); any other case launches the two separately (same results).
 // A/B: -1 = each DualWgrad's own order, 0 interleaved, 1 data gradient first
 void conv_dual_set_order(int order);
+// bn_wgrad.hip: the BatchNorm backward dx pass of a layer (bn_backward_dx's arguments) and the weight
+// gradient d of the conv ABOVE it (whose dY the previous backward step produced) in ONE launch —
+// the cheap, memory-bound dx pass runs beside the weight gradient's K loops instead of alone
+// between two data gradients.  bf16 only (else hipErrorNotSupported: nothing launched).
+hipError_t bn_backward_dx_wgrad(int dtype, const void* dz, const void* x, void* dx, int64_t M, int C,
+                                const float* weight, const float* save_mean, const float* save_invstd, int training,
+                                const double* sums, float* dweight, float* dbias, const DualWgrad& d,
+                                const void* zero, hipStream_t stream);
 }  // namespace hyp
 
 namespace hyp {

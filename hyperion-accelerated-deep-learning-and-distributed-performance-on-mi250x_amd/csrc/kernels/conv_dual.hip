@@ -118,6 +118,7 @@ hipError_t conv_dual_launch(const ConvArgs& a, int dtype, int bm, int bn, int nb
   if (dtype != kBF16 || nb < 1 || nb > 3 || variant < 0 || variant > 2) return hipErrorNotSupported;
   if (!((bm == 64 && bn == 64) || (bm == 128 && bn == 64) || (bm == 128 && bn == 128))) return hipErrorNotSupported;
   if (a.splits != 1 && a.sd != 2) return hipErrorNotSupported;  // split-K data gradients need their reduce first
+  if (d.bm != 64 || d.bn != 64) return hipErrorNotSupported;
   WgradArgs w;
   hipError_t e = conv_wgrad_prepare(&w, dtype, d, a.zero);
   if (e != hipSuccess) return e;

@@ -192,7 +192,8 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
   auto wgrad_after = [&]() -> hipError_t {
     if (dual == nullptr) return hipSuccess;
     return conv_wgrad(dtype, dual->dy, dual->x, dual->dw, dual->partials, zero, dual->N, dual->H, dual->W, dual->C,
-                      dual->K, dual->P, dual->Q, dual->R, dual->S, dual->sh, dual->sw, dual->ph, dual->pw, 64, 64,
+                      dual->K, dual->P, dual->Q, dual->R, dual->S, dual->sh, dual->sw, dual->ph, dual->pw, dual->bm,
+                      dual->bn,
                       dual->splits, dual->steps_per_split, st, 1.f, dual->pending, dual->defer_reduce);
   };
   if (a.splits > 1 && !sd2) {

@@ -447,7 +447,7 @@ hipError_t wgrad_fill(WgradArgs& a, int dtype, const void* dy, const void* x, vo
 
 hipError_t conv_wgrad_prepare(WgradArgs* a, int dtype, const DualWgrad& d, const void* zero) {
   return wgrad_fill(*a, dtype, d.dy, d.x, d.dw, d.partials, zero, d.N, d.H, d.W, d.C, d.K, d.P, d.Q, d.R, d.S, d.sh,
-                    d.sw, d.ph, d.pw, 64, 64, d.splits, d.steps_per_split, 1.f, d.pending, 0);
+                    d.sw, d.ph, d.pw, d.bm, d.bn, d.splits, d.steps_per_split, 1.f, d.pending, 0);
 }
 
 hipError_t conv_wgrad(int dtype, const void* dy, const void* x, void* dw, float* partials, const void* zero, int N,

@@ -196,6 +196,23 @@ class LlamaForCausalLM(nn.Module):
     def gradient_checkpointing_enable(self) -> None:
         self.model.gradient_checkpointing = True
 
+    @classmethod
+    def from_pretrained(cls, path: str, torch_dtype: Optional[torch.dtype] = None,
+                        device: Optional[torch.device] = None, config: Optional[LlamaConfig] = None,
+                        strict: bool = True) -> "LlamaForCausalLM":
+        """A LOCAL HF checkpoint directory (config.json + safetensors shards; models/hf_checkpoint.py):
+        the reference's ``AutoModelForCausalLM.from_pretrained`` without the network.  Weights-only
+        loading, tensor by tensor into the built model."""
+        from .hf_checkpoint import load_hf_weights, load_llama_config
+
+        cfg = config or load_llama_config(path)
+        with torch.device(device or "cpu"):
+            m = cls(cfg)
+        if torch_dtype is not None:
+            m = m.to(torch_dtype)
+        load_hf_weights(m, path, strict=strict)
+        return m
+
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 labels: Optional[torch.Tensor] = None, return_logits: Optional[bool] = None) -> CausalLMOutput:
         h = self.model(input_ids, attention_mask)

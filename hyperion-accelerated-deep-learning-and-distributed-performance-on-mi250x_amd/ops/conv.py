@@ -156,7 +156,7 @@ def wgrad_request(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, pa
                   w_param: Optional[torch.Tensor] = None) -> Optional[WgradRequest]:
     """A request for :func:`_dgrad` when the fused launch applies (bf16 channels-last operands of one
     dtype, the native weight-gradient envelope), else None."""
-    if _DUAL == "0" or _streams.enabled():
+    if WGRAD_FUSE != "dgrad" or _DUAL == "0" or _streams.enabled():
         return None
     if not (dy.dtype == torch.bfloat16 and x.dtype == dy.dtype and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last) and _wgrad_native_ok(dy, x)):
@@ -369,10 +369,110 @@ def branch_sum_link(x: torch.Tensor) -> Optional[BranchSumLink]:
 DEFER_WGRAD_REDUCE = os.environ.get("HYPERION_WGRAD_DEFER", "1") == "1"
 _defer_state = {"pending": False, "queued": False}
 
+# Where a layer's weight gradient runs (HYPERION_WGRAD_FUSE):
+# * "dgrad" (default): in the layer's own data-gradient launch (csrc/kernels/conv_dual.hip);
+# * "bn": PARKED until the next BatchNorm dx pass of the backward (the layer below) and run in that
+#   pass's launch (csrc/kernels/bn_wgrad.hip), the data gradients keeping their own kernels —
+#   measured no faster than separate launches (4.80 vs 4.79 ms; "dgrad" 4.67, profiles/r05/
+#   dual_ab.txt): every workgroup of the fused launch takes the larger register / LDS footprint,
+#   so the bandwidth-bound dx blocks lose the occupancy they stream with;
+# * "0": its own launch.
+# A parked gradient is handed to autograd unwritten, so the same rules as the deferred reduce apply
+# (``_can_defer``: a leaf whose .grad is None — stolen, never read before the flush), and every
+# in-backward reader flushes first (flush_wgrad: DDP / FSDP hooks, the end-of-backward callback).
+WGRAD_FUSE = os.environ.get("HYPERION_WGRAD_FUSE", "dgrad")
+
+
+class _ParkedWgrad:
+    """A parked weight gradient.  Its output is held by STORAGE, not as a tensor: a second tensor
+    reference would stop AccumulateGrad from stealing the gradient — it would clone the
+    not-yet-written values instead (the deferred reduce's rule, conv_ops.cpp PendingWgrad)."""
+
+    __slots__ = ("dy", "x", "R", "S", "stride", "padding", "store", "meta", "plan")
+
+    def __init__(self, dy, x, w, stride, padding, dw, plan):
+        self.dy, self.x, self.R, self.S = dy, x, w.shape[2], w.shape[3]
+        self.stride, self.padding, self.plan = tuple(stride), tuple(padding), plan
+        self.store = dw.untyped_storage()
+        self.meta = (dw.dtype, dw.device, dw.storage_offset(), tuple(dw.shape), tuple(dw.stride()))
+
+    @property
+    def dw(self) -> torch.Tensor:
+        """A fresh tensor over the parked output's storage (the kernel writes through it)."""
+        dt, dev, off, shape, stride = self.meta
+        return torch.empty(0, dtype=dt, device=dev).set_(self.store, off, shape, stride)
+
+
+_parked: dict = {"req": None}
+
+
+def _fused_wgrad_tile(plan) -> tuple:
+    """(bm, bn, splits) of a parked weight gradient from its tuned standalone plan: the fused launch
+    runs 64 x 64 / 128 x 64 / 64 x 128 tiles (a 128 x 128 plan becomes 128 x 64, same splits)."""
+    if plan is None:
+        return 64, 64, -1
+    bm, bn, splits = plan[0], plan[1], plan[2]
+    if bm not in (64, 128) or bn not in (64, 128):
+        return 64, 64, -1
+    if bm == 128 and bn == 128:
+        bn = 64
+    return bm, bn, splits
+
+
+def _flush_parked() -> None:
+    """Run a parked weight gradient in its own launch (nobody consumed it); its split-K reduce is
+    deferred into the next weight-gradient launch or the final flush."""
+    req, _parked["req"] = _parked["req"], None
+    if req is None:
+        return
+    bm, bn, splits = _fused_wgrad_tile(req.plan)
+    _native.native().conv_wgrad(req.dy, req.x, req.R, req.S, req.stride[0], req.stride[1], req.padding[0],
+                                req.padding[1], bm, bn, splits, defer=True, out=req.dw)
+    _defer_state["pending"] = True
+
+
+def _park_ok(dy: torch.Tensor, x: torch.Tensor, w_param: Optional[torch.Tensor]) -> bool:
+    return (WGRAD_FUSE == "bn" and not _streams.enabled() and dy.dtype == torch.bfloat16 and x.dtype == dy.dtype
+            and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and dy.is_contiguous(memory_format=torch.channels_last) and _wgrad_native_ok(dy, x)
+            and _can_defer(w_param))
+
+
+def _park_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+    """Park this layer's weight gradient (caller checked :func:`_park_ok`); returns its dW tensor,
+    written by the launch that consumes the request (or a flush)."""
+    _flush_parked()  # one slot: an earlier request nobody consumed runs now
+    _native.count("wgrad")
+    dw = torch.empty(w.shape, dtype=x.dtype, device=x.device).contiguous(memory_format=torch.channels_last)
+    P, Q = dy.shape[2], dy.shape[3]
+    plan = _plan("wgrad", dy.shape[0] * P * Q, dy.shape[1], x.shape[1], w.shape[2], w.shape[3], stride[0])
+    _parked["req"] = _ParkedWgrad(dy, x, w, stride, padding, dw, plan)
+    _defer_state["pending"] = True
+    return dw
+
+
+def _bn_dx(C, dout, yc, bn_w, mean, invstd, sums):
+    """The BN dx pass (dz already masked, sums complete), carrying the parked weight gradient of the
+    layer above when there is one."""
+    req = _parked["req"]
+    if req is None or dout.dtype != torch.bfloat16:
+        return C.bn_bwd_dx(dout, yc, bn_w, mean, invstd, True, sums)
+    _parked["req"] = None
+    bm, bn, splits = _fused_wgrad_tile(req.plan)
+    _native.count("wgrad_bn_fused")
+    dyc, dbw, dbb, _ = C.bn_bwd_dx_wgrad(dout, yc, bn_w, mean, invstd, True, sums, wg_dy=req.dy, wg_x=req.x,
+                                         wg_R=req.R, wg_S=req.S, wg_sh=req.stride[0], wg_sw=req.stride[1],
+                                         wg_ph=req.padding[0], wg_pw=req.padding[1], wg_bm=bm, wg_bn=bn,
+                                         wg_splits=splits, wg_defer=True, wg_out=req.dw)
+    _defer_state["pending"] = True
+    return dyc, dbw, dbb
+
 
 def flush_wgrad() -> None:
-    """Run a deferred weight-gradient reduce now (no-op when none is pending)."""
+    """Run a parked weight gradient and a deferred weight-gradient reduce now (no-op when none)."""
     _defer_state["queued"] = False
+    if _parked["req"] is not None:
+        _flush_parked()
     if _defer_state["pending"]:
         _defer_state["pending"] = False
         _native.native().conv_wgrad_flush()
@@ -486,7 +586,8 @@ class _ConvBNActFn(torch.autograd.Function):
         own = ctx.bnlink
         if own is not None and own.dz is not None and dout is own.dz:
             # the consumer's dgrad epilogue already masked dout and summed Σdz, Σdz·x: dx pass only
-            dyc, dbw, dbb = _native.native().bn_bwd_dx(dout, yc, bn_w, mean, invstd, True, own.sums)
+            # (carrying the parked weight gradient of the layer above, WGRAD_FUSE "bn")
+            dyc, dbw, dbb = _bn_dx(_native.native(), dout, yc, bn_w, mean, invstd, own.sums)
             dres = dout if need_res else None
         else:
             if own is not None and own.used:
@@ -506,9 +607,11 @@ class _ConvBNActFn(torch.autograd.Function):
             dw = _streams.run_on_side(lambda: _wgrad(dyc, x, w, stride, padding), [dyc, x], dyc.device)
         dx = None
         prod = ctx.prod
-        # this layer's weight gradient rides in the data gradient's launch when both are native
+        # this layer's weight gradient: parked for the next BN dx pass (WGRAD_FUSE "bn"), or in the
+        # data gradient's launch ("dgrad"), or its own launch
+        park = dw is None and ctx.needs_input_grad[1] and _park_ok(dyc, x, ctx.w_param)
         wg = (wgrad_request(dyc, x, w, stride, padding, ctx.w_param)
-              if dw is None and ctx.needs_input_grad[1] and ctx.needs_input_grad[0] else None)
+              if dw is None and not park and ctx.needs_input_grad[1] and ctx.needs_input_grad[0] else None)
         if ctx.needs_input_grad[0]:
             if branch is not None and branch.users == 2 and _will_run(branch.nodes[1 - bidx]):
                 pend, branch.pending = branch.pending, None
@@ -524,6 +627,8 @@ class _ConvBNActFn(torch.autograd.Function):
                 # the whole gradient of x unless another op consumes x outside our links (then the
                 # producer sees a summed gradient and takes its full path)
                 dx = _dgrad(dyc, x, w, stride, padding, addend=add, bn=prod, wg=wg)
+        if dw is None and park:
+            dw = _park_wgrad(dyc, x, w, stride, padding)
         if dw is None and wg is not None and wg.dw is not None:
             dw = wg.dw
         if dw is None and ctx.needs_input_grad[1]:

@@ -612,8 +612,11 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
     REPLICATED whenever it fits (Llama-2-7B on MI355X: 13.5 GB of 288 GB), which makes the run
     FSDP over the adapters only — DDP-like traffic; ``replicate_frozen=False`` shards the base
     like the reference's torch FSDP.  ``'ddp'`` reproduces the reference (DDP over a replicated
-    model).  ``lora=False``: full bf16 FSDP with ``LlamaDecoderLayer`` units.  ``hf_token`` /
-    ``model_id`` are accepted for CLI compatibility; weights are random-init (no network).
+    model).  ``lora=False``: full bf16 FSDP with ``LlamaDecoderLayer`` units.  ``model_id``: a LOCAL
+    HF checkpoint directory (config.json + safetensors shards, models/hf_checkpoint.py) is loaded
+    weights-only before LoRA / FSDP wrapping, as the reference's ``from_pretrained`` (:465-468,
+    484-487); a hub id (no network here) falls back to random init of ``config`` (Llama-2-7B by
+    default).  ``hf_token`` is accepted for CLI compatibility.
     ``mask_pad_labels`` fixes the reference's unmasked pad labels (:517) when set.
     ``replicate_frozen`` ("auto" | True | False): under FSDP keep the frozen base whole on every rank
     when it fits (auto: <= 1/4 of HBM — 13.5 GB of 288 GB on MI355X), so only the adapters are
@@ -629,13 +632,22 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
     device = setup(rank, world, timeout_s=opts.timeout_s) if world > 1 else _single_device()
     seed_everything(opts.seed, 0)
     out = _out_dir(base_dir)
-    cfg = config or LlamaConfig.llama2_7b()
+    from ..models.hf_checkpoint import is_hf_dir, load_hf_weights, load_llama_config
+
+    pretrained = is_hf_dir(model_id)
+    cfg = config or (load_llama_config(model_id) if pretrained else LlamaConfig.llama2_7b())
     ds = _wikitext(opts, base_dir)
     sampler, loader = _loader(ds, world, rank, batch_size, opts, device)
     precision = opts.precision or ("bf16" if device.type == "cuda" else "fp32")
     pdt = _amp(precision) or torch.float32
     with torch.device(device):
         base = LlamaForCausalLM(cfg)
+    if pretrained:  # every rank reads the checkpoint; FSDP then keeps its own shard
+        load_hf_weights(base, model_id)
+        if rank == 0:
+            opts.log(f"[llama] weights from {model_id}")
+    elif rank == 0 and model_id and not os.path.isdir(str(model_id)):
+        opts.log(f"[llama] {model_id}: not a local HF checkpoint directory -> random-init weights")
     if lora:
         base = apply_lora(base, r=16, alpha=32, dropout=0.05)
         mode = f"lora_{precision}"
@@ -708,7 +720,8 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
     if world > 1:
         cleanup()
     return {"replicas": replicas, "run_id": run_id, "history": history, "checkpoint": ck, "mode": mode,
-            "graphed": runner._captured is not None, "graph_reason": runner.graph_reason}
+            "graphed": runner._captured is not None, "graph_reason": runner.graph_reason,
+            "weights": f"pretrained:{model_id}" if pretrained else "random-init"}
 
 
 def _save_adapter_from_sd(sd: Dict[str, torch.Tensor], out_dir: str) -> str:

@@ -154,8 +154,8 @@ def test_dual_resnet50_backward_matches_separate():
     gy = torch.randn(8, 16, device="cuda").bfloat16()
 
     def run(dual):
-        prev = hconv._DUAL
-        hconv._DUAL = dual
+        prev, prevf = hconv._DUAL, hconv.WGRAD_FUSE
+        hconv._DUAL, hconv.WGRAD_FUSE = dual, "dgrad"
         try:
             for q in m.parameters():
                 q.grad = None
@@ -164,11 +164,105 @@ def test_dual_resnet50_backward_matches_separate():
             torch.cuda.synchronize()
             return [q.grad.float().clone() for q in m.parameters()], _native.counters()
         finally:
-            hconv._DUAL = prev
+            hconv._DUAL, hconv.WGRAD_FUSE = prev, prevf
 
     (ref, c0), (ref2, _), (got, c1) = run("0"), run("0"), run("1")
     assert c0.get("wgrad_dual", 0) == 0
     assert c1.get("wgrad_dual", 0) >= 50, c1  # every conv but the stem (52 of 53)
+    for u, u2, v in zip(ref, ref2, got):
+        noise = (u2 - u).norm().item()
+        assert (v - u).norm().item() <= 4 * noise + 1e-2 * u.norm().item() + 1e-6
+
+
+# ---- BN dx pass + the weight gradient of the conv above it (csrc/kernels/bn_wgrad.hip) ----------
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("tile", [(64, 64), (128, 64), (64, 128)])
+def test_bn_dx_wgrad_matches_separate(shape, tile):
+    """bn_bwd_dx_wgrad == bn_bwd_dx + conv_wgrad (same tile / split plan), bitwise, for every conv
+    geometry of the ResNets; the BN layer is a different tensor (the layer below)."""
+    from hyperion.ops import _native
+
+    C_ = _native.native()
+    N, C, H, K, R, s, p = shape
+    if C % tile[1] != 0:
+        pytest.skip("bn must divide C")
+    x, w, dy = _case(shape, seed=4)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    Cb = 128
+    dz = torch.randn(N, Cb, 20, 20, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    yc = torch.randn(N, Cb, 20, 20, device="cuda", generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    bw = torch.rand(Cb, device="cuda", generator=g) + 0.5
+    mean = torch.randn(Cb, device="cuda", generator=g) * 0.1
+    invstd = torch.rand(Cb, device="cuda", generator=g) + 0.5
+    sums = torch.randn(_native.STAT_SLOTS * 2 * Cb, device="cuda", generator=g, dtype=torch.float64)
+    dx_ref, dbw_ref, dbb_ref = C_.bn_bwd_dx(dz, yc, bw, mean, invstd, True, sums)
+    dw_ref = C_.conv_wgrad(dy, x, R, R, s, s, p, p, tile[0], tile[1])
+    out = torch.full(w.shape, 7.0, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    dx, dbw, dbb, dw = C_.bn_bwd_dx_wgrad(dz, yc, bw, mean, invstd, True, sums, wg_dy=dy, wg_x=x, wg_R=R, wg_S=R,
+                                          wg_sh=s, wg_sw=s, wg_ph=p, wg_pw=p, wg_bm=tile[0], wg_bn=tile[1], wg_out=out)
+    torch.cuda.synchronize()
+    assert dw.data_ptr() == out.data_ptr()  # written in place
+    assert torch.equal(dx, dx_ref) and torch.equal(dbw, dbw_ref) and torch.equal(dbb, dbb_ref)
+    assert torch.equal(dw, dw_ref)
+
+
+def test_bn_dx_wgrad_deferred_chain():
+    """The fused launch runs an earlier deferred split-K reduce and defers its own; a flush ends it."""
+    from hyperion.ops import _native
+
+    C_ = _native.native()
+    x1, w1, dy1 = _case(SHAPES[0], seed=6)
+    x2, w2, dy2 = _case(SHAPES[2], seed=7)
+    ref1 = C_.conv_wgrad(dy1, x1, 1, 1, 1, 1, 0, 0, 64, 64)
+    ref2 = C_.conv_wgrad(dy2, x2, 3, 3, 1, 1, 1, 1, 64, 64)
+    dz = _t((4, 64, 28, 28))
+    yc = _t((4, 64, 28, 28))
+    ones, zeros = torch.ones(64, device="cuda"), torch.zeros(64, device="cuda")
+    sums = torch.zeros(_native.STAT_SLOTS * 2 * 64, device="cuda", dtype=torch.float64)
+    assert not C_.conv_wgrad_flush()
+    dw1 = C_.conv_wgrad(dy1, x1, 1, 1, 1, 1, 0, 0, 64, 64, defer=True)
+    _, _, _, dw2 = C_.bn_bwd_dx_wgrad(dz, yc, ones, zeros, ones, True, sums, wg_dy=dy2, wg_x=x2, wg_R=3, wg_S=3,
+                                      wg_sh=1, wg_sw=1, wg_ph=1, wg_pw=1, wg_defer=True)
+    assert C_.conv_wgrad_flush()
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, ref1)
+    assert torch.equal(dw2, ref2)
+
+
+@pytest.mark.parametrize("fuse", ["bn", "dgrad"])
+def test_wgrad_fusion_resnet50_backward_matches_separate(fuse):
+    """A ResNet-50 backward with parked weight gradients riding on the next BN dx pass ("bn") or on
+    their own data gradient ("dgrad") vs separate launches: same gradients to the BN atomics' noise,
+    and the fused launches served most layers."""
+    import hyperion.ops.conv as hconv
+    from hyperion.models.resnet import resnet50
+    from hyperion.ops import _native
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=16).cuda().to(memory_format=torch.channels_last)
+    cast_for_compute(m, torch.bfloat16)
+    x0 = torch.randn(8, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, 16, device="cuda").bfloat16()
+
+    def run(mode):
+        prev = hconv.WGRAD_FUSE
+        hconv.WGRAD_FUSE = mode
+        try:
+            for q in m.parameters():
+                q.grad = None
+            _native.reset_counters()
+            m(x0).backward(gy)
+            torch.cuda.synchronize()
+            assert hconv._parked["req"] is None and not hconv._defer_state["pending"]
+            return [q.grad.float().clone() for q in m.parameters()], _native.counters()
+        finally:
+            hconv.WGRAD_FUSE = prev
+
+    (ref, c0), (ref2, _), (got, c1) = run("0"), run("0"), run(fuse)
+    assert c0.get("wgrad_bn_fused", 0) == 0 and c0.get("wgrad_dual", 0) == 0
+    key = "wgrad_bn_fused" if fuse == "bn" else "wgrad_dual"
+    assert c1.get(key, 0) >= (40 if fuse == "bn" else 50), c1
     for u, u2, v in zip(ref, ref2, got):
         noise = (u2 - u).norm().item()
         assert (v - u).norm().item() <= 4 * noise + 1e-2 * u.norm().item() + 1e-6
