@@ -947,6 +947,8 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("wg_sw"), pybind11::arg("wg_ph"), pybind11::arg("wg_pw"), pybind11::arg("wg_bm") = 64,
         pybind11::arg("wg_bn") = 64, pybind11::arg("wg_splits") = -1, pybind11::arg("wg_defer") = false,
         pybind11::arg("wg_out") = pybind11::none());
+  m.def("conv_set_persist", [](int64_t on) { hyp::conv_set_persist((int)on); },
+        "persistent conv launches (conv_persist.h: next tile's loads behind the current epilogue): 0 off, 1 on");
   m.def("conv_dual_set_order", [](int64_t o) { hyp::conv_dual_set_order((int)o); },
         "A/B: grid order of conv_dgrad_wgrad launches (-1 per call, 0 interleaved, 1 data gradient first)");
   m.def("conv_wgrad", &conv_wgrad, "NHWC conv weight gradient on MFMA (split-K, transposed LDS reads)",

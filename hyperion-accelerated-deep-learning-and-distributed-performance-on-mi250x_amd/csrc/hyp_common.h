@@ -55,6 +55,29 @@ __device__ __forceinline__ float f16_lo(uint32_t w) { return (float)__builtin_bi
 __device__ __forceinline__ float f16_hi(uint32_t w) { return (float)__builtin_bit_cast(f16_t, (uint16_t)(w >> 16)); }
 
 // ---- 8-wide vector IO -------------------------------------------------------------------
+// 16-byte GLOBAL store written through to memory (sc1): the line leaves the XCD's L2 at once, so a
+// large output leaves no dirty lines for the kernel-end write-back (a dependent kernel boundary
+// costs ~1.5 us + the dirty bytes / ~6 TB/s; writer + trivial successor in a hipGraph, MI355X:
+// 16 MB 6.21 -> 5.03 us, 32 MB 8.67 -> 7.07 us, profiles/r05/boundary_wt.jsonl).  Global
+// addresses only.  HYP_WT_STORES=0 compiles plain stores (A/B).  The store is inline asm, which the
+// compiler's hazard recognizer does not see: a VALU writing the store's data VGPRs in the next
+// cycles would race the store's read of them (gfx9 "VMEM store data > 8 bytes" hazard: observed as
+// dx = dres in the small-M BN backward, whose next pack reuses the registers at once), so the asm
+// carries its own wait states (s_nop 1).  Its vmcnt bookkeeping does not see the store either,
+// which only ever makes its waits stricter.
+#ifndef HYP_WT_STORES
+#define HYP_WT_STORES 1
+#endif
+__device__ __forceinline__ void st16_wt(void* p, uint4 v) {
+#if HYP_WT_STORES
+  typedef unsigned hyp_u32x4 __attribute__((ext_vector_type(4)));
+  const hyp_u32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+#else
+  *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+
 template <typename T>
 struct Vec8;
 
@@ -69,6 +92,10 @@ struct Vec8<float> {
   static __device__ __forceinline__ void store(float* __restrict__ p, const float (&v)[8]) {
     reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
     reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  static __device__ __forceinline__ void store_wt(float* __restrict__ p, const float (&v)[8]) {
+    st16_wt(p, uint4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+    st16_wt(p + 4, uint4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
   }
 };
 
@@ -91,6 +118,10 @@ struct Vec8<bf16_t> {
     r.w = pack_bf16x2(v[6], v[7]);
     *reinterpret_cast<uint4*>(p) = r;
   }
+  static __device__ __forceinline__ void store_wt(bf16_t* __restrict__ p, const float (&v)[8]) {
+    st16_wt(p, uint4{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                     pack_bf16x2(v[6], v[7])});
+  }
 };
 
 template <>
@@ -111,6 +142,10 @@ struct Vec8<f16_t> {
     r.z = pack_f16x2(v[4], v[5]);
     r.w = pack_f16x2(v[6], v[7]);
     *reinterpret_cast<uint4*>(p) = r;
+  }
+  static __device__ __forceinline__ void store_wt(f16_t* __restrict__ p, const float (&v)[8]) {
+    st16_wt(p, uint4{pack_f16x2(v[0], v[1]), pack_f16x2(v[2], v[3]), pack_f16x2(v[4], v[5]),
+                     pack_f16x2(v[6], v[7])});
   }
 };
 

@@ -331,6 +331,8 @@ hipError_t conv_wgrad_prepare(WgradArgs* a, int dtype, const DualWgrad& d, const
 // gradient without split-K); any other case launches the two separately (same results).
 // A/B: -1 = each DualWgrad's own order, 0 interleaved, 1 data gradient first
 void conv_dual_set_order(int order);
+// persistent conv launches (conv_persist.h) for the variants they cover: 0 off, 1 on
+void conv_set_persist(int on);
 // bn_wgrad.hip: the BatchNorm backward dx pass of a layer (bn_backward_dx's arguments) and the weight
 // gradient d of the conv ABOVE it (whose dY the previous backward step produced) in ONE launch —
 // the cheap, memory-bound dx pass runs beside the weight gradient's K loops instead of alone

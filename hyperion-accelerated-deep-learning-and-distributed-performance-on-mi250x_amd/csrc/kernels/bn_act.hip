@@ -197,8 +197,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_k(const T* __restrict__ x, co
       v0[j] = a;
       v1[j] = b;
     }
-    Vec8<T>::store(y + off, v0);
-    Vec8<T>::store(y + off + step, v1);
+    Vec8<T>::store_wt(y + off, v0);
+    Vec8<T>::store_wt(y + off + step, v1);
   }
   if (row < row1) {
     float v[8], rr[8];
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_k(const T* __restrict__ x, co
       if (ACT) a = fmaxf(a, 0.f);
       v[j] = a;
     }
-    Vec8<T>::store(y + off, v);
+    Vec8<T>::store_wt(y + off, v);
   }
 }
 
@@ -375,8 +375,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_small_k(const T* __restrict__ dy, c
         g[j] = d;
         xv[j] = fmaf(A[j], d, fmaf(B[j], xv[j], Cc[j]));
       }
-      Vec8<T>::store(dx + off, xv);
-      if (RES) Vec8<T>::store(dres + off, g);
+      Vec8<T>::store_wt(dx + off, xv);
+      if (RES) Vec8<T>::store_wt(dres + off, g);
     }
   }
 }

@@ -155,8 +155,8 @@ __device__ __forceinline__ void bn_bwd_dx_body(const T* __restrict__ dy, const T
       g[j] = d;
       xo[j] = fmaf(A[j], d, fmaf(B[j], xi[j], Cc[j]));
     }
-    Vec8<T>::store(dx + o, xo);
-    if (RES) Vec8<T>::store(dres + o, g);
+    Vec8<T>::store_wt(dx + o, xo);
+    if (RES) Vec8<T>::store_wt(dres + o, g);
   };
   for (; row + rpi < row1; row += 2 * rpi, off += 2 * step) {  // two rows' loads in flight
     float g0[8], x0[8], y0[8], g1[8], x1[8], y1[8];

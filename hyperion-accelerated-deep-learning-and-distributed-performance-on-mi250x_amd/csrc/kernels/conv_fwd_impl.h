@@ -744,7 +744,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a, const int blk, 
         }
         Vec8<T>::store(reinterpret_cast<T*>(&v), o);
       }
-      *reinterpret_cast<uint4*>(a.out + orow(m) * a.K + k) = v;
+      st16_wt(a.out + orow(m) * a.K + k, v);
     }
   }
   if (a.stamps != nullptr) tse = realtime_stamp();

@@ -20,7 +20,10 @@
 // ROUNDED outputs, added atomically into the [2][K] sums the BN apply finalizes inline
 // (bn_act.hip), so BN's separate statistics pass over y and its finalize launch disappear.
 // Requirements: C % 64 == 0 (every ResNet conv but the 3-channel stem), 16-byte aligned tensors.
+#include <type_traits>
+
 #include "conv_fwd_impl.h"
+#include "conv_persist.h"
 
 namespace hyp {
 namespace {
@@ -48,6 +51,39 @@ hipError_t launch_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) 
   else
     hipLaunchKernelGGL((conv_fwd_k<T, BM, BN, false, false, NB>), dim3(tiles), dim3(kThreads), 0, st, a);
   return hipGetLastError();
+}
+
+// Persistent launch (conv_persist.h) of the supported variants: grid = the resident capacity
+// (occupancy query x CUs), tiles spread evenly, a multiple of 8 workgroups
+int g_persist = 0;  // conv_set_persist
+
+template <typename T, int BM, int BN, bool STATS, bool DGRAD, int NB, bool LEAN>
+hipError_t launch_persist_k(const ConvArgs& a, int ntiles, hipStream_t st) {
+  auto kern = conv_persist_k<T, BM, BN, STATS, DGRAD, NB, LEAN>;
+  static int cap = 0;  // per instantiation: resident workgroups on the whole device
+  if (cap == 0) {
+    int occ = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kThreads, 0) != hipSuccess || occ < 1) occ = 1;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    cap = occ * cus;
+  }
+  const int per = (ntiles + cap - 1) / cap;
+  int nblk = (ntiles + per - 1) / per;
+  nblk = (nblk + 7) / 8 * 8;  // tile blk + i * nblk stays on its plain-launch XCD
+  hipLaunchKernelGGL(kern, dim3(nblk), dim3(kThreads), 0, st, a, nblk);
+  return hipGetLastError();
+}
+
+template <typename T, int BM, int BN, int NB>
+hipError_t launch_persist_nb(const ConvArgs& a, bool stats, bool dgrad, hipStream_t st) {
+  const int ntiles = ((a.M + BM - 1) / BM) * ((a.K + BN - 1) / BN) * (a.sd == 2 ? 4 : 1);
+  if (dgrad && stats && a.bnb.mode <= 1 && a.addend == nullptr)
+    return launch_persist_k<T, BM, BN, true, true, NB, true>(a, ntiles, st);
+  if (dgrad && stats) return launch_persist_k<T, BM, BN, true, true, NB, false>(a, ntiles, st);
+  if (dgrad) return launch_persist_k<T, BM, BN, false, true, NB, false>(a, ntiles, st);
+  if (stats) return launch_persist_k<T, BM, BN, true, false, NB, false>(a, ntiles, st);
+  return hipErrorNotSupported;
 }
 
 int g_stages = 0;  // 0 = automatic (conv_set_stages, for tuning sweeps)
@@ -98,6 +134,8 @@ int conv_fwd_group(int M, int K, int RS, int bm, int bn) {
 void conv_set_stamps(void* buf) { g_stamps = static_cast<unsigned long long*>(buf); }
 
 void conv_set_stages(int nb) { g_stages = (nb >= 1 && nb <= 4) ? nb : 0; }
+
+void conv_set_persist(int on) { g_persist = on; }
 
 void conv_set_xf_debug(int bits) { g_xf_dbg = bits & 7; }
 
@@ -220,6 +258,26 @@ hipError_t conv_fwd(int dtype, const void* in, const void* w, void* out, const v
     return e != hipSuccess ? e : wgrad_after();
   }
   const bool stats = (psum != nullptr && psq != nullptr) || bnb != nullptr;
+  // persistent launch: bf16, no split-K / XF / DIRECT / affine epilogue; forward only with BN
+  // statistics (no addend); every data-gradient variant (also the stride-2 phase split)
+  const bool persist_ok = g_persist && dual == nullptr && dtype == kBF16 && xf == nullptr && !a.direct && !aff &&
+                          ep == nullptr && (dgrad || (stats && addend == nullptr)) && a.splits == (a.sd == 2 ? 4 : 1);
+  if (persist_ok) {
+    const int nbv = a.nb > 0 ? a.nb : (g_stages > 0 ? g_stages : 2);
+    hipError_t e = hipErrorNotSupported;
+    if (nbv >= 1 && nbv <= 3) {
+      auto go = [&](auto nbc) -> hipError_t {
+        constexpr int NBv = decltype(nbc)::value;
+        if (bm == 128 && bn == 128) return launch_persist_nb<bf16_t, 128, 128, NBv>(a, stats, dgrad, st);
+        if (bm == 128 && bn == 64) return launch_persist_nb<bf16_t, 128, 64, NBv>(a, stats, dgrad, st);
+        if (bm == 64 && bn == 64) return launch_persist_nb<bf16_t, 64, 64, NBv>(a, stats, dgrad, st);
+        return hipErrorNotSupported;  // other tiles: the plain launch
+      };
+      e = nbv == 1 ? go(std::integral_constant<int, 1>{})
+                   : (nbv == 2 ? go(std::integral_constant<int, 2>{}) : go(std::integral_constant<int, 3>{}));
+    }
+    if (e != hipErrorNotSupported) return e;
+  }
   if (dual != nullptr) {
     // launch_nb's variant choice for a data gradient: LEAN BN-backward (mode 0/1, no addend), full
     // BN-backward, plain

@@ -116,7 +116,7 @@ __device__ __forceinline__ void wgrad_store_tile(const f32x4 (&acc)[BM / 32][BN 
       for (int e = 0; e < 4; ++e) st1<T>(o + e, a.alpha * v[e]);
       *reinterpret_cast<uint2*>(outT + off) = *reinterpret_cast<const uint2*>(o);
     } else {
-      *reinterpret_cast<f32x4*>(part + off) = v;
+      st16_wt(part + off, __builtin_bit_cast(uint4, v));
     }
   }
 }

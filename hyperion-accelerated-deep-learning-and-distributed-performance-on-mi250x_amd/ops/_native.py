@@ -49,6 +49,8 @@ def _load():
         raise RuntimeError(f"{name}: built with kStatSlots={_MOD.STAT_SLOTS}, Python expects {STAT_SLOTS}; rebuild")
     if _MOD is not None and os.environ.get("HYPERION_WS_DEPTH") and hasattr(_MOD, "ws_set_depth"):
         _MOD.ws_set_depth(int(os.environ["HYPERION_WS_DEPTH"]))  # weight-streaming k-steps in flight (A/B)
+    if _MOD is not None and os.environ.get("HYPERION_CONV_PERSIST") and hasattr(_MOD, "conv_set_persist"):
+        _MOD.conv_set_persist(int(os.environ["HYPERION_CONV_PERSIST"]))  # persistent fwd/dgrad convs (A/B)
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")

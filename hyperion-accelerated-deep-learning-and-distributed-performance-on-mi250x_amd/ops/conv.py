@@ -324,13 +324,19 @@ class ResidualLink:
     leaves only, ``retain_graph=True``) gets the plain per-op gradients.
     """
 
-    __slots__ = ("src", "armed", "dres", "first_node")
+    __slots__ = ("_src", "armed", "dres", "first_node")
 
     def __init__(self, src: torch.Tensor):
-        self.src = src
+        # held weakly: the link rides ctx attributes (not saved tensors), so a strong reference
+        # would keep one activation per layer alive under activation checkpointing
+        self._src = weakref.ref(src)
         self.armed = False
         self.dres: Optional[torch.Tensor] = None
         self.first_node = None
+
+    @property
+    def src(self) -> Optional[torch.Tensor]:
+        return self._src()
 
 
 class BranchSumLink:
@@ -347,13 +353,17 @@ class BranchSumLink:
     ``Bottleneck.forward`` (``out += identity``).
     """
 
-    __slots__ = ("src", "users", "pending", "nodes")
+    __slots__ = ("_src", "users", "pending", "nodes")
 
     def __init__(self, src: torch.Tensor):
-        self.src = src
+        self._src = weakref.ref(src)  # weakly, as ResidualLink
         self.users = 0
         self.pending = None  # (owner consumer index, dX)
         self.nodes = [None, None]  # grad_fn of each consumer's output
+
+    @property
+    def src(self) -> Optional[torch.Tensor]:
+        return self._src()
 
 
 def branch_sum_link(x: torch.Tensor) -> Optional[BranchSumLink]:

@@ -52,8 +52,25 @@ DEFAULT_MAX_LOGITS_BYTES = 4 << 30
 # larger chunks keep the dX / dW GEMMs efficient).  HYPERION_CE_CHUNK forces a class count.
 CE_BLOCK_BYTES = int(os.environ.get("HYPERION_CE_BLOCK_MB", "256")) << 20
 CE_CHUNK = int(os.environ.get("HYPERION_CE_CHUNK", "0"))
-# logits budget of the materialised schedule (module docstring); 0 forces the no-logits schedule
-CE_MATERIALIZE_BYTES = int(os.environ.get("HYPERION_CE_MATERIALIZE_MB", "8192")) << 20
+# logits budget of the materialised schedule (module docstring); 0 forces the no-logits schedule.
+# Default: 1/32 of the device's HBM (9 GiB on a 288 GB MI355X, 2 GiB on a 64 GB MI250X GCD), and
+# never more than half of what is free at the call
+_CE_MAT_ENV = os.environ.get("HYPERION_CE_MATERIALIZE_MB")
+CE_MATERIALIZE_BYTES = int(_CE_MAT_ENV) << 20 if _CE_MAT_ENV is not None else None
+_HBM_BUDGET = {}
+
+
+def _materialize_budget(dev: torch.device) -> int:
+    if CE_MATERIALIZE_BYTES is not None:
+        return CE_MATERIALIZE_BYTES
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _HBM_BUDGET:
+        _HBM_BUDGET[idx] = torch.cuda.get_device_properties(idx).total_memory // 32
+    budget = _HBM_BUDGET[idx]
+    if torch.cuda.is_current_stream_capturing():
+        return budget  # no free-memory query inside a capture; the graph pool was sized eagerly
+    free, _ = torch.cuda.mem_get_info(idx)
+    return min(budget, free // 2)
 
 
 def _ce_chunk(N: int, V: int, elt: int) -> int:
@@ -97,7 +114,7 @@ class _FusedLinearCE(torch.autograd.Function):
         scale = (1.0 / n_valid).reshape(1)
         native = _native.use_native(x2, op="ce") and cdt in _native.DTYPE_CODE
         if native and cdt in (torch.bfloat16, torch.float16) and x2.is_cuda:
-            if N * (-(-V // 8) * 8) * x2.element_size() <= CE_MATERIALIZE_BYTES:
+            if N * (-(-V // 8) * 8) * x2.element_size() <= _materialize_budget(x2.device):
                 return _FusedLinearCE._materialized(ctx, x, x2, w, bias, t, ignore_index, scale, shape)
             if x2.shape[1] % 64 == 0:
                 return _FusedLinearCE._fused(ctx, x, x2, w, bias, t, ignore_index, scale, n_valid, shape)

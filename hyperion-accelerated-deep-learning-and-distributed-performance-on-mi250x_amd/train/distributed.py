@@ -588,7 +588,8 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
 def train_gpt2_fsdp(rank: int, world: int, epochs: int = 3, base_dir: str = DEFAULT_BASE_DIR,
                     opts: Optional[RunOptions] = None, batch_size: int = 32) -> Dict:
     """BASELINE.json config 4: GPT-2-small-shaped causal LM (12 x 768, 12 heads, ff 3072, GELU,
-    124M parameters with the tied-size head) under FSDP FULL_SHARD with one unit per transformer
+    162.3M parameters: GPT-2-small's 124M plus an UNTIED 50257 x 768 output head, as the FSDP
+    records report) under FSDP FULL_SHARD with one unit per transformer
     layer, bf16 mixed precision, global clip 1.0, on WikiText-2-shaped data (128 tokens).  The
     reference's FSDP run used the 2-layer 256-d LM (``distributed_utils.py:290-406``); this is the
     same trainer (:func:`train_language_model_fsdp`) on the larger model."""
