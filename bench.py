@@ -46,6 +46,15 @@ def parse(argv=None):
     ap.add_argument("--graph-multi", type=int, default=1,
                     help="N>1: capture fwd+bwd and the optimizer as two hipGraphs around eager bucket all-reduces")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--ddp-schedule", default="segmented", choices=["auto", "segmented"],
+                    help="N>1 (or --ddp-world1) graphed DDP schedule: segmented (default) = the whole step "
+                         "captured as graph segments with each bucket's all-reduce issue / wait as eager holes, "
+                         "so every bucket overlaps the rest of the backward; auto = 3 graphs split at the "
+                         "model's graph_stages.  Measured at world 1 with the native RCCL communicator: "
+                         "5.15 vs 14.5 ms/step (profiles/r05/ddp_schedule_ab.json)")
+    ap.add_argument("--ddp-world1", type=int, default=0,
+                    help="A/B only: wrap the 1-GPU model in DDP with buckets and the native RCCL communicator "
+                         "(the N>1 schedule's collectives at world 1)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--channels-last", type=int, default=1)
     ap.add_argument("--loss", default="torch", choices=["torch", "fused"],
@@ -88,10 +97,17 @@ def main(argv=None) -> int:
         from hyperion.train.amp import cast_for_compute
 
         cast_for_compute(model, amp)
-    if n_gpus > 1:
+    if n_gpus > 1 or args.ddp_world1:
         # fp32 gradient buckets by default (the reference reduced fp32 grads); --comm-dtype bf16 opt-in
+        kw = {}
+        if n_gpus == 1:
+            from hyperion.bench.models import _ensure_pg
+            from hyperion.parallel.comm import NativeComm
+
+            _ensure_pg()  # a world-1 process group for the communicator's bootstrap
+            kw = dict(buckets_at_world_1=True, comm=NativeComm(dev))
         model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
-                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+                    comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, **kw)
     opt = FusedAdam(model.parameters(), lr=1e-3, zero_grad_in_step=True)
     # the reference's nn.MSELoss (mean) — Hyperion's fused forward+gradient pass on gfx950
     from hyperion.ops.losses import MSELoss
@@ -104,7 +120,8 @@ def main(argv=None) -> int:
         x = x.to(amp)
     y = torch.rand(B, 1000, device=dev)
     use_graph = bool(args.graph) and dev.type == "cuda" and (n_gpus == 1 or bool(args.graph_multi))
-    step = TrainStep(model, opt, loss_fn, amp_dtype=None if copies else amp, graph=use_graph)
+    step = TrainStep(model, opt, loss_fn, amp_dtype=None if copies else amp, graph=use_graph,
+                     ddp_schedule=args.ddp_schedule)
 
     for _ in range(args.warmup):
         step(x, y)
@@ -171,7 +188,9 @@ def main(argv=None) -> int:
                 "loss": "MSE vs rand(B,1000) (reference benchmark_model)",
                 "optimizer": "Adam lr=1e-3 (hyperion FusedAdam, multi-tensor)",
                 "hipgraph": use_graph,
-                "ddp_schedule": (None if n_gpus == 1 else
+                "ddp_schedule": (None if (n_gpus == 1 and not args.ddp_world1) else
+                                 f"segmented: {step.seg.num_segments} graph segments, bucket all-reduce holes"
+                                 if step.seg is not None else
                                  "3 graphs: top fwd+bwd | bottom bwd overlapping the top buckets' RCCL all-reduce | optimizer"
                                  if step.graph3 is not None else
                                  "2 graphs around eager bucket all-reduces" if step.graph2 is not None else

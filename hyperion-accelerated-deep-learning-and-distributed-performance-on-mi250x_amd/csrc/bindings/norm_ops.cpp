@@ -206,6 +206,15 @@ void clip_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& 
                                        total_sq.data_ptr<float>(), (float)max_norm, cur_stream()));
 }
 
+void copy_mt(const at::Tensor& ptrs, const at::Tensor& sizes, const at::Tensor& blocks, int64_t T, int64_t chunk,
+             int64_t src_dtype, int64_t dst_dtype) {
+  TORCH_CHECK(ptrs.numel() == 2 * T && sizes.numel() == T, "copy_mt: table of 2 x T pointers and T sizes");
+  const at::DeviceGuard guard(ptrs.device());
+  HYP_CHECK_HIP(hyp::copy_multi_tensor((int)src_dtype, (int)dst_dtype, ptrs.data_ptr<int64_t>(),
+                                       sizes.data_ptr<int64_t>(), blocks.data_ptr<int>(), (int)blocks.size(0), (int)T,
+                                       (int)chunk, cur_stream()));
+}
+
 // ---- STREAM ----------------------------------------------------------------------------------
 void stream(int64_t op, const at::Tensor& a, const c10::optional<at::Tensor>& b, at::Tensor& c, double s,
             bool nontemporal, int64_t blocks) {
@@ -251,6 +260,7 @@ void register_norm_ops(pybind11::module& m) {
   m.def("unscale_mt", &unscale_mt, "multi-tensor unscale + non-finite check");
   m.def("sumsq_mt", &sumsq_mt, "multi-tensor sum of squares");
   m.def("clip_mt", &clip_mt, "multi-tensor clip by global norm (device scalar)");
+  m.def("copy_mt", &copy_mt, "multi-tensor copy with dtype conversion (ptrs [2][T]: sources, destinations)");
   m.def("stream", &stream, "STREAM copy/scale/add/triad");
 }
 

@@ -47,6 +47,8 @@ hipError_t unscale_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64
                                 int nblocks, int chunk, const float* inv_scale, float* found_inf, hipStream_t stream);
 hipError_t sumsq_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
                               int chunk, float* partials, float* out, hipStream_t stream);
+hipError_t copy_multi_tensor(int src_dtype, int dst_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks,
+                             int nblocks, int T, int chunk, hipStream_t stream);
 hipError_t clip_multi_tensor(int grad_dtype, const int64_t* ptrs, const int64_t* sizes, const int* blocks, int nblocks,
                              int chunk, const float* total_sq, float max_norm, hipStream_t stream);
 

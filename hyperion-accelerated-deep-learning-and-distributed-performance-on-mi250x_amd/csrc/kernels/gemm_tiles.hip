@@ -38,7 +38,9 @@ namespace {
 using namespace mfl;
 
 constexpr int kBK = 32;
-constexpr int kNB = 4;  // LDS ring depth
+// LDS ring depth: a template parameter (NBR) — 4 for the 2-workgroups-per-CU tiles, 6-8 for the
+// deep-ring tiles that run one workgroup per CU and keep 5-7 stages in flight (the k-loop of the
+// small transformer GEMMs is latency-bound: a 32-deep stage per ~latency / (NBR - 1))
 constexpr int kGroupM = 8;
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -276,8 +278,20 @@ struct GemmP {
 // SAFE = false: every piece on the fast path — needs M >= BM, N >= BN, K % 32 == 0 (the last tile
 // row / column is shifted back to end at M / N: overlapping tiles write identical values, so the
 // host sends beta != 0 with ragged M / N to SAFE); SAFE = true: the per-lane path (ragged K, M < BM).
-template <typename T, typename OutT, int BM, int BN, int WM, int WN, bool ATR, bool BTR, bool SAFE>
+// vmcnt wait for "stage t landed" with `ahead` (<= A) later stages of L pieces each in flight
+template <int L, int A>
+__device__ __forceinline__ void wait_ahead_n(int ahead) {
+  if constexpr (A == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (ahead >= A) wait_vmcnt<A * L>();
+    else wait_ahead_n<L, A - 1>(ahead);
+  }
+}
+
+template <typename T, typename OutT, int BM, int BN, int WM, int WN, bool ATR, bool BTR, bool SAFE, int NBR>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
+  constexpr int kNB = NBR;
   constexpr int NW = WM * WN;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
   static_assert(FN * 16 == 64, "wave tiles are 64 columns wide (epilogue patch)");
@@ -361,12 +375,8 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
       else a[i] = frag_row(lds_addr(sa), am + (half * FH + i) * 16, lane);
     }
   };
-  auto wait_ahead = [&](int ahead) {  // this wave's glds of a stage landed, `ahead` later stages in flight
-    if (ahead >= 3) wait_vmcnt<3 * kL>();
-    else if (ahead == 2) wait_vmcnt<2 * kL>();
-    else if (ahead == 1) wait_vmcnt<kL>();
-    else wait_vmcnt<0>();
-  };
+  static_assert((kNB - 1) * kL < 64, "vmcnt is 6 bits");
+  auto wait_ahead = [&](int ahead) { wait_ahead_n<kL, kNB - 1>(ahead); };  // this wave's glds of a stage landed
 
 #pragma unroll
   for (int s = 0; s < kNB; ++s)
@@ -481,28 +491,32 @@ struct TileCfg {
 constexpr TileCfg kTiles[4] = {
     {256, 256, 8, 1, 1.0}, {256, 128, 8, 1, 0.80}, {128, 128, 4, 2, 0.62}, {128, 128, 4, 2, 0.55}};
 
-template <typename T, typename OutT, int BM, int BN, int WM, int WN, bool SAFE>
+template <typename T, typename OutT, int BM, int BN, int WM, int WN, bool SAFE, int NBR>
 hipError_t launch_layout(const GemmP& p, bool atr, bool btr, int nwg, hipStream_t st) {
   const dim3 grid(nwg), block(WM * WN * 64);
   if (!atr && !btr)
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, false, SAFE>), grid, block, 0, st, p);
+    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, false, SAFE, NBR>), grid, block, 0, st, p);
   else if (!atr && btr)
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, true, SAFE>), grid, block, 0, st, p);
+    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, true, SAFE, NBR>), grid, block, 0, st, p);
   else if (atr && btr)
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, true, SAFE>), grid, block, 0, st, p);
+    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, true, SAFE, NBR>), grid, block, 0, st, p);
   else
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, false, SAFE>), grid, block, 0, st, p);
+    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, false, SAFE, NBR>), grid, block, 0, st, p);
   return hipGetLastError();
 }
 
-// tile 3 = the 128x128 SAFE kernel (ragged K, M or N below the tile, accumulate over ragged tiles)
+// tile 3 = the 128x128 SAFE kernel (ragged K, M or N below the tile, accumulate over ragged tiles).
+// Deep rings at one workgroup per CU (128x128 with 8 stages, 256x128 with 6) were measured SLOWER
+// on every transformer shape (1.1-2x, profiles/r05/gemm_probe_deep_ring.json): with one wave per
+// SIMD nothing hides the fragment reads behind the MFMAs — occupancy, not bytes in flight, bounds
+// these k-loops.  NBR stays a template parameter for such sweeps.
 template <typename T, typename OutT>
 hipError_t launch_tile(const GemmP& p, bool atr, bool btr, int tile, int nwg, hipStream_t st) {
   switch (tile) {
-    case 0: return launch_layout<T, OutT, 256, 256, 2, 4, false>(p, atr, btr, nwg, st);
-    case 1: return launch_layout<T, OutT, 256, 128, 4, 2, false>(p, atr, btr, nwg, st);
-    case 2: return launch_layout<T, OutT, 128, 128, 2, 2, false>(p, atr, btr, nwg, st);
-    default: return launch_layout<T, OutT, 128, 128, 2, 2, true>(p, atr, btr, nwg, st);
+    case 0: return launch_layout<T, OutT, 256, 256, 2, 4, false, 4>(p, atr, btr, nwg, st);
+    case 1: return launch_layout<T, OutT, 256, 128, 4, 2, false, 4>(p, atr, btr, nwg, st);
+    case 2: return launch_layout<T, OutT, 128, 128, 2, 2, false, 4>(p, atr, btr, nwg, st);
+    default: return launch_layout<T, OutT, 128, 128, 2, 2, true, 4>(p, atr, btr, nwg, st);
   }
 }
 

@@ -217,7 +217,9 @@ class zero_scope:
         if _ARENAS or self.device.type != "cuda":
             return self
         sizes = self.owner.__dict__.setdefault("_zero_arena_sizes", {})
-        n = sizes.get(self.key, 0)
+        # a key not seen yet (a graph stage captured after warm-up ran the whole forward) borrows
+        # the largest learnt size: one fill of a slightly larger buffer instead of one per layer
+        n = sizes.get(self.key, 0) or max(sizes.values(), default=0)
         self.arena = ZeroArena(torch.zeros(n, device=self.device, dtype=torch.float64) if n else None)
         _ARENAS.append(self.arena)
         return self

@@ -70,7 +70,7 @@ class MultiTensorTable:
                 "hyperion: multi-tensor table built during hipGraph capture; tensor addresses changed "
                 "since warm-up (keep .grad allocated: zero_grad(set_to_none=False) inside the captured step)"
             )
-        dev_t = [h.to(dev) for h in host]
+        dev_t = [_h2d(h, dev) for h in host]
         self.ptrs, self.sizes, self.blocks = dev_t
         if self.nblocks == 0:
             self.blocks = self.blocks[:0]
@@ -92,9 +92,21 @@ class MultiTensorTable:
         host = torch.tensor(ptrs, dtype=torch.int64)
         if self.ptrs.is_cuda and torch.cuda.is_current_stream_capturing():
             _PENDING.append((self.ptrs, host))
+        elif self.ptrs.is_cuda:
+            # stream-ordered, no host sync: with set_to_none gradients every eager step re-points
+            # the table, and a blocking pageable copy stalled the host until the backward drained
+            # (the next step's launches then started from an idle GPU: ViT-B/16 fp32 "optimizer
+            # time" 6.6 ms vs torch's 1.6 ms, profiles/r04/models)
+            self.ptrs.copy_(host.pin_memory(), non_blocking=True)
         else:
             self.ptrs.copy_(host)
         self.key = self.key_of(groups)
+
+
+def _h2d(h: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    if dev.type != "cuda":
+        return h.to(dev)
+    return h.pin_memory().to(dev, non_blocking=True)  # pinned block reused once the copy's event passed
 
 
 def _capturing(dev) -> bool:

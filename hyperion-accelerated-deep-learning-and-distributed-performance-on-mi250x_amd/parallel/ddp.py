@@ -78,6 +78,16 @@ def _param_view(flat: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
     return flat.view(p.shape)
 
 
+def _mt_ok(g: torch.Tensor, slot: torch.Tensor) -> bool:
+    """The multi-tensor pack applies: same element order, 16-byte aligned, a native dtype."""
+    from ..ops import _native
+
+    return (g.is_cuda and g.shape == slot.shape and g.data_ptr() % 16 == 0 and g.dtype in _native.DTYPE_CODE
+            and slot.dtype in _native.DTYPE_CODE and _native.use_native(g, op="copy_mt")
+            and all(sa == sb for sa, sb, n in zip(g.stride(), slot.stride(), g.shape) if n > 1)
+            and (g.is_contiguous() or g.is_contiguous(memory_format=torch.channels_last)))
+
+
 class _Bucket:
     __slots__ = ("index", "params", "offsets", "buf", "ready", "got", "work", "launched")
 
@@ -137,6 +147,9 @@ class DistributedDataParallel(nn.Module):
         self._next_launch = 0
         self._callback_queued = False
         self._hooks = []
+        from ..ops.multi_tensor import TableCache
+
+        self._tables = TableCache()  # multi-tensor pack tables, one per bucket and dtype pair
         if self.world > 1 or (buckets_at_world_1 and self.comm is not None):
             if self.world > 1:
                 _flat_broadcast([p.data for p in module.parameters()] + list(module.buffers()), 0, process_group)
@@ -191,34 +204,54 @@ class DistributedDataParallel(nn.Module):
         # forward op that consumed it — where the gradient was produced)
         if not self._sync or p.grad is None:
             return
-        _flush_wgrad()  # a deferred weight-gradient reduce may still owe this gradient its values
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
         b, i = self._where[p]
         if b.got[i]:
             return
-        off, n = b.offsets[i], p.numel()
-        slot = _param_view(b.buf[off : off + n], p)
-        g = p.grad
-        if g.data_ptr() != slot.data_ptr():  # else AccumulateGrad already summed into the slot
-            with torch.no_grad():
-                if g.is_cuda and _streams.pending(g.device):
-                    # the gradient may still be in flight on the weight-gradient side stream: pack
-                    # it there (the bucket's all-reduce joins that stream first)
-                    side = _streams.side_stream(g.device)
-                    side.wait_stream(torch.cuda.current_stream(g.device))  # g may be a main-stream result
-                    with torch.cuda.stream(side):
-                        slot.copy_(g)
-                    g.record_stream(side)
-                else:
-                    slot.copy_(g)  # pack (+ up-convert into an fp32 bucket); the all-reduce averages
-        if slot.dtype != p.dtype:
-            p.grad = None  # consumed: the optimizer reads p.main_grad; the next backward steals
         b.got[i] = True
         b.ready += 1
-        if b.ready == len(b.params) and not self.defer_allreduce:
-            self._launch_ready()
+        if b.ready == len(b.params):
+            self._pack(b)
+            if not self.defer_allreduce:
+                self._launch_ready()
+
+    def _pack(self, b: _Bucket) -> None:
+        """Copy (+ up-convert) a complete bucket's gradients into its slots: one multi-tensor
+        launch per (gradient dtype, bucket dtype) pair instead of one copy kernel per parameter.
+        Gradients wait in ``p.grad`` until their bucket is complete; a deferred weight-gradient
+        reduce (or a parked weight gradient, ops/conv.py) may still owe the LAST of them its values,
+        so the one flush happens here, before the pack reads them."""
+        _flush_wgrad()
+        dev = b.buf.device
+        if b.buf.is_cuda:
+            _streams.join(dev)  # gradients produced on the weight-gradient side stream
+        groups: Dict[Tuple[torch.dtype, torch.dtype], Tuple[List[torch.Tensor], List[torch.Tensor]]] = {}
+        with torch.no_grad():
+            for i, p in enumerate(b.params):
+                g = p.grad
+                if g is None or not b.got[i]:  # an unused parameter: _finalize zero-fills its slot
+                    continue
+                off, n = b.offsets[i], p.numel()
+                slot = _param_view(b.buf[off : off + n], p)
+                if g.data_ptr() == slot.data_ptr():  # AccumulateGrad already summed into the slot
+                    continue
+                if (b.buf.is_cuda and _mt_ok(g, slot)):
+                    srcs, dsts = groups.setdefault((g.dtype, slot.dtype), ([], []))
+                    srcs.append(g)
+                    dsts.append(slot)
+                else:
+                    slot.copy_(g)  # pack (+ up-convert into an fp32 bucket); the all-reduce averages
+            for (sdt, ddt), (srcs, dsts) in groups.items():
+                tab = self._tables.get(f"pack{b.index}_{sdt}_{ddt}", [srcs, dsts])
+                from ..ops import _native
+
+                _native.native().copy_mt(tab.ptrs, tab.sizes, tab.blocks, tab.T, tab.chunk,
+                                         _native.DTYPE_CODE[sdt], _native.DTYPE_CODE[ddt])
+            for p in b.params:
+                if p.grad is not None and b.buf.dtype != p.dtype:
+                    p.grad = None  # consumed: the optimizer reads p.main_grad; the next backward steals
 
     def _launch_ready(self) -> None:
         while self._next_launch < len(self._buckets):
@@ -252,6 +285,7 @@ class DistributedDataParallel(nn.Module):
         # parameters that got no gradient this step contribute zeros (find_unused_parameters)
         for b in self._buckets[self._next_launch :]:
             if b.ready < len(b.params):
+                self._pack(b)  # the gradients that did arrive
                 with torch.no_grad():
                     for i, (p, off) in enumerate(zip(b.params, b.offsets)):
                         if not b.got[i]:

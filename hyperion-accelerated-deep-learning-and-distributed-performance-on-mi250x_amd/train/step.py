@@ -64,7 +64,18 @@ class TrainStep:
         warmup_iters: int = 3,
         scaler=None,
         split_backward: bool = True,
+        ddp_schedule: str = "auto",
     ):
+        """``ddp_schedule`` (a bucketed Hyperion DDP model, graph mode): ``"auto"`` = three graphs
+        (top forward+backward | bottom backward overlapping the top buckets' all-reduce | optimizer)
+        when the model exposes ``graph_stages``, else two graphs around the all-reduces;
+        ``"segmented"`` = the whole step captured as segments with every bucket's all-reduce issue
+        and wait as eager holes (``train/segments.py``): each bucket overlaps the rest of the
+        captured backward, at the cost of one graph launch per hole."""
+        if ddp_schedule not in ("auto", "segmented"):
+            raise ValueError(f"ddp_schedule {ddp_schedule!r}")
+        self.ddp_schedule = ddp_schedule
+        self.seg = None
         self.model = model
         self.opt = optimizer
         self.loss_fn = loss_fn
@@ -222,6 +233,13 @@ class TrainStep:
 
     def _capture_graphs(self) -> None:
         ddp = self._ddp()
+        if ddp is not None and self.ddp_schedule == "segmented":
+            from .segments import SegmentedGraph
+
+            seg = SegmentedGraph()
+            self.static_loss = seg.capture(lambda: self._body(self.static_x, self.static_y))
+            self.seg, self.graph = seg, seg.graphs[0]
+            return
         stages = self._stages()
         if ddp is not None and stages is not None:  # three graphs: top fwd+bwd | bottom bwd | optimizer
             g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -260,12 +278,18 @@ class TrainStep:
         if self.graph is None:
             ddp = self._ddp()
             if ddp is not None:
-                ddp.defer_allreduce = True  # warm-up and replays: all-reduce between the graphs
+                # graph schedules: the all-reduces run between the graphs; segmented: from the
+                # bucket hooks, as holes of the capture
+                ddp.defer_allreduce = self.ddp_schedule != "segmented"
             self._capture(x, y)
         if x.data_ptr() != self.static_x.data_ptr():
             self.static_x.copy_(x, non_blocking=True)
         if y.data_ptr() != self.static_y.data_ptr():
             self.static_y.copy_(y, non_blocking=True)
+        if self.seg is not None:
+            self.seg.replay()
+            self._counters.replayed()
+            return self.static_loss
         self.graph.replay()
         self._counters.replayed()
         if self.graph3 is not None:

@@ -124,7 +124,7 @@ def test_ddp_graph_step_grads_match_eager(split, native):
         dist.destroy_process_group()
 
 
-def _two_rank_graph(rank, world, steps):
+def _two_rank_graph(rank, world, steps, schedule="auto"):
     os.environ["HYPERION_COMM"] = "torch"  # gloo collectives between the two processes
     torch.cuda.set_device(0)
     _pin_deterministic()
@@ -143,11 +143,12 @@ def _two_rank_graph(rank, world, steps):
         opt = FusedAdam(ddp.parameters(), lr=1e-3, zero_grad_in_step=True)
         losses = []
         if mode == "graph":
-            st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=True, warmup_iters=1)
+            st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=True, warmup_iters=1,
+                           ddp_schedule=schedule)
             losses.append(float(st(xs[0], ys[0])))  # warm-up step + capture + replay: step 0 twice
             for i in range(1, steps):
                 losses.append(float(st(xs[i], ys[i])))
-            graphs = st.graph3 is not None
+            graphs = st.graph3 is not None if schedule == "auto" else st.seg is not None
         else:
             ddp.defer_allreduce = True
             st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=False)
@@ -161,8 +162,11 @@ def _two_rank_graph(rank, world, steps):
     return res
 
 
-def test_two_rank_gloo_three_graph_step_replicas_identical():
-    res = run_world(_two_rank_graph, 2, (4,), timeout=600)
+@pytest.mark.parametrize("schedule", ["auto", "segmented"])
+def test_two_rank_gloo_graph_step_replicas_identical(schedule):
+    """auto: the three-graph split; segmented: bench.py's N>1 default (graph segments with the
+    bucket all-reduces as eager holes)."""
+    res = run_world(_two_rank_graph, 2, (4, schedule), timeout=600)
     assert res[0]["graph"]["graph3"] and res[1]["graph"]["graph3"]
     for a, b in zip(res[0]["graph"]["params"], res[1]["graph"]["params"]):
         assert torch.equal(a, b)  # replicas bit-identical after captured steps
@@ -171,3 +175,53 @@ def test_two_rank_gloo_three_graph_step_replicas_identical():
         assert all(torch.equal(g["before"][k], e["before"][k]) for k in g["before"])
         assert_losses_match(g["losses"], e["losses"], rtol=1e-2, what=f"rank {r}")
         assert_update_parity(e["before"], g["after"], e["after"], rel=2e-2, what=f"rank {r}")
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_ddp_segmented_schedule_matches_eager(native):
+    """``TrainStep(ddp_schedule="segmented")``: the whole step captured as graph segments with the
+    bucket all-reduces as eager holes (bench.py --ddp-schedule segmented).  Per-step losses and the
+    parameter update over 4 steps equal the eager DDP step from the same start."""
+    import torch.distributed as dist
+
+    from hyperion.ops.optim import FusedAdam
+    from hyperion.parallel import DDP
+    from hyperion.train.step import TrainStep
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    prev = _pin_deterministic()
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        g = torch.Generator(device="cuda").manual_seed(3)
+        xs = [torch.rand(16, 3, 32, 32, device="cuda", generator=g).bfloat16().contiguous(
+            memory_format=torch.channels_last) for _ in range(4)]
+        ys = [torch.rand(16, 10, device="cuda", generator=g) for _ in range(4)]
+        res = {}
+        for mode in ("segmented", "eager"):
+            comm = None
+            if native:
+                from hyperion.parallel.comm import NativeComm
+
+                comm = NativeComm(torch.device("cuda", 0))
+            ddp = DDP(_make(), bucket_cap_mb=2.0, first_bucket_mb=0.5, broadcast_buffers=False,
+                      buckets_at_world_1=True, comm=comm)
+            before = snapshot(ddp.module.named_parameters())
+            opt = FusedAdam(ddp.parameters(), lr=1e-3, zero_grad_in_step=mode == "segmented")
+            st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=mode == "segmented",
+                           warmup_iters=1, ddp_schedule="segmented")
+            losses = [float(st(xs[0], ys[0]))]  # graph mode: warm-up step + capture + replay = step 0 twice
+            if mode == "eager":
+                losses = [float(st(xs[0], ys[0]))]
+            for i in range(1, 4):
+                losses.append(float(st(xs[i], ys[i])))
+            torch.cuda.synchronize()
+            if mode == "segmented":
+                assert st.seg is not None and st.seg.num_segments > len(ddp.bucket_sizes())  # holes per bucket
+            res[mode] = (before, snapshot(ddp.module.named_parameters()), losses)
+        (b0, a_seg, l_seg), (b1, a_eag, l_eag) = res["segmented"], res["eager"]
+        assert all(torch.equal(b0[k], b1[k]) for k in b0)
+        assert_losses_match(l_seg, l_eag, rtol=1e-2, what="segmented vs eager")
+        assert_update_parity(b1, a_seg, a_eag, rel=2e-2, what="segmented vs eager")
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+        dist.destroy_process_group()
