@@ -139,6 +139,7 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step(x, y)
+    host_s = time.perf_counter() - t0  # launch-side time of the timed loop (before the final sync)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     if n_gpus > 1:
@@ -204,6 +205,8 @@ def main(argv=None) -> int:
             },
             "baseline": {"value": BASELINE_SAMPLES_PER_S, "ms_per_step": 56.32, "hw": "1x MI250X GCD, fp32"},
             "final_loss": round(final_loss, 6),
+            # host time per step issuing the timed loop: close to ms_per_step means launch-bound
+            "host_ms_per_step": round(host_s / args.steps * 1e3, 3),
         }
         if replicas is not None:
             rec["replicas"] = replicas

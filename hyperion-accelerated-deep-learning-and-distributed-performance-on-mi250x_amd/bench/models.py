@@ -209,7 +209,8 @@ def _ensure_pg() -> None:
 
 def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps: int = 10, warmup: int = 3,
                     graph: bool = False, replicate_frozen="auto", persistent=None,
-                    collectives_at_world_1: bool = False, loss_curve: bool = False, lr: float = 1e-4) -> Dict:
+                    collectives_at_world_1: bool = False, loss_curve: bool = False, lr: float = 1e-4,
+                    ring: int = 0) -> Dict:
     """One FSDP FULL_SHARD training step exactly as the FSDP trainers run it (C25 / BASELINE config
     4 / C26): Hyperion's FSDP over the native RCCL communicator, bf16 mixed precision (param /
     reduce / buffer), FusedAdamW, global-norm clip 1.0.  ``model``: ``lm256`` (size-based wrap,
@@ -217,7 +218,8 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
     one unit per decoder layer, frozen base weights sharded too).  World size = the launcher's
     (1 on a single GPU: the gathers / reduce-scatters are then identity collectives, but every
     flat-buffer pack, cast and hook runs).  ``graph=True``: the step is captured once as graph
-    segments with the collectives as eager holes (``train/segments.py``; persistent FSDP buffers)."""
+    segments with the collectives as eager holes (``train/segments.py``; persistent FSDP buffers, or
+    with ``ring`` >= 2 the FULL_SHARD ring of fixed-address gathered-unit slots)."""
     import torch.distributed as dist
 
     from ..data.synthetic import SyntheticWikiText2
@@ -249,7 +251,8 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
         vocab = 50257
     m = FSDP(base, auto_wrap_policy=policy, device_id=dev, mixed_precision=MixedPrecision(bf, bf, bf),
              replicate_frozen=replicate_frozen if model == "llama7b_lora" else False,
-             persistent=True if graph else persistent, collectives_at_world_1=collectives_at_world_1)
+             persistent=(True if graph and not ring else persistent), collectives_at_world_1=collectives_at_world_1,
+             ring=ring)
     params = [p for p in m.parameters() if p.requires_grad]
     opt = FusedAdam(params, lr=lr, weight_decay=0.01, adamw=True)
     ds = SyntheticWikiText2(n=batch, seq_len=seq, seed=dist.get_rank())
@@ -290,6 +293,7 @@ def bench_fsdp_step(model: str = "lm256", batch: int = 32, seq: int = 128, steps
     world = dist.get_world_size()
     tok = batch * (seq if model.startswith("llama7b") else seq - 1)
     return {"model": model, "fsdp": True, "world": world, "graph": graph, "persistent": m.persistent,
+            "ring": m.ring, "memory_plan": m.memory_plan(),
             "persistent_reason": m.persistent_reason, "collectives_at_world_1": collectives_at_world_1,
             "comm": type(m.comm).__name__,
             "replicate_frozen": m.replicate_frozen,

@@ -174,6 +174,8 @@ struct GemmTiledArgs {
   RngState drng{};
 };
 void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits);
+// split-K reduce in the last-arriving workgroup of each tile (1, default) or a separate kernel (0)
+void gemm_set_splitk_inkernel(int on);
 int gemm_tiled_splits(const GemmTiledArgs& a);
 hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st);
 }  // namespace hyp

@@ -29,6 +29,8 @@
 //    +residual, rounding to the output dtype.
 // Out-of-range rows/columns read clamped (discarded) or the zero page; the reduction tail reads
 // the zero page, so any K % 8 == 0 works.
+#include <mutex>
+
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 #include "mfma_lds.h"
@@ -270,6 +272,7 @@ struct GemmP {
   const uint16_t* B;
   const uint16_t* zero;
   float* part;  // split-K slabs [splits][M][N] fp32 (null: epilogue in-kernel)
+  unsigned* cnt;  // split-K arrival counters, one per tile (null: gemm_splitk_epi_k reduces)
   Epi e;
   int M, N, K, lda, ldb, kper, splits;
   int64_t a_ext, b_ext;  // operand extents in elements from their bases (debug-build bounds checks)
@@ -458,11 +461,48 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
       const float4 q = *reinterpret_cast<const float4*>(patch + rr * kRS + cc);
       v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
       if (row < p.M && col < p.N) {
-        if (p.part != nullptr) st4<float>(p.part + ((int64_t)z * p.M + row) * p.N + col, v);
-        else epi4<OutT>(p.e, row, col, v);
+        if (p.part == nullptr) epi4<OutT>(p.e, row, col, v);
+        else if (p.cnt != nullptr) st16_wt(p.part + ((int64_t)z * p.M + row) * p.N + col, __builtin_bit_cast(uint4, q));
+        else st4<float>(p.part + ((int64_t)z * p.M + row) * p.N + col, v);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // patch reads retired before the next half overwrites it
+  }
+  if (p.part == nullptr || p.cnt == nullptr) return;
+
+  // ---- split-K, last arriver reduces (no gemm_splitk_epi_k launch): every slice stored its slab
+  // write-through (sc1) and drained it; one lane per workgroup counts the tile's arrivals with an
+  // agent-scope atomic; the workgroup whose add returns splits - 1 takes an agent-scope acquire,
+  // resets the counter for the next launch, and sums the slabs in slice order z = 0 .. splits-1
+  // (the same order as the separate reduce: bitwise-identical results) into the fused epilogue.
+  // (MI355X_MICROARCH § visibility, Valid forms, producer row 1 with the acquire kept.)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(p.splits - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (*flag == 0) return;
+  constexpr int kQ = BN / 4;  // column quads per tile row
+  const int64_t slab = (int64_t)p.M * p.N;
+  for (int idx = tid; idx < BM * kQ; idx += NW * 64) {
+    const int row = m0 + idx / kQ, col = n0 + (idx % kQ) * 4;
+    if (row >= p.M || col >= p.N) continue;
+    const float* src = p.part + (int64_t)row * p.N + col;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int zz = 0; zz < p.splits; ++zz) {
+      const float4 q = *reinterpret_cast<const float4*>(src + zz * slab);
+      v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+    }
+    epi4<OutT>(p.e, row, col, v);
   }
 }
 
@@ -520,7 +560,51 @@ hipError_t launch_tile(const GemmP& p, bool atr, bool btr, int tile, int nwg, hi
   }
 }
 
+// Split-K arrival counters: one hipMalloc'd, zeroed pool per device (the last arriver of a tile
+// resets its counter, so a range is reusable by the next launch in stream order).  Eager launches
+// cycle through the first kEagerRing counters (a range is reused only ~kEagerRing / tiles
+// launches later); launches under hipGraph capture take never-reused ranges after it (the graph
+// replays them), and fall back to the separate reduce kernel when that region is exhausted or
+// the pool does not exist yet (no hipMalloc inside a capture).
+constexpr int64_t kEagerRing = 1 << 20, kCntTotal = 1 << 22;
+struct CntPool {
+  unsigned* base = nullptr;
+  int64_t eager_next = 0, cap_next = kEagerRing;
+};
+std::mutex g_cnt_mu;
+CntPool g_cnt[64];
+
+unsigned* splitk_counters(int ntiles, hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || ntiles <= 0 || ntiles > kEagerRing / 8) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_cnt_mu);
+  CntPool& c = g_cnt[dev];
+  if (c.base == nullptr) {
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
+    void* b = nullptr;
+    if (hipMalloc(&b, kCntTotal * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(b, 0, kCntTotal * sizeof(unsigned)) != hipSuccess) return nullptr;
+    c.base = static_cast<unsigned*>(b);
+  }
+  if (cs == hipStreamCaptureStatusNone) {
+    if (c.eager_next + ntiles > kEagerRing) c.eager_next = 0;
+    unsigned* r = c.base + c.eager_next;
+    c.eager_next += ntiles;
+    return r;
+  }
+  if (c.cap_next + ntiles > kCntTotal) return nullptr;
+  unsigned* r = c.base + c.cap_next;
+  c.cap_next += ntiles;
+  return r;
+}
+
+int g_splitk_inkernel = 1;  // gemm_set_splitk_inkernel (A/B)
+
 }  // namespace
+
+void gemm_set_splitk_inkernel(int on) { g_splitk_inkernel = on; }
 
 void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits) {
   const int cus = 256;
@@ -579,6 +663,7 @@ hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st) {
   p.B = static_cast<const uint16_t*>(a.B);
   p.zero = static_cast<const uint16_t*>(a.zero);
   p.part = splits > 1 ? a.part : nullptr;
+  p.cnt = nullptr;
   p.e = Epi{a.C, a.aux, a.bias, a.R, a.alpha, a.beta, a.ldc, a.ldr, a.act, a.bias_dtype, 0u, 0.f, a.drng};
   if (a.drop_p > 0.f) {
     if (a.act == 0 || a.R != nullptr || a.drop_p >= 1.f) return hipErrorInvalidValue;
@@ -595,14 +680,16 @@ hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st) {
   p.a_ext = a.a_tr ? (int64_t)(a.K - 1) * a.lda + a.M : (int64_t)(a.M - 1) * a.lda + a.K;
   p.b_ext = a.b_tr ? (int64_t)(a.K - 1) * a.ldb + a.N : (int64_t)(a.N - 1) * a.ldb + a.K;
   const TileCfg& c = kTiles[tile];
-  const int nwg = ((a.M + c.bm - 1) / c.bm) * ((a.N + c.bn - 1) / c.bn) * splits;
+  const int ntiles = ((a.M + c.bm - 1) / c.bm) * ((a.N + c.bn - 1) / c.bn);
+  const int nwg = ntiles * splits;
+  if (splits > 1 && g_splitk_inkernel) p.cnt = splitk_counters(ntiles, st);
   hipError_t err;
   if (a.in_dtype == kBF16) {
     HYP_DISPATCH_FLOAT(a.out_dtype, TO, { err = launch_tile<bf16_t, TO>(p, a.a_tr, a.b_tr, tile, nwg, st); });
   } else {
     HYP_DISPATCH_FLOAT(a.out_dtype, TO, { err = launch_tile<f16_t, TO>(p, a.a_tr, a.b_tr, tile, nwg, st); });
   }
-  if (err != hipSuccess || splits == 1) return err;
+  if (err != hipSuccess || splits == 1 || p.cnt != nullptr) return err;
   const int64_t n4 = (int64_t)a.M * a.N / 4;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
   HYP_DISPATCH_FLOAT(a.out_dtype, TO, {

@@ -51,6 +51,8 @@ def _load():
         _MOD.ws_set_depth(int(os.environ["HYPERION_WS_DEPTH"]))  # weight-streaming k-steps in flight (A/B)
     if _MOD is not None and os.environ.get("HYPERION_CONV_PERSIST") and hasattr(_MOD, "conv_set_persist"):
         _MOD.conv_set_persist(int(os.environ["HYPERION_CONV_PERSIST"]))  # persistent fwd/dgrad convs (A/B)
+    if _MOD is not None and os.environ.get("HYPERION_SPLITK_INKERNEL") and hasattr(_MOD, "gemm_set_splitk_inkernel"):
+        _MOD.gemm_set_splitk_inkernel(int(os.environ["HYPERION_SPLITK_INKERNEL"]))  # 0: separate reduce (A/B)
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")

@@ -121,7 +121,9 @@ class FusedAdam(torch.optim.Optimizer):
                 vs = [s["exp_avg_sq"] for s in sts]
                 masters = [s["master"] for s in sts] if pdt != torch.float32 else None
                 ok = native and pdt in _native.DTYPE_CODE and gdt in _native.DTYPE_CODE and all(
-                    _dense(p) and _dense(g) and _same_layout(p, g) and _same_layout(p, m) for p, g, m in zip(ps, gs, ms)
+                    (g.stride() == p.stride() and m.stride() == p.stride() and p.is_contiguous())  # fast path
+                    or (_dense(p) and _dense(g) and _same_layout(p, g) and _same_layout(p, m))
+                    for p, g, m in zip(ps, gs, ms)
                 )
                 if ok:
                     groups = [ps, gs, ms, vs] + ([masters] if masters is not None else [])

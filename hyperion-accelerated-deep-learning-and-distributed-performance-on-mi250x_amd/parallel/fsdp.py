@@ -131,10 +131,26 @@ class _SlotWork:
         _seg.eager(lambda: slot[0].wait())
 
 
+class _Ring:
+    """K fixed-address buffers shared by the units' gathered parameters (or full gradients) in
+    ring mode: unit i lives in slot i % K while it is gathered, so memory is K x the largest unit
+    (FULL_SHARD's reshard-after-forward bound) and every address is fixed — the step stays
+    capturable as graph segments.  ``owner[k]``: the group whose data slot k holds."""
+
+    def __init__(self, k: int, numel: int, dtype: torch.dtype, device: torch.device):
+        self.bufs = [torch.empty(numel, dtype=dtype, device=device) for _ in range(k)]
+        self.owner: List[Optional["_FlatGroup"]] = [None] * k
+
+    @property
+    def nbytes(self) -> int:
+        return sum(b.numel() * b.element_size() for b in self.bufs)
+
+
 class _FlatGroup:
     """One flat parameter: the trainable (fp32 master shard) or frozen (param-dtype shard) params of a unit."""
 
-    def __init__(self, fsdp: "FullyShardedDataParallel", params: List[nn.Parameter], trainable: bool, tag: str):
+    def __init__(self, fsdp: "FullyShardedDataParallel", params: List[nn.Parameter], trainable: bool, tag: str,
+                 ring_member: bool = False):
         self.fsdp = fsdp
         self.tag = tag
         self.trainable = trainable
@@ -165,9 +181,19 @@ class _FlatGroup:
                 flat[o : o + n].copy_(p.detach().reshape(-1))
             shard = flat[r * self.shard_numel : (r + 1) * self.shard_numel].clone()
         self.flat_param = nn.Parameter(shard, requires_grad=trainable)
-        self.full = self.flat_param.data if self.resident else torch.empty(self.padded, dtype=self.cdtype, device=dev)
+        # ring mode: the gathered parameters / full gradient are views of a shared ring slot,
+        # attached after every unit exists (attach_ring); nothing of their own is allocated
+        self.ring: Optional[_Ring] = None
+        self.grad_ring: Optional[_Ring] = None
+        self.slot = -1
+        self.ring_member = ring_member and not self.resident
+        if self.ring_member:
+            self.full = torch.empty(0, dtype=self.cdtype, device=dev)
+            self.full_grad = torch.empty(0, dtype=self.rdtype, device=dev) if trainable else None
+        else:
+            self.full = self.flat_param.data if self.resident else torch.empty(self.padded, dtype=self.cdtype, device=dev)
+            self.full_grad = torch.empty(self.padded, dtype=self.rdtype, device=dev) if trainable else None
         self._full_bytes = self.full.untyped_storage().nbytes()
-        self.full_grad = torch.empty(self.padded, dtype=self.rdtype, device=dev) if trainable else None
         self._grad_bytes = self.full_grad.untyped_storage().nbytes() if trainable else 0
         self.gathered = True
         self.gather_work = None
@@ -186,6 +212,9 @@ class _FlatGroup:
         self.grad_ready: Set[int] = set()
         self._pending: List[Tuple[int, torch.Tensor]] = []  # (param index, grad) not yet in full_grad
         self.reduced = False
+        if self.ring_member:
+            self.gathered = False
+            return
         # module parameters become views of the full buffer (the same Parameter objects)
         for p, o, n, shp in zip(params, self.offsets, self.numels, self.shapes):
             p.data = self.full[o : o + n].view(shp)
@@ -200,8 +229,25 @@ class _FlatGroup:
                 self.full_grad.untyped_storage().resize_(0)
 
     # -- storage ------------------------------------------------------------------------
+    def attach_ring(self, ring: _Ring, grad_ring: Optional[_Ring], slot: int) -> None:
+        """Ring mode: this group's full parameters (and full gradient) are views of slot ``slot``."""
+        self.ring, self.grad_ring, self.slot = ring, grad_ring, slot
+        self.full = ring.bufs[slot][: self.padded]
+        self._full_bytes = self.full.untyped_storage().nbytes()
+        for p, o, n, shp in zip(self.params, self.offsets, self.numels, self.shapes):
+            p.data = self.full[o : o + n].view(shp)
+        if self.trainable:
+            self.full_grad = grad_ring.bufs[slot][: self.padded]
+            self._grad_bytes = self.full_grad.untyped_storage().nbytes()
+        self.gathered = False
+
+    def holds_slot(self) -> bool:
+        return self.ring is not None and self.ring.owner[self.slot] is self
+
     def free_full(self) -> None:
-        if self.resident or self.fsdp.persistent:  # persistent: the storage stays, the content stays valid
+        if self.resident or self.fsdp.persistent or self.ring_member:
+            # persistent: the storage stays, the content stays valid; ring: the slot is overwritten
+            # by the unit that takes it next (no release, no re-allocation: fixed addresses)
             return
         if self.gather_work is not None:
             self.wait_gather()
@@ -210,6 +256,14 @@ class _FlatGroup:
             self.gathered = False
 
     def gather(self, async_op: bool = False) -> None:
+        if self.ring is not None:
+            prev = self.ring.owner[self.slot]
+            if prev is not self:
+                if prev is not None:  # evict: its later use re-gathers (same comm stream: ours lands last)
+                    prev.gathered = False
+                    prev.gather_work = None
+                self.ring.owner[self.slot] = self
+                self.gathered = False
         if self.resident or self.gathered or self.gather_work is not None:
             return
         st = self.full.untyped_storage()
@@ -242,6 +296,17 @@ class _FlatGroup:
 
     # -- gradients ------------------------------------------------------------------------
     def _grad_buf(self) -> torch.Tensor:
+        if self.grad_ring is not None:
+            occ = self.grad_ring.owner[self.slot]
+            if occ is not self:
+                if occ is not None and occ.rs_work is not None:
+                    occ.rs_work.wait()  # its reduce-scatter still reads the slot (stream-ordered wait)
+                    occ.rs_work = None
+                self.grad_ring.owner[self.slot] = self
+                if self.padded > self.numel:  # the previous occupant's bytes would enter the clip norm
+                    with torch.no_grad():
+                        self.full_grad.data[self.numel :].zero_()
+            return self.full_grad.data
         st = self.full_grad.untyped_storage()
         if st.nbytes() != self._grad_bytes:
             st.resize_(self._grad_bytes)
@@ -294,6 +359,11 @@ class _FlatGroup:
             if i not in self.grad_ready:  # unused this step: contributes zeros
                 buf[o : o + n].zero_()
         if self.fsdp.identity:
+            if self.grad_ring is not None:  # the slot is reused by a later unit: take the shard now
+                with torch.no_grad():
+                    self._grad_shard.copy_(buf[: self.shard_numel])
+                self.rs_out, self.rs_work = self._grad_shard, None
+                return
             self.rs_out, self.rs_work = buf, None
             return
         # AVG in RCCL; the output lands in a persistent buffer — straight in the fp32 shard
@@ -322,22 +392,23 @@ class _FlatGroup:
             else:
                 self.flat_param.grad.add_(g)
         self.rs_out = None
-        if not self.fsdp.persistent:
+        if not self.fsdp.persistent and self.grad_ring is None:
             self.full_grad.untyped_storage().resize_(0)
 
 
 class _Unit:
     """A wrapped module: its frozen and trainable parameter groups are gathered/released together."""
 
-    def __init__(self, fsdp: "FullyShardedDataParallel", module: nn.Module, params: List[nn.Parameter], index: int):
+    def __init__(self, fsdp: "FullyShardedDataParallel", module: nn.Module, params: List[nn.Parameter], index: int,
+                 ring_member: bool = False):
         self.fsdp = fsdp
         self.module = module
         self.index = index
         self.params = params
         train = [p for p in params if p.requires_grad]
         frozen = [p for p in params if not p.requires_grad]
-        self.train = _FlatGroup(fsdp, train, True, f"u{index}t") if train else None
-        self.frozen = _FlatGroup(fsdp, frozen, False, f"u{index}f") if frozen else None
+        self.train = _FlatGroup(fsdp, train, True, f"u{index}t", ring_member) if train else None
+        self.frozen = _FlatGroup(fsdp, frozen, False, f"u{index}f", ring_member) if frozen else None
         self.groups = [g for g in (self.frozen, self.train) if g is not None]
         self._pidx = {id(p): i for i, p in enumerate(train)}
 
@@ -354,6 +425,13 @@ class _Unit:
     def wait_gather(self) -> None:
         for g in self.groups:
             g.wait_gather()
+
+    def ring_slot_busy(self, active: Optional["_Unit"]) -> bool:
+        """A prefetch of this unit would overwrite the ring slot the ACTIVE unit computes from."""
+        if active is None or active is self:
+            return False
+        return any(g.ring is not None and g.ring.owner[g.slot] is not None and g.ring.owner[g.slot] in active.groups
+                   for g in self.groups)
 
     def reshard(self) -> None:
         for g in self.groups:
@@ -406,10 +484,17 @@ class FullyShardedDataParallel(nn.Module):
         replicate_frozen=False,
         persistent=None,
         collectives_at_world_1: bool = False,
+        ring: int = 0,
     ):
         """collectives_at_world_1: on a single rank, still run every gather / reduce-scatter as a
         collective (the native RCCL communicator on GPU) instead of the identity copies — the
-        multi-GPU transport path, exercised and timed on one device."""
+        multi-GPU transport path, exercised and timed on one device.
+
+        ring (FULL_SHARD, >= 2): the wrapped units' gathered parameters and full gradients live in
+        a ring of ``ring`` fixed-address slots (unit i in slot i % ring) instead of being freed and
+        re-allocated: reshard-after-forward memory (ring x the largest unit, not every unit) with
+        the fixed addresses a captured step needs.  A unit keeps its slot until another unit takes
+        it, so the last units of the forward are still gathered when the backward starts."""
         super().__init__()
         if sharding_strategy not in ("FULL_SHARD", "SHARD_GRAD_OP"):
             raise ValueError("sharding_strategy must be FULL_SHARD or SHARD_GRAD_OP (NO_SHARD = use DDP)")
@@ -466,6 +551,17 @@ class FullyShardedDataParallel(nn.Module):
             else:
                 persistent = False
                 self.persistent_reason = "auto: not a GPU device"
+        if (not ring and persistent in (None, "auto") and sharding_strategy == "FULL_SHARD" and self.world > 1
+                and self.device.type == "cuda"):
+            # FULL_SHARD across ranks: the ring keeps the real reshard-after-forward memory bound
+            # (3 units' worth, not the whole model on every rank) and a capturable step
+            ring = 3
+        self.ring = int(ring) if ring and sharding_strategy == "FULL_SHARD" else 0
+        if self.ring == 1:
+            raise ValueError("FSDP ring needs >= 2 slots (a unit and the one being prefetched)")
+        if self.ring:
+            persistent = False
+            self.persistent_reason = f"ring of {self.ring} gathered-unit slots"
         self.persistent = bool(persistent)
         self.sharding = sharding_strategy
         self.reshard_after_forward = sharding_strategy == "FULL_SHARD" and not self.persistent
@@ -491,8 +587,13 @@ class FullyShardedDataParallel(nn.Module):
                 if id(p) not in claimed:
                     claimed.add(id(p))
                     params.append(p)
-            self.units.append(_Unit(self, um, params, len(self.units)))
+            # the root unit (embeddings, head) stays gathered for the whole step: never in the ring
+            self.units.append(_Unit(self, um, params, len(self.units), ring_member=bool(self.ring) and um is not module))
         self.root_unit = self.units[-1]
+        self._rings: Dict[str, _Ring] = {}
+        if self.ring:
+            self._build_rings()
+        self._active: Optional[_Unit] = None
         self._unit_of_param = {id(p): u for u in self.units for p in u.params}
         self._fwd_order: List[_Unit] = []
         self._recording = True
@@ -505,6 +606,35 @@ class FullyShardedDataParallel(nn.Module):
             for p in u.params:
                 if p.requires_grad:
                     self._handles.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
+
+    def _build_rings(self) -> None:
+        """One parameter ring per (kind, dtype) and one gradient ring, each slot sized to the
+        largest member; unit i (module order = forward order for stacked layers) takes slot i % K."""
+        members = [u for u in self.units if u is not self.root_unit]
+        for kind in ("train", "frozen"):
+            groups = [getattr(u, kind) for u in members if getattr(u, kind) is not None]
+            groups = [g for g in groups if g.ring_member]
+            if not groups:
+                continue
+            pr = _Ring(self.ring, max(g.padded for g in groups), groups[0].cdtype, self.device)
+            gr = (_Ring(self.ring, max(g.padded for g in groups), groups[0].rdtype, self.device)
+                  if kind == "train" else None)
+            self._rings[kind] = pr
+            if gr is not None:
+                self._rings["grad"] = gr
+            for i, g in enumerate(groups):
+                g.attach_ring(pr, gr, i % self.ring)
+
+    def memory_plan(self) -> Dict[str, float]:
+        """GiB of gathered-parameter / full-gradient buffers this configuration keeps allocated."""
+        gib = 2.0 ** 30
+        if self.ring:
+            ring = sum(r.nbytes for r in self._rings.values())
+            root = sum(g._full_bytes + g._grad_bytes for g in self.root_unit.groups if not g.resident)
+            return {"mode": f"ring{self.ring}", "gathered_gib": (ring + root) / gib}
+        tot = sum(g.padded * (g.full.element_size() + (g.full_grad.element_size() if g.trainable else 0))
+                  for g in self.flat_groups() if not g.resident)
+        return {"mode": "persistent" if self.persistent else "reshard (peak: the units in flight)", "gathered_gib": tot / gib}
 
     @property
     def comm(self):
@@ -536,10 +666,11 @@ class FullyShardedDataParallel(nn.Module):
                     torch.autograd.graph.register_multi_grad_hook(ins, lambda grads: self._input_grads(u), mode="all")
             if self._recording and u not in self._fwd_order:
                 self._fwd_order.append(u)
+            self._active = u
             u.gather()
             if self.forward_prefetch and not self._recording:
                 nxt = self._neighbour(u, +1)
-                if nxt is not None:
+                if nxt is not None and not nxt.ring_slot_busy(u):
                     nxt.gather(async_op=True)
             return None
 
@@ -568,10 +699,11 @@ class FullyShardedDataParallel(nn.Module):
         def hook(grad):
             with self._on_compute_stream():
                 self._ensure_backward_started()
+                self._active = u
                 u.gather()
                 if self.backward_prefetch:
                     prv = self._neighbour(u, -1)
-                    if prv is not None and not prv.reduced:
+                    if prv is not None and not prv.reduced and not prv.ring_slot_busy(u):
                         prv.gather(async_op=True)
 
         return hook
@@ -613,15 +745,16 @@ class FullyShardedDataParallel(nn.Module):
                 if not g.trainable:
                     continue  # frozen weights never change: a persistent gathered copy stays valid
                 g.send_valid = False  # the optimizer steps next: recast on the next forward gather
-                if self.persistent and not g.resident:
+                if (self.persistent or g.ring_member) and not g.resident:
                     g.gathered = False  # ... and re-gather (the persistent buffer keeps its storage)
         self._in_backward = False
+        self._active = None
 
     def invalidate_gather_cache(self) -> None:
         """Call after changing the flat shards outside an optimizer step that follows backward."""
         for g in self.flat_groups():
             g.send_valid = False
-            if self.persistent and not g.resident:
+            if (self.persistent or g.ring_member) and not g.resident:
                 g.gathered = False
 
     # -- forward ----------------------------------------------------------------------------

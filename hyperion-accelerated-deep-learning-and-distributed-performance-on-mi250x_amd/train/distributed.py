@@ -70,6 +70,10 @@ class RunOptions:
     # after training, all-gather per-parameter checksums and raise if the data-parallel replicas
     # differ (parallel/debug.py); the count of compared tensors is returned as "replicas"
     check_replicas: bool = False
+    # FSDP FULL_SHARD ring slots (>= 2): gathered units share fixed-address buffers (reshard-after-
+    # forward memory, capturable step); 0 = the wrapper's default (ring 3 at world > 1 on GPU,
+    # persistent buffers at world 1)
+    fsdp_ring: int = 0
     log: Callable[[str], None] = field(default=print)
 
 
@@ -151,8 +155,8 @@ class _EpochRunner:
         from ..parallel.fsdp import FullyShardedDataParallel
 
         why = ""
-        if isinstance(self.model, FullyShardedDataParallel) and not self.model.persistent:
-            why = "FSDP step without persistent buffers (storage released / re-allocated per unit)"
+        if isinstance(self.model, FullyShardedDataParallel) and not (self.model.persistent or self.model.ring):
+            why = "FSDP step without persistent or ring buffers (storage released / re-allocated per unit)"
         elif isinstance(self.model, DistributedDataParallel) and self.world > 1 and not self.model.bucketed:
             why = "DDP without gradient buckets"
         elif (isinstance(self.model, DistributedDataParallel) and self.world > 1 and self.model.broadcast_buffers
@@ -539,7 +543,8 @@ def train_language_model_fsdp(rank: int, world: int, epochs: int = 3, base_dir: 
     pdt = _amp(precision)
     policy = (transformer_auto_wrap_policy({TransformerEncoderLayer}) if wrap == "layer"
               else size_based_auto_wrap_policy(min_num_params))
-    model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt))
+    model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt),
+                 ring=opts.fsdp_ring)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, True, opts)
     res = _maybe_resume(opts, model, opt, None, out, run_name)
@@ -660,7 +665,7 @@ def train_llama_fsdp(rank: int, world: int, *, epochs: int = 1, base_dir: str = 
         model = DDP(model) if world > 1 else model
     else:
         model = FSDP(base, auto_wrap_policy=policy, device_id=device, mixed_precision=MixedPrecision(pdt, pdt, pdt),
-                     replicate_frozen=replicate_frozen if lora else False)
+                     replicate_frozen=replicate_frozen if lora else False, ring=opts.fsdp_ring)
     opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, adamw=True)
     runner = _EpochRunner(rank, world, device, model, opt, None, None, 1.0, isinstance(model, FSDP), opts)
     res = _maybe_resume(opts, model, opt, None, out, "llama")

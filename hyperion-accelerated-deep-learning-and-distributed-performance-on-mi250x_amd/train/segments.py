@@ -17,11 +17,24 @@ keeps its address on every replay; the actions must only touch persistent buffer
 """
 from __future__ import annotations
 
+import warnings
 from typing import Callable, List, Optional
 
 import torch
 
 _ACTIVE: Optional["SegmentedGraph"] = None
+
+
+def _capture_is_empty() -> bool:
+    """Nothing recorded yet by the capture on the current stream (native query; False if unknown)."""
+    try:
+        from ..ops import _native
+
+        if not _native.available():
+            return False
+        return bool(_native.native().capture_is_empty(torch.cuda.current_stream().cuda_stream))
+    except Exception:  # noqa: BLE001 - an unknown answer keeps the segment
+        return False
 
 
 def active() -> Optional["SegmentedGraph"]:
@@ -43,6 +56,9 @@ class SegmentedGraph:
     def __init__(self):
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.actions: List[Callable[[], object]] = []  # actions[i] runs after graphs[i]
+        # empty[i]: segment i recorded no work (two holes back to back, e.g. one unit's gather wait
+        # and the next unit's gather issue): never replayed, so the holes run as one action
+        self.empty: List[bool] = []
         self.stream: Optional[torch.cuda.Stream] = None
         self._pool = None
         self.out = None
@@ -61,7 +77,11 @@ class SegmentedGraph:
         g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
 
     def _end(self) -> None:
-        self.graphs[-1].capture_end()
+        empty = _capture_is_empty()
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # "The CUDA Graph is empty": expected, never replayed
+            self.graphs[-1].capture_end()
+        self.empty.append(empty)
 
     def hole(self, fn: Callable[[], object]):
         """End the current segment, run ``fn`` eagerly (recorded), start the next segment."""
@@ -92,6 +112,7 @@ class SegmentedGraph:
                     except Exception:
                         pass
                 self.graphs.clear()
+                self.empty.clear()
                 raise
             finally:
                 _ACTIVE = None
@@ -105,7 +126,8 @@ class SegmentedGraph:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for i, g in enumerate(self.graphs):
-                g.replay()
+                if not self.empty[i]:
+                    g.replay()
                 if i < len(self.actions):
                     self.actions[i]()
         torch.cuda.current_stream().wait_stream(s)
@@ -113,7 +135,12 @@ class SegmentedGraph:
 
     @property
     def num_segments(self) -> int:
-        return len(self.graphs)
+        """Graph segments replayed per step (empty ones are skipped)."""
+        return sum(1 for e in self.empty if not e)
+
+    @property
+    def num_holes(self) -> int:
+        return len(self.actions)
 
 
 class SegmentedStep:

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--out", default="gpurun_out/gemm_probe.json")
     a = ap.parse_args()
     C = _native.native()
+    if os.environ.get("HYPERION_SPLITK_INKERNEL") is not None:  # A/B: 0 = the separate reduce kernel
+        C.gemm_set_splitk_inkernel(int(os.environ["HYPERION_SPLITK_INKERNEL"]))
     rows = []
     for name, M, N, K, act, p in SHAPES:
         x = torch.randn(M, K, device="cuda").bfloat16()

@@ -13,6 +13,9 @@ if which == "fsdp":  # fsdp <lm256|gpt2_small|llama7b_lora> [graph] [shardbase] 
     kw = dict(graph="graph" in sys.argv[3:], collectives_at_world_1="coll" in sys.argv[3:])
     if "reshard" in sys.argv[3:]:
         kw["persistent"] = False
+    for a in sys.argv[3:]:
+        if a.startswith("ring"):  # ring2 / ring3: FULL_SHARD ring of gathered-unit slots
+            kw["ring"] = int(a[4:])
     if "shardbase" in sys.argv[3:]:
         kw["replicate_frozen"] = False
     if model == "gpt2_small":

@@ -7,11 +7,11 @@ import torch
 from dist_utils import run_world
 
 
-def _make_model(seed=0):
+def _make_model(seed=0, layers=2):
     from hyperion.models.simple_lm import simple_lm_256
 
     torch.manual_seed(seed)
-    return simple_lm_256(vocab_size=64, emb_dim=32, n_heads=2, n_layers=2, ff_dim=48, dropout=0.0)
+    return simple_lm_256(vocab_size=64, emb_dim=32, n_heads=2, n_layers=layers, ff_dim=48, dropout=0.0)
 
 
 def _batch(step, n=8):
@@ -20,8 +20,8 @@ def _batch(step, n=8):
     return ids[:, :-1], ids[:, 1:]
 
 
-def _reference_train(steps, lr=1e-2, clip=None):
-    m = _make_model()
+def _reference_train(steps, lr=1e-2, clip=None, layers=2):
+    m = _make_model(layers=layers)
     # SGD keeps the comparison strict: Adam would turn the (exactly zero in exact arithmetic) key-bias
     # gradient's rounding noise into +-lr steps that depend on the summation order across ranks
     opt = torch.optim.SGD(m.parameters(), lr=lr * 10, momentum=0.9, weight_decay=0.01)
@@ -36,7 +36,7 @@ def _reference_train(steps, lr=1e-2, clip=None):
     return {k: v.detach().clone() for k, v in m.state_dict().items()}
 
 
-def _fsdp_train(rank, world, steps, policy_kind, clip, strategy, persistent=None):
+def _fsdp_train(rank, world, steps, policy_kind, clip, strategy, persistent=None, ring=0, layers=2):
     from hyperion.models.transformer import TransformerEncoderLayer
     from hyperion.parallel.fsdp import FSDP, size_based_auto_wrap_policy, transformer_auto_wrap_policy
 
@@ -45,8 +45,12 @@ def _fsdp_train(rank, world, steps, policy_kind, clip, strategy, persistent=None
               # every Linear its own unit (the reference's min_num_params=100_000 at full size):
               # the FFN / attention projections must be CALLED as modules for the gather hooks
               "leaf": size_based_auto_wrap_policy(500), "none": None}[policy_kind]
-    m = FSDP(_make_model(), auto_wrap_policy=policy, device_id=torch.device("cpu"), sharding_strategy=strategy,
-             persistent=persistent)
+    m = FSDP(_make_model(layers=layers), auto_wrap_policy=policy, device_id=torch.device("cpu"),
+             sharding_strategy=strategy, persistent=persistent, ring=ring)
+    if ring:  # every ring slot starts poisoned: a unit must never compute from a slot it does not own
+        for r in m._rings.values():
+            for b in r.bufs:
+                b.fill_(float("nan"))
     if persistent:
         for g in m.flat_groups():  # an allocated-but-unfilled full buffer must never be read as gathered
             if not g.resident:
@@ -63,7 +67,7 @@ def _fsdp_train(rank, world, steps, policy_kind, clip, strategy, persistent=None
         opt.step()
         opt.zero_grad(set_to_none=True)
     sd = m.full_state_dict(rank0_only=True)
-    return {"sd": sd, "units": m.unit_sizes()}
+    return {"sd": sd, "units": m.unit_sizes(), "plan": m.memory_plan()}
 
 
 @pytest.mark.parametrize("policy", ["layer", "size", "leaf", "none"])
@@ -88,6 +92,22 @@ def test_fsdp_persistent_matches_single_process(world):
     res = run_world(_fsdp_train, world, (3, "layer", None, "FULL_SHARD", True))
     for k in ref:
         torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("ring", [2, 3])
+def test_fsdp_ring_matches_single_process(world, ring):
+    """FULL_SHARD ring mode: 5 layer units share `ring` fixed-address gathered-parameter / gradient
+    slots (slots poisoned with NaN first; units evict each other every step, forward and backward,
+    with prefetch); training with global clipping matches the single-process reference, and the
+    kept buffers are `ring` units' worth, not all five."""
+    ref = _reference_train(3, clip=0.05, layers=5)
+    res = run_world(_fsdp_train, world, (3, "layer", 0.05, "FULL_SHARD", None, ring, 5))
+    for k in ref:
+        torch.testing.assert_close(res[0]["sd"][k], ref[k], rtol=1e-4, atol=1e-5, msg=k)
+    assert res[0]["plan"]["mode"] == f"ring{ring}"
+    per_unit = max(res[0]["units"][:-1])
+    assert res[0]["plan"]["gathered_gib"] * 2**30 < (ring + 2) * per_unit * 8  # ring slots + root, fp32 p + g
 
 
 def test_fsdp_global_grad_clip_matches_single_process():

@@ -20,24 +20,24 @@ from parity import assert_losses_match, assert_update_parity
 pytestmark = pytest.mark.gpu
 
 
-def _lm(seed=0):
+def _lm(seed=0, layers=2):
     from hyperion.models.simple_lm import SimpleTransformerLM
 
     torch.manual_seed(seed)
-    return SimpleTransformerLM(vocab_size=512, emb_dim=128, n_heads=2, n_layers=2, ff_dim=256, dropout=0.0,
+    return SimpleTransformerLM(vocab_size=512, emb_dim=128, n_heads=2, n_layers=layers, ff_dim=256, dropout=0.0,
                                causal=True).cuda()
 
 
-def _fsdp_run(steps, graphed, seed=0, rank=0, coll=False):
+def _fsdp_run(steps, graphed, seed=0, rank=0, coll=False, ring=0, layers=2):
     from hyperion.models.transformer import TransformerEncoderLayer
     from hyperion.ops.optim import FusedAdam
     from hyperion.parallel.fsdp import FSDP, MixedPrecision, transformer_auto_wrap_policy
     from hyperion.train.segments import SegmentedStep
 
     bf = torch.bfloat16
-    m = FSDP(_lm(seed), auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}),
-             device_id=torch.device("cuda", 0), mixed_precision=MixedPrecision(bf, bf, bf), persistent=True,
-             collectives_at_world_1=coll)
+    m = FSDP(_lm(seed, layers), auto_wrap_policy=transformer_auto_wrap_policy({TransformerEncoderLayer}),
+             device_id=torch.device("cuda", 0), mixed_precision=MixedPrecision(bf, bf, bf), persistent=not ring,
+             collectives_at_world_1=coll, ring=ring)
     opt = FusedAdam(list(m.parameters()), lr=1e-3, weight_decay=0.01, adamw=True)
     g = torch.Generator(device="cuda").manual_seed(7 + rank)
     data = [torch.randint(0, 512, (4, 33), device="cuda", generator=g) for _ in range(steps)]
@@ -118,10 +118,11 @@ def test_fsdp_native_collectives_at_world_1_segmented_matches_eager():
     _parity(a, b, "native collectives")
 
 
-def _two_rank(rank, world, steps):
+def _two_rank(rank, world, steps, ring=0, layers=2):
     os.environ["HYPERION_COMM"] = "torch"  # gloo collectives between the two processes
     torch.cuda.set_device(0)
-    return {"graph": _fsdp_run(steps, True, rank=rank), "eager": _fsdp_run(steps, False, rank=rank)}
+    return {"graph": _fsdp_run(steps, True, rank=rank, ring=ring, layers=layers),
+            "eager": _fsdp_run(steps, False, rank=rank, ring=ring, layers=layers)}
 
 
 def test_fsdp_segmented_capture_two_gloo_ranks():
@@ -132,3 +133,37 @@ def test_fsdp_segmented_capture_two_gloo_ranks():
         assert torch.equal(g0["params"][k], g1["params"][k])  # one set of gathered params on both ranks
     for r in (0, 1):
         _parity(res[r]["graph"], res[r]["eager"], f"rank {r}")
+
+
+def test_fsdp_ring_native_collectives_segmented_matches_eager():
+    """FULL_SHARD ring (2 fixed-address slots for 4 layer units, evicting each other every step)
+    captured as graph segments with real RCCL gathers / reduce-scatters at world 1: the captured
+    steps match the eager identity schedule, and the ring keeps 2 units' buffers, not 4."""
+    import socket
+
+    import torch.distributed as dist
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    os.environ["HYPERION_COMM"] = "native"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        a = _fsdp_run(4, graphed=True, coll=True, ring=2, layers=4)
+        b = _fsdp_run(4, graphed=False, layers=4)
+    finally:
+        dist.destroy_process_group()
+        os.environ["HYPERION_COMM"] = "torch"
+    assert a["comm"] == "NativeComm" and not a["identity"]
+    assert a["segments"] > 1
+    _parity(a, b, "ring native collectives")
+
+
+def test_fsdp_ring_segmented_capture_two_gloo_ranks():
+    res = run_world(_two_rank, 2, (3, 2, 4), timeout=600)
+    g0, g1 = res[0]["graph"], res[1]["graph"]
+    for k in g0["params"]:
+        assert torch.equal(g0["params"][k], g1["params"][k])
+    for r in (0, 1):
+        _parity(res[r]["graph"], res[r]["eager"], f"ring rank {r}")

@@ -106,3 +106,55 @@ def test_gemm_strided_operands_and_auto_plan():
     for shape in [(6304, 768, 3072), (6304, 3072, 768), (768, 3072, 6304), (8192, 8192, 8192), (128, 4096, 4096)]:
         t, s = _C().gemm_plan(*shape)
         assert 0 <= t <= 2 and s >= 1
+
+
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("splits", [2, 5])
+def test_split_k_last_arriver_matches_separate_reduce(layout, splits):
+    """Split-K reduced by the last-arriving workgroup of each tile (arrival counters, write-through
+    slabs) == the separate gemm_splitk_epi_k reduce, bitwise (same slice order), with the fused
+    bias + GELU + aux epilogue; repeated launches reuse the self-resetting counters."""
+    M, N, K = 1000, 776, 2048
+    a_tr, b_tr = layout[0] == "t", layout[1] == "n"
+    torch.manual_seed(2)
+    a, b, ref = _operands(M, N, K, a_tr, b_tr, torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    C = _C()
+    outs = {}
+    try:
+        for mode in (0, 1):
+            C.gemm_set_splitk_inkernel(mode)
+            aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            rs = [C.gemm(a, b, a_tr=a_tr, b_tr=b_tr, bias=bias, act=2, aux=aux, tile=2, splits=splits) for _ in range(3)]
+            outs[mode] = (rs, aux.clone())
+    finally:
+        C.gemm_set_splitk_inkernel(1)
+    torch.cuda.synchronize()
+    for r in outs[1][0]:
+        assert torch.equal(r, outs[0][0][0])
+    assert torch.equal(outs[1][1], outs[0][1])
+    z = ref + bias
+    torch.testing.assert_close(outs[1][1].float(), z, rtol=2e-2, atol=2e-2 * K ** 0.5)
+
+
+def test_split_k_last_arriver_under_graph_capture():
+    """A captured split-K GEMM takes its own counter range; replays give the eager result."""
+    M, N, K = 512, 384, 3072
+    torch.manual_seed(3)
+    a, b, ref = _operands(M, N, K, False, False, torch.bfloat16)
+    C = _C()
+    eager = C.gemm(a, b, out_dtype=torch.float32, tile=2, splits=4)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        C.gemm(a, b, out_dtype=torch.float32, tile=2, splits=4)  # warm-up off the capture
+        with torch.cuda.graph(g):
+            out = C.gemm(a, b, out_dtype=torch.float32, tile=2, splits=4)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
+    torch.testing.assert_close(eager, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
