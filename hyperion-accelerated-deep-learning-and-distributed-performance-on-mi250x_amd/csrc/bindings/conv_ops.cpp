@@ -733,6 +733,32 @@ at::Tensor stem_s2d(const at::Tensor& x) {
   return out;
 }
 
+at::Tensor stem_weight4(const at::Tensor& w) {
+  HYP_CHECK_CUDA_TENSOR(w);
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 7 && w.size(3) == 7 && w.size(1) >= 1 && w.size(1) <= 4,
+              "stem_weight4: W [K, C <= 4, 7, 7]");
+  const int K = w.size(0), C = w.size(1);
+  const at::DeviceGuard guard(w.device());
+  auto w4 = at::empty({K, 64, 4, 1}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  HYP_CHECK_HIP(hyp::stem_weight4(dtype_code(w), w.data_ptr(), w4.data_ptr(), K, C, w.stride(0), w.stride(1),
+                                  w.stride(2), w.stride(3), cur_stream()));
+  return w4;
+}
+
+at::Tensor stem_weight4_grad(const at::Tensor& dw4, int64_t C, bool channels_last) {
+  HYP_CHECK_CUDA_TENSOR(dw4);
+  TORCH_CHECK(dw4.dim() == 4 && dw4.size(1) == 64 && dw4.size(2) == 4 && dw4.size(3) == 1 &&
+                  dw4.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_weight4_grad: channels-last dW4 [K, 64, 4, 1]");
+  const int K = dw4.size(0);
+  const at::DeviceGuard guard(dw4.device());
+  auto dw = at::empty({K, C, 7, 7}, dw4.options().memory_format(channels_last ? at::MemoryFormat::ChannelsLast
+                                                                              : at::MemoryFormat::Contiguous));
+  HYP_CHECK_HIP(hyp::stem_weight4_grad(dtype_code(dw4), dw4.data_ptr(), dw.data_ptr(), K, (int)C, dw.stride(0),
+                                       dw.stride(1), dw.stride(2), dw.stride(3), cur_stream()));
+  return dw;
+}
+
 namespace {
 void check_stem(const at::Tensor& xs, int64_t K) {
   HYP_CHECK_CUDA_TENSOR(xs);
@@ -908,6 +934,9 @@ void register_conv_ops(pybind11::module& m) {
   }, "diagnostic: record a per-workgroup timeline (int64 [>= 6 * workgroups]) of the next conv_fwd launches",
         pybind11::arg("buf") = pybind11::none());
   m.def("stem_s2d", &stem_s2d, "ResNet 7x7/s2/p3 stem input as space-to-depth Xs [N, 16, P+3, Q+3]");
+  m.def("stem_weight4", &stem_weight4, "stem W [K, C, 7, 7] -> W4 channels-last [K, 64, 4, 1] (one launch)");
+  m.def("stem_weight4_grad", &stem_weight4_grad, "dW4 [K, 64, 4, 1] -> dW [K, C, 7, 7] (one launch)",
+        pybind11::arg("dw4"), pybind11::arg("C"), pybind11::arg("channels_last") = false);
   m.def("stem_conv_fwd", &stem_conv_fwd, "the stem conv (R=4 x 64 over Xs, pixel stride 16) + BN statistics");
   m.def("stem_conv_wgrad", &stem_conv_wgrad, "dW4 [K, 64, 4, 1] of the stem conv", pybind11::arg("dy"),
         pybind11::arg("xs"), pybind11::arg("splits") = -1);

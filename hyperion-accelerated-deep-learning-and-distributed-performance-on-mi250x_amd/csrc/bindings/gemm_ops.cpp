@@ -153,7 +153,7 @@ void register_gemm_ops(pybind11::module& m) {
         pybind11::arg("tile") = -1, pybind11::arg("splits") = -1, pybind11::arg("drop_p") = 0.0,
         pybind11::arg("rng") = pybind11::none());
   m.def("gemm_set_splitk_inkernel", [](int64_t on) { hyp::gemm_set_splitk_inkernel((int)on); },
-        "A/B: split-K reduce in the last-arriving workgroup (1, default) or the separate reduce kernel (0)");
+        "A/B: split-K reduce in the last-arriving workgroup (1) or the separate reduce kernel (0, default)");
   m.def("gemm_plan", &gemm_plan, "(tile, splits) the automatic plan picks for an M x N x K GEMM");
   m.def("gemm_f32_nt", &gemm_f32_nt, "C = alpha * A @ B.T, fp32 in, on the fp32-input MFMA", pybind11::arg("a"),
         pybind11::arg("b"), pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("alpha") = 1.0);

@@ -174,7 +174,7 @@ struct GemmTiledArgs {
   RngState drng{};
 };
 void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits);
-// split-K reduce in the last-arriving workgroup of each tile (1, default) or a separate kernel (0)
+// split-K reduce in the last-arriving workgroup of each tile (1) or a separate kernel (0, default)
 void gemm_set_splitk_inkernel(int on);
 int gemm_tiled_splits(const GemmTiledArgs& a);
 hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st);
@@ -384,6 +384,11 @@ void conv_set_stamps(void* buf);
 // ---- stem.hip: the 7x7/s2/p3 stem (C <= 4) as a stride-1 R=4 x S=1 conv with pixel stride 16:
 // Xs [N, Hs = P + 3, Ws = Q + 3, 16] (space-to-depth) from x [N, H, W, C] (both channels-last)
 hipError_t stem_s2d(int dtype, const void* x, void* out, int N, int H, int W, int C, int Hs, int Ws, hipStream_t st);
+// W [K, C, 7, 7] (element strides sk, sc, sr, sq) -> W4 channels-last [K, 64, 4, 1]; and back for dW
+hipError_t stem_weight4(int dtype, const void* w, void* w4, int K, int C, int64_t sk, int64_t sc, int64_t sr,
+                        int64_t sq, hipStream_t st);
+hipError_t stem_weight4_grad(int dtype, const void* dw4, void* dw, int K, int C, int64_t sk, int64_t sc, int64_t sr,
+                             int64_t sq, hipStream_t st);
 // out[N,H,W,C] = addend (optional) + comp[N,P,Q,C] scattered to pixels (p*sh, q*sw), zeros elsewhere
 hipError_t upsample_add(int dtype, const void* comp, const void* addend, void* out, int N, int H, int W, int C, int P,
                         int Q, int sh, int sw, hipStream_t st);

@@ -600,7 +600,7 @@ unsigned* splitk_counters(int ntiles, hipStream_t st) {
   return r;
 }
 
-int g_splitk_inkernel = 1;  // gemm_set_splitk_inkernel (A/B)
+int g_splitk_inkernel = 0;  // gemm_set_splitk_inkernel (A/B; off: measured slower, profiles/r05/splitk_last_arriver_ab.txt)
 
 }  // namespace
 

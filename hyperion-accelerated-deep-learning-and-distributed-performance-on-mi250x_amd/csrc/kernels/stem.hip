@@ -58,7 +58,60 @@ __global__ __launch_bounds__(256) void stem_s2d_k(const T* __restrict__ x, T* __
   Vec8<T>::store(out + t * 16 + 8, hi);
 }
 
+// W [K, C, 7, 7] (any strides, in elements) -> W4 channels-last [K, 64, 4, 1], memory
+// [k][dr][ds*16 + (2a+b)*C + c] = W[k, c, 2dr+a, 2ds+b] (zero past tap 6 and past 4C): one launch
+// in place of pad + index_select + layout copy (3-4 torch kernels per step)
+template <typename T>
+__global__ __launch_bounds__(256) void stem_w4_k(const T* __restrict__ w, T* __restrict__ w4, int K, int C,
+                                                 int64_t sk, int64_t sc, int64_t sr, int64_t sq) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= K * 256) return;
+  const int k = i >> 8, col = i & 255, dr = col >> 6, e = col & 63, ds = e >> 4, ch = e & 15;
+  const int ab = ch / C, c = ch - ab * C, r = 2 * dr + (ab >> 1), q = 2 * ds + (ab & 1);
+  T v = T(0.f);
+  if (ab < 4 && r < 7 && q < 7) v = w[k * sk + c * sc + r * sr + q * sq];
+  w4[i] = v;
+}
+
+// dW4 (the same [k][dr][64] memory order) -> dW [K, C, 7, 7] contiguous: every W element feeds
+// exactly one W4 column
+template <typename T>
+__global__ __launch_bounds__(256) void stem_w4_grad_k(const T* __restrict__ dw4, T* __restrict__ dw, int K, int C,
+                                                      int64_t sk, int64_t sc, int64_t sr, int64_t sq) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= K * C * 49) return;
+  const int k = i / (C * 49), rem = i - k * C * 49, c = rem / 49, rq = rem - c * 49, r = rq / 7, q = rq - r * 7;
+  const int col = (r >> 1) * 64 + (q >> 1) * 16 + ((r & 1) * 2 + (q & 1)) * C + c;
+  dw[k * sk + c * sc + r * sr + q * sq] = dw4[k * 256 + col];
+}
+
 }  // namespace
+
+hipError_t stem_weight4(int dtype, const void* w, void* w4, int K, int C, int64_t sk, int64_t sc, int64_t sr,
+                        int64_t sq, hipStream_t st) {
+  if (C < 1 || C > 4 || K < 1 || (dtype != kBF16 && dtype != kF16)) return hipErrorInvalidValue;
+  const unsigned blocks = (unsigned)((K * 256 + 255) / 256);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(stem_w4_k<bf16_t>, dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(w),
+                       static_cast<bf16_t*>(w4), K, C, sk, sc, sr, sq);
+  else
+    hipLaunchKernelGGL(stem_w4_k<f16_t>, dim3(blocks), dim3(256), 0, st, static_cast<const f16_t*>(w),
+                       static_cast<f16_t*>(w4), K, C, sk, sc, sr, sq);
+  return hipGetLastError();
+}
+
+hipError_t stem_weight4_grad(int dtype, const void* dw4, void* dw, int K, int C, int64_t sk, int64_t sc, int64_t sr,
+                             int64_t sq, hipStream_t st) {
+  if (C < 1 || C > 4 || K < 1 || (dtype != kBF16 && dtype != kF16)) return hipErrorInvalidValue;
+  const unsigned blocks = (unsigned)((K * C * 49 + 255) / 256);
+  if (dtype == kBF16)
+    hipLaunchKernelGGL(stem_w4_grad_k<bf16_t>, dim3(blocks), dim3(256), 0, st, static_cast<const bf16_t*>(dw4),
+                       static_cast<bf16_t*>(dw), K, C, sk, sc, sr, sq);
+  else
+    hipLaunchKernelGGL(stem_w4_grad_k<f16_t>, dim3(blocks), dim3(256), 0, st, static_cast<const f16_t*>(dw4),
+                       static_cast<f16_t*>(dw), K, C, sk, sc, sr, sq);
+  return hipGetLastError();
+}
 
 hipError_t stem_s2d(int dtype, const void* x, void* out, int N, int H, int W, int C, int Hs, int Ws,
                     hipStream_t st) {

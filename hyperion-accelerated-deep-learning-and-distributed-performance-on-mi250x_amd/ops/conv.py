@@ -808,13 +808,15 @@ class _StemConvBNActFn(torch.autograd.Function):
         C = _native.native()
         K, Cin = w.shape[0], w.shape[1]
         xs = C.stem_s2d(x.contiguous(memory_format=torch.channels_last))
-        w4 = stem_weight(w.detach())
+        w4 = C.stem_weight4(w.detach())  # == stem_weight(w) in one launch
         sums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
         ctx.bsums = _native.zeroed(_native.STAT_SLOTS * 2 * K, x.device)
         yc = C.stem_conv_fwd(xs, w4, sums)
         out, mean, invstd = C.bn_fwd_sums(yc, None, sums, bn_w, bn_b, rm, rv, momentum, eps, act)
         ctx.save_for_backward(xs, yc, bn_w, bn_b, mean, invstd)
         ctx.cfg = (Cin, act)
+        # the gradient in the weight's own layout (AccumulateGrad then steals it: no copy kernel)
+        ctx.w_cl = not w.is_contiguous() and w.is_contiguous(memory_format=torch.channels_last)
         return out
 
     @staticmethod
@@ -828,7 +830,8 @@ class _StemConvBNActFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             _native.count("wgrad")
-            dw = stem_weight_grad(C.stem_conv_wgrad(dyc, xs), Cin)
+            dw4 = C.stem_conv_wgrad(dyc, xs).contiguous(memory_format=torch.channels_last)
+            dw = C.stem_weight4_grad(dw4, Cin, ctx.w_cl)  # == stem_weight_grad(dw4, Cin), one launch
         return (None, dw, dbw if ctx.needs_input_grad[2] else None, dbb if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None)
 

@@ -187,6 +187,9 @@ class _FlatGroup:
         self.grad_ring: Optional[_Ring] = None
         self.slot = -1
         self.ring_member = ring_member and not self.resident
+        # pinned: buffers never released (persistent mode; in ring mode also the root unit's —
+        # a capturable step allocates nothing)
+        self.pinned = fsdp.persistent or bool(fsdp.ring)
         if self.ring_member:
             self.full = torch.empty(0, dtype=self.cdtype, device=dev)
             self.full_grad = torch.empty(0, dtype=self.rdtype, device=dev) if trainable else None
@@ -218,12 +221,12 @@ class _FlatGroup:
         # module parameters become views of the full buffer (the same Parameter objects)
         for p, o, n, shp in zip(params, self.offsets, self.numels, self.shapes):
             p.data = self.full[o : o + n].view(shp)
-        if not (self.resident or fsdp.persistent):
+        if not (self.resident or self.pinned):
             self.free_full()
         elif not self.resident:
             self.gathered = False  # persistent: the full buffer is allocated but not filled yet
         if trainable:
-            if fsdp.persistent:
+            if self.pinned:
                 self.full_grad.zero_()
             else:
                 self.full_grad.untyped_storage().resize_(0)
@@ -245,7 +248,7 @@ class _FlatGroup:
         return self.ring is not None and self.ring.owner[self.slot] is self
 
     def free_full(self) -> None:
-        if self.resident or self.fsdp.persistent or self.ring_member:
+        if self.resident or self.pinned:
             # persistent: the storage stays, the content stays valid; ring: the slot is overwritten
             # by the unit that takes it next (no release, no re-allocation: fixed addresses)
             return
@@ -392,7 +395,7 @@ class _FlatGroup:
             else:
                 self.flat_param.grad.add_(g)
         self.rs_out = None
-        if not self.fsdp.persistent and self.grad_ring is None:
+        if not self.pinned:
             self.full_grad.untyped_storage().resize_(0)
 
 
@@ -535,6 +538,13 @@ class FullyShardedDataParallel(nn.Module):
         # capturable (train/segments.py).  "auto"/None: on GPU when every unit's full parameters +
         # gradients take at most a quarter of the device memory.
         self.persistent_reason = "requested" if persistent is True else "off"
+        if (not ring and persistent in (None, "auto") and sharding_strategy == "FULL_SHARD" and self.world > 1
+                and self.device.type == "cuda"):
+            # FULL_SHARD across ranks: the ring keeps the real reshard-after-forward memory bound
+            # (3 units' worth, not the whole model on every rank) and a capturable step
+            ring = 3
+        if ring:
+            persistent = False
         if persistent is None or persistent == "auto":
             if self.device.type == "cuda":
                 need = sum(p.numel() for p in module.parameters()) * (
@@ -551,11 +561,6 @@ class FullyShardedDataParallel(nn.Module):
             else:
                 persistent = False
                 self.persistent_reason = "auto: not a GPU device"
-        if (not ring and persistent in (None, "auto") and sharding_strategy == "FULL_SHARD" and self.world > 1
-                and self.device.type == "cuda"):
-            # FULL_SHARD across ranks: the ring keeps the real reshard-after-forward memory bound
-            # (3 units' worth, not the whole model on every rank) and a capturable step
-            ring = 3
         self.ring = int(ring) if ring and sharding_strategy == "FULL_SHARD" else 0
         if self.ring == 1:
             raise ValueError("FSDP ring needs >= 2 slots (a unit and the one being prefetched)")
@@ -745,7 +750,7 @@ class FullyShardedDataParallel(nn.Module):
                 if not g.trainable:
                     continue  # frozen weights never change: a persistent gathered copy stays valid
                 g.send_valid = False  # the optimizer steps next: recast on the next forward gather
-                if (self.persistent or g.ring_member) and not g.resident:
+                if g.pinned and not g.resident:
                     g.gathered = False  # ... and re-gather (the persistent buffer keeps its storage)
         self._in_backward = False
         self._active = None
@@ -754,7 +759,7 @@ class FullyShardedDataParallel(nn.Module):
         """Call after changing the flat shards outside an optimizer step that follows backward."""
         for g in self.flat_groups():
             g.send_valid = False
-            if (self.persistent or g.ring_member) and not g.resident:
+            if g.pinned and not g.resident:
                 g.gathered = False
 
     # -- forward ----------------------------------------------------------------------------

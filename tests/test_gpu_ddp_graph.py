@@ -216,7 +216,8 @@ def test_ddp_segmented_schedule_matches_eager(native):
                 losses.append(float(st(xs[i], ys[i])))
             torch.cuda.synchronize()
             if mode == "segmented":
-                assert st.seg is not None and st.seg.num_segments > len(ddp.bucket_sizes())  # holes per bucket
+                # an issue and a wait hole per bucket (adjacent holes share one replayed segment boundary)
+                assert st.seg is not None and st.seg.num_holes >= len(ddp.bucket_sizes()) and st.seg.num_segments > 1
             res[mode] = (before, snapshot(ddp.module.named_parameters()), losses)
         (b0, a_seg, l_seg), (b1, a_eag, l_eag) = res["segmented"], res["eager"]
         assert all(torch.equal(b0[k], b1[k]) for k in b0)

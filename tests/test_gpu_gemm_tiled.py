@@ -128,7 +128,7 @@ def test_split_k_last_arriver_matches_separate_reduce(layout, splits):
             rs = [C.gemm(a, b, a_tr=a_tr, b_tr=b_tr, bias=bias, act=2, aux=aux, tile=2, splits=splits) for _ in range(3)]
             outs[mode] = (rs, aux.clone())
     finally:
-        C.gemm_set_splitk_inkernel(1)
+        C.gemm_set_splitk_inkernel(0)
     torch.cuda.synchronize()
     for r in outs[1][0]:
         assert torch.equal(r, outs[0][0][0])
@@ -143,6 +143,14 @@ def test_split_k_last_arriver_under_graph_capture():
     torch.manual_seed(3)
     a, b, ref = _operands(M, N, K, False, False, torch.bfloat16)
     C = _C()
+    C.gemm_set_splitk_inkernel(1)
+    try:
+        _captured_split_k(C, a, b, ref, K)
+    finally:
+        C.gemm_set_splitk_inkernel(0)
+
+
+def _captured_split_k(C, a, b, ref, K):
     eager = C.gemm(a, b, out_dtype=torch.float32, tile=2, splits=4)
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()

@@ -27,6 +27,28 @@ def test_stem_s2d_kernel_is_the_reference_rewrite(shape, dtype):
     assert torch.equal(got, ref)  # a pure gather: bit-exact
 
 
+@pytest.mark.parametrize("C", [1, 3, 4])
+@pytest.mark.parametrize("cl", [False, True])
+def test_stem_weight_transforms_one_launch_match_reference(C, cl):
+    """stem_weight4 / stem_weight4_grad (one launch each) == the torch index-gather forms, bitwise,
+    for either weight layout; dW comes back in the weight's own layout."""
+    from hyperion.ops import _native
+    from hyperion.ops.conv import stem_weight, stem_weight_grad
+
+    torch.manual_seed(0)
+    w = torch.randn(64, C, 7, 7, device="cuda").bfloat16()
+    if cl:
+        w = w.contiguous(memory_format=torch.channels_last)
+    N = _native.native()
+    w4 = N.stem_weight4(w)
+    ref = stem_weight(w).contiguous(memory_format=torch.channels_last)
+    assert w4.is_contiguous(memory_format=torch.channels_last) and torch.equal(w4, ref)
+    dw4 = torch.randn(64, 64, 4, 1, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    dw = N.stem_weight4_grad(dw4, C, cl)
+    assert torch.equal(dw, stem_weight_grad(dw4, C))
+    assert dw.is_contiguous(memory_format=torch.channels_last) == cl or C == 1
+
+
 @pytest.mark.parametrize("N,H", [(4, 64), (2, 224)])
 def test_stem_conv_bn_relu_native_matches_fp32(N, H):
     from hyperion.ops import _native
