@@ -174,6 +174,7 @@ struct GemmTiledArgs {
   RngState drng{};
 };
 void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits);
+void gemm_tiled_plan_layout(int M, int N, int K, bool a_tr, bool b_tr, int* tile, int* splits);
 // split-K reduce in the last-arriving workgroup of each tile (1) or a separate kernel (0, default)
 void gemm_set_splitk_inkernel(int on);
 int gemm_tiled_splits(const GemmTiledArgs& a);

@@ -528,34 +528,54 @@ struct TileCfg {
   int bm, bn, waves, occ;
   double eff;  // relative per-CU throughput of a full tile (calibrated on MI355X)
 };
-constexpr TileCfg kTiles[4] = {
-    {256, 256, 8, 1, 1.0}, {256, 128, 8, 1, 0.80}, {128, 128, 4, 2, 0.62}, {128, 128, 4, 2, 0.55}};
+constexpr int kNumTiles = 8;
+constexpr TileCfg kTiles[kNumTiles] = {{256, 256, 8, 1, 1.0},  {256, 128, 8, 1, 0.80}, {128, 128, 4, 2, 0.62},
+                                       {128, 128, 4, 2, 0.55}, {64, 64, 2, 4, 0.30},   {128, 64, 2, 3, 0.42},
+                                       {64, 128, 4, 3, 0.42},  {192, 128, 4, 2, 0.70}};
+
+bool tile_layout_ok(int t, bool atr, bool btr) {
+  const TileCfg& c = kTiles[t];
+  return (!atr || c.bm % 128 == 0) && (!btr || c.bn % 128 == 0);
+}
 
 template <typename T, typename OutT, int BM, int BN, int WM, int WN, bool SAFE, int NBR>
 hipError_t launch_layout(const GemmP& p, bool atr, bool btr, int nwg, hipStream_t st) {
+  // layouts a tile can stage: the row form needs BM (BN) % (16 x waves) == 0 (every tile here),
+  // the transposed form 128-column image blocks (BM / BN % 128 == 0)
   const dim3 grid(nwg), block(WM * WN * 64);
-  if (!atr && !btr)
+  if ((atr && BM % 128 != 0) || (btr && BN % 128 != 0)) return hipErrorInvalidValue;
+  if (!atr && !btr) {
     hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, false, SAFE, NBR>), grid, block, 0, st, p);
-  else if (!atr && btr)
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, true, SAFE, NBR>), grid, block, 0, st, p);
-  else if (atr && btr)
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, true, SAFE, NBR>), grid, block, 0, st, p);
-  else
-    hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, false, SAFE, NBR>), grid, block, 0, st, p);
+  } else if (!atr && btr) {
+    if constexpr (BN % 128 == 0)
+      hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, false, true, SAFE, NBR>), grid, block, 0, st, p);
+  } else if (atr && btr) {
+    if constexpr (BM % 128 == 0 && BN % 128 == 0)
+      hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, true, SAFE, NBR>), grid, block, 0, st, p);
+  } else {
+    if constexpr (BM % 128 == 0)
+      hipLaunchKernelGGL((gemm_tile_k<T, OutT, BM, BN, WM, WN, true, false, SAFE, NBR>), grid, block, 0, st, p);
+  }
   return hipGetLastError();
 }
 
 // tile 3 = the 128x128 SAFE kernel (ragged K, M or N below the tile, accumulate over ragged tiles).
+// Tiles 4-7 size the grid for the small transformer GEMMs (M ~ 2k tokens): a 2032 x 768 output is
+// 96 workgroups at 128x128 (37 % of the 256 CUs) but 192-384 at 64x64 / 128x64 / 64x128, and
+// 2032 x 3072 is 264 at 192x128 — the vendor library's choice of one full wave of workgroups.
 // Deep rings at one workgroup per CU (128x128 with 8 stages, 256x128 with 6) were measured SLOWER
 // on every transformer shape (1.1-2x, profiles/r05/gemm_probe_deep_ring.json): with one wave per
-// SIMD nothing hides the fragment reads behind the MFMAs — occupancy, not bytes in flight, bounds
-// these k-loops.  NBR stays a template parameter for such sweeps.
+// SIMD nothing hides the fragment reads behind the MFMAs.  NBR stays a template parameter.
 template <typename T, typename OutT>
 hipError_t launch_tile(const GemmP& p, bool atr, bool btr, int tile, int nwg, hipStream_t st) {
   switch (tile) {
     case 0: return launch_layout<T, OutT, 256, 256, 2, 4, false, 4>(p, atr, btr, nwg, st);
     case 1: return launch_layout<T, OutT, 256, 128, 4, 2, false, 4>(p, atr, btr, nwg, st);
     case 2: return launch_layout<T, OutT, 128, 128, 2, 2, false, 4>(p, atr, btr, nwg, st);
+    case 4: return launch_layout<T, OutT, 64, 64, 2, 1, false, 4>(p, atr, btr, nwg, st);
+    case 5: return launch_layout<T, OutT, 128, 64, 2, 1, false, 4>(p, atr, btr, nwg, st);
+    case 6: return launch_layout<T, OutT, 64, 128, 2, 2, false, 4>(p, atr, btr, nwg, st);
+    case 7: return launch_layout<T, OutT, 192, 128, 2, 2, false, 4>(p, atr, btr, nwg, st);
     default: return launch_layout<T, OutT, 128, 128, 2, 2, true, 4>(p, atr, btr, nwg, st);
   }
 }
@@ -606,11 +626,14 @@ int g_splitk_inkernel = 0;  // gemm_set_splitk_inkernel (A/B; off: measured slow
 
 void gemm_set_splitk_inkernel(int on) { g_splitk_inkernel = on; }
 
-void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits) {
+void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits) { gemm_tiled_plan_layout(M, N, K, false, false, tile, splits); }
+
+void gemm_tiled_plan_layout(int M, int N, int K, bool a_tr, bool b_tr, int* tile, int* splits) {
   const int cus = 256;
   double best = 1e30;
   int bt = 2, bs = 1;
-  for (int t = 0; t < 3; ++t) {
+  for (int t = 0; t < kNumTiles; ++t) {
+    if (t == 3 || !tile_layout_ok(t, a_tr, b_tr) || M < kTiles[t].bm || N < kTiles[t].bn) continue;
     const TileCfg& c = kTiles[t];
     const int64_t tiles = (int64_t)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     const int nk = (K + kBK - 1) / kBK;
@@ -642,12 +665,13 @@ hipError_t gemm_tiled(const GemmTiledArgs& a, hipStream_t st) {
   int tile = a.tile, splits = a.splits;
   if (tile < 0 || splits < 1) {
     int t, s;
-    gemm_tiled_plan(a.M, a.N, a.K, &t, &s);
+    gemm_tiled_plan_layout(a.M, a.N, a.K, a.a_tr, a.b_tr, &t, &s);
     if (tile < 0) tile = t;
     if (splits < 1) splits = s;
   }
-  if (tile > 3) return hipErrorInvalidValue;
-  if (tile < 3) {  // the fast (unclamped) kernels: see gemm_tile_k's SAFE
+  if (tile >= kNumTiles) return hipErrorInvalidValue;
+  if (!tile_layout_ok(tile, a.a_tr, a.b_tr)) return hipErrorInvalidValue;
+  if (tile != 3) {  // the fast (unclamped) kernels: see gemm_tile_k's SAFE
     const TileCfg& f = kTiles[tile];
     const bool ragged = a.M % f.bm != 0 || a.N % f.bn != 0;
     const bool fast = a.M >= f.bm && a.N >= f.bn && a.K % kBK == 0 &&
@@ -702,7 +726,7 @@ int gemm_tiled_splits(const GemmTiledArgs& a) {
   int tile = a.tile, splits = a.splits;
   if (tile < 0 || splits < 1) {
     int t, s;
-    gemm_tiled_plan(a.M, a.N, a.K, &t, &s);
+    gemm_tiled_plan_layout(a.M, a.N, a.K, a.a_tr, a.b_tr, &t, &s);
     if (splits < 1) splits = s;
   }
   const int nk = (a.K + kBK - 1) / kBK;

@@ -65,14 +65,23 @@ def _time(fn, reps: int = 5) -> float:
     return s.elapsed_time(e)
 
 
-def _candidates(K: int):
-    for t in (0, 1, 2):
+# (BM, BN) of the tiled kernel's tiles (gemm_tiles.hip kTiles; 3 = the ragged-shape 128x128)
+TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128), 7: (192, 128)}
+
+
+def _candidates(K: int, M: int = 1 << 30, N: int = 1 << 30, a_tr: bool = False, b_tr: bool = False):
+    """(tile, splits) pairs worth timing: tiles the layout can stage (a transposed operand needs a
+    128-multiple tile side) and that fit the output, split-K slices >= 256 deep."""
+    for t, (bm, bn) in TILES.items():
+        if (a_tr and bm % 128) or (b_tr and bn % 128) or bm > M or bn > N:
+            continue
         for sp in (1, 2, 3, 4, 6, 8, 12, 16):
             if sp == 1 or K // sp >= 256:
                 yield (t, sp)
 
 
-def _pick(key: Tuple, K: int, native_fn, vendor_fn) -> Optional[Tuple[int, int]]:
+def _pick(key: Tuple, K: int, native_fn, vendor_fn, M: int = 1 << 30, N: int = 1 << 30, a_tr: bool = False,
+          b_tr: bool = False) -> Optional[Tuple[int, int]]:
     """(tile, splits) for the tiled kernel, (-1, -1) = its static plan, or None = vendor."""
     if _MODE == "native":
         return _CHOICE.get(key, (-1, -1)) or (-1, -1)
@@ -81,8 +90,11 @@ def _pick(key: Tuple, K: int, native_fn, vendor_fn) -> Optional[Tuple[int, int]]
     if torch.cuda.is_current_stream_capturing():
         return (-1, -1)  # no timing under capture: static plan
     best, bt = _time(vendor_fn), None
-    for c in _candidates(K):
-        tc = _time(lambda: native_fn(*c))
+    for c in _candidates(K, M, N, a_tr, b_tr):
+        try:
+            tc = _time(lambda: native_fn(*c))
+        except RuntimeError:  # a (tile, layout) the kernel refuses
+            continue
         if tc < best:
             best, bt = tc, c
     _CHOICE[key] = bt
@@ -122,7 +134,7 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
             y = C.dropout(y, dropout_p, rng)
         return y + residual if residual is not None else y
 
-    c = _pick(key, x.shape[1], nat, ven)
+    c = _pick(key, x.shape[1], nat, ven, x.shape[0], w.shape[0])
     if c is None:
         return None
     _native.count("gemm_nt")
@@ -140,7 +152,7 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, residual: Optional[torch.Tensor] = 
     key = ("nn", dy.shape[0], w.shape[1], dy.shape[1]) + (("res",) if residual is not None else ())
     ven = (lambda: dy @ w) if residual is None else (lambda: torch.addmm(residual, dy, w))
     c = _pick(key, dy.shape[1], lambda t=-1, sp=-1: C.gemm(dy, w, b_tr=True, residual=residual, tile=t, splits=sp),
-              ven)
+              ven, dy.shape[0], w.shape[1], b_tr=True)
     if c is None:
         return None
     _native.count("gemm_nn")
@@ -160,7 +172,7 @@ def mm_tn(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
         return (dy.t() @ x).to(odt)
 
     c = _pick(key, dy.shape[0], lambda t=-1, sp=-1: C.gemm(dy, x, a_tr=True, b_tr=True, out_dtype=odt, tile=t,
-                                                           splits=sp), ven)
+                                                           splits=sp), ven, dy.shape[1], x.shape[1], True, True)
     if c is None:
         return None
     _native.count("gemm_tn")

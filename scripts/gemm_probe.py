@@ -22,6 +22,8 @@ SHAPES = [  # name, M, N, K, act, dropout
     ("gpt2_out", 2032, 768, 768, 0, 0.0),
     ("vit_fc1_gelu", 6304, 3072, 768, 2, 0.0),
     ("lm256_fc1_relu_drop", 4064, 2048, 256, 1, 0.1),
+    ("llama_gateup_128tok", 128, 22016, 4096, 0, 0.0),  # Llama-2-7B LoRA forward (weight-streaming regime)
+    ("llama_qkv_128tok", 128, 12288, 4096, 0, 0.0),
 ]
 
 
@@ -53,7 +55,7 @@ def main():
         r = {"shape": name, "M": M, "N": N, "K": K, "act": act, "dropout": p,
              "vendor_us": round(gtime(ven), 2), "vendor_gemm_only_us": round(gtime(lambda: torch.addmm(b, x, w.t())), 2)}
         best = None
-        for tile in (-1, 0, 1, 2):
+        for tile in (-1, 0, 1, 2, 4, 5, 6, 7):
             for sp in (-1, 1, 2, 3, 4):
                 try:
                     us = gtime(lambda: C.gemm(x, w, bias=b, act=act, aux=aux, tile=tile, splits=sp, drop_p=p, rng=rng))

@@ -26,14 +26,22 @@ def _operands(M, N, K, a_tr, b_tr, dtype):
     return a, b, af @ bf.t()
 
 
+TILE_SHAPES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128), 7: (192, 128)}
+
+
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
-@pytest.mark.parametrize("tile", [0, 1, 2])
-@pytest.mark.parametrize("shape", [(256, 256, 64), (392, 776, 200), (1000, 264, 1032)])
+@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7])
+@pytest.mark.parametrize("shape", [(256, 256, 64), (392, 776, 200), (1000, 264, 1032), (2032, 768, 768)])
 def test_gemm_layouts_tiles_fp32_out(layout, tile, shape):
     M, N, K = shape
     a_tr, b_tr = layout[0] == "t", layout[1] == "n"
     torch.manual_seed(0)
     a, b, ref = _operands(M, N, K, a_tr, b_tr, torch.bfloat16)
+    bm, bn = TILE_SHAPES[tile]
+    if (a_tr and bm % 128) or (b_tr and bn % 128):
+        with pytest.raises(RuntimeError):  # a transposed operand needs 128-column tile sides
+            _C().gemm(a, b, a_tr=a_tr, b_tr=b_tr, out_dtype=torch.float32, tile=tile, splits=1)
+        return
     c = _C().gemm(a, b, a_tr=a_tr, b_tr=b_tr, out_dtype=torch.float32, tile=tile, splits=1)
     torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
 
@@ -54,7 +62,7 @@ def test_gemm_fp16_and_identity():
     n = 256
     a = torch.eye(n, device="cuda", dtype=torch.float16)
     b = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.float16)
-    for tile in (0, 1, 2):
+    for tile in (0, 1, 2, 4, 5, 6, 7):
         c = _C().gemm(a, b, out_dtype=torch.float32, tile=tile, splits=1)
         torch.testing.assert_close(c, b.float().t())
 
@@ -105,7 +113,7 @@ def test_gemm_strided_operands_and_auto_plan():
     torch.testing.assert_close(c.float(), x.float() @ w.float().t(), rtol=2e-2, atol=5e-2)
     for shape in [(6304, 768, 3072), (6304, 3072, 768), (768, 3072, 6304), (8192, 8192, 8192), (128, 4096, 4096)]:
         t, s = _C().gemm_plan(*shape)
-        assert 0 <= t <= 2 and s >= 1
+        assert 0 <= t <= 7 and t != 3 and s >= 1
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
@@ -166,3 +174,18 @@ def _captured_split_k(C, a, b, ref, K):
         torch.cuda.synchronize()
         assert torch.equal(out, eager)
     torch.testing.assert_close(eager, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+
+
+@pytest.mark.parametrize("tile", [4, 5, 6, 7])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_small_tiles_fused_epilogue_ragged(tile, splits):
+    """The grid-filling tiles with bias + GELU (+ aux) and split-K on a ragged GPT-2-like shape."""
+    M, N, K = 2032, 776, 1536
+    torch.manual_seed(4)
+    a, b, ref = _operands(M, N, K, False, False, torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y = _C().gemm(a, b, bias=bias, act=2, aux=aux, tile=tile, splits=splits)
+    z = ref + bias
+    torch.testing.assert_close(aux.float(), z, rtol=2e-2, atol=2e-2 * K ** 0.5)
+    torch.testing.assert_close(y.float(), torch.nn.functional.gelu(aux.float()), rtol=2e-2, atol=2e-2)
