@@ -46,11 +46,12 @@ def parse(argv=None):
     ap.add_argument("--graph-multi", type=int, default=1,
                     help="N>1: capture fwd+bwd and the optimizer as two hipGraphs around eager bucket all-reduces")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--ddp-schedule", default="segmented", choices=["auto", "segmented"],
+    ap.add_argument("--ddp-schedule", default="segmented", choices=["auto", "segmented", "graph"],
                     help="N>1 (or --ddp-world1) graphed DDP schedule: segmented (default) = the whole step "
                          "captured as graph segments with each bucket's all-reduce issue / wait as eager holes, "
                          "so every bucket overlaps the rest of the backward; auto = 3 graphs split at the "
-                         "model's graph_stages.  Measured at world 1 with the native RCCL communicator: "
+                         "model's graph_stages; graph = ONE graph with the RCCL all-reduces recorded into it.  "
+                         "Measured at world 1 with the native RCCL communicator: "
                          "5.15 vs 14.5 ms/step (profiles/r05/ddp_schedule_ab.json)")
     ap.add_argument("--ddp-world1", type=int, default=0,
                     help="A/B only: wrap the 1-GPU model in DDP with buckets and the native RCCL communicator "
@@ -105,7 +106,10 @@ def main(argv=None) -> int:
             from hyperion.parallel.comm import NativeComm
 
             _ensure_pg()  # a world-1 process group for the communicator's bootstrap
-            kw = dict(buckets_at_world_1=True, comm=NativeComm(dev))
+            # HYPERION_COMM=torch: torch.distributed's world-1 no-op all-reduce (isolates the
+            # segment-boundary cost from the native RCCL issue / wait)
+            comm = None if os.environ.get("HYPERION_COMM") == "torch" else NativeComm(dev)
+            kw = dict(buckets_at_world_1=True, comm=comm)
         model = DDP(model, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                     comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32, **kw)
     opt = FusedAdam(model.parameters(), lr=1e-3, zero_grad_in_step=True)
@@ -192,6 +196,8 @@ def main(argv=None) -> int:
                 "ddp_schedule": (None if (n_gpus == 1 and not args.ddp_world1) else
                                  f"segmented: {step.seg.num_segments} graph segments, bucket all-reduce holes"
                                  if step.seg is not None else
+                                 "one graph, bucket all-reduces captured on the comm stream"
+                                 if args.ddp_schedule == "graph" and use_graph else
                                  "3 graphs: top fwd+bwd | bottom bwd overlapping the top buckets' RCCL all-reduce | optimizer"
                                  if step.graph3 is not None else
                                  "2 graphs around eager bucket all-reduces" if step.graph2 is not None else
@@ -212,6 +218,8 @@ def main(argv=None) -> int:
             rec["replicas"] = replicas
         if smi is not None:
             rec["smi"] = smi.summary()
+        if os.environ.get("HYPERION_SEG_PROFILE") == "1" and getattr(step, "seg", None) is not None:
+            rec["seg_host_profile"] = step.seg.host_profile()
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:

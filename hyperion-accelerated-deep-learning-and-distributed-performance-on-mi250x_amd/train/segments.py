@@ -17,12 +17,15 @@ keeps its address on every replay; the actions must only touch persistent buffer
 """
 from __future__ import annotations
 
+import os
+import time
 import warnings
 from typing import Callable, List, Optional
 
 import torch
 
 _ACTIVE: Optional["SegmentedGraph"] = None
+_PROFILE = os.environ.get("HYPERION_SEG_PROFILE") == "1"
 
 
 def _capture_is_empty() -> bool:
@@ -59,6 +62,7 @@ class SegmentedGraph:
         # empty[i]: segment i recorded no work (two holes back to back, e.g. one unit's gather wait
         # and the next unit's gather issue): never replayed, so the holes run as one action
         self.empty: List[bool] = []
+        self.host_s: dict = {}
         self.stream: Optional[torch.cuda.Stream] = None
         self._pool = None
         self.out = None
@@ -124,14 +128,25 @@ class SegmentedGraph:
     def replay(self):
         s = self.stream
         s.wait_stream(torch.cuda.current_stream())
+        prof = _PROFILE
         with torch.cuda.stream(s):
             for i, g in enumerate(self.graphs):
+                t0 = time.perf_counter() if prof else 0.0
                 if not self.empty[i]:
                     g.replay()
+                if prof:
+                    t1 = time.perf_counter()
+                    self.host_s[("graph", i)] = self.host_s.get(("graph", i), 0.0) + t1 - t0
                 if i < len(self.actions):
                     self.actions[i]()
+                    if prof:
+                        self.host_s[("hole", i)] = self.host_s.get(("hole", i), 0.0) + time.perf_counter() - t1
         torch.cuda.current_stream().wait_stream(s)
         return self.out
+
+    def host_profile(self) -> dict:
+        """HYPERION_SEG_PROFILE=1: host seconds spent per graph replay / hole action, summed over replays."""
+        return {f"{k}{i}": round(v, 6) for (k, i), v in sorted(self.host_s.items(), key=lambda kv: -kv[1])}
 
     @property
     def num_segments(self) -> int:

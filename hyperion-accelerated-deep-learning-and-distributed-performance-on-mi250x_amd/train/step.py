@@ -71,8 +71,10 @@ class TrainStep:
         when the model exposes ``graph_stages``, else two graphs around the all-reduces;
         ``"segmented"`` = the whole step captured as segments with every bucket's all-reduce issue
         and wait as eager holes (``train/segments.py``): each bucket overlaps the rest of the
-        captured backward, at the cost of one graph launch per hole."""
-        if ddp_schedule not in ("auto", "segmented"):
+        captured backward, at the cost of one graph launch per hole; ``"graph"`` = ONE graph with
+        the bucket all-reduces recorded into it (the native RCCL communicator's comm stream forked
+        from and joined into the capture: no host holes at all)."""
+        if ddp_schedule not in ("auto", "segmented", "graph"):
             raise ValueError(f"ddp_schedule {ddp_schedule!r}")
         self.ddp_schedule = ddp_schedule
         self.seg = None
@@ -233,14 +235,16 @@ class TrainStep:
 
     def _capture_graphs(self) -> None:
         ddp = self._ddp()
-        if ddp is not None and self.ddp_schedule == "segmented":
+        if ddp is not None and self.ddp_schedule == "graph":
+            ddp = None  # the single-graph capture below records the all-reduces too
+        elif ddp is not None and self.ddp_schedule == "segmented":
             from .segments import SegmentedGraph
 
             seg = SegmentedGraph()
             self.static_loss = seg.capture(lambda: self._body(self.static_x, self.static_y))
             self.seg, self.graph = seg, seg.graphs[0]
             return
-        stages = self._stages()
+        stages = self._stages() if ddp is not None else None
         if ddp is not None and stages is not None:  # three graphs: top fwd+bwd | bottom bwd | optimizer
             g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
@@ -280,7 +284,7 @@ class TrainStep:
             if ddp is not None:
                 # graph schedules: the all-reduces run between the graphs; segmented: from the
                 # bucket hooks, as holes of the capture
-                ddp.defer_allreduce = self.ddp_schedule != "segmented"
+                ddp.defer_allreduce = self.ddp_schedule == "auto"
             self._capture(x, y)
         if x.data_ptr() != self.static_x.data_ptr():
             self.static_x.copy_(x, non_blocking=True)

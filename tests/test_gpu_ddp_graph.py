@@ -177,8 +177,8 @@ def test_two_rank_gloo_graph_step_replicas_identical(schedule):
         assert_update_parity(e["before"], g["after"], e["after"], rel=2e-2, what=f"rank {r}")
 
 
-@pytest.mark.parametrize("native", [False, True])
-def test_ddp_segmented_schedule_matches_eager(native):
+@pytest.mark.parametrize("native,schedule", [(False, "segmented"), (True, "segmented"), (True, "graph")])
+def test_ddp_segmented_schedule_matches_eager(native, schedule):
     """``TrainStep(ddp_schedule="segmented")``: the whole step captured as graph segments with the
     bucket all-reduces as eager holes (bench.py --ddp-schedule segmented).  Per-step losses and the
     parameter update over 4 steps equal the eager DDP step from the same start."""
@@ -208,16 +208,18 @@ def test_ddp_segmented_schedule_matches_eager(native):
             before = snapshot(ddp.module.named_parameters())
             opt = FusedAdam(ddp.parameters(), lr=1e-3, zero_grad_in_step=mode == "segmented")
             st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=mode == "segmented",
-                           warmup_iters=1, ddp_schedule="segmented")
+                           warmup_iters=1, ddp_schedule=schedule)
             losses = [float(st(xs[0], ys[0]))]  # graph mode: warm-up step + capture + replay = step 0 twice
             if mode == "eager":
                 losses = [float(st(xs[0], ys[0]))]
             for i in range(1, 4):
                 losses.append(float(st(xs[i], ys[i])))
             torch.cuda.synchronize()
-            if mode == "segmented":
+            if mode == "segmented" and schedule == "segmented":
                 # an issue and a wait hole per bucket (adjacent holes share one replayed segment boundary)
                 assert st.seg is not None and st.seg.num_holes >= len(ddp.bucket_sizes()) and st.seg.num_segments > 1
+            elif mode == "segmented":  # ONE graph, the RCCL all-reduces recorded into it
+                assert st.seg is None and st.graph is not None and st.graph2 is None
             res[mode] = (before, snapshot(ddp.module.named_parameters()), losses)
         (b0, a_seg, l_seg), (b1, a_eag, l_eag) = res["segmented"], res["eager"]
         assert all(torch.equal(b0[k], b1[k]) for k in b0)
