@@ -42,6 +42,41 @@ from .rope import rope_table
 
 WS_MAX_M = int(os.environ.get("HYPERION_WS_MAX_M", "512"))
 RANK_SPLITS = 4  # slices of the rank-r split-partial stacks (t: k-splits of lora_down, du: n-splits)
+# rank-r LoRA kernels on a side stream, concurrent with the weight-streaming GEMM that reads the
+# same activation (lora_down beside the projection, lora_bwd_t beside its data gradient) and with
+# the rest of the layer's backward (lora_bwd_a: its dA is only read by the optimizer) — 192
+# latency-bound ~7 us launches per Llama-2-7B step that otherwise serialise with the weight
+# stream.  Fork / join are stream-event edges, so a captured step keeps the overlap.  Measured
+# SLOWER (graphed Llama-2-7B LoRA step 16.5-16.7 vs 14.9 ms, scripts/gpu_r05s.sh): the rank-r
+# workgroups take CU slots from the weight stream and every join is a stream-event wait — opt-in.
+LORA_STREAM = os.environ.get("HYPERION_LORA_STREAM", "0") == "1"
+
+
+class _Side:
+    """Fork work onto the LoRA side stream and join it back (no-op when disabled / on CPU)."""
+
+    def __init__(self, dev: torch.device):
+        self.on = LORA_STREAM and dev.type == "cuda"
+        if self.on:
+            from .streams import side_stream
+
+            self.main = torch.cuda.current_stream(dev)
+            self.side = side_stream(dev)
+        self.pending = False
+
+    def run(self, fn) -> None:
+        if not self.on:
+            fn()
+            return
+        self.side.wait_stream(self.main)  # inputs produced so far on the main stream
+        with torch.cuda.stream(self.side):
+            fn()
+        self.pending = True
+
+    def join(self) -> None:
+        if self.on and self.pending:
+            self.main.wait_stream(self.side)
+            self.pending = False
 DEBUG: Optional[dict] = None  # tests / scripts: set to a dict to capture the backward intermediates
 
 
@@ -268,9 +303,12 @@ class _LlamaLayerFn(torch.autograd.Function):
             t_all = torch.empty(RANK_SPLITS, M, 4 * spec.r, device=dev, dtype=torch.float32)
             t_qkv = t_all[:, :, :3 * spec.r]
             du_bufs = torch.empty(RANK_SPLITS, M, 4 * spec.r, device=dev, dtype=torch.float32)
-            C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p)
+        side = _Side(dev)
+        if lora:
+            side.run(lambda: C.lora_down(h, [Aq, Ak, Av], t_qkv, rq, spec.p))
         pj = _Proj(C, h, spec.W_qkv)
         qkv = torch.empty(M, 3 * H, device=dev, dtype=dt)
+        side.join()
         pj.epi(C, M, 3 * H, 1, qkv, t=t_qkv, lw=[Bq, Bk, Bv] if lora else [], segw=H,
                       lscale=spec.c, rope_segs=2, seq=S, theta=spec.theta)
         q5 = qkv.view(Bsz, S, 3, spec.nh, spec.hd)
@@ -280,9 +318,10 @@ class _LlamaLayerFn(torch.autograd.Function):
         o2 = o.view(M, H)
         if lora:
             t_o = t_all[:, :, 3 * spec.r:]
-            C.lora_down(o2, [Ao], t_o, ro, spec.p)
+            side.run(lambda: C.lora_down(o2, [Ao], t_o, ro, spec.p))
         pj = _Proj(C, o2, spec.W_o)
         a = torch.empty(M, H, device=dev, dtype=dt)
+        side.join()
         pj.epi(C, M, H, 1, a, t=t_o, lw=[Bo] if lora else [], segw=H, lscale=spec.c)
         h2, s2, _, rstd2 = C.ln_fwd(a, s, spec.w2, None, spec.eps, True)
         pj = _Proj(C, h2, spec.W_gu)
@@ -323,15 +362,17 @@ class _LlamaLayerFn(torch.autograd.Function):
         # O projection (+ LoRA)
         grads = [None] * 8
         du_o = None
+        side = _Side(dev)
         if lora:
             du_o = du_bufs[:, :, 3 * spec.r:]
             dAo, dBo = torch.empty_like(Ao), torch.empty_like(Bo)
-            C.lora_bwd_t(dsum2, H, [Bo], [dBo], t_o, du_o, spec.c)
+            side.run(lambda: C.lora_bwd_t(dsum2, H, [Bo], [dBo], t_o, du_o, spec.c))
         pj = _Proj(C, dsum2, spec.W_o, True)
         do = torch.empty(M, H, device=dev, dtype=dt)
         if lora:
+            side.join()
             pj.epi(C, M, H, 4, do, t=du_o, lw=[Ao], rng=ro, p_drop=spec.p)
-            C.lora_bwd_a(o.view(M, H), [dAo], du_o, ro, spec.p)
+            side.run(lambda: C.lora_bwd_a(o.view(M, H), [dAo], du_o, ro, spec.p))  # joined at the end
             grads[6], grads[7] = dAo, dBo
         else:
             pj.epi(C, M, H, 0, do, nn=True)
@@ -353,16 +394,18 @@ class _LlamaLayerFn(torch.autograd.Function):
             du_qkv = du_bufs[:, :, :3 * spec.r]
             dA = [torch.empty_like(Aq), torch.empty_like(Ak), torch.empty_like(Av)]
             dB = [torch.empty_like(Bq), torch.empty_like(Bk), torch.empty_like(Bv)]
-            C.lora_bwd_t(dqkv, H, [Bq, Bk, Bv], dB, t_qkv, du_qkv, spec.c)
+            side.run(lambda: C.lora_bwd_t(dqkv, H, [Bq, Bk, Bv], dB, t_qkv, du_qkv, spec.c))
         pj = _Proj(C, dqkv, spec.W_qkv, True)
         dh = torch.empty(M, H, device=dev, dtype=dt)
         if lora:
+            side.join()
             pj.epi(C, M, H, 4, dh, t=du_qkv, lw=[Aq, Ak, Av], rng=rq, p_drop=spec.p)
-            C.lora_bwd_a(h, dA, du_qkv, rq, spec.p)
+            side.run(lambda: C.lora_bwd_a(h, dA, du_qkv, rq, spec.p))
             grads[0], grads[1], grads[2], grads[3], grads[4], grads[5] = dA[0], dB[0], dA[1], dB[1], dA[2], dB[2]
         else:
             pj.epi(C, M, H, 0, dh, nn=True)
         dsum1 = C.ln_bwd(dh, s, spec.w1, rstd1, rstd1, dsum2, False, False, True)[0]
+        side.join()  # dA of q/k/v and o: the gradients returned below are read on the main stream
         if DEBUG is not None:
             DEBUG.update(dgu=dgu, dh2=dh2, dsum2=dsum2, do=do, dqkv=dqkv, dh=dh, dsum1=dsum1, h=h, s=s, qkv=qkv, o=o,
                          s2=s2, gu=gu, dd=dd2, ds2=ds2c, t_qkv=_summed(t_qkv), t_o=_summed(t_o), du_o=_summed(du_o),
