@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--out", default="configs/conv_plans_mi355x.json")
     ap.add_argument("--raw", default="gpurun_out/conv_tune.json")
     ap.add_argument("--warm", action="store_true", help="time repeat loops (operands cache-resident)")
+    ap.add_argument("--dual", action="store_true",
+                    help="time every data-gradient plan INSIDE the fused data + weight gradient launch "
+                         "(conv_dgrad_wgrad, what the training step runs): no dgrad split-K there")
     a = ap.parse_args()
     global gtime
     if a.warm:
@@ -83,12 +86,16 @@ def main():
             geo = dict(stride=2, H=H, W=H) if s == 2 else {}
             nkd = R * R * K // 64
 
+            wgk = dict(wg_x=x, wg_R=R, wg_S=R, wg_sh=s, wg_sw=s, wg_ph=p, wg_pw=p)
+            dfn = C_.conv_dgrad_wgrad if a.dual else C_.conv_dgrad
+
             def dg(bm=-1, bn=-1, sp=-1, nb=0):
-                return C_.conv_dgrad(dy, w, p, p, bm, bn, sp, bn_x=yc, bn_mean=mean, bn_invstd=invstd, bn_mode=1,
-                                     bn_sums=bsums, stages=nb, **geo)
+                kw = dict(wgk) if a.dual else {}
+                return dfn(dy, w, p, p, bm, bn, sp, bn_x=yc, bn_mean=mean, bn_invstd=invstd, bn_mode=1,
+                           bn_sums=bsums, stages=nb, **geo, **kw)
 
             dgr = {}
-            for cfg in configs(nkd, strided_dgrad=s == 2):
+            for cfg in configs(nkd, strided_dgrad=s == 2 or a.dual):
                 bm, bn, sp, nb = cfg
                 dgr[cfg] = gtime(lambda: dg(bm, bn, sp, nb))
             auto = gtime(lambda: dg())
@@ -104,11 +111,12 @@ def main():
             add = torch.randn_like(x)
 
             def dg2(bm=-1, bn=-1, sp=-1, nb=0):
-                return C_.conv_dgrad(dy, w, p, p, bm, bn, sp, addend=add, bn_x=yc, bn_y=yy, bn_mean=mean,
-                                     bn_invstd=invstd, bn_mode=2, bn_sums=bsums, stages=nb, **geo)
+                kw = dict(wgk) if a.dual else {}
+                return dfn(dy, w, p, p, bm, bn, sp, addend=add, bn_x=yc, bn_y=yy, bn_mean=mean,
+                           bn_invstd=invstd, bn_mode=2, bn_sums=bsums, stages=nb, **geo, **kw)
 
             dg2r = {}
-            for cfg in configs(nkd, strided_dgrad=s == 2):
+            for cfg in configs(nkd, strided_dgrad=s == 2 or a.dual):
                 bm, bn, sp, nb = cfg
                 dg2r[cfg] = gtime(lambda: dg2(bm, bn, sp, nb))
             auto = gtime(lambda: dg2())
@@ -124,10 +132,12 @@ def main():
             geo = dict(stride=2, H=H, W=H) if (s == 2 and R > 1) else {}
             nkd = R * R * K // 64
             pd = {}
-            for cfg in configs(nkd, strided_dgrad=s == 2 and R > 1):
+            wgp = dict(wg_x=x, wg_R=R, wg_S=R, wg_sh=s, wg_sw=s, wg_ph=p, wg_pw=p) if a.dual else {}
+            dfp = C_.conv_dgrad_wgrad if a.dual else C_.conv_dgrad
+            for cfg in configs(nkd, strided_dgrad=(s == 2 and R > 1) or a.dual):
                 bm, bn, sp, nb = cfg
-                pd[cfg] = gtime(lambda: C_.conv_dgrad(dy, w, p, p, bm, bn, sp, stages=nb, **geo))
-            auto = gtime(lambda: C_.conv_dgrad(dy, w, p, p, **geo))
+                pd[cfg] = gtime(lambda: dfp(dy, w, p, p, bm, bn, sp, stages=nb, **geo, **wgp))
+            auto = gtime(lambda: dfp(dy, w, p, p, **geo, **wgp))
             best = min(pd, key=pd.get)
             row["dgrad"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(pd[best], 2)}
             Mg = N * P * P if s1x1 else N * H * H
