@@ -86,7 +86,8 @@ def _plan(op: str, M: int, K: int, C: int, R: int, S: int, stride: int):
                 with open(path) as f:
                     for pl in json.load(f).get("plans", []):
                         key = (pl["op"], pl["M"], pl["K"], pl["C"], pl["R"], pl["S"], pl["stride"])
-                        _PLANS[key] = (int(pl["bm"]), int(pl["bn"]), int(pl["splits"]), int(pl["stages"]))
+                        _PLANS[key] = (int(pl["bm"]), int(pl["bn"]), int(pl["splits"]), int(pl["stages"]),
+                                       int(pl.get("order", -1)))
             except (OSError, ValueError, KeyError):
                 _PLANS = {}
     return _PLANS.get((op, M, K, C, R, S, stride))
@@ -177,7 +178,8 @@ def _dual_call(Cn, wg: Optional[WgradRequest], dyc: torch.Tensor, w: torch.Tenso
     dx, wg.dw = Cn.conv_dgrad_wgrad(dyc, w, ph, pw, bm, bn, splits, wg_x=wg.x, wg_R=wg.R, wg_S=wg.S,
                                     wg_sh=wg.stride[0], wg_sw=wg.stride[1], wg_ph=wg.padding[0], wg_pw=wg.padding[1],
                                     wg_splits=pl[2] if pl is not None else -1, wg_defer=defer,
-                                    order=1 if _DUAL == "2" else 0, **kw)
+                                    order=(pl[4] if pl is not None and pl[4] >= 0 and _DUAL == "2"
+                                           else (1 if _DUAL == "2" else 0)), **kw)
     if defer:
         _defer_state["pending"] = True
     return dx

@@ -102,6 +102,24 @@ def main():
             best = min(dgr, key=dgr.get)
             row["dgrad_bnb"] = {"auto_us": round(auto, 2), "best": list(best), "best_us": round(dgr[best], 2),
                                 "all": {",".join(map(str, k)): round(v, 2) for k, v in dgr.items()}}
+            if a.dual:  # the fused launch's own knobs at that plan: weight-gradient split-K, grid order
+                bm0, bn0, sp0, nb0 = best
+                dual = {}
+                for wsp in (-1, 2, 4, 8, 16, 32):
+                    for order in (0, 1):
+                        try:
+                            dual[(wsp, order)] = gtime(lambda: C_.conv_dgrad_wgrad(
+                                dy, w, p, p, bm0, bn0, sp0, bn_x=yc, bn_mean=mean, bn_invstd=invstd, bn_mode=1,
+                                bn_sums=bsums, stages=nb0, order=order, **geo, **dict(wgk, wg_splits=wsp)))
+                        except RuntimeError:
+                            pass
+                if dual:
+                    bd = min(dual, key=dual.get)
+                    row["dual_knobs"] = {"best": list(bd), "best_us": round(dual[bd], 2),
+                                         "all": {",".join(map(str, k)): round(v, 2) for k, v in dual.items()}}
+                    plans.append({"op": "wgrad_dual", "M": N * P * P, "K": K, "C": C, "R": R, "S": R, "stride": s,
+                                  "pad": p, "bm": 64, "bn": 64, "splits": bd[0], "stages": 0, "order": bd[1],
+                                  "us": round(dual[bd], 2), "auto_us": round(dual.get((-1, 1), dual[bd]), 2)})
             plans.append({"op": "dgrad_bnb", "M": N * H * H, "K": C, "C": K, "R": R, "S": R, "stride": s, "pad": p,
                           "bm": best[0], "bn": best[1], "splits": best[2], "stages": best[3],
                           "us": round(dgr[best], 2), "auto_us": round(auto, 2)})
@@ -165,9 +183,10 @@ def main():
                               "bm": best[0], "bn": best[1], "splits": best[2], "stages": 0,
                               "us": round(wg[best], 2), "auto_us": round(auto, 2)})
         raw.append(row)
-        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad")}),
+        print(json.dumps({k: v for k, v in row.items() if k not in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad",
+                                                                     "dual_knobs")}),
               json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "all"} for k, v in row.items()
-                          if k in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad")}), flush=True)
+                          if k in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad", "dual_knobs")}), flush=True)
     doc = {"device": torch.cuda.get_device_name(), "batch": a.batch,
            "note": "native conv launch plans by GEMM shape (M = output pixels, K = output channels, C = "
                    "reduction channels); written by scripts/conv_tune.py",
@@ -176,7 +195,7 @@ def main():
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         with open(path, "w") as f:
             json.dump(obj, f, indent=1)
-    for op in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad"):
+    for op in ("fwd", "dgrad_bnb", "dgrad_bnb2", "dgrad", "wgrad", "wgrad_dual"):
         ps = [pl for pl in plans if pl["op"] == op]
         print(json.dumps({"op": op, "n": len(ps), "sum_auto_us": round(sum(pl["auto_us"] for pl in ps), 1),
                           "sum_best_us": round(sum(pl["us"] for pl in ps), 1)}))
