@@ -338,6 +338,10 @@ hipError_t conv_wgrad_prepare(WgradArgs* a, int dtype, const DualWgrad& d, const
 void conv_dual_set_order(int order);
 // persistent conv launches (conv_persist.h) for the variants they cover: 0 off, 1 on
 void conv_set_persist(int on);
+// BN apply / dx pass grid (bn_act.hip): row-block cap and minimum row iterations per thread
+int bn_apply_blocks();
+int bn_min_iters();
+void bn_set_geom(int apply_blocks, int min_iters);
 // bn_wgrad.hip: the BatchNorm backward dx pass of a layer (bn_backward_dx's arguments) and the weight
 // gradient d of the conv ABOVE it (whose dY the previous backward step produced) in ONE launch —
 // the cheap, memory-bound dx pass runs beside the weight gradient's K loops instead of alone

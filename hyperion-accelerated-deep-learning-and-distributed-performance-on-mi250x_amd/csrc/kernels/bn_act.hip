@@ -465,7 +465,7 @@ hipError_t bn_forward(int dtype, const void* x, const void* res, void* y, int64_
                                 sums, save_mean, save_invstd, stream);
   }
   BnGeom ga;
-  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  if (!apply_geom(M, C, ga)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_eval_consts_k, dim3((C + 255) / 256), dim3(256), 0, stream, C, weight, bias, running_mean,
                      running_var, eps, save_mean, save_invstd, scale, shift);
   HYP_DISPATCH_FLOAT(dtype, T, {
@@ -482,7 +482,7 @@ hipError_t bn_forward_from_sums(int dtype, const void* x, const void* res, void*
                                 float momentum, float eps, int act, const double* sums, float* save_mean,
                                 float* save_invstd, hipStream_t stream) {
   BnGeom ga;
-  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  if (!apply_geom(M, C, ga)) return hipErrorInvalidValue;
   const FwdFin fin{sums,        weight,     bias, running_mean, running_var, momentum, eps, save_mean,
                    save_invstd, 1.0 / (double)M, M > 1 ? (double)M / (double)(M - 1) : 1.0};
   HYP_DISPATCH_FLOAT(dtype, T, {
@@ -515,7 +515,7 @@ hipError_t bn_backward(int dtype, const void* dy, const void* x, const void* y, 
                        const float* weight, const float* bias, const float* save_mean, const float* save_invstd,
                        int training, int act, double* sums, float* dweight, float* dbias, hipStream_t stream) {
   BnGeom gs, ga;
-  if (!stats_geom(M, C, gs) || !bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  if (!stats_geom(M, C, gs) || !apply_geom(M, C, ga)) return hipErrorInvalidValue;
   // act with no forward output given: recompute the ReLU mask from x (training stats only: the
   // eval-mode constants are running stats, which the mask recomputation below does not model)
   const bool maskx = act && y == nullptr;
@@ -548,13 +548,21 @@ hipError_t bn_backward_dx(int dtype, const void* dz, const void* x, void* dx, in
                           const float* save_mean, const float* save_invstd, int training, const double* sums,
                           float* dweight, float* dbias, hipStream_t stream) {
   BnGeom ga;
-  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  if (!apply_geom(M, C, ga)) return hipErrorInvalidValue;
   const BwdFin fin{weight, save_mean, save_invstd, training, dweight, dbias, sums, 1.0 / (double)M};
   HYP_DISPATCH_FLOAT(dtype, T, {
     launch_bn_dx<T>(false, false, false, dim3(ga.P, ga.gy), stream, static_cast<const T*>(dz),
                     static_cast<const T*>(x), nullptr, static_cast<T*>(dx), nullptr, fin, M, C, ga, nullptr);
   });
   return hipGetLastError();
+}
+
+int g_bn_apply_blocks = 2048, g_bn_min_iters = 4;
+int bn_apply_blocks() { return g_bn_apply_blocks; }
+int bn_min_iters() { return g_bn_min_iters; }
+void bn_set_geom(int apply_blocks, int min_iters) {
+  g_bn_apply_blocks = apply_blocks > 0 ? apply_blocks : 2048;
+  g_bn_min_iters = min_iters > 0 ? min_iters : 4;
 }
 
 }  // namespace hyp

@@ -15,6 +15,7 @@ constexpr int kStatsBlocks = 512;  // row blocks of the statistics kernels (= at
 constexpr int kFinCh = 256;        // channels per apply / dx block: one inline-finalized channel per thread
 constexpr int kApplyBlocks = 2048;
 
+
 struct BnGeom {
   int tpr;   // threads per row (each owns 8 channels)
   int rpi;   // rows per block-iteration
@@ -25,7 +26,7 @@ struct BnGeom {
 
 // max_tpr: channel-vectors per block row (the apply / dx kernels cap a block at kFinCh channels,
 // so their inline finalize is one channel per thread)
-bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g, int max_tpr = kBlock) {
+bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g, int max_tpr = kBlock, int min_iters = 4) {
   if (C % 8 != 0) return false;
   const int cv = C / 8;
   if (cv <= max_tpr) {
@@ -39,7 +40,7 @@ bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g, int max_tpr = kBlock) 
   g.rpi = kBlock / g.tpr;
   // >= 4 row iterations per thread, and >= 16K elements per block so each block's atomics are a
   // tiny fraction of its traffic
-  int64_t min_rows = (int64_t)g.rpi * 4;
+  int64_t min_rows = (int64_t)g.rpi * min_iters;
   const int64_t by_size = (16384 + C - 1) / C;
   if (max_blocks <= kStatsBlocks && by_size > min_rows) min_rows = by_size;
   int64_t want = (M + min_rows - 1) / min_rows;
@@ -52,6 +53,10 @@ bool bn_geom(int64_t M, int C, int max_blocks, BnGeom& g, int max_tpr = kBlock) 
   if (g.P < 1) g.P = 1;
   return true;
 }
+
+// the apply / dx passes' grid: <= bn_apply_blocks() row blocks, >= bn_min_iters() row iterations
+// per thread (bn_set_geom: A/B sweeps; defaults kApplyBlocks and 4)
+bool apply_geom(int64_t M, int C, BnGeom& g) { return bn_geom(M, C, bn_apply_blocks(), g, kFinCh / 8, bn_min_iters()); }
 
 struct BwdFin {
   const float* weight;

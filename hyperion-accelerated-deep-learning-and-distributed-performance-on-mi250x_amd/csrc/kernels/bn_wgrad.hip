@@ -84,7 +84,7 @@ hipError_t bn_backward_dx_wgrad(int dtype, const void* dz, const void* x, void* 
                                 const void* zero, hipStream_t stream) {
   if (dtype != kBF16) return hipErrorNotSupported;
   BnGeom ga;
-  if (!bn_geom(M, C, kApplyBlocks, ga, kFinCh / 8)) return hipErrorInvalidValue;
+  if (!apply_geom(M, C, ga)) return hipErrorInvalidValue;
   WgradArgs w;
   hipError_t e = conv_wgrad_prepare(&w, dtype, d, zero);
   if (e != hipSuccess) return e;

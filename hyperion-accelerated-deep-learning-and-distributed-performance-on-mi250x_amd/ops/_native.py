@@ -53,6 +53,9 @@ def _load():
         _MOD.conv_set_persist(int(os.environ["HYPERION_CONV_PERSIST"]))  # persistent fwd/dgrad convs (A/B)
     if _MOD is not None and os.environ.get("HYPERION_SPLITK_INKERNEL") and hasattr(_MOD, "gemm_set_splitk_inkernel"):
         _MOD.gemm_set_splitk_inkernel(int(os.environ["HYPERION_SPLITK_INKERNEL"]))  # 0: separate reduce (A/B)
+    if _MOD is not None and os.environ.get("HYPERION_BN_GEOM") and hasattr(_MOD, "bn_set_geom"):
+        b, it = (int(v) for v in os.environ["HYPERION_BN_GEOM"].split(","))  # "blocks,iters" (A/B)
+        _MOD.bn_set_geom(b, it)
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")
