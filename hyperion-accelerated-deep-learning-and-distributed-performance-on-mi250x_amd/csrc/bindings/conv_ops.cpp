@@ -976,6 +976,8 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("wg_sw"), pybind11::arg("wg_ph"), pybind11::arg("wg_pw"), pybind11::arg("wg_bm") = 64,
         pybind11::arg("wg_bn") = 64, pybind11::arg("wg_splits") = -1, pybind11::arg("wg_defer") = false,
         pybind11::arg("wg_out") = pybind11::none());
+  m.def("conv_set_group", [](int64_t mode) { hyp::conv_set_group((int)mode); },
+        "A/B: conv tile-order group (M-tiles per L2 group): 0 model, > 0 fixed, -1 x2, -2 x0.5");
   m.def("bn_set_geom", [](int64_t blocks, int64_t iters) { hyp::bn_set_geom((int)blocks, (int)iters); },
         "A/B: BN apply / dx pass grid — row-block cap (default 2048) and min row iterations per thread (4)");
   m.def("conv_set_persist", [](int64_t on) { hyp::conv_set_persist((int)on); },

@@ -338,6 +338,7 @@ hipError_t conv_wgrad_prepare(WgradArgs* a, int dtype, const DualWgrad& d, const
 void conv_dual_set_order(int order);
 // persistent conv launches (conv_persist.h) for the variants they cover: 0 off, 1 on
 void conv_set_persist(int on);
+void conv_set_group(int mode);  // tile-order group: 0 model, > 0 fixed, -1 x2, -2 x0.5 (A/B)
 // BN apply / dx pass grid (bn_act.hip): row-block cap and minimum row iterations per thread
 int bn_apply_blocks();
 int bn_min_iters();

@@ -125,11 +125,18 @@ bool conv_fwd_supported(int C, int K) { return C % 64 == 0 && K % 8 == 0; }
 // filter slice is R*S*BN/BM times an activation slice; the footprint group*a + (T/8/group)*b is
 // smallest at group = sqrt(T*b / (8a)).  (ResNet layer4 3x3: 200 tiles -> group 15; the old fixed
 // 8 made every XCD stream all 4.7 MB of filter through a 4 MB L2.)
+int g_group_mode = 0;  // conv_set_group (A/B sweeps): 0 the model below, > 0 fixed, -1 x2, -2 x0.5
+
 int conv_fwd_group(int M, int K, int RS, int bm, int bn) {
   const int tm = (M + bm - 1) / bm, tn = (K + bn - 1) / bn;
-  const double g = sqrt((double)tm * tn * RS * bn / (8.0 * bm));
+  double g = sqrt((double)tm * tn * RS * bn / (8.0 * bm));
+  if (g_group_mode > 0) g = g_group_mode;
+  else if (g_group_mode == -1) g *= 2.0;
+  else if (g_group_mode == -2) g *= 0.5;
   return max(1, min(tm, (int)(g + 0.5)));
 }
+
+void conv_set_group(int mode) { g_group_mode = mode; }
 
 void conv_set_stamps(void* buf) { g_stamps = static_cast<unsigned long long*>(buf); }
 

@@ -56,6 +56,8 @@ def _load():
     if _MOD is not None and os.environ.get("HYPERION_BN_GEOM") and hasattr(_MOD, "bn_set_geom"):
         b, it = (int(v) for v in os.environ["HYPERION_BN_GEOM"].split(","))  # "blocks,iters" (A/B)
         _MOD.bn_set_geom(b, it)
+    if _MOD is not None and os.environ.get("HYPERION_CONV_GROUP") and hasattr(_MOD, "conv_set_group"):
+        _MOD.conv_set_group(int(os.environ["HYPERION_CONV_GROUP"]))  # tile-order group sweep (A/B)
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")

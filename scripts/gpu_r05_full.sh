@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 5: the whole GPU test suite (what the driver runs at round end), one pytest process
+set -o pipefail
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/r05full; mkdir -p $O
+timeout -k 10 1100 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+rc=$?
+grep -E "FAILED|ERROR" $O/pytest.log | head -20
+tail -3 $O/pytest.log
+exit $rc
