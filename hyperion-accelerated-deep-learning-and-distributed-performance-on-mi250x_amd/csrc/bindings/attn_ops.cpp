@@ -205,7 +205,7 @@ std::vector<at::Tensor> ln_fwd(const at::Tensor& x, const c10::optional<at::Tens
 std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, const c10::optional<at::Tensor>& weight,
                                const at::Tensor& mean, const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
                                bool need_dw, bool need_db, bool rms, double drop_p,
-                               const c10::optional<at::Tensor>& rng, bool branch_sum) {
+                               const c10::optional<at::Tensor>& rng, bool branch_sum, int64_t bsum_dtype) {
   const int d = xin.size(-1);
   const int64_t rows = xin.numel() / d;
   at::Tensor g = dy.is_contiguous() ? dy : dy.contiguous();
@@ -220,7 +220,15 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
   auto wopt = wt ? xin.options() : fopt;  // dγ / dβ in the weight's dtype
   // LayerNorm: dγ and dβ come out of one combine pass into one [2, d] buffer (both computed)
   at::Tensor dw, db, dwdb, dbs;
-  if (branch_sum) {  // [dγ | dβ | Σ branch gradient] (RMS: [dγ | Σ]) from one combine
+  // bsum_dtype (>= 0, a DTYPE_CODE): the branch sums in the consuming linear's bias dtype, their own
+  // buffer written by the same combine (no cast kernel after it when the norm keeps fp32 weights)
+  const bool own_bs = branch_sum && bsum_dtype >= 0 && bsum_dtype != dtype_code(wopt.dtype().toScalarType());
+  if (own_bs) {
+    dwdb = at::empty({rms ? 1 : 2, d}, wopt);
+    dw = dwdb[0];
+    if (!rms) db = dwdb[1];
+    dbs = at::empty({d}, xin.options().dtype(scalar_of_code(bsum_dtype)));
+  } else if (branch_sum) {  // [dγ | dβ | Σ branch gradient] (RMS: [dγ | Σ]) from one combine
     dwdb = at::empty({rms ? 2 : 3, d}, wopt);
     dw = dwdb[0];
     if (!rms) db = dwdb[1];
@@ -249,7 +257,7 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
                                         dw.defined() ? dw.data_ptr() : nullptr, db.defined() ? db.data_ptr() : nullptr,
                                         rows, d, P, rpw, cur_stream(), wt, dxa.defined() ? dxa.data_ptr() : nullptr,
                                         (float)drop_p, drop_p > 0.0 ? &rs : nullptr,
-                                        dbs.defined() ? dbs.data_ptr() : nullptr));
+                                        dbs.defined() ? dbs.data_ptr() : nullptr, own_bs ? (int)bsum_dtype : -1));
   return {dx, need_dw ? dw : at::Tensor(), need_db ? db : at::Tensor(), dxa, dbs};
 }
 
@@ -266,7 +274,7 @@ void register_attn_ops(pybind11::module& m) {
         pybind11::arg("xin"), pybind11::arg("weight"), pybind11::arg("mean"), pybind11::arg("rstd"),
         pybind11::arg("dres"), pybind11::arg("need_dw"), pybind11::arg("need_db"), pybind11::arg("rms"),
         pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none(),
-        pybind11::arg("branch_sum") = false);
+        pybind11::arg("branch_sum") = false, pybind11::arg("bsum_dtype") = -1);
 }
 
 }  // namespace hypbind

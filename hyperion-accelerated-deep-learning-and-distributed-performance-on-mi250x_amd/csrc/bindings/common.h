@@ -16,8 +16,8 @@ hyp::RngState unpack_rng(const at::Tensor& t);
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-inline int dtype_code(const at::Tensor& t) {
-  switch (t.scalar_type()) {
+inline int dtype_code(at::ScalarType t) {
+  switch (t) {
     case at::kFloat:
       return hyp::kF32;
     case at::kBFloat16:
@@ -25,8 +25,15 @@ inline int dtype_code(const at::Tensor& t) {
     case at::kHalf:
       return hyp::kF16;
     default:
-      TORCH_CHECK(false, "hyperion: unsupported dtype ", t.scalar_type());
+      TORCH_CHECK(false, "hyperion: unsupported dtype ", t);
   }
+}
+
+inline int dtype_code(const at::Tensor& t) { return dtype_code(t.scalar_type()); }
+
+inline at::ScalarType scalar_of_code(int64_t code) {
+  TORCH_CHECK(code == hyp::kF32 || code == hyp::kBF16 || code == hyp::kF16, "hyperion: bad dtype code ", code);
+  return code == hyp::kF32 ? at::kFloat : (code == hyp::kBF16 ? at::kBFloat16 : at::kHalf);
 }
 
 #define HYP_CHECK_HIP(expr)                                                                          \

@@ -72,10 +72,11 @@ hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xi
                               const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
                               void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt = 0,
                               void* dxa = nullptr, float drop_p = 0.f, const struct RngState* rs = nullptr,
-                              void* dbs = nullptr);
-// dbs (d <= 2048): also Σ_rows of the branch gradient as stored (dxa when dropping, else dx), in the
-// weight dtype, at dw + d (no bias) or dw + 2d (with db) — the bias gradient of the linear layer
-// that produced the norm's input, combined in the same launch as dγ / dβ
+                              void* dbs = nullptr, int dbs_dtype = -1);
+// dbs (d <= 2048): also Σ_rows of the branch gradient as stored (dxa when dropping, else dx) — the
+// bias gradient of the linear layer that produced the norm's input, combined in the same launch as
+// dγ / dβ.  dbs_dtype < 0: the weight dtype, at dw + d (no bias) or dw + 2d (with db); else any
+// buffer of that dtype (the linear's bias dtype: no cast kernel when the norm keeps fp32 weights)
 }  // namespace hyp
 
 namespace hyp {
@@ -369,6 +370,9 @@ hipError_t mse_fwd_bwd(int dtype, const void* x, const float* t, int64_t n, floa
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,
                       hipStream_t st, int* tickets = nullptr);
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st);
+// columns [0, split) into out (out_dtype), [split, N) into out2 (out2_dtype); split % 4 == 0
+hipError_t colsum_combine_split(const float* part, int P, int N, void* out, int out_dtype, int split, void* out2,
+                                int out2_dtype, hipStream_t st);
 // dy = dh·act'(z) (act 1: ReLU with z = output; 2: exact GELU with z = pre-activation) and its column
 // sums into db (out_dtype; null: skip) — the FFN activation backward + bias gradient.
 // drop_p > 0: dh is the gradient of dropout(act(z)) (dropout.hip mask of *rs, element index r*N + c)

@@ -550,12 +550,13 @@ template <typename T, bool RMS>
 hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const float* mean, const float* rstd,
                            const T* dres, T* dx, float* pdw, float* pdb, void* dw, void* db, int64_t rows, int d,
                            int P, int rows_per_wave, hipStream_t st, int wt, int wdt, T* dxa, const LnDrop* drop,
-                           void* dbs) {
+                           void* dbs, int dbs_dt) {
   if (drop != nullptr && (d > 2048 || dxa == nullptr)) return hipErrorInvalidValue;
   if (dbs != nullptr) {  // the branch-gradient sums follow dw (| db) in the combined output
     const size_t wb = wdt == kF32 ? 4 : 2;
     if (d > 2048 || dw == nullptr ||
-        static_cast<char*>(dbs) != static_cast<char*>(dw) + (size_t)(pdb != nullptr ? 2 : 1) * d * wb)
+        (dbs_dt < 0 &&
+         static_cast<char*>(dbs) != static_cast<char*>(dw) + (size_t)(pdb != nullptr ? 2 : 1) * d * wb))
       return hipErrorInvalidValue;
     if (pdb != nullptr) pdb = pdw + d;
     const int bs_off = pdb != nullptr ? 2 * d : d;
@@ -589,7 +590,9 @@ hipError_t ln_bwd_dispatch(const T* dy, const T* xin, const float* w, const floa
     }
 #undef HYP_LN_BS
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = colsum_combine(pdw, P, bs_off + d, dw, wdt, st);
+    if (e == hipSuccess)
+      e = dbs_dt < 0 ? colsum_combine(pdw, P, bs_off + d, dw, wdt, st)
+                     : colsum_combine_split(pdw, P, bs_off + d, dw, wdt, bs_off, dbs, dbs_dt, st);
     return e;
   }
   // with a bias: dγ and dβ partials interleave per block row ([P][2d]) and ONE combine writes
@@ -707,7 +710,7 @@ hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, v
 hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xin, const float* w, const float* mean,
                               const float* rstd, const void* dres, void* dx, float* pdw, float* pdb, void* dw,
                               void* db, int64_t rows, int d, int P, int rows_per_wave, hipStream_t st, int wt,
-                              void* dxa, float drop_p, const RngState* rs, void* dbs) {
+                              void* dxa, float drop_p, const RngState* rs, void* dbs, int dbs_dtype) {
   const int wdt = wt ? dtype : kF32;  // dγ / dβ in the weight's dtype
   if (!layernorm_supported(d)) return hipErrorInvalidValue;
   if (drop_p > 0.f && (rs == nullptr || drop_p >= 1.f || dxa == nullptr)) return hipErrorInvalidValue;
@@ -716,9 +719,9 @@ hipError_t layernorm_backward(int dtype, int rms, const void* dy, const void* xi
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (rms)
       return ln_bwd_dispatch<T, true>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                      db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr, dbs);
+                                      db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr, dbs, dbs_dtype);
     return ln_bwd_dispatch<T, false>((const T*)dy, (const T*)xin, w, mean, rstd, (const T*)dres, (T*)dx, pdw, pdb, dw,
-                                     db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr, dbs);
+                                     db, rows, d, P, rows_per_wave, st, wt, wdt, (T*)dxa, dptr, dbs, dbs_dtype);
   });
   return hipSuccess;
 }

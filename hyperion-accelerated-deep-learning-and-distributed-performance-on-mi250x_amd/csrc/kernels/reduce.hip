@@ -199,9 +199,12 @@ __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict
   if (tickets != nullptr) colsum_last_block(part, N, tickets + blockIdx.y, out, odt, &red[0][0]);
 }
 
-template <typename O>
+// columns [0, split) go to out, [split, N) to out2 (its own dtype): a norm's dγ | dβ and the
+// producing linear's bias gradient (the linear's dtype) from one combine, no cast kernel after it
+template <typename O, typename O2 = O>
 __global__ __launch_bounds__(kThreads) void colsum_final_k(const float* __restrict__ part, int P, int N,
-                                                           O* __restrict__ out) {
+                                                           O* __restrict__ out, int split = 1 << 30,
+                                                           O2* __restrict__ out2 = nullptr) {
   __shared__ float red[kFinLanes][64];
   const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
   const int c = blockIdx.x * 64 + tx * 4;
@@ -237,7 +240,8 @@ __global__ __launch_bounds__(kThreads) void colsum_final_k(const float* __restri
       float a = 0.f;
 #pragma unroll
       for (int l = 0; l < kFinLanes; ++l) a += red[l][threadIdx.x];
-      st1<O>(out + cc, a);
+      if (cc < split) st1<O>(out + cc, a);
+      else st1<O2>(out2 + (cc - split), a);
     }
   }
 }
@@ -276,6 +280,33 @@ hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dt
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+template <typename O>
+static hipError_t combine_split_to(const float* part, int P, int N, O* out, int split, void* out2, int dt2,
+                                   hipStream_t st) {
+  const dim3 grid((N + 63) / 64);
+  if (dt2 == kF32)
+    hipLaunchKernelGGL((colsum_final_k<O, float>), grid, dim3(kThreads), 0, st, part, P, N, out, split,
+                       static_cast<float*>(out2));
+  else if (dt2 == kBF16)
+    hipLaunchKernelGGL((colsum_final_k<O, bf16_t>), grid, dim3(kThreads), 0, st, part, P, N, out, split,
+                       static_cast<bf16_t*>(out2));
+  else if (dt2 == kF16)
+    hipLaunchKernelGGL((colsum_final_k<O, f16_t>), grid, dim3(kThreads), 0, st, part, P, N, out, split,
+                       static_cast<f16_t*>(out2));
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t colsum_combine_split(const float* part, int P, int N, void* out, int out_dtype, int split, void* out2,
+                                int out2_dtype, hipStream_t st) {
+  if (N % 4 != 0 || P < 1 || split % 4 != 0 || split < 0 || split > N) return hipErrorInvalidValue;
+  if (out_dtype == kF32) return combine_split_to(part, P, N, static_cast<float*>(out), split, out2, out2_dtype, st);
+  if (out_dtype == kBF16) return combine_split_to(part, P, N, static_cast<bf16_t*>(out), split, out2, out2_dtype, st);
+  if (out_dtype == kF16) return combine_split_to(part, P, N, static_cast<f16_t*>(out), split, out2, out2_dtype, st);
+  return hipErrorInvalidValue;
 }
 
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,

@@ -149,6 +149,19 @@ def use_native(*tensors: torch.Tensor, op: Optional[str] = None) -> bool:
     return True
 
 
+# fp32 eager layers on the vendor ops (A/B: HYPERION_FP32_FUSED=1 keeps the fused autograd Functions).
+# fp32 is outside the MFMA bf16/fp16 kernels: the fused Functions then only save an epilogue launch
+# (bias+ReLU, dropout) and cost ~20-30 us of Python host time each per forward+backward — the fp32
+# CustomTransformer row (512 tokens, launch-bound) ran 5.66 ms vs torch's 4.13 ms through them
+# (profiles/r05/ct32_host_profile_*.txt).
+PLAIN_FP32 = os.environ.get("HYPERION_FP32_FUSED", "0") != "1"
+
+
+def plain_fp32(x: torch.Tensor) -> bool:
+    """True when a linear / linear+activation on ``x`` should run as plain vendor ops (fp32 eager)."""
+    return PLAIN_FP32 and x.dtype == torch.float32 and not torch.is_autocast_enabled(x.device.type)
+
+
 _COUNTS: dict = {}
 
 

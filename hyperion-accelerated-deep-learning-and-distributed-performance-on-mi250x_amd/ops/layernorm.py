@@ -49,10 +49,11 @@ class BiasGradLink:
     here; the linear's backward uses it when the gradient it receives IS that tensor (else it sums
     dy itself).  ``armed`` is set by the linear (it has a bias and ran the native path)."""
 
-    __slots__ = ("armed", "db", "g")
+    __slots__ = ("armed", "db", "g", "dtype")
 
     def __init__(self):
         self.armed = False
+        self.dtype = None  # the linear's bias dtype: the kernel writes the sums in it (no cast)
         self.db = None
         self.g = None
 
@@ -104,8 +105,9 @@ class _LNFn(torch.autograd.Function):
         p, st = ctx.drop
         blink = ctx.blink
         bsum = blink is not None and blink.armed and ctx.needs_input_grad[0]
+        bdt = _native.DTYPE_CODE.get(blink.dtype, -1) if bsum else -1
         dx, dw, db, dxa, dbs = _native.native().ln_bwd(dy, xin, weight, mean, rstd, ds, need_dw, need_db, ctx.rms, p,
-                                                       st, bsum)
+                                                       st, bsum, bdt)
         if bsum and dbs is not None:
             blink.db, blink.g = dbs, (dxa if p > 0.0 else dx)
         dres = dx if ctx.has_res and ctx.needs_input_grad[1] else None

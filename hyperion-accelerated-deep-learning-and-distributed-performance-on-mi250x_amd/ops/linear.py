@@ -137,6 +137,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.blink = blink
         if blink is not None and b is not None:
             blink.armed = True  # the consuming norm's backward will sum our output's gradient
+            blink.dtype = b.dtype
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -165,7 +166,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, l
     autocast, x and w are cast to the autocast dtype first (differentiable casts, like torch's own
     autocast of ``F.linear``), so the native kernels serve the AMP trainers too.  ``link``: a
     ``ResidualLink`` on x (see :func:`arm_link`)."""
-    if not (x.is_cuda and _native.use_native(x, op="linear")):
+    if not (x.is_cuda and _native.use_native(x, op="linear")) or _native.plain_fp32(x):
         return F.linear(x, w, b)
     if torch.is_autocast_enabled(x.device.type):
         dt = torch.get_autocast_dtype(x.device.type)

@@ -142,6 +142,7 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], acti
     """``dropout(act(x Wᵀ + b))`` — pass ``dropout_p`` only in training (applied whenever > 0).
     ``link``: a ``ResidualLink`` on x (its parked residual gradient rides the data-gradient GEMM)."""
     native_drop = dropout_p == 0.0 or (x.is_cuda and _native.use_native(x, op="dropout") and dropout_p < 1.0)
+    native_drop = native_drop and not _native.plain_fp32(x)
     fn = None
     if activation == "relu" and x.is_cuda and b is not None and native_drop:
         fn = _LinearReLU

@@ -370,3 +370,59 @@ def test_vit_bias_grads_from_norm_backward(monkeypatch, ckpt):
     for n in res[0][0]:
         a, b = res[1][0][n].float(), res[0][0][n].float()
         assert float((a - b).norm() / (b.norm() + 1e-12)) < 2e-2, n
+
+
+def test_ln_bwd_branch_sums_in_bias_dtype():
+    """fp32 LayerNorm weights (cast_for_compute keeps norms fp32) with a bf16 producing linear: the
+    branch-gradient sums come out of the same combine in bf16 (``bsum_dtype``) — no cast kernel —
+    and equal the column sums of the returned gradient; dγ / dβ stay fp32."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    torch.manual_seed(0)
+    rows, d = 1000, 768
+    x = torch.randn(rows, d, device="cuda").bfloat16()
+    w = torch.randn(d, device="cuda") * 0.5 + 1.0
+    b = torch.randn(d, device="cuda") * 0.1
+    y, _, mean, rstd = C.ln_fwd(x, None, w, b, 1e-5, False)
+    dy = torch.randn(rows, d, device="cuda").bfloat16()
+    ref = C.ln_bwd(dy, x, w, mean, rstd, None, True, True, False, 0.0, None, True)
+    out = C.ln_bwd(dy, x, w, mean, rstd, None, True, True, False, 0.0, None, True, _native.DTYPE_CODE[torch.bfloat16])
+    dx, dw, db, _, dbs = out
+    assert dbs.dtype == torch.bfloat16 and dw.dtype == torch.float32 and db.dtype == torch.float32
+    assert ref[4].dtype == torch.float32  # default: the weight dtype, packed after dγ | dβ
+    torch.testing.assert_close(dx, ref[0], rtol=0, atol=0)
+    torch.testing.assert_close(dw, ref[1], rtol=0, atol=0)
+    torch.testing.assert_close(db, ref[2], rtol=0, atol=0)
+    torch.testing.assert_close(dbs.float(), ref[4].bfloat16().float(), rtol=0, atol=0)
+    torch.testing.assert_close(dbs.float(), dx.float().sum(0), rtol=2e-2, atol=2e-2)
+
+
+def test_vit_compute_copies_bias_grads_without_cast(monkeypatch):
+    """ViT with bf16 compute copies and fp32 norms (the bench's cast_for_compute): the fused bias
+    gradients arrive in the bias dtype and match the unfused column sums."""
+    from hyperion.models.vit import VisionTransformer
+    from hyperion.ops import _native
+    from hyperion.ops import layernorm as ln_mod
+    from hyperion.train.amp import cast_for_compute
+
+    torch.manual_seed(0)
+    m = VisionTransformer(64, 16, 3, 4, 256, 512, num_classes=10).cuda()
+    cast_for_compute(m, torch.bfloat16)
+    assert m.encoder.ln.weight.dtype == torch.float32 and m.heads.head.weight.dtype == torch.bfloat16
+    x0 = torch.randn(4, 3, 64, 64, device="cuda").bfloat16()
+    res = []
+    for fuse in (False, True):
+        monkeypatch.setattr(ln_mod, "FUSE_BIAS_GRAD", fuse)
+        m.zero_grad(set_to_none=True)
+        _native.reset_counters()
+        m(x0).float().square().mean().backward()
+        torch.cuda.synchronize()
+        res.append(({n: q.grad.clone() for n, q in m.named_parameters() if q.grad is not None},
+                    dict(_native.counters())))
+    assert res[1][1].get("bias_grad_from_norm") == 6, res[1][1]
+    params = dict(m.named_parameters())
+    for n in res[0][0]:
+        a, b = res[1][0][n], res[0][0][n]
+        assert a.dtype == params[n].dtype, n
+        assert float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)) < 2e-2, n
