@@ -150,7 +150,7 @@ std::vector<at::Tensor> act_bwd_colsum(const at::Tensor& dh, const at::Tensor& z
   const auto odt = db_dtype.value_or(dh.scalar_type());
   auto db = at::empty({N}, dh.options().dtype(odt));
   const bool fused = colsum_fused_ok();
-  const int P = fused ? hyp::colsum_partials_fused(M, (int)N) : hyp::colsum_partials(M, (int)N);
+  const int P = fused ? hyp::colsum_partials_fused(M, (int)N) : hyp::act_colsum_partials(M, (int)N);
   auto part = at::empty({(int64_t)P * N}, dh.options().dtype(at::kFloat));
   hyp::RngState rs{};
   if (drop_p > 0.0) {
@@ -252,6 +252,8 @@ void register_norm_ops(pybind11::module& m) {
   }, "mean-squared error and its gradient 2(x - t)/n in one pass", pybind11::arg("x"), pybind11::arg("target"));
   m.def("colsum_set_fused", [](int64_t max_p) { hyp::colsum_set_fused((int)max_p); },
         "column sums: partial-row cap of the one-launch last-arriver combine (0 = two launches, the default)");
+  m.def("colsum_set_act_wgs", [](int64_t wgs) { hyp::colsum_set_act_wgs((int)wgs); },
+        "act_bwd_colsum: target workgroup count of the partial pass (A/B; default 1024)");
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),
         pybind11::arg("out_dtype") = pybind11::none());
   m.def("act_bwd_colsum", &act_bwd_colsum, "activation backward + bias gradient in one pass (act 1 relu, 2 gelu)",

@@ -361,6 +361,8 @@ namespace hyp {
 int colsum_partials(int64_t M, int N);
 // the partial count of the one-launch (last-arriver) combine, and its cap (0 = two launches)
 int colsum_partials_fused(int64_t M, int N);
+int act_colsum_partials(int64_t M, int N);  // act_bwd_colsum's P (more row blocks than colsum_partials)
+void colsum_set_act_wgs(int wgs);
 void colsum_set_fused(int max_p);
 int colsum_fused_max_p();
 // loss = mean((x - t)^2) (fp32 scalar) and g = 2 (x - t) / n in x's dtype; one block (small n)

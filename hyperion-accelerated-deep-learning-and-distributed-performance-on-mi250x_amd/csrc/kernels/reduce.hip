@@ -161,10 +161,18 @@ __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict
       if (ACT == 1) {
         d = zz[j] > 0.f ? g[j] : 0.f;
       } else {
+        // Φ(x) + x·φ(x) with ONE exp: erf(u), u = |x|/√2, by Abramowitz-Stegun 7.1.26
+        // (|error| <= 1.5e-7, far below the bf16 / f16 rounding of dy) reuses φ's exp(-x²/2) =
+        // exp(-u²); erff's own polynomial made this pass VALU-bound (40 us for ViT-B/16's
+        // [6304, 3072] at 2.9 TB/s)
         const float x = zz[j];
-        const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-        const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-        d = g[j] * (cdf + x * pdf);
+        const float e = __expf(-0.5f * x * x);
+        const float t = __builtin_amdgcn_rcpf(fmaf(0.23164189f, fabsf(x), 1.f));  // 1 / (1 + p·u), p/√2
+        const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
+                                         -0.284496736f), 0.254829592f);
+        const float erf_abs = fmaf(-poly, e, 1.f);
+        const float cdf = 0.5f + 0.5f * copysignf(erf_abs, x);
+        d = g[j] * fmaf(x * 0.39894228040143268f, e, cdf);
       }
       o[j] = rnd<T>(d);  // the column sums see what is stored (the vendor bias grad reads dy)
       a[j] += o[j];
@@ -256,6 +264,21 @@ int colsum_partials(int64_t M, int N) {
   if (P < 1) P = 1;
   return (int)P;
 }
+
+// the activation backward (act_bwd_colsum_k) computes per element and stores a second stream:
+// more resident waves than the plain column sum's ~2 workgroups per CU (colsum_set_act_wgs: A/B)
+int g_act_colsum_wgs = 1024;
+
+int act_colsum_partials(int64_t M, int N) {
+  const int slabs = (N + kColThreads * 8 - 1) / (kColThreads * 8);
+  int64_t P = (g_act_colsum_wgs + slabs - 1) / slabs;
+  const int64_t max_p = (M + 4 * kRowGroups - 1) / (4 * kRowGroups);  // >= 16 rows per slab
+  if (P > max_p) P = max_p;
+  if (P < 1) P = 1;
+  return (int)P;
+}
+
+void colsum_set_act_wgs(int wgs) { g_act_colsum_wgs = wgs < 64 ? 64 : (wgs > 8192 ? 8192 : wgs); }
 
 int g_colsum_fused_max_p = 0;  // colsum_set_fused (0: the two-launch path — measured faster, see README)
 

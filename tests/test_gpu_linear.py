@@ -185,3 +185,20 @@ def test_linear_wgrad_native_matches_mm(shape):
     assert c.get("gemm_tn", 0) == int(not small and M % 8 == 0)
     ref = dy.float().t() @ x.float()
     assert (dw.float() - ref).norm() <= 5e-3 * ref.norm()
+
+
+def test_gelu_backward_fast_erf_within_rounding():
+    """act_bwd_colsum's GELU derivative (one exp + an A&S 7.1.26 erf) against the fp64 derivative
+    over a dense sweep of pre-activations: within one bf16 rounding of the exact value."""
+    import math
+
+    from hyperion.ops import _native
+
+    z64 = torch.linspace(-12, 12, 8192 * 8, dtype=torch.float64)
+    z = z64.to("cuda").bfloat16().view(-1, 64)
+    dh = torch.ones_like(z)
+    dy, _ = _native.native().act_bwd_colsum(dh, z, 2, torch.float32)
+    x = z.double()
+    ref = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    err = (dy.double() - ref).abs()
+    assert float((err - ref.abs() * 2.0 ** -8 - 1e-6).max()) <= 0, float(err.max())
