@@ -125,7 +125,8 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
     def ven():
         y = torch.addmm(bias.to(x.dtype), x, w.t()) if bias is not None else x @ w.t()
         if a == 2:  # what the vendor fallback of linear_act runs: GELU + dropout in one native pass
-            return C.dropout(y, dropout_p, rng, act=2) + (residual if residual is not None else 0)
+            h = C.dropout(y, dropout_p, rng, act=2)
+            return h + residual if residual is not None else h  # (no "+ 0": an extra full-size add kernel)
         if a == 1:
             y = torch.relu(y)
         elif a == 3:
