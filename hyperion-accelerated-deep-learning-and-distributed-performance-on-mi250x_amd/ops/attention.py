@@ -102,7 +102,7 @@ def attention(
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
     if _native.use_native(q, op="attn") and q.shape == k.shape == v.shape and _native_ok(q, k, v):
         kpm = key_padding_mask.to(torch.uint8) if key_padding_mask is not None else None
-        return _AttnFn.apply(q, k, v, causal, float(dropout_p), kpm, scale)
+        return _native.apply_fn(_AttnFn, q, k, v, causal, float(dropout_p), kpm, scale)
     return attention_reference(q, k, v, causal, dropout_p, key_padding_mask, scale)
 
 
@@ -118,5 +118,5 @@ def attention_packed(
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
     if _native.use_native(qkv, op="attn") and _native_ok(q, k, v):
         kpm = key_padding_mask.to(torch.uint8) if key_padding_mask is not None else None
-        return _AttnPackedFn.apply(qkv, causal, float(dropout_p), kpm, scale)
+        return _native.apply_fn(_AttnPackedFn, qkv, causal, float(dropout_p), kpm, scale)
     return attention_reference(q, k, v, causal, dropout_p, key_padding_mask, scale)

@@ -115,7 +115,7 @@ def bn_act(
         and (weight is None or weight.dtype == torch.float32)
         and (running_mean is None or running_mean.dtype == torch.float32)
     ):
-        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act)
+        return _native.apply_fn(_BNActFn, x, residual, weight, bias, running_mean, running_var, momentum, eps, training, act)
     return bn_act_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, act)
 
 

@@ -889,7 +889,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
         _native.count("stem_s2d")
         _native.count("conv_bn_act")
         bn._host_batches += 1
-        return _StemConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.momentum),
+        return _native.apply_fn(_StemConvBNActFn, x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.momentum),
                                       float(bn.eps), bool(bn.act))
     use = use and _native_conv_ok(x, conv, w)
     if not use:
@@ -915,7 +915,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
     prod = getattr(x.grad_fn, "bnlink", None) if (FUSE_BN_BACKWARD and x.grad_fn is not None) else None
     defer = (defer and FUSE_BN_APPLY and bool(bn.act) and residual is None and torch.is_grad_enabled()
              and x.dtype == torch.bfloat16 and w.dtype == x.dtype and bn.num_features <= 512)
-    out = _ConvBNActFn.apply(x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
+    out = _native.apply_fn(_ConvBNActFn, x, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, residual,
                              stride, padding, float(bn.momentum), float(bn.eps), bool(bn.act),
                              link_in, link_out, branch, bidx, prod, pend, defer)
     if out.grad_fn is not None:  # (no graph under no_grad: nothing to link)

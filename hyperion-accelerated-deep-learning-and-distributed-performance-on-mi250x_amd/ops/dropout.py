@@ -42,7 +42,7 @@ def dropout(x: torch.Tensor, p: float = 0.5, training: bool = True) -> torch.Ten
     if not training or p == 0.0:
         return x
     if _native_ok(x) and 0.0 < p < 1.0:
-        return _DropoutFn.apply(x, float(p))
+        return _native.apply_fn(_DropoutFn, x, float(p))
     return F.dropout(x, p, training)
 
 

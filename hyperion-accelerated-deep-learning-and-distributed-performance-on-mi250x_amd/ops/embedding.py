@@ -38,7 +38,7 @@ def embedding(ids: torch.Tensor, w: torch.Tensor, padding_idx: Optional[int] = N
     if (w.is_cuda and w.dim() == 2 and w.shape[1] % 8 == 0 and w.is_contiguous() and ids.dtype == torch.long
             and w.dtype in (torch.bfloat16, torch.float16, torch.float32) and _native.use_native(w, op="embedding")):
         pad = -1 if padding_idx is None else (padding_idx if padding_idx >= 0 else padding_idx + w.shape[0])
-        return _EmbedFn.apply(ids, w, pad)
+        return _native.apply_fn(_EmbedFn, ids, w, pad)
     return F.embedding(ids, w, padding_idx)
 
 

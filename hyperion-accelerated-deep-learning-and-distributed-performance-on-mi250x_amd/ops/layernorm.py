@@ -159,7 +159,7 @@ def layer_norm(
     if native:
         if link is not None and residual is not link.src:
             link = None
-        return _LNFn.apply(x, residual, weight, bias, eps, rms, return_sum, float(dropout_p), link, blink)
+        return _native.apply_fn(_LNFn, x, residual, weight, bias, eps, rms, return_sum, float(dropout_p), link, blink)
     y, s = _ref(x, residual, weight, bias, eps, rms, dropout_p)
     return (y, s) if return_sum else y
 

@@ -173,9 +173,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, l
         if dt not in (torch.bfloat16, torch.float16):
             return F.linear(x, w, b)
         with torch.autocast(x.device.type, enabled=False):
-            return _LinearFn.apply(x.to(dt), w.to(dt), b)  # (a cast copy: the link stays unarmed)
+            return _native.apply_fn(_LinearFn, x.to(dt), w.to(dt), b)  # (a cast copy: the link stays unarmed)
     link = arm_link(link, x)
-    y = _LinearFn.apply(x, w, b, link, blink)
+    y = _native.apply_fn(_LinearFn, x, w, b, link, blink)
     if link is not None and y.grad_fn is not None:
         link.first_node = weakref.ref(y.grad_fn)
     return y

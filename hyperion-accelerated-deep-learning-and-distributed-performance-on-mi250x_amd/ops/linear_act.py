@@ -150,7 +150,7 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], acti
         fn = _LinearGELU
     if fn is not None:
         link = arm_link(link, x)
-        y = fn.apply(x, w, b, float(dropout_p), link)
+        y = _native.apply_fn(fn, x, w, b, float(dropout_p), link)
         if link is not None and y.grad_fn is not None:
             link.first_node = weakref.ref(y.grad_fn)
         return y

@@ -59,14 +59,14 @@ def _nhwc_ok(x: torch.Tensor) -> bool:
 def max_pool2d(x: torch.Tensor, kernel_size, stride=None, padding=0) -> torch.Tensor:
     k, s, p = _pair(kernel_size), _pair(stride if stride is not None else kernel_size), _pair(padding)
     if _nhwc_ok(x) and k[0] == k[1] and s[0] == s[1] and p[0] == p[1] and p[0] < k[0] and k[0] * k[0] <= 256:
-        return _MaxPoolFn.apply(x, k[0], s[0], p[0])
+        return _native.apply_fn(_MaxPoolFn, x, k[0], s[0], p[0])
     return F.max_pool2d(x, k, s, p)
 
 
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     """``[N, C, H, W] -> [N, C, 1, 1]`` mean over H, W."""
     if _nhwc_ok(x):
-        return _GapFn.apply(x).view(x.shape[0], x.shape[1], 1, 1)
+        return _native.apply_fn(_GapFn, x).view(x.shape[0], x.shape[1], 1, 1)
     return F.adaptive_avg_pool2d(x, 1)
 
 

@@ -77,5 +77,5 @@ def apply_rope(q: torch.Tensor, k: torch.Tensor, positions: Optional[torch.Tenso
     D = q.shape[-1]
     if (_native.use_native(q, k, op="rope") and q.dtype in _native.DTYPE_CODE and q.dtype == k.dtype and D % 16 == 0
             and q.stride(-1) == 1 and k.stride(-1) == 1):
-        return _RopeFn.apply(q, k, positions, theta)
+        return _native.apply_fn(_RopeFn, q, k, positions, theta)
     return rope_reference(q, k, positions, theta)

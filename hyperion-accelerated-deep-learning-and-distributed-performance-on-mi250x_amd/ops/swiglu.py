@@ -28,5 +28,5 @@ class _SwiGLUFn(torch.autograd.Function):
 def swiglu(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     if (_native.use_native(gate, up, op="swiglu") and gate.dtype in _native.DTYPE_CODE and gate.dtype == up.dtype
             and gate.shape == up.shape and gate.numel() % 8 == 0):
-        return _SwiGLUFn.apply(gate, up)
+        return _native.apply_fn(_SwiGLUFn, gate, up)
     return F.silu(gate) * up
