@@ -255,6 +255,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
     __syncthreads();                // ... every wave's; and tile kt-1's buffer is free
     if (kt + 1 < nkt) dma_kv(k0 + KB, (kt + 1) & 1);
     if (p.causal && k0 > wave_last_q) continue;  // wave-uniform: every key of the tile is masked
+    if (wq0 >= p.S) continue;  // wave-uniform: the padded query tail (S = 197: rows 224-255) — nothing stored
     const uint16_t* Kc = Ks[kt & 1];
     const uint16_t* Vc = Vs[kt & 1];
 
@@ -548,7 +549,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
 #pragma unroll
     for (int qbk = 0; qbk < NQB; ++qbk) {
       const int qbase = q0 + 32 * qbk;
-      if (p.causal && kw0 > qbase + 31) {  // wave-uniform: the whole block is masked
+      // wave-uniform: the whole block is masked (causal), past the sequence end (the padded query
+      // tail of S = 197: ViT), or this wave's 32 keys are all past it — P = dS = 0 there, so only
+      // the zero dSᵀ entries are needed (dV / dK / dQ terms of the block are exactly zero)
+      if ((p.causal && kw0 > qbase + 31) || qbase >= p.S || kw0 >= p.S) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int u = 8 * qbk + 2 * g + hh;
