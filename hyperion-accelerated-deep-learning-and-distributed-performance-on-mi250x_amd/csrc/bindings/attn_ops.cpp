@@ -270,6 +270,8 @@ void register_attn_ops(pybind11::module& m) {
   m.def("ln_fwd", &ln_fwd, "LayerNorm/RMSNorm forward (+fused residual add, + dropout on x)", pybind11::arg("x"),
         pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("eps"),
         pybind11::arg("rms"), pybind11::arg("drop_p") = 0.0, pybind11::arg("rng") = pybind11::none());
+  m.def("ln_set_waves", [](int64_t w) { hyp::ln_set_waves((int)w); },
+        "LayerNorm forward / backward grid: target wave count (A/B; 0 = defaults)");
   m.def("ln_bwd", &ln_bwd, "LayerNorm/RMSNorm backward (+ the dropped input's gradient)", pybind11::arg("dy"),
         pybind11::arg("xin"), pybind11::arg("weight"), pybind11::arg("mean"), pybind11::arg("rstd"),
         pybind11::arg("dres"), pybind11::arg("need_dw"), pybind11::arg("need_db"), pybind11::arg("rms"),

@@ -65,6 +65,7 @@ void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave);
 // wt = 1: w / b (and dw / db) are in the activation dtype instead of fp32 (pointers reinterpreted)
 // drop_p > 0 (d <= 2048; forward needs r): s = r + dropout(x) with the dropout.hip mask of *rs; the
 // backward then also writes dxa = dropout(dx), the gradient of the dropped input.
+void ln_set_waves(int waves);  // LayerNorm narrow-row grids: target wave count (0 = defaults)
 hipError_t layernorm_forward(int dtype, int rms, const void* x, const void* r, void* s, void* y, const float* w,
                              const float* b, float* mean, float* rstd, int64_t rows, int d, float eps,
                              hipStream_t st, int wt = 0, float drop_p = 0.f, const struct RngState* rs = nullptr);

@@ -17,6 +17,9 @@ namespace hyp {
 namespace {
 
 constexpr int kWavesPerBlock = 4;
+// wave-count target of the narrow-row forward / backward grids (0: the defaults of
+// ln_fwd_dispatch / layernorm_bwd_geom; ln_set_waves: A/B sweeps)
+int g_ln_waves = 0;
 
 // Each lane handles VPL vectors of 8 elements: lane l, vector v covers [ (v*64 + l)*8, +8 ).
 // Latency structure (the kernels are HBM-bound only when enough loads are in flight): the affine
@@ -519,6 +522,7 @@ hipError_t ln_fwd_dispatch(const T* x, const T* r, T* s, T* y, const float* w, c
   // rows per wave: 2+ once there are enough rows to keep ~2048 waves busy (the prefetch needs a next row)
   int rpw = 1;
   if (rows >= 4096) rpw = (int)((rows + 2047) / 2048 < 8 ? (rows + 2047) / 2048 : 8);
+  if (g_ln_waves > 0) rpw = (int)std::min<int64_t>(8, std::max<int64_t>(1, (rows + g_ln_waves - 1) / g_ln_waves));
   const int64_t waves = (rows + rpw - 1) / rpw;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(64 * kWavesPerBlock);
 #define HYP_LN_F(V)                                                                                          \
@@ -656,6 +660,8 @@ bool layernorm_supported(int d) {
   return vpl <= 4 || vpl == 8;
 }
 
+void ln_set_waves(int waves) { g_ln_waves = waves < 0 ? 0 : (waves > 16384 ? 16384 : waves); }
+
 void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave) {
   if (d > 2048) {  // wide rows: one 256-thread block per row group (ln_bwd_wide_k)
     const int rpb = wide_rows_per_block(rows);
@@ -671,6 +677,7 @@ void layernorm_bwd_geom(int64_t rows, int d, int* P, int* rows_per_wave) {
   int64_t waves = (rows + 3) / 4;  // ~4 rows per wave (the next row prefetched while one is reduced)
   const int64_t floor_waves = rows < 2048 ? rows : 2048;
   if (waves < floor_waves) waves = floor_waves;
+  if (g_ln_waves > 0) waves = std::min<int64_t>(rows, g_ln_waves);
   if (waves > 4096) waves = 4096;
   if (waves < 1) waves = 1;
   int rpw = (int)((rows + waves - 1) / waves);
