@@ -565,7 +565,10 @@ hipError_t launch_layout(const GemmP& p, bool atr, bool btr, int nwg, hipStream_
 // 2032 x 3072 is 264 at 192x128 — the vendor library's choice of one full wave of workgroups.
 // Deep rings at one workgroup per CU (128x128 with 8 stages, 256x128 with 6) were measured SLOWER
 // on every transformer shape (1.1-2x, profiles/r05/gemm_probe_deep_ring.json): with one wave per
-// SIMD nothing hides the fragment reads behind the MFMAs.  NBR stays a template parameter.
+// SIMD nothing hides the fragment reads behind the MFMAs.  NBR stays a template parameter.  So was
+// 256x128 on 4 waves of 128x64 with a 3-deep ring (25 % fewer LDS fragment bytes per MFMA, two
+// workgroups per CU): 1.5-2x slower than tile 1 on every shape, 8192^3 1186 vs 1091 us
+// (profiles/r05/gemm_tile8_4wave_sweep.jsonl) — fewer waves per SIMD costs more than the LDS saves.
 template <typename T, typename OutT>
 hipError_t launch_tile(const GemmP& p, bool atr, bool btr, int tile, int nwg, hipStream_t st) {
   switch (tile) {

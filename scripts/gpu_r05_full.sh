@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: the whole GPU test suite (what the driver runs at round end), one pytest process
+# round 5: the whole GPU test suite (what the driver runs at round end), one pytest process, then smoke()
 set -o pipefail
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r05full; mkdir -p $O
@@ -7,4 +7,6 @@ timeout -k 10 1100 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-m
 rc=$?
 grep -E "FAILED|ERROR" $O/pytest.log | head -20
 tail -3 $O/pytest.log
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -10 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log

@@ -41,3 +41,24 @@ for i in range(0, len(args), 3):
             continue
         row[name] = {"warm_us": round(warm, 1), "cold_us": round(cold, 1), "warm_tf": round(flop / warm / 1e6, 0)}
     print(json.dumps(row), flush=True)
+
+# weight-gradient (TN) shapes: env GEMM_TN="N K T,..." (dy [T, N], x [T, K] -> [N, K]), tiles 1 / 8 / 0 / 2
+import os  # noqa: E402
+
+for spec in [s for s in os.environ.get("GEMM_TN", "").split(",") if s.strip()]:
+    N, K, T = (int(v) for v in spec.split())
+    dy = torch.randn(T, N, device="cuda").bfloat16()
+    x = torch.randn(T, K, device="cuda").bfloat16()
+    flop = 2.0 * N * K * T
+    row = {"tn": [N, K, T], "vendor": round(t_us(lambda: dy.t() @ x, False), 1)}
+    for t in (0, 1, 2):
+        for sp in (1, 2, 3, 4, 6, 8):
+            try:
+                us = t_us(lambda: C.gemm(dy, x, a_tr=True, b_tr=True, tile=t, splits=sp), False)
+            except RuntimeError:
+                continue
+            row[f"t{t}s{sp}"] = round(us, 1)
+    best = min((v, k) for k, v in row.items() if k.startswith("t") and k != "tn")
+    row["best"] = best[1]
+    row["best_tf"] = round(flop / best[0] / 1e6, 0)
+    print(json.dumps(row), flush=True)
