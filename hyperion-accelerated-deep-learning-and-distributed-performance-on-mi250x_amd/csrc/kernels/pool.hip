@@ -64,6 +64,111 @@ __global__ __launch_bounds__(256) void maxpool_fwd_k(const T* __restrict__ x, T*
   *reinterpret_cast<uint2*>(idx + o) = packed;
 }
 
+// The ResNet stem's 3x3 / stride-2 window at compile time: the 9 taps' loads are issued together
+// (the runtime-k loop above waits one memory round trip per tap: 25 us per ResNet-50 step) —
+// same tap order and NaN rule, so the values and recorded taps are identical.
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void maxpool_fwd_fixed_k(const T* __restrict__ x, T* __restrict__ y,
+                                                           uint8_t* __restrict__ idx, PoolGeom g) {
+  const int cv = g.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)g.N * g.P * g.Q * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int q = (int)(pix % g.Q);
+  pix /= g.Q;
+  const int p = (int)(pix % g.P);
+  const int n = (int)(pix / g.P);
+  const int h0 = p * S - g.pad, w0 = q * S - g.pad;
+  float v[K * K][8];
+#pragma unroll
+  for (int r = 0; r < K; ++r)
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const int h = min(max(h0 + r, 0), g.H - 1), w = min(max(w0 + c, 0), g.W - 1);  // clamped (masked below)
+      Vec8<T>::load(x + (((int64_t)n * g.H + h) * g.W + w) * g.C + c0, v[r * K + c]);
+    }
+  float best[8];
+  uint8_t arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    best[j] = -INFINITY;
+    arg[j] = 0;
+  }
+#pragma unroll
+  for (int r = 0; r < K; ++r)
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      if ((unsigned)(h0 + r) >= (unsigned)g.H || (unsigned)(w0 + c) >= (unsigned)g.W) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float vv = v[r * K + c][j];
+        if (vv > best[j] || (vv != vv && best[j] == best[j])) {
+          best[j] = vv;
+          arg[j] = (uint8_t)(r * K + c);
+        }
+      }
+    }
+  const int64_t o = (((int64_t)n * g.P + p) * g.Q + q) * g.C + c0;
+  Vec8<T>::store(y + o, best);
+  uint2 packed;
+  packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+  packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
+  *reinterpret_cast<uint2*>(idx + o) = packed;
+}
+
+// backward gather with K < 2 S: at most two covering windows per axis (p_hi - 1, p_hi), all four
+// candidates' loads in flight at once, summed in the generic kernel's (p, q) ascending order
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void maxpool_bwd_fixed_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                           T* __restrict__ dx, PoolGeom g) {
+  static_assert(K < 2 * S + 1 && K > S, "two candidate windows per axis");
+  const int cv = g.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)g.N * g.H * g.W * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int w = (int)(pix % g.W);
+  pix /= g.W;
+  const int h = (int)(pix % g.H);
+  const int n = (int)(pix / g.H);
+  const int ph = (h + g.pad) / S, qh = (w + g.pad) / S;
+  uint2 pk[2][2];
+  float gv[2][2][8];
+  bool ok[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int p = ph - 1 + a, q = qh - 1 + b;
+      const int r = h + g.pad - p * S, c = w + g.pad - q * S;
+      ok[a][b] = p >= 0 && p < g.P && q >= 0 && q < g.Q && r >= 0 && r < K && c >= 0 && c < K;
+      const int pc = min(max(p, 0), g.P - 1), qc = min(max(q, 0), g.Q - 1);
+      const int64_t o = (((int64_t)n * g.P + pc) * g.Q + qc) * g.C + c0;
+      pk[a][b] = *reinterpret_cast<const uint2*>(idx + o);
+      Vec8<T>::load(dy + o, gv[a][b]);
+    }
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (!ok[a][b]) continue;
+      const int r = h + g.pad - (ph - 1 + a) * S, c = w + g.pad - (qh - 1 + b) * S;
+      const uint32_t tap = (uint32_t)(r * K + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t word = j < 4 ? pk[a][b].x : pk[a][b].y;
+        if (((word >> (8 * (j & 3))) & 0xff) == tap) acc[j] += gv[a][b][j];
+      }
+    }
+  Vec8<T>::store(dx + (((int64_t)n * g.H + h) * g.W + w) * g.C + c0, acc);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                      T* __restrict__ dx, PoolGeom g) {
@@ -193,7 +298,11 @@ hipError_t maxpool2d_forward(int dtype, const void* x, void* y, uint8_t* idx, in
   const PoolGeom g{N, H, W, C, (H + 2 * pad - k) / s + 1, (W + 2 * pad - k) / s + 1, k, s, pad};
   const int64_t total = (int64_t)N * g.P * g.Q * (C / 8);
   HYP_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL(maxpool_fwd_k<T>, dim3(blocks_for(total)), dim3(256), 0, st, (const T*)x, (T*)y, idx, g);
+    if (k == 3 && s == 2)
+      hipLaunchKernelGGL((maxpool_fwd_fixed_k<T, 3, 2>), dim3(blocks_for(total)), dim3(256), 0, st, (const T*)x, (T*)y,
+                         idx, g);
+    else
+      hipLaunchKernelGGL(maxpool_fwd_k<T>, dim3(blocks_for(total)), dim3(256), 0, st, (const T*)x, (T*)y, idx, g);
   });
   return hipGetLastError();
 }
@@ -204,7 +313,11 @@ hipError_t maxpool2d_backward(int dtype, const void* dy, const uint8_t* idx, voi
   const PoolGeom g{N, H, W, C, (H + 2 * pad - k) / s + 1, (W + 2 * pad - k) / s + 1, k, s, pad};
   const int64_t total = (int64_t)N * H * W * (C / 8);
   HYP_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(blocks_for(total)), dim3(256), 0, st, (const T*)dy, idx, (T*)dx, g);
+    if (k == 3 && s == 2)
+      hipLaunchKernelGGL((maxpool_bwd_fixed_k<T, 3, 2>), dim3(blocks_for(total)), dim3(256), 0, st, (const T*)dy, idx,
+                         (T*)dx, g);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(blocks_for(total)), dim3(256), 0, st, (const T*)dy, idx, (T*)dx, g);
   });
   return hipGetLastError();
 }

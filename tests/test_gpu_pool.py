@@ -7,7 +7,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 128, 56, 56), 3, 2, 1),
-                                         ((3, 16, 9, 11), 2, 2, 0), ((2, 8, 7, 7), 3, 1, 1)])
+                                         ((3, 16, 9, 11), 2, 2, 0), ((2, 8, 7, 7), 3, 1, 1),
+                                         ((3, 16, 9, 11), 3, 2, 0), ((2, 8, 13, 15), 3, 2, 1)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_maxpool_fwd_bwd_match_torch(shape, k, s, p, dtype):
     from hyperion.ops.pool import max_pool2d
