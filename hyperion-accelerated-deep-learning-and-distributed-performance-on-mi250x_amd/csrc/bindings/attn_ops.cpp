@@ -6,6 +6,10 @@
 namespace hypbind {
 namespace {
 
+// attn_set_qsplit: 0 = automatic query split of the S <= 128 backward, 1 = off, n > 1 = at most n
+int g_attn_qsplit = 0;
+
+
 void check_bshd(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 4, name, " must be a [B,S,H,D] GPU tensor");
   TORCH_CHECK(t.stride(3) == 1, name, " must have a contiguous head dim");
@@ -84,9 +88,24 @@ void attn_bwd_impl(const at::Tensor& dout, const at::Tensor& q, const at::Tensor
   const int nkb = (S + 127) / 128;
   const int dq_slabs = (nkb >= 2 && nkb <= 4) ? nkb : 0;
   if (S > 128) dq_acc = at::empty({(int64_t)(dq_slabs ? dq_slabs : 1) * B * H * S * D}, fopt);
+  // S <= 128 with few (b, h) pairs (Llama-2-7B at batch 1: 32 heads = 32 workgroups on 256 CUs):
+  // split each head's query slices over qsplit workgroups; dK / dV come back as fp32 partials
+  // summed in order by one small pass (dQ of a slice is still complete in its workgroup)
+  int qsplit = 1;
+  at::Tensor dkv_part;
+  if (S <= 128 && g_attn_qsplit != 1) {
+    const int nsl = (S + (4096 / D) - 1) / (4096 / D);
+    const int cap = g_attn_qsplit > 1 ? g_attn_qsplit : nsl;
+    // up to 128 workgroups (GPT-2's 192 (b, h) pairs measured no better split: the partial-sum pass
+    // costs what the wider grid saves)
+    while ((int64_t)B * H * qsplit < 128 && qsplit * 2 <= nsl && qsplit * 2 <= cap) qsplit *= 2;
+    if (qsplit > 1) dkv_part = at::empty({(int64_t)qsplit * 2 * B * H * S * D}, fopt);
+  }
   at::Tensor kpm_u8;
   if (kpm.has_value() && kpm->defined()) kpm_u8 = kpm->to(at::kByte).contiguous();
   hyp::AttnBwdParams p{};
+  p.qsplit = qsplit;
+  p.dkv_part = dkv_part.defined() ? dkv_part.data_ptr<float>() : nullptr;
   p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr(); p.dout = g.data_ptr();
   p.dq = dq.data_ptr(); p.dk = dk.data_ptr(); p.dv = dv.data_ptr();
   p.sqb = q.stride(0); p.sqs = q.stride(1); p.sqh = q.stride(2);
@@ -266,6 +285,8 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
 void register_attn_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, "flash attention forward (MFMA)");
   m.def("attn_bwd", &attn_bwd, "flash attention backward (MFMA)");
+  m.def("attn_set_qsplit", [](int64_t n) { g_attn_qsplit = (int)n; },
+        "S <= 128 attention backward: 0 automatic query split, 1 off, n > 1 at most n (A/B)");
   m.def("attn_bwd_rope", &attn_bwd_rope, "flash attention backward with the inverse RoPE fused into dQ / dK");
   m.def("ln_fwd", &ln_fwd, "LayerNorm/RMSNorm forward (+fused residual add, + dropout on x)", pybind11::arg("x"),
         pybind11::arg("residual"), pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("eps"),

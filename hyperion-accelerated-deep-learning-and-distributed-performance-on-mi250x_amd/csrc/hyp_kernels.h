@@ -100,6 +100,8 @@ struct AttnBwdParams {
   int64_t sdob, sdos, sdoh, sdqb, sdqs, sdqh, sdkb, sdks, sdkh, sdvb, sdvs, sdvh;
   const float* lse; float* delta; float* dq_acc;  // delta [B*H*S], dq_acc [B*H*S*D] fp32 workspaces
   int dq_slabs;  // > 0: dq_acc holds one fp32 dQ slab per key block (plain stores, no zeroing / atomics)
+  int qsplit;         // S <= 128: query slices split over qsplit workgroups per (b, h) (few heads: fill the CUs)
+  float* dkv_part;    // qsplit > 1: [qsplit][2 (dK, dV)][B*H][S][D] fp32 partials, summed by attn_bwd_kv_sum_k
   int rope; const float2* rope_cs;  // rope: dQ / dK through the inverse rotary embedding (D = 128, no
                                     // dropout); rope_cs [S][64] (cos, sin) of position x inv_freq(i)
   const uint8_t* kpm;

@@ -431,12 +431,15 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int nkb = (p.S + BKB - 1) / BKB;
-  const int total = nkb * p.B * p.H;
+  const int qsplit = DIRECT ? p.qsplit : 1;  // query-slice split of one (b, h) (adjacent ids: one XCD)
+  const int total = nkb * p.B * p.H * qsplit;
   int bid = blockIdx.x;
   {
     const int q8 = total / 8, r8 = total % 8, xcd = bid % 8, idx = bid / 8;
     bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + idx;
   }
+  const int zq = bid % qsplit;
+  bid /= qsplit;
   const int bh = bid / nkb, kblk = bid - bh * nkb;
   const int b = bh / p.H, hd = bh - b * p.H;
   const int k0 = kblk * BKB, kw0 = k0 + 32 * w, key = kw0 + r;
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
   const int qstart = p.causal ? (k0 / QS) * QS : 0;
   const int nsl = qstart < p.S ? (p.S - qstart + QS - 1) / QS : 0;
   dma_rows(kb, p.sks, k0, Ks, KPC);
-  if (nsl > 0) dma_slice(qstart, 0);
+  if (zq < nsl) dma_slice(qstart + zq * QS, 0);
 
   f32x16 dvt[NDB], dkt[NDB];
 #pragma unroll
@@ -522,11 +525,11 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
   // dSᵀ write of register group g (block qbk): row 32 w + r, unit 8 qbk + 2 g + hh
   const int ds_row = 32 * w + r;
 
-  for (int sl = 0; sl < nsl; ++sl) {
-    const int q0 = qstart + sl * QS, cur = sl & 1;
+  for (int sl = zq, it = 0; sl < nsl; sl += qsplit, ++it) {  // this workgroup's slices zq, zq + qsplit, ...
+    const int q0 = qstart + sl * QS, cur = it & 1;
     __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of slice sl (and the K tile) has landed ...
-    __syncthreads();                // ... every wave's; slice sl-1's buffers and dSt are free
-    if (sl + 1 < nsl) dma_slice(q0 + QS, cur ^ 1);
+    __syncthreads();                // ... every wave's; the previous slice's buffers and dSt are free
+    if (sl + qsplit < nsl) dma_slice(q0 + qsplit * QS, cur ^ 1);
     const uint16_t* Qc = Qs[cur];
     const uint16_t* Gc = dOs[cur];
     if constexpr (FDELTA) {  // delta[q] = Σ_d dO·O: 8 threads per query row, 16 columns each
@@ -694,6 +697,22 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
           dkt[n + 2][e] = x1 * kcs[n][e].x - x0 * kcs[n][e].y;
         }
     }
+    if (qsplit > 1) {  // partial sums over this workgroup's query slices: fp32, summed by attn_bwd_kv_sum_k
+      const int64_t plane = (int64_t)p.B * p.H * p.S * D;
+      float* pk = p.dkv_part + (int64_t)zq * 2 * plane + ((int64_t)bh * p.S + key) * D;
+      float* pv = pk + plane;
+#pragma unroll
+      for (int n = 0; n < NDB; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          *reinterpret_cast<float4*>(pk + 32 * n + 8 * g + 4 * hh) =
+              make_float4(dkt[n][4 * g] * p.scale, dkt[n][4 * g + 1] * p.scale, dkt[n][4 * g + 2] * p.scale,
+                          dkt[n][4 * g + 3] * p.scale);
+          *reinterpret_cast<float4*>(pv + 32 * n + 8 * g + 4 * hh) =
+              make_float4(dvt[n][4 * g], dvt[n][4 * g + 1], dvt[n][4 * g + 2], dvt[n][4 * g + 3]);
+        }
+      return;
+    }
 #pragma unroll
     for (int n = 0; n < NDB; ++n)
 #pragma unroll
@@ -708,6 +727,31 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_k(AttnBwdParam
         *reinterpret_cast<u16x4*>(dv + 32 * n + 8 * g + 4 * hh) = vv;
       }
   }
+}
+
+// dK, dV = Σ_z partial[z] (fixed order: deterministic) of the query-split direct backward
+template <typename T, int D>
+__global__ __launch_bounds__(256) void attn_bwd_kv_sum_k(AttnBwdParams p) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // over 2 * B*H*S*D/4 quads
+  const int64_t plane = (int64_t)p.B * p.H * p.S * D;
+  const int64_t half = plane / 4;
+  if (i >= 2 * half) return;
+  const int which = i >= half ? 1 : 0;
+  const int64_t e = (i - which * half) * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < p.qsplit; ++z) {
+    const float4 u = *reinterpret_cast<const float4*>(p.dkv_part + ((int64_t)z * 2 + which) * plane + e);
+    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  }
+  const int64_t row = e / D;
+  const int d = (int)(e - row * D);
+  const int key = (int)(row % p.S);
+  const int bh = (int)(row / p.S);
+  const int b = bh / p.H, hd = bh - b * p.H;
+  uint16_t* dst = which == 0 ? static_cast<uint16_t*>(p.dk) + b * p.sdkb + hd * p.sdkh + (int64_t)key * p.sdks + d
+                             : static_cast<uint16_t*>(p.dv) + b * p.sdvb + hd * p.sdvh + (int64_t)key * p.sdvs + d;
+  u16x4 o = {MM<T>::cvt(v.x), MM<T>::cvt(v.y), MM<T>::cvt(v.z), MM<T>::cvt(v.w)};
+  *reinterpret_cast<u16x4*>(dst) = o;
 }
 
 template <typename T, int D>
@@ -759,9 +803,18 @@ hipError_t bwd_launch(const AttnBwdParams& p, hipStream_t st) {
   if (direct) {
     AttnBwdParams q = p;
     q.dq_acc = nullptr;
-    if (rope) hipLaunchKernelGGL((attn_bwd_k<T, D, false, true, D == 128>), grid, dim3(256), 0, st, q);
-    else if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, true>), grid, dim3(256), 0, st, q);
-    else hipLaunchKernelGGL((attn_bwd_k<T, D, false, true>), grid, dim3(256), 0, st, q);
+    constexpr int QS = 4096 / D;
+    const int nsl = (p.S + QS - 1) / QS;
+    if (q.qsplit < 1 || q.dkv_part == nullptr) q.qsplit = 1;
+    if (q.qsplit > nsl) return hipErrorInvalidValue;  // every split must own a slice (its partial is summed)
+    const dim3 g2(grid.x * q.qsplit);
+    if (rope) hipLaunchKernelGGL((attn_bwd_k<T, D, false, true, D == 128>), g2, dim3(256), 0, st, q);
+    else if (drop) hipLaunchKernelGGL((attn_bwd_k<T, D, true, true>), g2, dim3(256), 0, st, q);
+    else hipLaunchKernelGGL((attn_bwd_k<T, D, false, true>), g2, dim3(256), 0, st, q);
+    if (q.qsplit > 1) {
+      const int64_t quads = 2 * (int64_t)p.B * p.H * p.S * D / 4;
+      hipLaunchKernelGGL((attn_bwd_kv_sum_k<T, D>), dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, st, q);
+    }
     return hipGetLastError();
   }
   if (rope) hipLaunchKernelGGL((attn_bwd_k<T, D, false, false, D == 128>), grid, dim3(256), 0, st, p);

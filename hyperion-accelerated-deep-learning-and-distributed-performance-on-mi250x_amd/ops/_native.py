@@ -62,6 +62,8 @@ def _load():
         _MOD.colsum_set_act_wgs(int(os.environ["HYPERION_ACT_COLSUM_WGS"]))  # act_bwd_colsum grid (A/B)
     if _MOD is not None and os.environ.get("HYPERION_LN_WAVES") and hasattr(_MOD, "ln_set_waves"):
         _MOD.ln_set_waves(int(os.environ["HYPERION_LN_WAVES"]))  # LayerNorm grid sweep (A/B)
+    if _MOD is not None and os.environ.get("HYPERION_ATTN_QSPLIT") and hasattr(_MOD, "attn_set_qsplit"):
+        _MOD.attn_set_qsplit(int(os.environ["HYPERION_ATTN_QSPLIT"]))  # attention bwd query split (A/B)
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")
