@@ -285,6 +285,8 @@ std::vector<at::Tensor> ln_bwd(const at::Tensor& dy, const at::Tensor& xin, cons
 void register_attn_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, "flash attention forward (MFMA)");
   m.def("attn_bwd", &attn_bwd, "flash attention backward (MFMA)");
+  m.def("attn_set_fwd_narrow", [](int64_t on) { hyp::attn_set_fwd_narrow((int)on); },
+        "attention forward: one-wave workgroups for grids below 128 workgroups (A/B; default off)");
   m.def("attn_set_qsplit", [](int64_t n) { g_attn_qsplit = (int)n; },
         "S <= 128 attention backward: 0 automatic query split, 1 off, n > 1 at most n (A/B)");
   m.def("attn_bwd_rope", &attn_bwd_rope, "flash attention backward with the inverse RoPE fused into dQ / dK");

@@ -114,6 +114,7 @@ struct AttnBwdParams {
 bool attention_supported(int dtype, int D);
 hipError_t attention_forward(int dtype, const AttnParams& p, hipStream_t st);
 hipError_t attention_backward(int dtype, const AttnBwdParams& p, hipStream_t st);
+void attn_set_fwd_narrow(int on);  // 1: one-wave forward workgroups when the default grid is < 128 (A/B)
 }  // namespace hyp
 
 namespace hyp {

@@ -135,7 +135,10 @@ __device__ __forceinline__ u16x8 read_t_pair(const uint16_t* t_img, int d, int c
 //    one barrier per tile.
 //  * XCD-aware block order: the query blocks of one (b, h) — which share K/V — run on one XCD
 //    (one L2), heaviest (causal) block first.
-constexpr int FQ = 128;
+constexpr int FQ = 128;  // query rows of the default (4-wave) forward workgroup
+// attn_set_fwd_narrow (A/B, default off): one-wave forward workgroups measured no faster on the
+// Llama LoRA step (14.58-14.60 vs 14.54-14.57 ms, profiles/r05/attn_fwd_narrow_ab.txt)
+int g_attn_fwd_narrow = 0;
 
 template <typename T>
 struct MM32;
@@ -170,8 +173,11 @@ __device__ __forceinline__ u16x4 read_tr(const uint16_t* lds, int off) {
   return __builtin_bit_cast(u16x4, v);
 }
 
-template <typename T, int D, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
+// NWV: waves per workgroup (FQ = 32 NWV query rows).  4 by default; 1 (opt-in) for grids that would
+// leave most CUs idle (Llama-2-7B at batch 1, S = 128: 32 workgroups of 4 waves -> 128 of 1)
+template <typename T, int D, bool DROP, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 2) void attn_fwd_k(AttnParams p) {
+  constexpr int FQ = 32 * NWV;
   constexpr int NS = D / 16;              // k-steps of the score product
   constexpr int NDB = D / 32;             // 32-wide head-dim blocks of Oᵀ
   constexpr int NCH = D / 8;              // 16-byte chunks per row
@@ -222,8 +228,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
   // SOURCE; rows past S re-read row S-1 (their scores are masked, their P is 0)
   auto dma_kv = [&](int k0, int buf) {
 #pragma unroll
-    for (int i = 0; i < NPC / 4; ++i) {
-      const int pc = 4 * i + w, t = 2 * pc + (lane >> 5);  // subtile
+    for (int i = 0; i < NPC / NWV; ++i) {
+      const int pc = NWV * i + w, t = 2 * pc + (lane >> 5);  // subtile
       const int row = 8 * (t / (NCH / 4)) + ((lane & 31) >> 2);
       const int ch = 4 * (t % (NCH / 4)) + ((lane & 3) ^ ((row >> 2) & 3));
       const int64_t gr = min(k0 + row, p.S - 1);
@@ -783,6 +789,13 @@ __global__ __launch_bounds__(256) void attn_bwd_post_k(AttnBwdParams p) {
 
 template <typename T, int D>
 hipError_t fwd_launch(const AttnParams& p, hipStream_t st) {
+  const int64_t bh = (int64_t)p.B * p.H;
+  if (g_attn_fwd_narrow && bh * ((p.S + FQ - 1) / FQ) < 128) {  // one wave per workgroup
+    const dim3 grid(((p.S + 31) / 32) * bh);
+    if (p.p_drop > 0.f) hipLaunchKernelGGL((attn_fwd_k<T, D, true, 1>), grid, dim3(64), 0, st, p);
+    else hipLaunchKernelGGL((attn_fwd_k<T, D, false, 1>), grid, dim3(64), 0, st, p);
+    return hipGetLastError();
+  }
   const dim3 grid(((p.S + FQ - 1) / FQ) * p.B * p.H);
   if (p.p_drop > 0.f) hipLaunchKernelGGL((attn_fwd_k<T, D, true>), grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL((attn_fwd_k<T, D, false>), grid, dim3(256), 0, st, p);
@@ -834,6 +847,8 @@ hipError_t attention_forward(int dtype, const AttnParams& p, hipStream_t st) {
   if (dtype == kBF16) return p.D == 64 ? fwd_launch<bf16_t, 64>(p, st) : fwd_launch<bf16_t, 128>(p, st);
   return p.D == 64 ? fwd_launch<f16_t, 64>(p, st) : fwd_launch<f16_t, 128>(p, st);
 }
+
+void attn_set_fwd_narrow(int on) { g_attn_fwd_narrow = on; }
 
 hipError_t attention_backward(int dtype, const AttnBwdParams& p, hipStream_t st) {
   if (!attention_supported(dtype, p.D)) return hipErrorInvalidValue;

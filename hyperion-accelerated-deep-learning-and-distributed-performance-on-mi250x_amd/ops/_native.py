@@ -64,6 +64,8 @@ def _load():
         _MOD.ln_set_waves(int(os.environ["HYPERION_LN_WAVES"]))  # LayerNorm grid sweep (A/B)
     if _MOD is not None and os.environ.get("HYPERION_ATTN_QSPLIT") and hasattr(_MOD, "attn_set_qsplit"):
         _MOD.attn_set_qsplit(int(os.environ["HYPERION_ATTN_QSPLIT"]))  # attention bwd query split (A/B)
+    if _MOD is not None and os.environ.get("HYPERION_ATTN_FWD_NARROW") and hasattr(_MOD, "attn_set_fwd_narrow"):
+        _MOD.attn_set_fwd_narrow(int(os.environ["HYPERION_ATTN_FWD_NARROW"]))  # 1-wave forward grid (A/B)
     mode = os.environ.get("HYPERION_KERNEL_CHECK", "")
     if _MOD is not None and mode:
         _MOD = CheckedModule(_MOD, nan=mode == "nan")

@@ -98,6 +98,28 @@ def test_attention_bwd_query_split_matches_unsplit(D, causal, p):
         assert err <= 1e-2 * b.float().abs().max().item() + 1e-6, err
 
 
+@pytest.mark.parametrize("D,causal", [(128, True), (64, False), (64, True)])
+@pytest.mark.parametrize("S", [128, 197])
+def test_attention_fwd_one_wave_grid_matches_default(D, causal, S):
+    """Few (b, h) pairs: the forward runs one-wave workgroups (32 query rows each) instead of
+    4-wave ones — the same per-row arithmetic, so O and the LSE are bit-identical."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(1, S, 4, D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    scale = 1.0 / math.sqrt(D)
+    res = []
+    try:
+        for on in (0, 1):
+            C.attn_set_fwd_narrow(on)
+            res.append(C.attn_fwd(q, k, v, causal, scale, 0.0, None, None, True))
+    finally:
+        C.attn_set_fwd_narrow(0)
+    torch.testing.assert_close(res[1][0], res[0][0], atol=0, rtol=0)
+    torch.testing.assert_close(res[1][1], res[0][1], atol=0, rtol=0)
+
+
 def test_attention_packed_and_padding_mask():
     from hyperion.ops.attention import attention_packed
 
