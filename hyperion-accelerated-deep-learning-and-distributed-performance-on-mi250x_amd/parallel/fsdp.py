@@ -263,6 +263,9 @@ class _FlatGroup:
             prev = self.ring.owner[self.slot]
             if prev is not self:
                 if prev is not None:  # evict: its later use re-gathers (same comm stream: ours lands last)
+                    if getattr(prev, "unit", None) in self.fsdp._live_fwd:
+                        raise RuntimeError(f"FSDP ring: gathering {self.tag} into slot {self.slot} would evict "
+                                           f"{prev.tag}, whose forward is still running")
                     prev.gathered = False
                     prev.gather_work = None
                 self.ring.owner[self.slot] = self
@@ -364,8 +367,16 @@ class _FlatGroup:
         if self.fsdp.identity:
             if self.grad_ring is not None:  # the slot is reused by a later unit: take the shard now
                 with torch.no_grad():
-                    self._grad_shard.copy_(buf[: self.shard_numel])
-                self.rs_out, self.rs_work = self._grad_shard, None
+                    if self.flat_param.grad is None:
+                        self._grad_shard.copy_(buf[: self.shard_numel])
+                        self.rs_out = self._grad_shard
+                    else:
+                        # .grad exists (accumulation, zero_grad(set_to_none=False), warm-up replays):
+                        # it may BE _grad_shard, so add the slot's gradient into it right here —
+                        # a copy into _grad_shard first would overwrite what is being accumulated
+                        self.flat_param.grad.add_(buf[: self.shard_numel])
+                        self.rs_out = None  # finish_reduce: nothing left to add
+                self.rs_work = None
                 return
             self.rs_out, self.rs_work = buf, None
             return
@@ -385,6 +396,10 @@ class _FlatGroup:
             self.rs_work.wait()
             self.rs_work = None
         g = self.rs_out
+        if g is None:  # identity ring: already accumulated into .grad by reduce()
+            if not self.pinned:
+                self.full_grad.untyped_storage().resize_(0)
+            return
         if self.fsdp.identity:  # rs_out is the full flat gradient buffer (released below)
             g = g[: self.shard_numel]
         with torch.no_grad():
@@ -413,6 +428,9 @@ class _Unit:
         self.train = _FlatGroup(fsdp, train, True, f"u{index}t", ring_member) if train else None
         self.frozen = _FlatGroup(fsdp, frozen, False, f"u{index}f", ring_member) if frozen else None
         self.groups = [g for g in (self.frozen, self.train) if g is not None]
+        for g in self.groups:
+            g.unit_index = index
+            g.unit = self
         self._pidx = {id(p): i for i, p in enumerate(train)}
 
     @property
@@ -430,11 +448,19 @@ class _Unit:
             g.wait_gather()
 
     def ring_slot_busy(self, active: Optional["_Unit"]) -> bool:
-        """A prefetch of this unit would overwrite the ring slot the ACTIVE unit computes from."""
-        if active is None or active is self:
-            return False
-        return any(g.ring is not None and g.ring.owner[g.slot] is not None and g.ring.owner[g.slot] in active.groups
-                   for g in self.groups)
+        """A prefetch of this unit would overwrite a ring slot that a running unit computes from:
+        the ACTIVE one, or (nested units) an enclosing unit whose forward or backward is still in
+        progress — with nesting, several units are live at once."""
+        live = self.fsdp._live_fwd | self.fsdp._live_bwd
+        for g in self.groups:
+            if g.ring is None:
+                continue
+            occ = g.ring.owner[g.slot]
+            if occ is None or occ in self.groups:
+                continue
+            if (active is not None and occ in active.groups) or getattr(occ, "unit", None) in live:
+                return True
+        return False
 
     def reshard(self) -> None:
         for g in self.groups:
@@ -456,12 +482,14 @@ class _Unit:
                 # unit's backward needs the full params any more.  (With frozen params — LoRA — the
                 # unit's input-grad hook releases them instead: frozen weights are still read after
                 # the last trainable grad lands.)
+                self.fsdp._live_bwd.discard(self)
                 self.reshard()
 
     def on_input_grads(self) -> None:
         """All grads w.r.t. the unit's inputs exist: its backward is over."""
         if self.train is not None and not self.train.reduced:
             self.train.reduce()
+        self.fsdp._live_bwd.discard(self)
         self.reshard()
 
     def finish(self) -> None:
@@ -584,6 +612,12 @@ class FullyShardedDataParallel(nn.Module):
                         setattr(m, name, b.to(self.mp.buffer_dtype))
         # units: policy-selected submodules (post-order, so nested units claim first), then the root
         unit_modules = _select_units(module, auto_wrap_policy)
+        if self.ring and self._ring_slots(module, unit_modules, self.ring) is None:
+            log.warning("FSDP ring=%d: wrapped units nest %d+ deep, no slot assignment keeps a unit "
+                        "out of its ancestors' slots; using reshard-after-forward without the ring",
+                        self.ring, self.ring)
+            self.ring = 0
+            self.persistent_reason = "ring disabled: nested units"
         claimed: Set[int] = set()
         self.units: List[_Unit] = []
         for um in unit_modules + [module]:
@@ -599,6 +633,8 @@ class FullyShardedDataParallel(nn.Module):
         if self.ring:
             self._build_rings()
         self._active: Optional[_Unit] = None
+        self._live_fwd: Set[_Unit] = set()  # units between their forward pre- and post-hooks
+        self._live_bwd: Set[_Unit] = set()  # units whose backward started and has not finished
         self._unit_of_param = {id(p): u for u in self.units for p in u.params}
         self._fwd_order: List[_Unit] = []
         self._recording = True
@@ -612,10 +648,45 @@ class FullyShardedDataParallel(nn.Module):
                 if p.requires_grad:
                     self._handles.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
 
+    @staticmethod
+    def _ring_slots(root: nn.Module, unit_modules: List[nn.Module], k: int) -> Optional[List[int]]:
+        """Ring slot of each wrapped unit (``unit_modules`` in unit-index order), or None when no
+        assignment is safe.
+
+        A unit nested inside another wrapped unit (size-based policies wrap ``linear1`` /
+        ``linear2`` AND the rest of their encoder layer) is gathered while its
+        ancestor still computes from its own slot, so a unit never shares a slot with any of its
+        ancestors.  Units are visited ancestors-first and cycle through the slots they may use
+        (unit i -> slot i % K for a flat stack of layers); a nesting K deep has no safe slot."""
+        index = {id(m): i for i, m in enumerate(unit_modules)}
+        ancestors: Dict[int, List[int]] = {}
+
+        def visit(m: nn.Module, chain: List[int]) -> None:
+            i = index.get(id(m))
+            if i is not None:
+                ancestors[i] = chain
+                chain = chain + [i]
+            for c in m.children():
+                visit(c, chain)
+
+        visit(root, [])
+        slots: List[int] = [-1] * len(unit_modules)
+        nxt = 0
+        for i in sorted(range(len(unit_modules)), key=lambda i: (len(ancestors.get(i, [])), i)):
+            banned = {slots[a] for a in ancestors.get(i, [])}
+            free = [s for s in ((nxt + j) % k for j in range(k)) if s not in banned]
+            if not free:
+                return None
+            slots[i] = free[0]
+            nxt = free[0] + 1
+        return slots
+
     def _build_rings(self) -> None:
         """One parameter ring per (kind, dtype) and one gradient ring, each slot sized to the
-        largest member; unit i (module order = forward order for stacked layers) takes slot i % K."""
+        largest member; slots come from ``_ring_slots`` (unit i -> slot i % K for a flat stack)."""
         members = [u for u in self.units if u is not self.root_unit]
+        slot_of = self._ring_slots(self.module, [u.module for u in members], self.ring)
+        assert slot_of is not None  # checked before the units were built (__init__)
         for kind in ("train", "frozen"):
             groups = [getattr(u, kind) for u in members if getattr(u, kind) is not None]
             groups = [g for g in groups if g.ring_member]
@@ -627,8 +698,8 @@ class FullyShardedDataParallel(nn.Module):
             self._rings[kind] = pr
             if gr is not None:
                 self._rings["grad"] = gr
-            for i, g in enumerate(groups):
-                g.attach_ring(pr, gr, i % self.ring)
+            for g in groups:
+                g.attach_ring(pr, gr, slot_of[g.unit_index])
 
     def memory_plan(self) -> Dict[str, float]:
         """GiB of gathered-parameter / full-gradient buffers this configuration keeps allocated."""
@@ -671,6 +742,7 @@ class FullyShardedDataParallel(nn.Module):
                     torch.autograd.graph.register_multi_grad_hook(ins, lambda grads: self._input_grads(u), mode="all")
             if self._recording and u not in self._fwd_order:
                 self._fwd_order.append(u)
+            self._live_fwd.add(u)
             self._active = u
             u.gather()
             if self.forward_prefetch and not self._recording:
@@ -683,6 +755,7 @@ class FullyShardedDataParallel(nn.Module):
 
     def _make_post_fwd(self, u: _Unit):
         def hook(module, args, output):
+            self._live_fwd.discard(u)
             grad = torch.is_grad_enabled()
             if self.reshard_after_forward or not grad:
                 u.reshard()
@@ -705,6 +778,7 @@ class FullyShardedDataParallel(nn.Module):
             with self._on_compute_stream():
                 self._ensure_backward_started()
                 self._active = u
+                self._live_bwd.add(u)
                 u.gather()
                 if self.backward_prefetch:
                     prv = self._neighbour(u, -1)
@@ -754,6 +828,7 @@ class FullyShardedDataParallel(nn.Module):
                     g.gathered = False  # ... and re-gather (the persistent buffer keeps its storage)
         self._in_backward = False
         self._active = None
+        self._live_bwd.clear()
 
     def invalidate_gather_cache(self) -> None:
         """Call after changing the flat shards outside an optimizer step that follows backward."""
@@ -767,6 +842,7 @@ class FullyShardedDataParallel(nn.Module):
         # the stream the step's compute runs on: backward hooks issue their copies and collectives
         # on it (see _on_compute_stream)
         self._compute_stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        self._live_fwd.clear()
         self.root_unit.gather()
         if self.forward_prefetch and not self._recording and self._fwd_order:
             self._fwd_order[0].gather(async_op=True)

@@ -286,3 +286,82 @@ def _replicated_roundtrip_subgroup(rank, world, tmp):
 def test_fsdp_replicated_frozen_subgroup_broadcast_source(tmp_path):
     res = run_world(_replicated_roundtrip_subgroup, 3, (str(tmp_path),))
     assert res[0] is None and res[1] and res[2]
+
+
+# ---- ring mode: gradient accumulation at world 1 and nested units (medium) ----
+def _fsdp_accum_train(rank, world, ring, policy_kind="layer", layers=3, steps=2):
+    """Two micro-batch backwards per step and zero_grad(set_to_none=False): .grad exists when the
+    second backward's gradients land, so every accumulation path runs."""
+    from hyperion.models.transformer import TransformerEncoderLayer
+    from hyperion.parallel.fsdp import FSDP, size_based_auto_wrap_policy, transformer_auto_wrap_policy
+
+    policy = {"layer": transformer_auto_wrap_policy({TransformerEncoderLayer}),
+              "leaf": size_based_auto_wrap_policy(500)}[policy_kind]
+    m = FSDP(_make_model(layers=layers), auto_wrap_policy=policy, device_id=torch.device("cpu"),
+             sharding_strategy="FULL_SHARD", ring=ring)
+    if ring:
+        for r in m._rings.values():
+            for b in r.bufs:
+                b.fill_(float("nan"))
+    opt = torch.optim.SGD(m.parameters(), lr=1e-1, momentum=0.9)
+    per = 8 // world
+    for s in range(steps):
+        x, y = _batch(s)
+        x, y = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
+        h = per // 2
+        for xx, yy in ((x[:h], y[:h]), (x[h:], y[h:])):
+            (m.forward_loss(xx, yy, ignore_index=-100) / 2).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=False)
+    return {"sd": m.full_state_dict(rank0_only=True), "ring": m.ring}
+
+
+@pytest.mark.parametrize("ring", [2, 3])
+def test_fsdp_ring_world1_accumulates_like_non_ring(ring):
+    """World 1 identity ring path with .grad already present (accumulation, set_to_none=False):
+    equal to the non-ring wrapper doing the same thing (the r05 bug doubled the latest gradient)."""
+    base = run_world(_fsdp_accum_train, 1, (0,))[0]["sd"]
+    got = run_world(_fsdp_accum_train, 1, (ring,))[0]
+    assert got["ring"] == ring
+    for k in base:
+        torch.testing.assert_close(got["sd"][k], base[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("ring", [2, 3])
+def test_fsdp_ring_nested_units_match_single_process(world, ring):
+    """Size-based wrapping nests units (the attention module holds its wrapped out-projection):
+    a nested unit never shares a ring slot with an ancestor, so the NaN-poisoned ring still
+    trains exactly like the non-ring wrapper."""
+    base = run_world(_fsdp_accum_train, world, (0, "leaf", 2))[0]["sd"]
+    got = run_world(_fsdp_accum_train, world, (ring, "leaf", 2))[0]
+    assert got["ring"] == ring
+    for k in base:
+        torch.testing.assert_close(got["sd"][k], base[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def test_fsdp_ring_slot_assignment_rules():
+    import torch.nn as nn
+
+    from hyperion.parallel.fsdp import FSDP
+
+    class Box(nn.Module):
+        def __init__(self, inner):
+            super().__init__()
+            self.inner = inner
+            self.w = nn.Linear(4, 4)
+
+    flat = nn.Sequential(*[nn.Linear(4, 4) for _ in range(5)])
+    assert FSDP._ring_slots(flat, list(flat), 3) == [0, 1, 2, 0, 1]
+    # Box(Box(Linear)): three nested units -> each in its own slot; needs 3 slots
+    leaf = nn.Linear(4, 4)
+    mid = Box(leaf)
+    top = Box(mid)
+    root = nn.Sequential(top)
+    units = [leaf, mid, top]  # post-order
+    slots = FSDP._ring_slots(root, units, 3)
+    assert len(set(slots)) == 3
+    assert FSDP._ring_slots(root, units, 2) is None  # nesting depth 3 > 2 slots
+    m = FSDP(root, auto_wrap_policy=lambda mod, n: isinstance(mod, (nn.Linear, Box)) and mod is not top.w
+             and mod is not mid.w, device_id=torch.device("cpu"), ring=2)
+    assert m.ring == 0  # fell back to reshard-after-forward
