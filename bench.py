@@ -11,8 +11,11 @@ gradient all-reduce (N>1) and optimizer update.
 Reference number: 568.22 samples/s = 56.32 ms/step (ResNet-50, batch 32, fp32, 1x MI250X GCD;
 ``Phase 1/results/benchmarks/Baseline/model_benchmarks.csv:2``).
 
-Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``; for N>1 run under
-``torch.distributed.run --nproc-per-node N``.  Rank 0 prints ONE JSON line.
+Usage: ``python bench.py [--gpus N] [--steps K] [--warmup W]``.  For N>1 either run it under
+``torch.distributed.run --nproc-per-node N`` (one rank per GPU), or give ``--gpus N`` alone: with
+no ``WORLD_SIZE`` in the environment it starts that launcher itself as a CHILD process (before
+anything touches the GPU; never an exec) and exits with its return code — rank 0's JSON line
+reaches stdout through the inherited file descriptor.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -45,12 +48,14 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (1-GPU; N>1 see --graph-multi)")
     ap.add_argument("--graph-multi", type=int, default=1,
                     help="N>1: capture fwd+bwd and the optimizer as two hipGraphs around eager bucket all-reduces")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--ddp-schedule", default="segmented", choices=["auto", "segmented", "graph"],
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="DDP bucket MiB (default: the all-reduce saturation point of configs/busbw_w{N}.json "
+                         "from `test_rccl --sweep --save-tuning`, else 64)")
+    ap.add_argument("--ddp-schedule", default="segmented", choices=["segmented", "graph", "split3"],
                     help="N>1 (or --ddp-world1) graphed DDP schedule: segmented (default) = the whole step "
                          "captured as graph segments with each bucket's all-reduce issue / wait as eager holes, "
-                         "so every bucket overlaps the rest of the backward; auto = 3 graphs split at the "
-                         "model's graph_stages; graph = ONE graph with the RCCL all-reduces recorded into it.  "
+                         "so every bucket overlaps the rest of the backward; split3 = A/B only, 3 graphs split at "
+                         "the model's graph_stages; graph = ONE graph with the RCCL all-reduces recorded into it.  "
                          "Measured at world 1 with the native RCCL communicator: "
                          "5.15 vs 14.5 ms/step (profiles/r05/ddp_schedule_ab.json)")
     ap.add_argument("--ddp-world1", type=int, default=0,
@@ -65,8 +70,34 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, argv) -> "int | None":
+    """``--gpus N`` (N > 1) outside a launcher: one rank per GPU via torch.distributed.run, as a
+    child process.  Returns its exit code, or None when this process is already a rank."""
+    if args.gpus is None or args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL between the ranks
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        return rc
     if args.kernels:
         os.environ["HYPERION_KERNELS"] = args.kernels
     import torch
@@ -207,7 +238,8 @@ def main(argv=None) -> int:
                 "kernels": _native.backend(),
                 "native_so": _native.loaded_path(),
                 "channels_last": bool(args.channels_last),
-                "grad_allreduce_dtype": (None if n_gpus == 1 else args.comm_dtype),
+                "grad_allreduce_dtype": (args.comm_dtype if (n_gpus > 1 or args.ddp_world1) else None),
+                "bucket_mb": getattr(model, "bucket_cap_mb", None),
             },
             "baseline": {"value": BASELINE_SAMPLES_PER_S, "ms_per_step": 56.32, "hw": "1x MI250X GCD, fp32"},
             "final_loss": round(final_loss, 6),

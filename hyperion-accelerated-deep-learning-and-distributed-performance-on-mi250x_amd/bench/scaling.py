@@ -137,3 +137,73 @@ def run_scaling_experiment(model_type: str, gpu_counts: Sequence[int] = (1, 2, 4
     if not dry_run:
         create_scaling_report(os.path.join(base_dir, "data", "distributed"))
     return cmds
+
+
+# ---------------------------------------------------------------- headline (bench.py) scaling
+BENCH_COLUMNS = ("gpus", "samples_per_s", "ms_per_step", "speedup", "efficiency", "replicas_in_sync")
+
+
+def scaling_rows(results: Dict[int, dict]) -> List[dict]:
+    """One row per GPU count from bench.py JSON records.  bench.py is weak scaling (a fixed
+    per-GPU batch), so the reference's epoch-time speedup t₁ / t_g (``distributed_utils.py:684-692``
+    — a fixed dataset) is the throughput ratio value_g / value_1; efficiency = speedup / g."""
+    base = results.get(1)
+    rows = []
+    for g in sorted(results):
+        r = results[g]
+        sp = (r["value"] / base["value"]) if base else None
+        rows.append({"gpus": g, "samples_per_s": r["value"], "ms_per_step": r["ms_per_step"],
+                     "speedup": None if sp is None else round(sp, 4),
+                     "efficiency": None if sp is None else round(sp / g, 4),
+                     "replicas_in_sync": (r.get("replicas") or {}).get("in_sync") if g > 1 else True})
+    return rows
+
+
+def write_scaling_csv(rows: List[dict], path: str) -> str:
+    import csv
+
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(BENCH_COLUMNS))
+        w.writeheader()
+        for r in rows:
+            w.writerow({k: r.get(k) for k in BENCH_COLUMNS})
+    return path
+
+
+def run_bench_scaling(gpu_counts: Sequence[int] = (1, 2, 4, 8), out_dir: str = "results/scaling",
+                      bench_args: Sequence[str] = (), timeout: float = 1800.0,
+                      bench: Optional[str] = None) -> Dict[int, dict]:
+    """The BASELINE headline at every GPU count: ``bench.py --gpus g`` in a FRESH child process per
+    count (it starts its own one-rank-per-GPU launcher for g > 1), its rank-0 JSON line kept as
+    ``bench_{g}gpus.json``, then ``scaling_resnet50.csv`` with speedup / efficiency."""
+    import json
+
+    bench = bench or os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                  "bench.py")
+    os.makedirs(out_dir, exist_ok=True)
+    results: Dict[int, dict] = {}
+    for g in gpu_counts:
+        cmd = [sys.executable, bench, "--gpus", str(g)] + list(bench_args)
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+        except subprocess.TimeoutExpired:
+            print(f"[scale_bench] {g} GPUs: timed out after {timeout:.0f} s")
+            continue
+        line = next((ln for ln in reversed(p.stdout.splitlines()) if ln.startswith("{")), None)
+        if p.returncode != 0 or line is None:
+            print(f"[scale_bench] {g} GPUs failed (rc={p.returncode}):\n{p.stderr[-2000:]}")
+            continue
+        rec = json.loads(line)
+        results[g] = rec
+        with open(os.path.join(out_dir, f"bench_{g}gpus.json"), "w") as f:
+            f.write(line + "\n")
+        print(f"[scale_bench] {g} GPUs: {rec['value']:.1f} {rec.get('unit', '')}, {rec['ms_per_step']:.3f} ms/step",
+              flush=True)
+    rows = scaling_rows(results)
+    metric = next(iter(results.values()))["metric"].split("_")[0] if results else "resnet50"
+    write_scaling_csv(rows, os.path.join(out_dir, f"scaling_{metric}.csv"))
+    for r in rows:
+        print(r)
+    return results

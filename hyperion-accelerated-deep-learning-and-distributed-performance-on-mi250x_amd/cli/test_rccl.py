@@ -108,6 +108,9 @@ def main(argv=None) -> int:
     ap.add_argument("--sizes_mb", default="0.25,1,4,16,64,256,1024")
     ap.add_argument("--timeout", type=float, default=60.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--save-tuning", action="store_true",
+                    help="also write configs/busbw_w{world}.json: DDP then sizes its buckets from this curve "
+                         "(parallel/tuning.py)")
     ap.add_argument("--backend", default=None, choices=["torch", "native"],
                     help="collectives through Hyperion's C++ RCCL communicator (native, GPU default) or torch.distributed")
     a = ap.parse_args(argv)
@@ -130,8 +133,13 @@ def main(argv=None) -> int:
         check(rank, world, device, comm)
         if a.sweep and gpu:
             rows = sweep(rank, world, device, [float(s) for s in a.sizes_mb.split(",")], comm=comm)
-            if rank == 0 and a.out:
-                with open(a.out, "w") as f:
+            outs = [a.out] if a.out else []
+            if a.save_tuning:
+                from hyperion.parallel.tuning import sweep_path
+
+                outs.append(sweep_path(world))
+            for path in outs if rank == 0 else []:
+                with open(path, "w") as f:
                     json.dump({"world": world, "rows": rows}, f, indent=2)
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001

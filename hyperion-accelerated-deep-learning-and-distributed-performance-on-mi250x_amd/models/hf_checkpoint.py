@@ -44,11 +44,25 @@ def is_hf_dir(path: Optional[str]) -> bool:
             and (os.path.isfile(os.path.join(path, INDEX)) or os.path.isfile(os.path.join(path, SINGLE))))
 
 
+# config fields whose non-default values this Llama does not implement: refusing them beats a model
+# that loads without error and runs with the wrong RoPE / projections (Llama-3.x rope_scaling, ...)
+_UNSUPPORTED = {"rope_scaling": None, "attention_bias": False, "mlp_bias": False, "hidden_act": "silu",
+                "pretraining_tp": 1}
+
+
 def load_llama_config(path: str):
     from .llama import LlamaConfig
 
     with open(os.path.join(path, "config.json")) as f:
         raw = json.load(f)
+    bad = {k: raw[k] for k, ok in _UNSUPPORTED.items() if k in raw and raw[k] is not None and raw[k] != ok}
+    hd = raw.get("head_dim")
+    if hd is not None and "hidden_size" in raw and "num_attention_heads" in raw and \
+            hd != raw["hidden_size"] // raw["num_attention_heads"]:
+        bad["head_dim"] = hd
+    if bad:
+        raise ValueError(f"{path}/config.json: unsupported Llama settings {bad} (this model implements plain "
+                         f"RoPE, bias-free projections, SiLU, head_dim = hidden_size / heads)")
     kw = {k: raw[k] for k in _CFG_FIELDS if k in raw and raw[k] is not None}
     if "num_key_value_heads" not in kw and "num_attention_heads" in kw:
         kw["num_key_value_heads"] = kw["num_attention_heads"]
@@ -101,8 +115,11 @@ def load_hf_weights(model: nn.Module, path: str, strict: bool = True) -> Dict[st
     missing = [n for n in dict(model.named_parameters()) if n not in set(loaded)
                and not (tied and n == "lm_head.weight")]
     if tied and "lm_head.weight" not in loaded and "model.embed_tokens.weight" in loaded:
-        with torch.no_grad():
-            targets["lm_head.weight"].copy_(targets["model.embed_tokens.weight"])
+        if hasattr(model, "tie_weights"):
+            model.tie_weights()  # one shared Parameter (trains as one)
+        else:
+            with torch.no_grad():
+                targets["lm_head.weight"].copy_(targets["model.embed_tokens.weight"])
     if strict and (missing or unknown):
         raise KeyError(f"checkpoint {path}: missing {missing[:8]}{'...' if len(missing) > 8 else ''}, "
                        f"unexpected {unknown[:8]}{'...' if len(unknown) > 8 else ''}")

@@ -185,6 +185,13 @@ class LlamaForCausalLM(nn.Module):
         self.model = LlamaModel(self.config)
         self.lm_head = LinearCrossEntropy(self.config.hidden_size, self.config.vocab_size, bias=False)
         self.apply(self._init_weights)
+        if self.config.tie_word_embeddings:
+            self.tie_weights()
+
+    def tie_weights(self) -> None:
+        """HF ``tie_word_embeddings``: ONE Parameter serves as the input embedding and the LM head,
+        so both train together (a copy would drift apart after the first optimizer step)."""
+        self.lm_head.weight = self.model.embed_tokens.weight
 
     def _init_weights(self, m: nn.Module) -> None:
         std = self.config.initializer_range
@@ -211,6 +218,8 @@ class LlamaForCausalLM(nn.Module):
         if torch_dtype is not None:
             m = m.to(torch_dtype)
         load_hf_weights(m, path, strict=strict)
+        if cfg.tie_word_embeddings:
+            m.tie_weights()
         return m
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,

@@ -60,6 +60,9 @@ CE_MATERIALIZE_BYTES = int(_CE_MAT_ENV) << 20 if _CE_MAT_ENV is not None else No
 _HBM_BUDGET = {}
 
 
+_SCHEDULE = {}  # (device, N, V-padded, element size) -> materialise the logits?
+
+
 def _materialize_budget(dev: torch.device) -> int:
     if CE_MATERIALIZE_BYTES is not None:
         return CE_MATERIALIZE_BYTES
@@ -70,7 +73,24 @@ def _materialize_budget(dev: torch.device) -> int:
     if torch.cuda.is_current_stream_capturing():
         return budget  # no free-memory query inside a capture; the graph pool was sized eagerly
     free, _ = torch.cuda.mem_get_info(idx)
+    # blocks the caching allocator holds but does not use are free for this op too
+    free += torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
     return min(budget, free // 2)
+
+
+def _materialize(dev: torch.device, N: int, V: int, elt: int) -> bool:
+    """The schedule (materialised logits or not) is decided ONCE per (device, shape, dtype) on the
+    first call and reused: a per-call free-memory check could flip it between steps (different
+    numerics and memory) or pick, under hipGraph capture, a logits buffer that eager warm-up
+    never sized."""
+    vp = -(-V // 8) * 8
+    if CE_MATERIALIZE_BYTES is not None:  # an explicit budget: a fixed rule, nothing to cache
+        return N * vp * elt <= CE_MATERIALIZE_BYTES
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, N, vp, elt)
+    if key not in _SCHEDULE:
+        _SCHEDULE[key] = N * key[2] * elt <= _materialize_budget(dev)
+    return _SCHEDULE[key]
 
 
 def _ce_chunk(N: int, V: int, elt: int) -> int:
@@ -114,7 +134,7 @@ class _FusedLinearCE(torch.autograd.Function):
         scale = (1.0 / n_valid).reshape(1)
         native = _native.use_native(x2, op="ce") and cdt in _native.DTYPE_CODE
         if native and cdt in (torch.bfloat16, torch.float16) and x2.is_cuda:
-            if N * (-(-V // 8) * 8) * x2.element_size() <= _materialize_budget(x2.device):
+            if _materialize(x2.device, N, V, x2.element_size()):
                 return _FusedLinearCE._materialized(ctx, x, x2, w, bias, t, ignore_index, scale, shape)
             if x2.shape[1] % 64 == 0:
                 return _FusedLinearCE._fused(ctx, x, x2, w, bias, t, ignore_index, scale, n_valid, shape)

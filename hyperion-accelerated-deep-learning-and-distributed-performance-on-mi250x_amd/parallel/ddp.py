@@ -114,7 +114,7 @@ class DistributedDataParallel(nn.Module):
         self,
         module: nn.Module,
         process_group=None,
-        bucket_cap_mb: float = 64.0,
+        bucket_cap_mb: Optional[float] = None,
         first_bucket_mb: float = 4.0,
         broadcast_buffers: bool = True,
         comm_dtype: Optional[torch.dtype] = torch.float32,
@@ -125,8 +125,16 @@ class DistributedDataParallel(nn.Module):
     ):
         """``comm_dtype``: gradient bucket / all-reduce dtype (fp32 default; ``None`` = each
         parameter's dtype).  ``buckets_at_world_1``: build the bucket machinery even for a single
-        rank (tests of the bucket / deferred-all-reduce / graph paths on a one-GPU box)."""
+        rank (tests of the bucket / deferred-all-reduce / graph paths on a one-GPU box).
+        ``bucket_cap_mb=None``: the all-reduce saturation point of a measured busbw sweep for this
+        world size (``parallel/tuning.py``), 64 MiB without one."""
         super().__init__()
+        if bucket_cap_mb is None:
+            from .tuning import bucket_mb
+
+            w = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+            bucket_cap_mb = bucket_mb(w)
+        self.bucket_cap_mb = float(bucket_cap_mb)
         self.module = module
         self.process_group = process_group
         # bucket all-reduces go through the comm layer: Hyperion's native RCCL communicator (own

@@ -64,17 +64,22 @@ class TrainStep:
         warmup_iters: int = 3,
         scaler=None,
         split_backward: bool = True,
-        ddp_schedule: str = "auto",
+        ddp_schedule: str = "segmented",
     ):
-        """``ddp_schedule`` (a bucketed Hyperion DDP model, graph mode): ``"auto"`` = three graphs
-        (top forward+backward | bottom backward overlapping the top buckets' all-reduce | optimizer)
-        when the model exposes ``graph_stages``, else two graphs around the all-reduces;
-        ``"segmented"`` = the whole step captured as segments with every bucket's all-reduce issue
-        and wait as eager holes (``train/segments.py``): each bucket overlaps the rest of the
-        captured backward, at the cost of one graph launch per hole; ``"graph"`` = ONE graph with
-        the bucket all-reduces recorded into it (the native RCCL communicator's comm stream forked
-        from and joined into the capture: no host holes at all)."""
-        if ddp_schedule not in ("auto", "segmented", "graph"):
+        """``ddp_schedule`` (a bucketed Hyperion DDP model, graph mode): ``"segmented"`` (default;
+        ``"auto"`` is an alias) = the whole step captured as segments with every bucket's
+        all-reduce issue and wait as eager holes (``train/segments.py``): each bucket overlaps the
+        rest of the captured backward, at the cost of one graph launch per hole (ResNet-50 at world
+        1 with the native RCCL communicator: 5.13 ms vs 4.58 plain, profiles/r05/ddp_schedule_ab.json);
+        ``"graph"`` = ONE graph with the bucket all-reduces recorded into it (the native RCCL
+        communicator's comm stream forked from and joined into the capture: no host holes at all);
+        ``"split3"`` = A/B only, three graphs (top forward+backward | bottom backward overlapping
+        the top buckets' all-reduce | optimizer) when the model exposes ``graph_stages``, else two
+        graphs around the all-reduces — measured 14.5 ms/step at world 1, 3x the plain step, so it
+        is never picked by default."""
+        if ddp_schedule == "auto":
+            ddp_schedule = "segmented"
+        if ddp_schedule not in ("split3", "segmented", "graph"):
             raise ValueError(f"ddp_schedule {ddp_schedule!r}")
         self.ddp_schedule = ddp_schedule
         self.seg = None
@@ -284,7 +289,7 @@ class TrainStep:
             if ddp is not None:
                 # graph schedules: the all-reduces run between the graphs; segmented: from the
                 # bucket hooks, as holes of the capture
-                ddp.defer_allreduce = self.ddp_schedule == "auto"
+                ddp.defer_allreduce = self.ddp_schedule == "split3"
             self._capture(x, y)
         if x.data_ptr() != self.static_x.data_ptr():
             self.static_x.copy_(x, non_blocking=True)

@@ -104,3 +104,55 @@ def test_reference_plots_from_csvs(tmp_path):
                 plot_precision_performance(str(tmp_path / "precision_results.csv")),
                 plot_memory_bandwidth(str(tmp_path / "bandwidth_results.csv"))):
         assert os.path.getsize(out) > 1000
+
+
+def test_scale_bench_dry_run_gloo_writes_csv(tmp_path):
+    """The headline scaling orchestrator (VERDICT r05 next #3b): bench.py per GPU count in fresh
+    children (``--gpus 2`` self-launches its torch.distributed.run child), gloo ranks on the CPU,
+    then scaling_resnet18.csv with the reference's speedup / efficiency columns."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo, HYPERION_DIST_BACKEND="gloo")
+    out = tmp_path / "scaling"
+    p = subprocess.run([sys.executable, "-m", "hyperion.cli.scale_bench", "--gpus", "1,2", "--out", str(out), "--",
+                        "--model", "resnet18", "--image", "32", "--batch", "2", "--steps", "1", "--warmup", "1"],
+                       capture_output=True, text=True, env=env, cwd=str(tmp_path), timeout=600)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    df = pd.read_csv(out / "scaling_resnet18.csv")
+    assert list(df.columns) == ["gpus", "samples_per_s", "ms_per_step", "speedup", "efficiency", "replicas_in_sync"]
+    assert list(df.gpus) == [1, 2]
+    assert df.speedup[0] == 1.0 and df.replicas_in_sync.all()
+    r2 = df[df.gpus == 2].iloc[0]
+    assert r2.efficiency == pytest.approx(r2.speedup / 2, abs=1e-3)
+    import json
+
+    rec = json.loads((out / "bench_2gpus.json").read_text())
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"  # the child really ran 2 ranks
+
+
+def test_bench_scaling_rows_formula():
+    from hyperion.bench.scaling import scaling_rows
+
+    rows = scaling_rows({1: {"value": 100.0, "ms_per_step": 10.0},
+                         8: {"value": 720.0, "ms_per_step": 11.1, "replicas": {"in_sync": True}}})
+    assert rows[1]["speedup"] == pytest.approx(7.2) and rows[1]["efficiency"] == pytest.approx(0.9)
+
+
+def test_bucket_mb_from_busbw_sweep(tmp_path, monkeypatch):
+    import json
+
+    from hyperion.parallel import tuning
+
+    rows = [{"op": "all_reduce", "bytes": mb << 20, "busbw_GBps": bw}
+            for mb, bw in ((1, 40.0), (4, 120.0), (16, 250.0), (64, 300.0), (256, 310.0))]
+    rows += [{"op": "all_gather", "bytes": 1 << 20, "busbw_GBps": 999.0}]
+    p = tmp_path / "busbw_w8.json"
+    p.write_text(json.dumps({"world": 8, "rows": rows}))
+    monkeypatch.setenv("HYPERION_BUSBW_JSON", str(p))
+    assert tuning.bucket_mb(8) == 64.0  # first size >= 90 % of 310 GB/s
+    assert tuning.bucket_mb(8, saturation=0.8) == 16.0
+    assert tuning.bucket_mb(4, default=33.0) == 33.0  # a sweep of another world size is not used
+    monkeypatch.setenv("HYPERION_BUSBW_JSON", str(tmp_path / "missing.json"))
+    assert tuning.bucket_mb(8) == 64.0

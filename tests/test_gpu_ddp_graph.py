@@ -90,7 +90,7 @@ def test_ddp_graph_step_grads_match_eager(split, native):
         assert {b.buf.dtype for b in ddp._buckets} == {torch.float32}  # fp32 reduction by default
         dopt = FusedAdam(ddp.parameters(), lr=1e-3, zero_grad_in_step=True)
         dstep = TrainStep(ddp, dopt, torch.nn.MSELoss(), amp_dtype=None, graph=True, warmup_iters=2,
-                          split_backward=split)
+                          split_backward=split, ddp_schedule="split3")
         dstep(x, y)  # warm-up + capture + one replay (weights move)
         assert dstep.graph2 is not None and (dstep.graph3 is not None) == split
         if split:
@@ -124,7 +124,7 @@ def test_ddp_graph_step_grads_match_eager(split, native):
         dist.destroy_process_group()
 
 
-def _two_rank_graph(rank, world, steps, schedule="auto"):
+def _two_rank_graph(rank, world, steps, schedule="split3"):
     os.environ["HYPERION_COMM"] = "torch"  # gloo collectives between the two processes
     torch.cuda.set_device(0)
     _pin_deterministic()
@@ -148,7 +148,7 @@ def _two_rank_graph(rank, world, steps, schedule="auto"):
             losses.append(float(st(xs[0], ys[0])))  # warm-up step + capture + replay: step 0 twice
             for i in range(1, steps):
                 losses.append(float(st(xs[i], ys[i])))
-            graphs = st.graph3 is not None if schedule == "auto" else st.seg is not None
+            graphs = st.graph3 is not None if schedule == "split3" else st.seg is not None
         else:
             ddp.defer_allreduce = True
             st = TrainStep(ddp, opt, torch.nn.MSELoss(), amp_dtype=None, graph=False)
@@ -162,7 +162,7 @@ def _two_rank_graph(rank, world, steps, schedule="auto"):
     return res
 
 
-@pytest.mark.parametrize("schedule", ["auto", "segmented"])
+@pytest.mark.parametrize("schedule", ["split3", "segmented"])
 def test_two_rank_gloo_graph_step_replicas_identical(schedule):
     """auto: the three-graph split; segmented: bench.py's N>1 default (graph segments with the
     bucket all-reduces as eager holes)."""

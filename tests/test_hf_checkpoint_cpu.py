@@ -102,3 +102,36 @@ def test_trainer_loads_local_model_id(tmp_path):
                           batch_size=2, progress_every=0, opts=opts,
                           config=__import__("hyperion.models.llama", fromlist=["LlamaConfig"]).LlamaConfig.tiny())
     assert r2["weights"] == "random-init"
+
+
+def test_tied_embeddings_share_one_parameter(tmp_path):
+    """tie_word_embeddings: the LM head IS the embedding Parameter after loading (a copy
+    drifted apart during training); only one tensor is saved."""
+    from hyperion.models.hf_checkpoint import save_hf_checkpoint
+    from hyperion.models.llama import LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(LlamaConfig.tiny(num_hidden_layers=1, tie_word_embeddings=True))
+    assert m.lm_head.weight is m.model.embed_tokens.weight
+    save_hf_checkpoint(m, str(tmp_path))
+    r = LlamaForCausalLM.from_pretrained(str(tmp_path))
+    assert r.lm_head.weight is r.model.embed_tokens.weight
+    assert torch.equal(r.lm_head.weight, m.lm_head.weight)
+    opt = torch.optim.SGD(r.parameters(), lr=0.1)
+    ids = torch.randint(0, 512, (2, 9))
+    r(ids, labels=ids).loss.backward()
+    opt.step()
+    assert r.lm_head.weight is r.model.embed_tokens.weight  # still one tensor after a step
+
+
+@pytest.mark.parametrize("field,value", [("rope_scaling", {"rope_type": "llama3", "factor": 8.0}),
+                                         ("attention_bias", True), ("head_dim", 48), ("hidden_act", "gelu")])
+def test_unsupported_config_fields_refused(tmp_path, field, value):
+    from hyperion.models.hf_checkpoint import load_llama_config, save_hf_checkpoint
+
+    save_hf_checkpoint(_tiny(), str(tmp_path))
+    cfg = json.load(open(tmp_path / "config.json"))
+    cfg[field] = value
+    json.dump(cfg, open(tmp_path / "config.json", "w"))
+    with pytest.raises(ValueError, match=field):
+        load_llama_config(str(tmp_path))
