@@ -56,17 +56,22 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, 
                 const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& aux,
                 const c10::optional<at::Tensor>& residual, double alpha, double beta,
                 const c10::optional<at::Tensor>& out, int64_t tile, int64_t splits, double drop_p,
-                const c10::optional<at::Tensor>& rng) {
+                const c10::optional<at::Tensor>& rng, int64_t n_out) {
   HYP_CHECK_CUDA_TENSOR(a);
   check_operand(a, "a");
   check_operand(b, "b");
   TORCH_CHECK(a.scalar_type() == b.scalar_type() && (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf),
               "gemm: bf16/f16 operands of one dtype");
   const int64_t M = a_tr ? a.size(1) : a.size(0), K = a_tr ? a.size(0) : a.size(1);
-  const int64_t N = b_tr ? b.size(1) : b.size(0), Kb = b_tr ? b.size(0) : b.size(1);
+  const int64_t NB = b_tr ? b.size(1) : b.size(0), Kb = b_tr ? b.size(0) : b.size(1);
+  // n_out > rows of a row-form B: output columns past B's rows are computed from zeros (the LM
+  // head's padded class columns, written so the padded logits buffer needs no separate fill)
+  TORCH_CHECK(n_out < 0 || (!b_tr && n_out >= NB), "gemm: n_out needs a row-form b with at most n_out rows");
+  const int64_t N = n_out > 0 ? n_out : NB;
   TORCH_CHECK(K == Kb, "gemm: reduction sizes differ (", K, " vs ", Kb, ")");
-  TORCH_CHECK(N % 4 == 0 && K % 8 == 0 && (!a_tr || M % 8 == 0) && (!b_tr || N % 8 == 0),
-              "gemm: needs N % 4 == 0, K % 8 == 0 (and M / N % 8 == 0 for transposed operands)");
+  TORCH_CHECK(N % 4 == 0 && (K % 8 == 0 || a_tr || b_tr) && (!a_tr || M % 8 == 0) && (!b_tr || N % 8 == 0),
+              "gemm: needs N % 4 == 0, K % 8 == 0 unless an operand is transposed (and M / N % 8 == 0 for "
+              "transposed operands)");
   TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "gemm: dims must fit int32");
   const at::DeviceGuard guard(a.device());
   at::Tensor c;
@@ -99,6 +104,7 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, 
   g.beta = (float)beta;
   g.tile = (int)tile;
   g.splits = (int)splits;
+  g.b_rows = (int)NB;
   g.zero = device_zero_page(a.device());
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->dim() == 1 && bias->numel() == N && bias->is_contiguous(), "gemm: bias must be [N] contiguous");
@@ -151,7 +157,7 @@ void register_gemm_ops(pybind11::module& m) {
         pybind11::arg("act") = 0, pybind11::arg("aux") = pybind11::none(), pybind11::arg("residual") = pybind11::none(),
         pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0, pybind11::arg("out") = pybind11::none(),
         pybind11::arg("tile") = -1, pybind11::arg("splits") = -1, pybind11::arg("drop_p") = 0.0,
-        pybind11::arg("rng") = pybind11::none());
+        pybind11::arg("rng") = pybind11::none(), pybind11::arg("n_out") = -1);
   m.def("gemm_set_splitk_inkernel", [](int64_t on) { hyp::gemm_set_splitk_inkernel((int)on); },
         "A/B: split-K reduce in the last-arriving workgroup (1) or the separate reduce kernel (0, default)");
   m.def("gemm_plan", &gemm_plan, "(tile, splits) the automatic plan picks for an M x N x K GEMM");

@@ -21,6 +21,7 @@ import argparse
 import concurrent.futures as cf
 import glob
 import hashlib
+import re
 import os
 import shutil
 import subprocess
@@ -51,11 +52,29 @@ def _torch_paths():
     return inc, lib, bool(torch._C._GLIBCXX_USE_CXX11_ABI)
 
 
-def _headers_digest() -> str:
+_INCLUDE = re.compile(rb'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _headers_digest(src: str) -> str:
+    """Digest of the in-tree headers ``src`` includes, transitively (quoted includes resolved
+    against the including file's directory, then csrc/): a header edit rebuilds only its users."""
     h = hashlib.sha1()
-    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
-        with open(p, "rb") as f:
-            h.update(f.read())
+    seen, stack = set(), [src]
+    while stack:
+        cur = stack.pop()
+        with open(cur, "rb") as f:
+            text = f.read()
+        if cur != src:
+            h.update(cur.encode() + text)
+        for inc in _INCLUDE.findall(text):
+            inc = inc.decode()
+            for base in (os.path.dirname(cur), CSRC):
+                cand = os.path.normpath(os.path.join(base, inc))
+                if os.path.isfile(cand):
+                    if cand not in seen:
+                        seen.add(cand)
+                        stack.append(cand)
+                    break
     return h.hexdigest()[:12]
 
 
@@ -109,9 +128,9 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool
         "-DTORCH_EXTENSION_NAME=" + ("_C_debug" if debug else "_C"),
         "-DTORCH_API_INCLUDE_EXTENSION_H",
     ]
-    hdr = _headers_digest()
     todo, objs = [], []
     for src in _sources():
+        hdr = _headers_digest(src)
         with open(src, "rb") as f:
             digest = hashlib.sha1(f.read() + hdr.encode() + " ".join(flags).encode()).hexdigest()[:12]
         rel = os.path.relpath(src, CSRC).replace(os.sep, "_")

@@ -177,6 +177,9 @@ struct GemmTiledArgs {
   // (element index row * ldc + col); aux keeps z
   float drop_p = 0.f;
   RngState drng{};
+  // rows of a row-form B operand when fewer than N (0 = N): output columns past them are computed
+  // from zeros (the LM head's class padding: N = ceil8(V) columns from V weight rows)
+  int b_rows = 0;
 };
 void gemm_tiled_plan(int M, int N, int K, int* tile, int* splits);
 void gemm_tiled_plan_layout(int M, int N, int K, bool a_tr, bool b_tr, int* tile, int* splits);

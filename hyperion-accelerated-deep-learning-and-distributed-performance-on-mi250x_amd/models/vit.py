@@ -10,7 +10,8 @@ ViT design for MI355X: pre-norm blocks whose residual adds are fused into the ne
 (``layer_norm(..., residual=r, return_sum=True)`` returns both ``LN(x + r)`` and ``x + r`` in one
 pass), packed-QKV flash attention on ``[B, 197, 3, 12, 64]`` without permutes, GELU in the FC1
 GEMM epilogue.  ``use_checkpoint=True`` recomputes each encoder block in backward (the
-BASELINE.json "ViT-Base bf16 + activation checkpointing" config).  State-dict keys equal
+BASELINE.json "ViT-Base bf16 + activation checkpointing" config); ``use_checkpoint="selective"``
+keeps the GEMM outputs and rebuilds only the LayerNorm / GELU outputs (``ops/recompute.py``).  State-dict keys equal
 torchvision's (``conv_proj``, ``class_token``, ``encoder.pos_embedding``,
 ``encoder.layers.encoder_layer_N.{ln_1,self_attention,ln_2,mlp.0,mlp.3}``, ``encoder.ln``,
 ``heads.head``).
@@ -27,6 +28,7 @@ import torch.nn as nn
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 from torch.utils.checkpoint import checkpoint
 
+from ..ops import recompute as _rc
 from ..ops.dropout import Dropout
 from ..ops.layernorm import LayerNorm, bias_grad_link, layer_norm
 from ..ops.linear import Linear
@@ -102,9 +104,15 @@ class Encoder(nn.Module):
         self.use_checkpoint = use_checkpoint
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.use_checkpoint == "selective":
+            # keep the GEMM outputs, rebuild LayerNorm / GELU outputs in backward (ops/recompute.py)
+            with _rc.selective(self.training):
+                return self._forward(x, False)
+        return self._forward(x, bool(self.use_checkpoint) and self.training and torch.is_grad_enabled())
+
+    def _forward(self, x: torch.Tensor, ckpt: bool) -> torch.Tensor:
         s = self.dropout(x + self.pos_embedding.to(x.dtype))
         d: Optional[torch.Tensor] = None
-        ckpt = self.use_checkpoint and self.training and torch.is_grad_enabled()
         for blk in self.layers.values():
             if ckpt:
                 if d is None:
@@ -148,8 +156,10 @@ class VisionTransformer(nn.Module):
         return self.encoder.use_checkpoint
 
     @use_checkpoint.setter
-    def use_checkpoint(self, v: bool) -> None:
-        self.encoder.use_checkpoint = bool(v)
+    def use_checkpoint(self, v) -> None:
+        """True: every block recomputed in backward; "selective": GEMM outputs kept, LayerNorm /
+        GELU outputs rebuilt (ops/recompute.py); False: nothing recomputed."""
+        self.encoder.use_checkpoint = v if v == "selective" else bool(v)
 
     def _process_input(self, x: torch.Tensor) -> torch.Tensor:
         """Patch embedding.  A p x p / stride-p convolution over non-overlapping patches IS a GEMM:

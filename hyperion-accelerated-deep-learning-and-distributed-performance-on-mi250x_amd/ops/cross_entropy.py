@@ -174,7 +174,7 @@ class _FusedLinearCE(torch.autograd.Function):
     @staticmethod
     def _materialized(ctx, x, x2, w, bias, t, ignore_index, scale, shape):
         """bf16 logits once, CE in place, then the two backward GEMMs on dz (module docstring)."""
-        from .gemm import mm_nn
+        from .gemm import lm_head_dx, lm_head_logits, mm_nn, mm_tn
 
         C = _native.native()
         _native.count("linear_ce_materialized")
@@ -182,9 +182,13 @@ class _FusedLinearCE(torch.autograd.Function):
         w = w.contiguous()
         t = t.contiguous()
         N, V = x2.shape[0], w.shape[0]
-        zb = torch.empty(N, -(-V // 8) * 8, dtype=x2.dtype, device=x2.device)
+        Vp = -(-V // 8) * 8
+        zb = torch.empty(N, Vp, dtype=x2.dtype, device=x2.device)
         z = zb[:, :V]  # 16-byte aligned rows
-        torch.mm(x2, w.t(), out=z)
+        if not lm_head_logits(x2, w, zb):
+            torch.mm(x2, w.t(), out=z)
+            if Vp > V:
+                zb[:, V:].zero_()  # the class-reducing dX GEMM reads the row padding
         b32 = None
         if bias is not None:
             b32 = bias.detach().float().contiguous()
@@ -195,13 +199,18 @@ class _FusedLinearCE(torch.autograd.Function):
         need_b = bias is not None and ctx.needs_input_grad[2]
         dx = None
         if ctx.needs_input_grad[0]:
-            Vm = V // 64 * 64
-            dx = mm_nn(zb[:, :Vm], w[:Vm]) if Vm > 0 else None
+            dx = lm_head_dx(zb, w)
             if dx is None:
-                dx = torch.mm(z, w)
-            elif Vm < V:
-                dx.addmm_(z[:, Vm:], w[Vm:])  # the odd class tail (rank V - Vm)
-        dw = torch.mm(z.t(), x2) if need_w else None
+                Vm = V // 64 * 64
+                dx = mm_nn(zb[:, :Vm], w[:Vm]) if Vm > 0 else None
+                if dx is None:
+                    dx = torch.mm(z, w)
+                elif Vm < V:
+                    dx.addmm_(z[:, Vm:], w[Vm:])  # the odd class tail (rank V - Vm)
+        dw = None
+        if need_w:
+            dwp = mm_tn(zb, x2)  # [Vp, E]: the padding classes' rows are dropped
+            dw = dwp[:V] if dwp is not None else torch.mm(z.t(), x2)
         db = C.column_sum(zb, torch.float32)[:V] if need_b else None
         loss = loss_rows.sum() * scale.reshape(())
         ctx.save_for_backward(dx.view(shape) if dx is not None else torch.empty(0),

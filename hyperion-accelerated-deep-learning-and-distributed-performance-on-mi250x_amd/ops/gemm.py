@@ -65,8 +65,10 @@ def _time(fn, reps: int = 5) -> float:
     return s.elapsed_time(e)
 
 
-# (BM, BN) of the tiled kernel's tiles (gemm_tiles.hip kTiles; 3 = the ragged-shape 128x128)
-TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128), 7: (192, 128)}
+# (BM, BN) of the tiled kernel's tiles (gemm_tiles.hip kTiles; 3 = the ragged-shape 128x128;
+# 8-11 = the ping-pong kernel gemm_pp_k)
+TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128), 7: (192, 128),
+         8: (256, 256), 9: (256, 128), 10: (128, 256), 11: (128, 128), 12: (256, 256)}
 
 
 def _candidates(K: int, M: int = 1 << 30, N: int = 1 << 30, a_tr: bool = False, b_tr: bool = False):
@@ -179,3 +181,52 @@ def mm_tn(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
     _native.count("gemm_tn")
     return C.gemm(dy, x, a_tr=True, b_tr=True, out_dtype=None if out is not None else odt, out=out, beta=beta,
                   tile=c[0], splits=c[1])
+
+
+# ---- LM head (V = 50257 classes: N % 4 != 0) ------------------------------------------------------
+def lm_head_logits(x: torch.Tensor, w: torch.Tensor, zb: torch.Tensor) -> bool:
+    """Logits ``x Wᵀ`` into ``zb[:, :V]`` (``zb`` [N, ceil8(V)], 16-byte aligned rows) on the native
+    GEMM: classes [0, floor8(V)) on the tiled kernel, the last V % 8 classes and the row padding as
+    one small launch whose weight rows past V read as zeros (the padding columns come out 0, so
+    the backward GEMMs that reduce over classes read finite zeros there).  False: the caller runs
+    the vendor GEMM (the autotuner found it faster, or the operands do not qualify)."""
+    V, Vp = w.shape[0], zb.shape[1]
+    Vm = V // 8 * 8
+    if not _ok(x, w) or x.shape[1] % 8 or Vm < 256 or Vp % 8 or Vp < V:
+        return False
+    C = _native.native()
+    key = ("lm_head", x.shape[0], V, x.shape[1])
+
+    def nat(tile=-1, splits=-1):
+        C.gemm(x, w[:Vm], out=zb[:, :Vm], tile=tile, splits=splits)
+        if Vp > Vm:
+            C.gemm(x, w[Vm:], out=zb[:, Vm:], n_out=Vp - Vm)
+        return zb
+
+    def ven():
+        return torch.mm(x, w.t(), out=zb[:, :V])
+
+    c = _pick(key, x.shape[1], nat, ven, x.shape[0], Vm)
+    if c is None:
+        return False
+    _native.count("gemm_lm_head")
+    nat(*c)
+    return True
+
+
+def lm_head_dx(zb: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
+    """``dz W`` reducing over the V classes of ``zb[:, :V]`` (its padding columns must be finite:
+    lm_head_logits writes zeros there) — one launch: the reduction's ragged end (V % 32) is staged
+    per lane with the weight rows past V read as zeros.  None = vendor."""
+    V = w.shape[0]
+    z = zb[:, :V]
+    if not _ok(zb, w) or w.shape[1] % 8:
+        return None
+    C = _native.native()
+    key = ("lm_head_dx", zb.shape[0], w.shape[1], V)
+    c = _pick(key, V, lambda t=-1, sp=-1: C.gemm(z, w, b_tr=True, tile=t, splits=sp),
+              lambda: torch.mm(z, w), zb.shape[0], w.shape[1], b_tr=True)
+    if c is None:
+        return None
+    _native.count("gemm_lm_head_dx")
+    return C.gemm(z, w, b_tr=True, tile=c[0], splits=c[1])

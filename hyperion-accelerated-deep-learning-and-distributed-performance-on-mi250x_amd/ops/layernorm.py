@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import recompute as _rc
 
 _SUPPORTED_D = lambda d: d % 8 == 0 and d <= 4096 and ((d + 511) // 512 <= 4 or (d + 511) // 512 == 8)  # noqa: E731
 
@@ -93,6 +94,8 @@ class _LNFn(torch.autograd.Function):
         ctx.link = link
         ctx.blink = blink
         ctx.save_for_backward(xin, weight, mean, rstd)
+        if _rc.active():  # selective recompute: the next GEMM saves a recipe, not y
+            _rc.register(y, _rc.ln_recipe(xin, weight, bias, eps, rms))
         if return_sum:
             return y, (s if residual is not None else x)
         return y

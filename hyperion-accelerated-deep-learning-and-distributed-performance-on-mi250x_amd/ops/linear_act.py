@@ -25,6 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native
+from . import recompute as _rc
 from .gemm import mm_nn, mm_nt
 import weakref
 
@@ -124,6 +125,9 @@ class _LinearGELU(torch.autograd.Function):
         ctx.save_for_backward(x2, wc, y)
         ctx.meta = (x.dtype, w.dtype, b.dtype, shape)
         ctx.drop = drop
+        if _rc.active() and y.is_cuda and y.dtype in (torch.bfloat16, torch.float16):
+            # selective recompute: the next GEMM (fc2) saves this recipe instead of h
+            _rc.register(h, lambda: _native.native().dropout(y, drop[0], drop[1], act=2))
         return h.view(*shape[:-1], w.shape[0])
 
     @staticmethod

@@ -32,6 +32,8 @@ elif which == "vitgraph":
     r = M.bench_vit_step(checkpointing=False, steps=20, warmup=5, graph=True)
 elif which == "vitckptgraph":
     r = M.bench_vit_step(checkpointing=True, steps=20, warmup=5, graph=True)
+elif which == "vitselgraph":
+    r = M.bench_vit_step(checkpointing="selective", steps=20, warmup=5, graph=True)
 elif which == "vitckpt":
     r = M.bench_vit_step(checkpointing=True, steps=5, warmup=3)
 elif which == "llama":
@@ -54,7 +56,7 @@ elif which == "lm":
     r = M.bench_lm_step(precision="bf16", steps=5, warmup=3)
 else:
     r = M.bench_lm_step(precision="bf16", graph=True, model="gpt2_small", batch=16, steps=10, warmup=3)
-if which in ("gpt2", "lmgraph", "lm", "vit", "vitgraph", "vitckptgraph"):
+if which in ("gpt2", "lmgraph", "lm", "vit", "vitgraph", "vitckptgraph", "vitselgraph"):
     from hyperion.ops import gemm as _gemm
 
     r["gemm_choices"] = {"x".join(map(str, k)): v for k, v in _gemm.choices().items()}

@@ -426,3 +426,102 @@ def test_vit_compute_copies_bias_grads_without_cast(monkeypatch):
         a, b = res[1][0][n], res[0][0][n]
         assert a.dtype == params[n].dtype, n
         assert float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)) < 2e-2, n
+
+
+@pytest.mark.parametrize("N,E", [(2032, 768), (4064, 256)])
+def test_lm_head_all_native_gemms(N, E):
+    """HYPERION_GEMM=native: the V = 50257 head runs every GEMM on the tiled kernel — logits as
+    classes [0, 50256) + one launch for the last class and the row padding (weight rows past V read
+    as zeros), dX reducing over 50257 classes (ragged last slice staged per lane), dW over the padded
+    class rows — and matches the fp32 reference; the padding columns of the logits are exact zeros."""
+    import hyperion.ops.cross_entropy as hce
+    from hyperion.ops import _native, gemm
+
+    torch.manual_seed(1)
+    V, pad = 50257, 50256
+    x = (torch.randn(N, E, device="cuda") * 0.5).bfloat16()
+    w = (torch.randn(V, E, device="cuda") * 0.05).bfloat16()
+    gemm.set_mode("native")
+    try:
+        zb = torch.full((N, 50264), float("nan"), device="cuda", dtype=torch.bfloat16)
+        assert gemm.lm_head_logits(x, w, zb)
+        ref = x.float() @ w.float().t()
+        torch.testing.assert_close(zb[:, :V].float(), ref, rtol=2e-2, atol=2e-2)
+        assert torch.equal(zb[:, V:], torch.zeros_like(zb[:, V:]))
+        dz = (torch.randn(N, V, device="cuda") * 0.01).bfloat16()
+        zb[:, :V] = dz
+        dx = gemm.lm_head_dx(zb, w)
+        torch.testing.assert_close(dx.float(), dz.float() @ w.float(), rtol=2e-2, atol=2e-2)
+        xr = x.detach().float().requires_grad_(True)
+        wr = w.detach().float().requires_grad_(True)
+        xg, wg = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        t = torch.randint(0, V, (N,), device="cuda")
+        t[::9] = pad
+        _native.reset_counters()
+        loss = hce.fused_linear_cross_entropy(xg, wg, None, t, ignore_index=pad)
+        loss.backward()
+        cnt = _native.counters()
+        assert cnt.get("gemm_lm_head") == 1 and cnt.get("gemm_lm_head_dx") == 1 and cnt.get("gemm_tn", 0) >= 1, cnt
+        refl = F.cross_entropy(F.linear(xr, wr), t, ignore_index=pad)
+        refl.backward()
+        torch.testing.assert_close(loss.float(), refl, rtol=2e-2, atol=2e-2)
+        for got, want in ((xg.grad, xr.grad), (wg.grad, wr.grad)):
+            assert (got.float() - want).norm() <= 3e-2 * want.norm() + 1e-6
+    finally:
+        gemm.set_mode("auto")
+
+
+def test_gemm_ragged_k_and_b_rows():
+    """K % 8 != 0 with one transposed operand (the other's row padding finite) and n_out > rows of
+    B (zero columns past them), on the fast tiles and the SAFE tile."""
+    from hyperion.ops import _native
+
+    C = _native.native()
+    torch.manual_seed(2)
+    M, N, K = 1000, 768, 1001
+    buf = torch.randn(M, 1008, device="cuda").bfloat16()
+    buf[:, K:] = 7.0  # finite padding: multiplied by the zero rows of B past K
+    a = buf[:, :K]
+    b = torch.randn(K, N, device="cuda").bfloat16()
+    ref = a.float() @ b.float()
+    for tile in (0, 2, 3, 8, 11):
+        for sp in (1, 3):
+            c = C.gemm(a, b, b_tr=True, out_dtype=torch.float32, tile=tile, splits=sp)
+            torch.testing.assert_close(c, ref, rtol=1e-4, atol=2e-2, msg=f"tile {tile} splits {sp}")
+    w = torch.randn(5, 256, device="cuda").bfloat16()
+    xa = torch.randn(300, 256, device="cuda").bfloat16()
+    out = torch.full((300, 8), float("nan"), device="cuda", dtype=torch.bfloat16)
+    C.gemm(xa, w, out=out, n_out=8)
+    torch.testing.assert_close(out[:, :5].float(), xa.float() @ w.float().t(), rtol=2e-2, atol=2e-2)
+    assert torch.equal(out[:, 5:], torch.zeros_like(out[:, 5:]))
+
+
+def test_vit_selective_recompute_matches_and_saves_memory():
+    """use_checkpoint="selective": LayerNorm and GELU outputs are rebuilt in backward from recipes
+    (ops/recompute.py) instead of being saved by the next GEMM — same gradients as the plain step
+    (the LN recompute is the same kernel; GELU comes from the fused GELU pass instead of the GEMM
+    epilogue: rounding-level differences), recipes really used, and lower peak memory."""
+    from hyperion.models.vit import VisionTransformer
+    from hyperion.ops import recompute
+
+    torch.manual_seed(0)
+    m = VisionTransformer(64, 16, 4, 4, 256, 1024, num_classes=10).cuda().bfloat16()
+    x0 = torch.randn(32, 3, 64, 64, device="cuda").bfloat16()
+    res = {}
+    for mode in (False, "selective", True):
+        m.use_checkpoint = mode
+        m.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        recompute.STATS.update(packed=0, recomputed=0)
+        m(x0).float().square().mean().backward()
+        torch.cuda.synchronize()
+        res[mode] = ({n: q.grad.float().clone() for n, q in m.named_parameters()},
+                     torch.cuda.max_memory_allocated() - base, dict(recompute.STATS))
+    g0, peak0, _ = res[False]
+    gs, peaks, st = res["selective"]
+    assert st["packed"] >= 4 * 3 and st["recomputed"] >= 4 * 3, st  # ln_1, ln_2, gelu per block
+    assert peaks < peak0, (peaks, peak0)
+    for n in g0:
+        assert float((gs[n] - g0[n]).norm() / (g0[n].norm() + 1e-12)) < 2e-2, n
