@@ -8,11 +8,10 @@ namespace gt {
 template <typename T, typename OutT>
 hipError_t launch_pp_typed(const GemmP& p, bool atr, bool btr, int tile, int nwg, hipStream_t st) {
   switch (tile) {
-    case 8: return launch_pp<T, OutT, 256, 256, 1, 4, 1, 4, true>(p, atr, btr, nwg, st);
-    case 9: return launch_pp<T, OutT, 256, 128, 2, 2, 1, 6, true>(p, atr, btr, nwg, st);
-    case 10: return launch_pp<T, OutT, 128, 256, 1, 4, 1, 6, true>(p, atr, btr, nwg, st);
-    case 11: return launch_pp<T, OutT, 128, 128, 2, 2, 2, 8, true>(p, atr, btr, nwg, st);
-    case 12: return launch_pp<T, OutT, 256, 256, 1, 4, 1, 4, false>(p, atr, btr, nwg, st);
+    case 8: return launch_pp<T, OutT, 256, 256, 1, 4, 1, 4>(p, atr, btr, nwg, st);
+    case 9: return launch_pp<T, OutT, 256, 128, 2, 2, 2, 6>(p, atr, btr, nwg, st);
+    case 10: return launch_pp<T, OutT, 128, 256, 1, 4, 2, 6>(p, atr, btr, nwg, st);
+    case 11: return launch_pp<T, OutT, 128, 128, 2, 2, 2, 6>(p, atr, btr, nwg, st);
     default: return hipErrorInvalidValue;
   }
 }

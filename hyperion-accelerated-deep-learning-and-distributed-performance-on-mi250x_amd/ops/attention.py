@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native
+from . import recompute as _rc
 
 def _rng(t: torch.Tensor, p: float):
     return _native.rng_state(t.device) if p > 0 else None
@@ -49,6 +50,14 @@ def attention_reference(q, k, v, causal=False, dropout_p=0.0, key_padding_mask=N
     return o.transpose(1, 2)
 
 
+def _recipe_o(o, q, k, v, causal, scale, p, seed, kpm) -> None:
+    """Selective recompute (ops/recompute.py): the attention output is rebuilt by re-running the
+    forward kernel on the saved q / k / v (same dropout seed: bit-identical) for the backward of
+    this op and of the output projection, instead of being kept (d_model per token per layer)."""
+    if _rc.active():
+        _rc.register(o, lambda: _native.native().attn_fwd(q, k, v, causal, scale, p, seed, kpm, True)[0])
+
+
 class _AttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, dropout_p, kpm, scale):
@@ -56,6 +65,7 @@ class _AttnFn(torch.autograd.Function):
         o, lse = _native.native().attn_fwd(q, k, v, causal, scale, dropout_p, seed, kpm, True)
         ctx.save_for_backward(q, k, v, o, lse, kpm)
         ctx.cfg = (causal, dropout_p, seed, scale)
+        _recipe_o(o, q, k, v, causal, scale, dropout_p, seed, kpm)
         return o
 
     @staticmethod
@@ -75,6 +85,7 @@ class _AttnPackedFn(torch.autograd.Function):
         o, lse = _native.native().attn_fwd(q, k, v, causal, scale, dropout_p, seed, kpm, True)
         ctx.save_for_backward(qkv, o, lse, kpm)
         ctx.cfg = (causal, dropout_p, seed, scale)
+        _recipe_o(o, q, k, v, causal, scale, dropout_p, seed, kpm)
         return o
 
     @staticmethod

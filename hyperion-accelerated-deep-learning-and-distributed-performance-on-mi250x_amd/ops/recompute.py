@@ -23,8 +23,10 @@ from typing import Callable, Dict, Optional, Tuple
 import torch
 
 _ACTIVE = 0
-_REG: Dict[Tuple[int, int, int, torch.dtype], Tuple["weakref.ref", Callable[[], torch.Tensor]]] = {}
-_PACKED: Dict[Tuple[int, int, int, torch.dtype], "_Recipe"] = {}
+# storage key -> (weakref to the registered tensor, its recipe).  A freed activation's memory is
+# reused by the next block's one (same key): a later register() replaces the entry, and a pack
+# only takes an entry whose tensor is still alive — so the key can never name stale data.
+_REG: Dict[Tuple[int, int, int, torch.dtype], Tuple["weakref.ref", "_Recipe"]] = {}
 STATS = {"packed": 0, "recomputed": 0}
 
 
@@ -41,7 +43,7 @@ def _key(t: torch.Tensor):
 def register(t: torch.Tensor, fn: Callable[[], torch.Tensor]) -> None:
     """``fn()`` rebuilds ``t`` (same values up to rounding, same dtype and numel) in backward."""
     if active() and t.is_contiguous():
-        _REG[_key(t)] = (weakref.ref(t), fn)
+        _REG[_key(t)] = (weakref.ref(t), _Recipe(fn, t.shape))
 
 
 class _Recipe:
@@ -60,15 +62,11 @@ class _Recipe:
 def _pack(t: torch.Tensor):
     if not t.is_contiguous():
         return t
-    k = _key(t)
-    e = _REG.get(k)
+    e = _REG.get(_key(t))
     if e is None or e[0]() is None:  # no recipe, or its tensor died (storage may be reused)
         return t
-    r = _PACKED.get(k)
-    if r is None:
-        r = _PACKED[k] = _Recipe(e[1], t.shape)
     STATS["packed"] += 1
-    return (r, t.shape)
+    return (e[1], t.shape)  # every save of one live tensor shares its recipe (rebuilt once)
 
 
 def _unpack(p):
@@ -92,7 +90,6 @@ def selective(enabled: bool = True):
         _ACTIVE -= 1
         if _ACTIVE == 0:
             _REG.clear()
-            _PACKED.clear()
 
 
 def ln_recipe(xin: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor], eps: float,

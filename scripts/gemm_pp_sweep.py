@@ -1,7 +1,7 @@
 """Native tiles (classic gemm_tile_k and ping-pong gemm_pp_k) vs the vendor GEMM per shape and
 layout, warm device time (median of 10 event-timed calls on randn operands):
 
-    python scripts/r06/gemm_pp_sweep.py [--big] > gpurun_out/.../sweep.jsonl
+    python scripts/gemm_pp_sweep.py [--big] > gpurun_out/.../sweep.jsonl
 """
 import json
 import sys
@@ -34,7 +34,7 @@ SHAPES = [
     ("nt", 2048, 2304, 768), ("nt", 2048, 3072, 768), ("nt", 2048, 768, 3072), ("nn", 2048, 768, 3072),
     ("tn", 3072, 768, 2048), ("nt", 2048, 50256, 768),
 ]
-TILES = [0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12]
+TILES = [0, 1, 2, 5, 6, 7, 8, 9, 10, 11]
 if "--big" in sys.argv:
     SHAPES = [("nt", 8192, 8192, 8192), ("nt", 4096, 4096, 4096)] + SHAPES
 

@@ -13,6 +13,11 @@
 #   bash scripts/gpu_suite.sh baseline                   reference-methodology model benchmarks + fused-vs-eager
 #   bash scripts/gpu_suite.sh pmc                        PMC counter passes over ResNet-50 steps -> per-kernel table
 #   bash scripts/gpu_suite.sh rccl                       RCCL reduce-scatter / all-reduce tail check
+#   bash scripts/gpu_suite.sh gemm                       native GEMM tiles (classic + ping-pong) vs vendor sweep
+#   bash scripts/gpu_suite.sh gemm_pmc                   PMC passes over single GEMM shapes (native vs vendor)
+#   bash scripts/gpu_suite.sh llama_pmc                  PMC passes over the Llama-2-7B LoRA step (weight streaming)
+#   bash scripts/gpu_suite.sh steps                      graphed model steps (WL="vitgraph vitselgraph ..."), one JSON each
+#   bash scripts/gpu_suite.sh final                      bench x2 + every README step row (one box, one call)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -99,6 +104,41 @@ pmc)
 rccl)
   timeout -k 10 200 python -u scripts/rccl_avg_check.py > "$out/rccl.log" 2>&1 || exit 1
   grep -E "^bad|^rs" "$out/rccl.log"
+  ;;
+gemm)
+  timeout -k 10 600 python -u scripts/gemm_pp_sweep.py --big > "$out/sweep.jsonl" 2> "$out/sweep.err" || { tail -5 "$out/sweep.err"; exit 1; }
+  python3 scripts/gemm_sweep_summary.py "$out/sweep.jsonl"
+  ;;
+gemm_pmc)
+  bash scripts/gemm_pmc.sh "$out"
+  ;;
+llama_pmc)
+  bash scripts/llama_pmc.sh "$out"
+  ;;
+steps)
+  for w in ${WL:-vitgraph vitselgraph vitckptgraph gpt2 lmgraph llamagraph}; do
+    timeout -k 10 400 python -u scripts/run_model_step.py $w > "$out/$w.json" 2> "$out/$w.err" || { echo "[$w] FAILED"; tail -5 "$out/$w.err"; exit 1; }
+    python3 -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(r['ms_per_step'],3), 'ms, peak', round(r.get('peak_mem_mb',0)), 'MB')" "$out/$w.json" $w
+  done
+  ;;
+final)
+  # the README's measured rows from ONE box: bench.py x2 (driver contract), DDP at world 1, graphed
+  # model steps, FSDP steps (ring / persistent, with the native collectives at world 1)
+  export HSA_ENABLE_IPC_MODE_LEGACY=0
+  for i in 1 2; do
+    timeout -k 10 300 python -u bench.py > "$out/bench$i.json" 2> "$out/bench$i.err" || { tail -5 "$out/bench$i.err"; exit 1; }
+    echo "bench$i $(json_ms "$out/bench$i.json")"
+  done
+  timeout -k 10 300 python -u bench.py --ddp-world1 1 > "$out/bench_ddp1.json" 2> "$out/bench_ddp1.err" || { tail -5 "$out/bench_ddp1.err"; exit 1; }
+  echo "bench_ddp1 $(json_ms "$out/bench_ddp1.json")"
+  for w in ${WL:-vitgraph vitselgraph vitckptgraph gpt2 lmgraph llamagraph20}; do
+    timeout -k 10 400 python -u scripts/run_model_step.py $w > "$out/$w.json" 2> "$out/$w.err" || { echo "[$w] FAILED"; tail -5 "$out/$w.err"; exit 1; }
+    echo "$w $(json_ms "$out/$w.json")"
+  done
+  for cfg in "gpt2_small graph ring3 coll" "gpt2_small graph coll" "gpt2_small graph ring3" "lm256 graph coll"; do
+    timeout -k 10 400 python -u scripts/run_model_step.py fsdp $cfg >> "$out/fsdp_steps.jsonl" 2>> "$out/fsdp_steps.err" || { tail -5 "$out/fsdp_steps.err"; exit 1; }
+    echo "fsdp $cfg $(tail -1 "$out/fsdp_steps.jsonl" | grep -o '"ms_per_step": [0-9.]*')"
+  done
   ;;
 *)
   echo "unknown stage $stage"; exit 2

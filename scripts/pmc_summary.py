@@ -38,7 +38,7 @@ def load(path):
     with open(path) as f:
         for r in csv.DictReader(f):
             k = short(r["Kernel_Name"])
-            if not (k.startswith("hyp::") or "CUDAFunctor_add" in k or "vectorized_elementwise" in k):
+            if not (k.startswith("hyp::") or "CUDAFunctor_add" in k or "vectorized_elementwise" in k or "Cijk" in k):
                 continue
             d = int(r["Dispatch_Id"])
             disp[k].add(d)
@@ -72,8 +72,8 @@ def main():
             m.update({kk: v for kk, v in c.items() if not kk.startswith("_")})
             m["_us_list"] = us
             m["_n"] = c["_n"]
-    lines = ["| target | kernel | dispatches | us/dispatch | MfmaUtil % | MFMA TF/s | HBM rd GB/s | HBM wr GB/s | L2 hit % | LDS confl/inst | waves/CU | wait % |",
-             "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    lines = ["| target | kernel | dispatches | us/dispatch | MfmaUtil % | MFMA TF/s | HBM rd GB/s | HBM wr GB/s | L2 hit % | LDS confl/inst | waves/CU | wait % | parked % |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for (t, k), c in sorted(merged.items()):
         us = min(c["_us_list"])  # the SQ pass perturbs timing least
         def g(name):
@@ -86,9 +86,10 @@ def main():
         lds = g("SQ_LDS_BANK_CONFLICT") / g("SQ_INSTS_LDS") if g("SQ_INSTS_LDS") else None
         occ = g("SQ_WAVE_CYCLES") / (g("GRBM_GUI_ACTIVE") / 8 * 256) if g("SQ_WAVE_CYCLES") and g("GRBM_GUI_ACTIVE") else None
         wait = 100 * g("SQ_WAIT_INST_ANY") / g("SQ_WAVE_CYCLES") if g("SQ_WAIT_INST_ANY") and g("SQ_WAVE_CYCLES") else None
+        parked = 100 * g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES") if g("SQ_WAIT_ANY") and g("SQ_WAVE_CYCLES") else None
         f = lambda v, p=1: "-" if v is None else f"{v:.{p}f}"  # noqa: E731
         lines.append(f"| {t} | `{k}` | {c['_n']} | {us:.1f} | {f(util)} | {f(tf, 0)} | {f(rd, 0)} | {f(wr, 0)} | {f(hit)} | "
-                     f"{f(lds, 2)} | {f(occ)} | {f(wait)} |")
+                     f"{f(lds, 2)} | {f(occ)} | {f(wait)} | {f(parked)} |")
     txt = "\n".join(lines)
     print(txt)
     if a.out:

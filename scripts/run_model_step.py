@@ -38,6 +38,8 @@ elif which == "vitckpt":
     r = M.bench_vit_step(checkpointing=True, steps=5, warmup=3)
 elif which == "llama":
     r = M.bench_llama_lora_step(steps=3, warmup=2, graph=False)
+elif which == "llama1":  # one warm-up + one timed eager step (PMC passes: small counter files)
+    r = M.bench_llama_lora_step(steps=1, warmup=1, graph=False)
 elif which == "llamagraph":
     r = M.bench_llama_lora_step(steps=5, warmup=3, graph=True)
 elif which == "llamagraph20":

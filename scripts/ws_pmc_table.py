@@ -1,5 +1,5 @@
 """Per-kernel-family table from the llama_pmc.sh passes: time share, bytes/s, TLB and L2 behaviour.
-    python scripts/r06/ws_pmc_table.py gpurun_out/r06/llama_pmc"""
+    python scripts/ws_pmc_table.py gpurun_out/r06/llama_pmc"""
 import csv
 import re
 import sys
