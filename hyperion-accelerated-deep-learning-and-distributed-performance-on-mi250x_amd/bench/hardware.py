@@ -53,7 +53,7 @@ def _events_ms(fn, repeat: int, warmup: int) -> List[float]:
 
 
 def matmul_tflops(n: int, precision: str, kernel: str = "hyperion", method: str = "proper", repeat: int = 20,
-                  warmup: int = 5, tiles=(0, 1, 2, 3, 8, 9, 10, 11)) -> Dict:
+                  warmup: int = 5, tiles=(0, 1, 2, 3, 8, 9, 10, 11, 12)) -> Dict:
     """TFLOPS of one n×n×n product (2n³ FLOP).  Hyperion computes C = A·Bᵀ with B stored [N, K] (the
     transpose is layout, not work: same 2n³ FLOPs)."""
     from ..ops import _native

@@ -8,10 +8,13 @@ namespace gt {
 template <typename T, typename OutT>
 hipError_t launch_pp_typed(const GemmP& p, bool atr, bool btr, int tile, int nwg, hipStream_t st) {
   switch (tile) {
-    case 8: return launch_pp<T, OutT, 256, 256, 1, 4, 1, 4>(p, atr, btr, nwg, st);
-    case 9: return launch_pp<T, OutT, 256, 128, 2, 2, 2, 6>(p, atr, btr, nwg, st);
-    case 10: return launch_pp<T, OutT, 128, 256, 1, 4, 2, 6>(p, atr, btr, nwg, st);
-    case 11: return launch_pp<T, OutT, 128, 128, 2, 2, 2, 6>(p, atr, btr, nwg, st);
+    // R (last template argument): LDS-DMA pieces per slice issued from the MFMA interval (measured:
+    // profiles/r06/gemm_pp_refill_split*.jsonl — 256²: R 3 of 4; 256x128 / 128x256: R 2 of 3)
+    case 8: return launch_pp<T, OutT, 256, 256, 1, 4, 1, 4, 3>(p, atr, btr, nwg, st);
+    case 9: return launch_pp<T, OutT, 256, 128, 2, 2, 2, 6, 2>(p, atr, btr, nwg, st);
+    case 10: return launch_pp<T, OutT, 128, 256, 1, 4, 2, 6, 2>(p, atr, btr, nwg, st);
+    case 11: return launch_pp<T, OutT, 128, 128, 2, 2, 2, 6, 1>(p, atr, btr, nwg, st);
+    case 12: return launch_pp<T, OutT, 256, 256, 1, 4, 1, 5, 3>(p, atr, btr, nwg, st);  // all 160 KiB: 5-deep ring
     default: return hipErrorInvalidValue;
   }
 }

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
   constexpr int kNB = NBR;
   constexpr int NW = WM * WN;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  static_assert(FN * 16 == 64, "wave tiles are 64 columns wide (epilogue patch)");
+  static_assert(FN % 4 == 0, "wave tiles are 64-column multiples (epilogue patch)");
   constexpr int kA = BM * kBK, kB = BN * kBK, kStage = kA + kB;
   __shared__ __attribute__((aligned(16))) uint16_t smem[kNB * kStage];
 
@@ -459,15 +459,17 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tile_k(const GemmP p) {
   constexpr int kRS = 68;
   float* patch = reinterpret_cast<float*>(smem) + wave * (32 * kRS);
   const int r16 = lane & 15, g4 = lane >> 4;
-  const int wrow0 = m0 + am, wcol0 = n0 + bn;
+  const int wrow0 = m0 + am;
 #pragma unroll
-  for (int h = 0; h < FM / 2; ++h) {
+  for (int hc = 0; hc < FM / 2 * (FN / 4); ++hc) {  // 32-row x 64-column pieces of the wave tile
+    const int h = hc / (FN / 4), c4 = hc % (FN / 4);
+    const int wcol0 = n0 + bn + c4 * 64;
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) patch[(ii * 16 + g4 * 4 + e) * kRS + j * 16 + r16] = acc[2 * h + ii][j][e];
+        for (int e = 0; e < 4; ++e) patch[(ii * 16 + g4 * 4 + e) * kRS + j * 16 + r16] = acc[2 * h + ii][c4 * 4 + j][e];
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's patch written (wave-private region)
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -563,15 +565,30 @@ __global__ __launch_bounds__(256) void gemm_splitk_epi_k(const float* __restrict
 // pieces of a slice land before the barrier that precedes the slice's first read.
 // Each group's wave tile: (BM/2)/WGM rows x BN/WGN (= 64) columns, so the epilogue is
 // gemm_tile_k's (per-wave fp32 patches of 32 x 64).
-// (Refilling the ring from the MFMA interval instead — the pieces spread between MFMA rows — was
-// measured slower: 8192^3 1226 vs 1002 us on one box, profiles/r06/gemm_sweep_pp.jsonl.)
-template <typename T, typename OutT, int BM, int BN, int WGM, int WGN, int KS, bool ATR, bool BTR, int NBR>
+// R (0 .. pieces per slice): the last R LDS-DMA pieces of each refilled slice are issued from the
+// MFMA interval instead, between MFMA rows — it balances the two intervals: an LDS-DMA issue costs
+// ~100-185 cycles in an interval of ds_reads, ~60 among bare MFMAs (MI355X_MICROARCH constants).
+// Moving ALL of them measured slower (8192^3 1226 vs 1002 us on one box); of the 256² tile's 4, 2
+// measured 985 vs 1180 us (R = 0) and 1037 (R = 1) on another, 3 measured 966 vs 1108 (R = 2) on a
+// third (profiles/r06/gemm_pp_refill_split*.jsonl).
+// With R > 0, group 1's MFMA-interval pieces of step j+1 are issued two steps ahead (PD >= 2 KS).
+template <int N>
+__device__ __forceinline__ void wait_vm_at_most(int n) {  // s_waitcnt vmcnt(min(n, N)), n >= 0
+  if constexpr (N == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N) wait_vmcnt<N>();
+    else wait_vm_at_most<N - 1>(n);
+  }
+}
+
+template <typename T, typename OutT, int BM, int BN, int WGM, int WGN, int KS, bool ATR, bool BTR, int NBR, int R>
 __global__ __launch_bounds__(512) void gemm_pp_k(const GemmP p) {
   constexpr int NW = 8, kNB = NBR, PD = kNB - KS;
   static_assert(WGM * WGN == 4, "four waves per group");
   constexpr int FM = BM / 2 / WGM / 16, FN = BN / WGN / 16;
   static_assert(FN == 4 && FM % 2 == 0 && FM >= 2, "wave tiles are FM*16 x 64");
-  static_assert(PD >= KS, "a step's slices are issued at least one step ahead");
+  static_assert(PD >= (R > 0 ? 2 * KS : KS), "a step's slices are issued ahead of the wait for them");
   constexpr int kA = BM * kBK, kB = BN * kBK, kStage = kA + kB;
   __shared__ __attribute__((aligned(16))) uint16_t smem[kNB * kStage];
 
@@ -625,6 +642,15 @@ __global__ __launch_bounds__(512) void gemm_pp_k(const GemmP p) {
     for (int q = 0; q < kLA + kLB; ++q) stage_piece(t, q);
   };
   auto wait_ahead = [&](int ahead) { wait_ahead_n<kL, PD - KS>(ahead); };
+  static_assert(R >= 0 && R <= kL, "pieces moved into the MFMA interval");
+  // pieces this wave issued after step j+1's last slice, at the end of group 1's LOAD(j): slices up to
+  // jKS+PD-1 complete, the KS slices refilled by LOAD(j) with kL - R pieces each (clamped to nk)
+  auto g1_outstanding = [&](int j) {
+    const int last = j * KS + 2 * KS - 1;
+    const int full = max(0, min(nk - 1, j * KS + PD - 1) - last);
+    const int part = max(0, min(nk, j * KS + PD + KS) - max(j * KS + PD, last + 1));
+    return full * kL + part * (kL - R);
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -666,26 +692,47 @@ __global__ __launch_bounds__(512) void gemm_pp_k(const GemmP p) {
   if (grp == 1) pp_barrier();  // group 1 runs one interval behind
   const int nsteps = nk / KS;
   for (int j = 0; j < nsteps; ++j) {
-    // ---- LOAD interval: step j's fragments, refill PD slices ahead
+    // ---- LOAD interval: step j's fragments, refill PD slices ahead (all but R pieces per slice)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) read_slice(j * KS + ks, ks);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int t = j * KS + PD + ks;
-      if (t < nk) stage(t);
+      if (t < nk) {
+#pragma unroll
+        for (int q = 0; q < kL - R; ++q) stage_piece(t, q);
+      }
     }
     lds_wait_fenced();
     const int ahead = min(nk - 1, j * KS + PD + KS - 1) - (j * KS + 2 * KS - 1);
-    if (grp == 1 && j + 1 < nsteps) wait_ahead(ahead);
+    if (grp == 1 && j + 1 < nsteps) {
+      if constexpr (R == 0) wait_ahead(ahead);
+      else wait_vm_at_most<(PD - 1) * kL>(g1_outstanding(j));
+    }
     pp_barrier();
-    // ---- MFMA interval
+    // ---- MFMA interval (R > 0: the refill's remaining pieces between MFMA rows)
     __builtin_amdgcn_s_setprio(1);
+    constexpr int RP = KS * R, RG = (KS * FM + RP) / (RP + 1);  // MFMA rows before each piece
+    constexpr int RIN = RP < (KS * FM - 1) / RG ? RP : (KS * FM - 1) / RG;  // pieces issued inside the row loop
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+    for (int r = 0; r < KS * FM; ++r) {
+      if constexpr (R > 0) {
+        if (r > 0 && r % RG == 0 && r / RG <= RP) {
+          const int q = r / RG - 1, t = j * KS + PD + q / R;
+          if (t < nk) stage_piece(t, kL - R + q % R);
+        }
+      }
+      const int ks = r / FM, i = r % FM;
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int jj = 0; jj < FN; ++jj) acc[i][jj] = mma16<T>(af[ks][i], bfr[ks][jj], acc[i][jj]);
+    }
+    if constexpr (R > 0) {
 #pragma unroll
-        for (int jj = 0; jj < FN; ++jj) acc[i][jj] = mma16<T>(af[ks][i], bfr[ks][jj], acc[i][jj]);
+      for (int q = RIN; q < RP; ++q) {  // pieces the row loop did not reach
+        const int t = j * KS + PD + q / R;
+        if (t < nk) stage_piece(t, kL - R + q % R);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     if (grp == 0 && j + 1 < nsteps) wait_ahead(ahead);
     pp_barrier();
@@ -729,26 +776,27 @@ struct TileCfg {
   double eff;  // relative per-CU throughput of a full tile (calibrated on MI355X)
   int ks = 0;  // > 0: the ping-pong kernel (gemm_pp_k) with KS 32-deep slices per step
 };
-constexpr int kNumTiles = 12;
+constexpr int kNumTiles = 13;
 constexpr TileCfg kTiles[kNumTiles] = {{256, 256, 8, 1, 1.0},       {256, 128, 8, 1, 0.80},     {128, 128, 4, 2, 0.62},
                                        {128, 128, 4, 2, 0.55},      {64, 64, 2, 4, 0.30},       {128, 64, 2, 3, 0.42},
                                        {64, 128, 4, 3, 0.42},       {192, 128, 4, 2, 0.70},
                                        // ping-pong tiles (gemm_pp_k): 256² KS 1 / NB 4; the others KS 2 / NB 6
                                        {256, 256, 8, 1, 1.25, 1},   {256, 128, 8, 1, 1.0, 2},
-                                       {128, 256, 8, 1, 1.0, 2},    {128, 128, 8, 1, 0.70, 2}};
+                                       {128, 256, 8, 1, 1.0, 2},    {128, 128, 8, 1, 0.70, 2},
+                                       {256, 256, 8, 1, 1.25, 1}};  // 256² with a 5-deep ring
 
 inline bool tile_layout_ok(int t, bool atr, bool btr) {
   const TileCfg& c = kTiles[t];
   return (!atr || c.bm % 128 == 0) && (!btr || c.bn % 128 == 0);
 }
 
-template <typename T, typename OutT, int BM, int BN, int WGM, int WGN, int KS, int NBR>
+template <typename T, typename OutT, int BM, int BN, int WGM, int WGN, int KS, int NBR, int R = 0>
 hipError_t launch_pp(const GemmP& p, bool atr, bool btr, int nwg, hipStream_t st) {
   const dim3 grid(nwg), block(512);
-  if (!atr && !btr) hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, false, false, NBR>), grid, block, 0, st, p);
-  else if (!atr && btr) hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, false, true, NBR>), grid, block, 0, st, p);
-  else if (atr && btr) hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, true, true, NBR>), grid, block, 0, st, p);
-  else hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, true, false, NBR>), grid, block, 0, st, p);
+  if (!atr && !btr) hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, false, false, NBR, R>), grid, block, 0, st, p);
+  else if (!atr && btr) hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, false, true, NBR, R>), grid, block, 0, st, p);
+  else if (atr && btr) hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, true, true, NBR, R>), grid, block, 0, st, p);
+  else hipLaunchKernelGGL((gemm_pp_k<T, OutT, BM, BN, WGM, WGN, KS, true, false, NBR, R>), grid, block, 0, st, p);
   return hipGetLastError();
 }
 

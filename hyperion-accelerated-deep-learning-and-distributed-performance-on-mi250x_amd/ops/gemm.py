@@ -68,7 +68,7 @@ def _time(fn, reps: int = 5) -> float:
 # (BM, BN) of the tiled kernel's tiles (gemm_tiles.hip kTiles; 3 = the ragged-shape 128x128;
 # 8-11 = the ping-pong kernel gemm_pp_k)
 TILES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128), 7: (192, 128),
-         8: (256, 256), 9: (256, 128), 10: (128, 256), 11: (128, 128)}
+         8: (256, 256), 9: (256, 128), 10: (128, 256), 11: (128, 128), 12: (256, 256)}
 
 
 def _candidates(K: int, M: int = 1 << 30, N: int = 1 << 30, a_tr: bool = False, b_tr: bool = False):

@@ -4,6 +4,7 @@ layout, warm device time (median of 10 event-timed calls on randn operands):
     python scripts/gemm_pp_sweep.py [--big] > gpurun_out/.../sweep.jsonl
 """
 import json
+import os
 import sys
 
 import torch
@@ -34,7 +35,9 @@ SHAPES = [
     ("nt", 2048, 2304, 768), ("nt", 2048, 3072, 768), ("nt", 2048, 768, 3072), ("nn", 2048, 768, 3072),
     ("tn", 3072, 768, 2048), ("nt", 2048, 50256, 768),
 ]
-TILES = [0, 1, 2, 5, 6, 7, 8, 9, 10, 11]
+TILES = [int(t) for t in os.environ.get("GEMM_TILES", "0,1,2,5,6,7,8,9,10,11,12").split(",")]
+if os.environ.get("GEMM_SHAPES"):  # "nt:M:N:K,nn:M:N:K,..."
+    SHAPES = [(f.split(":")[0],) + tuple(int(v) for v in f.split(":")[1:]) for f in os.environ["GEMM_SHAPES"].split(",")]
 if "--big" in sys.argv:
     SHAPES = [("nt", 8192, 8192, 8192), ("nt", 4096, 4096, 4096)] + SHAPES
 

@@ -121,6 +121,19 @@ steps)
     python3 -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(r['ms_per_step'],3), 'ms, peak', round(r.get('peak_mem_mb',0)), 'MB')" "$out/$w.json" $w
   done
   ;;
+steptrace)
+  # kernel trace of one graphed model step per workload (WL): per-step kernel table + vendor-GEMM count
+  export HSA_ENABLE_IPC_MODE_LEGACY=0
+  for w in ${WL:-vitgraph gpt2}; do
+    rm -rf "$out/raw_$w"
+    timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$PWD/$out/raw_$w" -o run -- \
+      python3 scripts/run_model_step.py $w > "$out/$w.json" 2> "$out/$w.err" || { echo "[$w] trace failed"; tail -5 "$out/$w.err"; exit 1; }
+    f=$(find "$out/raw_$w" -name "*kernel_trace.csv" | head -1)
+    python3 scripts/step_trace.py "$f" --step -2 --out "$out/step_$w.txt" > /dev/null || exit 1
+    rm -rf "$out/raw_$w"
+    echo "$w: $(grep -E '^step' "$out/step_$w.txt") vendor GEMM kernels: $(grep -c 'Cijk' "$out/step_$w.txt")"
+  done
+  ;;
 final)
   # the README's measured rows from ONE box: bench.py x2 (driver contract), DDP at world 1, graphed
   # model steps, FSDP steps (ring / persistent, with the native collectives at world 1)

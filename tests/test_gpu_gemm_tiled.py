@@ -28,11 +28,11 @@ def _operands(M, N, K, a_tr, b_tr, dtype):
 
 TILE_SHAPES = {0: (256, 256), 1: (256, 128), 2: (128, 128), 4: (64, 64), 5: (128, 64), 6: (64, 128), 7: (192, 128),
                # ping-pong tiles (gemm_pp_k: two 4-wave groups alternating MFMA / load intervals)
-               8: (256, 256), 9: (256, 128), 10: (128, 256), 11: (128, 128)}
+               8: (256, 256), 9: (256, 128), 10: (128, 256), 11: (128, 128), 12: (256, 256)}
 
 
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
-@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("tile", [0, 1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("shape", [(256, 256, 64), (392, 776, 200), (1000, 264, 1032), (2032, 768, 768)])
 def test_gemm_layouts_tiles_fp32_out(layout, tile, shape):
     M, N, K = shape
@@ -64,7 +64,7 @@ def test_gemm_fp16_and_identity():
     n = 256
     a = torch.eye(n, device="cuda", dtype=torch.float16)
     b = (torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) % 97).to(torch.float16)
-    for tile in (0, 1, 2, 4, 5, 6, 7, 8, 9, 10, 11):
+    for tile in (0, 1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12):
         c = _C().gemm(a, b, out_dtype=torch.float32, tile=tile, splits=1)
         torch.testing.assert_close(c, b.float().t())
 
@@ -193,7 +193,7 @@ def test_small_tiles_fused_epilogue_ragged(tile, splits):
     torch.testing.assert_close(y.float(), torch.nn.functional.gelu(aux.float()), rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("tile", [8, 9, 10, 11])
+@pytest.mark.parametrize("tile", [8, 9, 10, 11, 12])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
 @pytest.mark.parametrize("shape,splits", [((1536, 1280, 2048), 1), ((1000, 776, 3072), 3), ((6304, 768, 768), 2)])
 def test_pingpong_tiles_ragged_split_k(tile, layout, shape, splits):
@@ -211,7 +211,7 @@ def test_pingpong_tiles_ragged_split_k(tile, layout, shape, splits):
     torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
 
 
-@pytest.mark.parametrize("tile", [8, 9, 10, 11])
+@pytest.mark.parametrize("tile", [8, 9, 10, 11, 12])
 def test_pingpong_fused_epilogue_bf16(tile):
     M, N, K = 2048, 1024, 768
     torch.manual_seed(3)
