@@ -25,22 +25,87 @@ at::Tensor gemm_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::S
   return c;
 }
 
-// fp32 a [M, K], b [N, K] -> a @ b.T on the fp32-input MFMA (gemm_f32.hip)
-at::Tensor gemm_f32_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::ScalarType> out_dtype, double alpha) {
+// ---- fp32 (gemm_f32.hip) ---------------------------------------------------------------------
+// C = epi(alpha · A·Bᵀ) in fp32, A [M, K] (a_tr: [K, M]), B [N, K] (b_tr: [K, N]); + beta·out, + bias,
+// ReLU.  Any M / N; row-form operands need K % 4, tr-form operands M / N % 4; strides % 4.
+at::Tensor gemm_f32(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_tr, const c10::optional<at::Tensor>& bias,
+                    bool relu, double alpha, double beta, const c10::optional<at::Tensor>& out, int64_t splits,
+                    int64_t shape) {
   HYP_CHECK_CUDA_TENSOR(a);
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_f32_nt: expected a [M,K], b [N,K]");
-  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1, "gemm_f32_nt: K must be contiguous");
-  TORCH_CHECK(a.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "gemm_f32_nt: fp32 inputs");
-  const int M = (int)a.size(0), N = (int)b.size(0), K = (int)a.size(1);
-  TORCH_CHECK(hyp::gemm_f32_nt_supported(M, N, K, (int)a.stride(0), (int)b.stride(0)),
-              "gemm_f32_nt: shape not supported (M, N multiples of 128; K multiple of 32; 16-byte rows)");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
-              "gemm_f32_nt: 16-byte aligned bases required");
+  for (const at::Tensor* t : {&a, &b}) {
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "gemm_f32: operands must be fp32 2D, unit stride in dim 1, row stride % 4, 16-byte aligned");
+  }
+  const int M = (int)(a_tr ? a.size(1) : a.size(0)), K = (int)(a_tr ? a.size(0) : a.size(1));
+  const int N = (int)(b_tr ? b.size(1) : b.size(0));
+  TORCH_CHECK((b_tr ? b.size(0) : b.size(1)) == K, "gemm_f32: reduction extents differ");
+  at::Tensor c;
+  if (out.has_value()) {
+    c = *out;
+    TORCH_CHECK(c.scalar_type() == at::kFloat && c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1,
+                "gemm_f32: out must be fp32 [M, N] with unit column stride");
+  } else {
+    TORCH_CHECK(beta == 0.0, "gemm_f32: beta != 0 needs out");
+    c = at::empty({M, N}, a.options());
+  }
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N, "gemm_f32: bias [N] fp32");
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(hyp::gemm_f32_supported(M, N, K, a_tr, b_tr, (int)a.stride(0), (int)b.stride(0), (int)c.stride(0)),
+              "gemm_f32: unsupported shape / layout (row-form K % 4, tr-form M / N % 4)");
   const at::DeviceGuard guard(a.device());
-  auto c = at::empty({M, N}, a.options().dtype(out_dtype.has_value() ? *out_dtype : at::kFloat));
-  HYP_CHECK_HIP(hyp::gemm_f32_nt(dtype_code(c), a.data_ptr<float>(), b.data_ptr<float>(), c.data_ptr(), M, N, K,
-                                 (int)a.stride(0), (int)b.stride(0), N, (float)alpha, cur_stream()));
+  TORCH_CHECK(shape < 3, "gemm_f32: shape 0 (128x128), 1 (256x64), 2 (64x256) or < 0 (planned)");
+  const int sp = hyp::gemm_f32_splits(M, N, K, (int)splits, (int)shape);
+  at::Tensor part;
+  if (sp > 1) part = at::empty({(int64_t)sp * M * N}, a.options());
+  HYP_CHECK_HIP(hyp::gemm_f32(a.data_ptr<float>(), b.data_ptr<float>(), c.data_ptr<float>(),
+                              sp > 1 ? part.data_ptr<float>() : nullptr, bp,
+                              static_cast<const float*>(device_zero_page(a.device())), M, N, K, a_tr, b_tr,
+                              (int)a.stride(0), (int)b.stride(0), (int)c.stride(0), (float)alpha, (float)beta,
+                              relu ? 1 : 0, sp, (int)shape, cur_stream()));
   return c;
+}
+
+// fp32 a [M, K], b [N, K] -> a @ b.T (the C3 matmul sweep's fp32 row)
+at::Tensor gemm_f32_nt(const at::Tensor& a, const at::Tensor& b, c10::optional<at::ScalarType> out_dtype, double alpha) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_f32_nt: expected a [M,K], b [N,K]");
+  at::Tensor c = gemm_f32(a, b, false, false, c10::nullopt, false, alpha, 0.0, c10::nullopt, -1, -1);
+  return out_dtype.has_value() && *out_dtype != at::kFloat ? c.to(*out_dtype) : c;
+}
+
+// x: [N, C, H, W] fp32 channels-last -> cols [N*Ho*Wo, Kp] (Kp >= R*S*C, % 4)
+at::Tensor im2col_f32(const at::Tensor& x, int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                      int64_t Kp) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "im2col_f32: fp32 channels-last [N, C, H, W]");
+  const int Nb = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Ho = (int)((H + 2 * ph - R) / sh + 1), Wo = (int)((W + 2 * pw - S) / sw + 1);
+  TORCH_CHECK(Kp >= R * S * C && Ho > 0 && Wo > 0, "im2col_f32: bad geometry");
+  const at::DeviceGuard guard(x.device());
+  auto cols = at::empty({(int64_t)Nb * Ho * Wo, Kp}, x.options());
+  HYP_CHECK_HIP(hyp::im2col_f32(x.data_ptr<float>(), cols.data_ptr<float>(), Nb, H, W, C, Ho, Wo, (int)R, (int)S,
+                                (int)sh, (int)sw, (int)ph, (int)pw, (int)Kp, cur_stream()));
+  return cols;
+}
+
+// dcols [N*Ho*Wo, Kp] -> dx [N, C, H, W] fp32 channels-last (the adjoint of im2col_f32)
+at::Tensor col2im_f32(const at::Tensor& dcols, int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
+                      int64_t sh, int64_t sw, int64_t ph, int64_t pw) {
+  HYP_CHECK_CUDA_TENSOR(dcols);
+  const int64_t Ho = (H + 2 * ph - R) / sh + 1, Wo = (W + 2 * pw - S) / sw + 1;
+  TORCH_CHECK(dcols.scalar_type() == at::kFloat && dcols.dim() == 2 && dcols.is_contiguous() &&
+                  dcols.size(0) == Nb * Ho * Wo && dcols.size(1) >= R * S * C,
+              "col2im_f32: dcols must be contiguous fp32 [N*Ho*Wo, >= R*S*C]");
+  const at::DeviceGuard guard(dcols.device());
+  auto dx = at::empty({Nb, C, H, W}, dcols.options().memory_format(at::MemoryFormat::ChannelsLast));
+  HYP_CHECK_HIP(hyp::col2im_f32(dcols.data_ptr<float>(), dx.data_ptr<float>(), (int)Nb, (int)H, (int)W, (int)C, (int)Ho,
+                                (int)Wo, (int)R, (int)S, (int)sh, (int)sw, (int)ph, (int)pw, (int)dcols.size(1),
+                                cur_stream()));
+  return dx;
 }
 
 // Operand view: a 2D tensor with unit stride in its last dim.  row form (tr = false): X[i, k] at
@@ -161,6 +226,17 @@ void register_gemm_ops(pybind11::module& m) {
   m.def("gemm_set_splitk_inkernel", [](int64_t on) { hyp::gemm_set_splitk_inkernel((int)on); },
         "A/B: split-K reduce in the last-arriving workgroup (1) or the separate reduce kernel (0, default)");
   m.def("gemm_plan", &gemm_plan, "(tile, splits) the automatic plan picks for an M x N x K GEMM");
+  m.def("gemm_f32", &gemm_f32, "C = epi(alpha A·Bᵀ) in fp32 on the fp32-input MFMA (NT/NN/TN, any M/N, split-K)",
+        pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_tr") = false, pybind11::arg("b_tr") = false,
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("relu") = false, pybind11::arg("alpha") = 1.0,
+        pybind11::arg("beta") = 0.0, pybind11::arg("out") = pybind11::none(), pybind11::arg("splits") = -1,
+        pybind11::arg("shape") = -1);
+  m.def("im2col_f32", &im2col_f32, "NHWC fp32 im2col -> [N*Ho*Wo, Kp]", pybind11::arg("x"), pybind11::arg("R"),
+        pybind11::arg("S"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"),
+        pybind11::arg("Kp"));
+  m.def("col2im_f32", &col2im_f32, "adjoint of im2col_f32 -> channels-last dx", pybind11::arg("dcols"),
+        pybind11::arg("Nb"), pybind11::arg("C"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("R"),
+        pybind11::arg("S"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"), pybind11::arg("pw"));
   m.def("gemm_f32_nt", &gemm_f32_nt, "C = alpha * A @ B.T, fp32 in, on the fp32-input MFMA", pybind11::arg("a"),
         pybind11::arg("b"), pybind11::arg("out_dtype") = pybind11::none(), pybind11::arg("alpha") = 1.0);
   m.def("gemm_nt", &gemm_nt, "C = alpha * A @ B.T on MFMA (bf16/f16 in)", pybind11::arg("a"), pybind11::arg("b"),

@@ -148,10 +148,22 @@ hipError_t gemm_nt(int in_dtype, int out_dtype, const void* A, const void* B, vo
                    int ldb, int ldc, float alpha, int bk, hipStream_t st);
 
 // ---- gemm_f32.hip -----------------------------------------------------------------------------
-// C = alpha A·Bᵀ, fp32 in (fp32-input MFMA, exact fp32 products/accumulation); M, N % 128, K % 32
-bool gemm_f32_nt_supported(int M, int N, int K, int lda, int ldb);
-hipError_t gemm_f32_nt(int out_dtype, const float* A, const float* B, void* C, int M, int N, int K, int lda, int ldb,
-                       int ldc, float alpha, hipStream_t st);
+// C = epi(alpha Σ_k A(m,k) B(n,k)) in fp32 on the fp32-input MFMA (exact fp32 products / accumulation).
+// A(m,k) at A + m*lda + k (a_tr = 0) or A + k*lda + m (a_tr = 1), B likewise; epi: + beta*C_old,
+// + bias[n], ReLU.  Any M, N; row-form operands K % 4, tr-form operands M / N % 4, ld % 4.
+// splits / shape (0: 128x128, 1: 256x64, 2: 64x256) < 0: the cost-model plan; split-K needs
+// part = fp32 [splits * M * N] (gemm_f32_splits).
+bool gemm_f32_supported(int M, int N, int K, bool a_tr, bool b_tr, int lda, int ldb, int ldc);
+int gemm_f32_splits(int M, int N, int K, int splits, int shape);
+hipError_t gemm_f32(const float* A, const float* B, float* C, float* part, const float* bias, const float* zero,
+                    int M, int N, int K, bool a_tr, bool b_tr, int lda, int ldb, int ldc, float alpha, float beta,
+                    int relu, int splits, int shape, hipStream_t st);
+// NHWC fp32 im2col (cols [Nb*Ho*Wo, Kp], column (r*S + s)*C + c, pad columns zero) and its adjoint
+// (a deterministic per-input gather over the taps)
+hipError_t im2col_f32(const float* x, float* cols, int Nb, int H, int W, int C, int Ho, int Wo, int R, int S, int sh,
+                      int sw, int ph, int pw, int Kp, hipStream_t st);
+hipError_t col2im_f32(const float* dcols, float* dx, int Nb, int H, int W, int C, int Ho, int Wo, int R, int S, int sh,
+                      int sw, int ph, int pw, int Kp, hipStream_t st);
 
 // ---- gemm_tiles.hip --------------------------------------------------------------------------
 // C[M,N] = epi(alpha Σ_k A(m,k) B(n,k)); A(m,k) at A + m*lda + k (a_tr = 0) or A + k*lda + m (a_tr = 1),

@@ -23,6 +23,7 @@ from ..ops import _native
 from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv_f32 import Conv2d
 from ..ops.conv import branch_sum_link, conv_bn_act, residual_link, xf_consumer_ok
 from ..ops.linear import Linear
 
@@ -33,11 +34,11 @@ def _downsample(ds: nn.Sequential, x: torch.Tensor, branch=None) -> torch.Tensor
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+    return Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    return Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -100,7 +101,7 @@ class ResNet(nn.Module):
     ):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct2d(64, act=True)
         self.maxpool = MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])

@@ -29,6 +29,7 @@ from ..ops.pool import AdaptiveAvgPool2d, MaxPool2d
 from torch.utils.checkpoint import checkpoint
 
 from ..ops import recompute as _rc
+from ..ops.conv_f32 import Conv2d
 from ..ops.dropout import Dropout
 from ..ops.layernorm import LayerNorm, bias_grad_link, layer_norm
 from ..ops.linear import Linear
@@ -138,7 +139,7 @@ class VisionTransformer(nn.Module):
         self.image_size = image_size
         self.patch_size = patch_size
         self.hidden_dim = hidden_dim
-        self.conv_proj = nn.Conv2d(3, hidden_dim, kernel_size=patch_size, stride=patch_size)
+        self.conv_proj = Conv2d(3, hidden_dim, kernel_size=patch_size, stride=patch_size)
         seq_length = (image_size // patch_size) ** 2 + 1
         self.class_token = nn.Parameter(torch.zeros(1, 1, hidden_dim))
         self.encoder = Encoder(seq_length, num_layers, num_heads, hidden_dim, mlp_dim, dropout, attention_dropout,
@@ -201,10 +202,10 @@ def vit_tiny(num_classes: int = 10, image_size: int = 32, patch_size: int = 4, *
 def fallback_cnn(num_classes: int = 1000) -> nn.Sequential:
     """The CNN the reference actually benchmarked as "ViT" (212,328 params; keys 0/3/7)."""
     return nn.Sequential(
-        nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3),
+        Conv2d(3, 64, kernel_size=7, stride=2, padding=3),
         nn.ReLU(inplace=True),
         MaxPool2d(kernel_size=3, stride=2, padding=1),
-        nn.Conv2d(64, 128, kernel_size=3, padding=1),
+        Conv2d(64, 128, kernel_size=3, padding=1),
         nn.ReLU(inplace=True),
         MaxPool2d(kernel_size=3, stride=2, padding=1),
         AdaptiveAvgPool2d((1, 1)),
