@@ -166,20 +166,37 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_k(const F32Args p) {
     if (t + 1 < nk) stage(t + 1, smem + (cur ^ 1) * (IA + IB));
     const float* as = smem + cur * (IA + IB);
     const float* bs = as + IA;
+    // fragments double-buffered in registers: chunk c + 1's LDS reads are in flight while chunk
+    // c's 8 MFMAs (512 cycles) run — one register set would serialize read latency and MFMAs
+    f32x2 a[2][2], b[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[0][i] = frag<ATR, BM>(as, wm * 64 + i * 32 + r32, 0, h);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[0][j] = frag<BTR, BN>(bs, wn * 64 + j * 32 + r32, 0, h);
 #pragma unroll
     for (int c = 0; c < kBK / 4; ++c) {
-      f32x2 a[2], b[2];
+      const int q = c & 1;
+      if (c + 1 < kBK / 4) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = frag<ATR, BM>(as, wm * 64 + i * 32 + r32, c, h);
+        for (int i = 0; i < 2; ++i) a[q ^ 1][i] = frag<ATR, BM>(as, wm * 64 + i * 32 + r32, c + 1, h);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = frag<BTR, BN>(bs, wn * 64 + j * 32 + r32, c, h);
+        for (int j = 0; j < 2; ++j) b[q ^ 1][j] = frag<BTR, BN>(bs, wn * 64 + j * 32 + r32, c + 1, h);
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][i].x, b[q][j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][i].y, b[q][j].y, acc[i][j], 0, 0, 0);
         }
+      // interleave the next chunk's LDS reads between this chunk's MFMAs (hipcc otherwise issues
+      // them after the last MFMA and waits on them before the next chunk: ~10 % MFMA idle)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // up to 2 DS reads
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
     __builtin_amdgcn_s_waitcnt(0);  // next slice's LDS-DMA (this wave)
     __syncthreads();                // ... every wave's; everyone done with `cur`

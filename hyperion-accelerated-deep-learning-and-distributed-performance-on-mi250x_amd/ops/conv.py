@@ -41,7 +41,6 @@ import torch
 import torch.nn as nn
 
 from . import _native
-from . import conv_f32 as _f32
 from . import streams as _streams
 
 
@@ -895,9 +894,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optio
     use = use and _native_conv_ok(x, conv, w)
     if not use:
         _native.count("conv_bn_act_fallback")
-        if _f32.f32_conv_ok(x, conv):  # fp32: the native fp32 GEMM convolution, then the native BN
-            return bn(_f32.conv2d_f32(x, conv), residual=residual)
-        return bn(conv(x), residual=residual)
+        return bn(conv(x), residual=residual)  # fp32: Conv2d routes to the native fp32 path (conv_f32)
     _native.count("conv_bn_act")
     bn._host_batches += 1  # BatchNormAct2d's host-side num_batches_tracked mirror
     link_in = link_out = None

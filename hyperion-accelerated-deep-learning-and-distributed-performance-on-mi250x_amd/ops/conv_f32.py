@@ -134,8 +134,52 @@ class _Conv2dF32Fn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-def conv2d_f32(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-    """``conv(x)`` for an fp32 ``nn.Conv2d`` on the native fp32 path (channels-last output)."""
+# Per-convolution routing: the native path and the vendor convolution are timed (forward + both
+# gradients, on operands of the call's shape) on the first eager call of each geometry and the faster
+# runs from then on — the fp32 MFMA GEMM wins some ResNet shapes and loses others to MIOpen
+# (profiles/r06/fp32_conv_*.json), so per-layer routing beats either side alone.  ROUTE=native
+# forces the native path (tests, traces), ROUTE=vendor the vendor one.
+ROUTE = os.environ.get("HYPERION_CONV_F32_ROUTE", "auto")
+_ROUTE: Dict[tuple, bool] = {}
+
+
+def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    if ROUTE != "auto":
+        return ROUTE == "native"
+    w, b = conv.weight, conv.bias
+    key = (tuple(x.shape), tuple(w.shape), tuple(conv.stride), tuple(conv.padding), b is not None, x.requires_grad,
+           w.requires_grad)
+    c = _ROUTE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        from .gemm import _time
+
+        xt = torch.randn(x.shape, device=x.device).contiguous(memory_format=torch.channels_last)
+        xt.requires_grad_(x.requires_grad)
+        wt = w.detach().clone().requires_grad_(w.requires_grad)
+        bt = b.detach().clone().requires_grad_(b.requires_grad) if b is not None else None
+        ins = [t for t in (xt, wt, bt) if t is not None and t.requires_grad]
+
+        def run(native):
+            with torch.enable_grad():
+                y = (_Conv2dF32Fn.apply(xt, wt, bt, tuple(conv.stride), tuple(conv.padding)) if native
+                     else F.conv2d(xt, wt, bt, conv.stride, conv.padding))
+                if ins:
+                    torch.autograd.grad(y, ins, torch.ones_like(y))
+
+        run(True)
+        run(False)
+        c = _time(lambda: run(True), reps=3) < _time(lambda: run(False), reps=3)
+        _ROUTE[key] = c
+    return c
+
+
+def conv2d_f32(x: torch.Tensor, conv: nn.Conv2d) -> Optional[torch.Tensor]:
+    """``conv(x)`` for an fp32 ``nn.Conv2d`` on the native fp32 path (channels-last output), or None
+    when the vendor convolution measured faster for this geometry (the caller runs it)."""
+    if not _native_faster(x, conv):
+        return None
     return _native.apply_fn(_Conv2dF32Fn, x, conv.weight, conv.bias, tuple(conv.stride), tuple(conv.padding))
 
 
@@ -145,7 +189,9 @@ class Conv2d(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
         if f32_conv_ok(x, self):
-            return conv2d_f32(x, self)
+            y = conv2d_f32(x, self)
+            if y is not None:
+                return y
         return super().forward(x)
 
 

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import linear_f32 as _lf32
 from .gemm import mm_nn, mm_nt, mm_tn
 
 SKINNY_MAX_M = int(os.environ.get("HYPERION_SKINNY_MAX_M", "1024"))
@@ -167,6 +168,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None, l
     autocast of ``F.linear``), so the native kernels serve the AMP trainers too.  ``link``: a
     ``ResidualLink`` on x (see :func:`arm_link`)."""
     if not (x.is_cuda and _native.use_native(x, op="linear")) or _native.plain_fp32(x):
+        if _native.plain_fp32(x) and _lf32.applies(x, w):
+            return _lf32.linear_f32(x, w, b)  # large fp32 GEMMs: native fp32 MFMA where it is faster
         return F.linear(x, w, b)
     if torch.is_autocast_enabled(x.device.type):
         dt = torch.get_autocast_dtype(x.device.type)

@@ -25,6 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native
+from . import linear_f32 as _lf32
 from . import recompute as _rc
 from .gemm import mm_nn, mm_nt
 import weakref
@@ -158,7 +159,7 @@ def linear_act(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], acti
         if link is not None and y.grad_fn is not None:
             link.first_node = weakref.ref(y.grad_fn)
         return y
-    y = F.linear(x, w, b)
+    y = _lf32.linear_f32(x, w, b) if _native.plain_fp32(x) and _lf32.applies(x, w) else F.linear(x, w, b)
     y = F.gelu(y) if activation == "gelu" else F.relu(y)
     return F.dropout(y, dropout_p, True) if dropout_p > 0.0 else y
 

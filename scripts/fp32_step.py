@@ -27,3 +27,7 @@ for i in range(steps + 3):
     opt.step()
 torch.cuda.synchronize()
 print(f"{name} native={native} {1e3 * (time.perf_counter() - t0) / steps:.3f} ms/step")
+if native:
+    print("routes (native faster):", sum(conv_f32._ROUTE.values()), "of", len(conv_f32._ROUTE))
+    for k, v in conv_f32._ROUTE.items():
+        print("  ", k[0], k[1], k[2], k[3], "native" if v else "vendor")

@@ -7,6 +7,14 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _native_route(monkeypatch):
+    """The numerics tests exercise the native path whatever the per-shape timing would pick."""
+    from hyperion.ops import conv_f32
+
+    monkeypatch.setattr(conv_f32, "ROUTE", "native")
+
+
 def _bound(a, b):
     # a k-ordered fp32 fma chain (or a few of them, summed): error ≲ K·eps·Σ|a||b|; generous factor
     return 8 * 4e-7 * (a.abs() @ b.abs().t()) + 1e-30
@@ -125,3 +133,42 @@ def test_resnet18_fp32_step_native_matches_vendor():
     assert abs(l0 - l1) <= 1e-5 * abs(l0)
     for a, b in zip(g0, g1):
         torch.testing.assert_close(b, a, rtol=1e-3, atol=1e-4 * (a.abs().max().item() + 1e-12))
+
+
+@pytest.mark.parametrize("shape", [(2, 197, 768, 3072), (3, 100, 260, 68)])
+def test_linear_f32_native_matches_fp64(shape, monkeypatch):
+    """ops/linear_f32.py with the native kernel forced for all three GEMMs vs fp64 F.linear."""
+    from hyperion.ops import _native, linear_f32
+
+    monkeypatch.setattr(linear_f32, "_choose", lambda key, native, vendor: native())
+    b_, t, fin, fout = shape
+    torch.manual_seed(0)
+    x = torch.randn(b_, t, fin, device="cuda", requires_grad=True)
+    w = (torch.randn(fout, fin, device="cuda") / fin ** 0.5).requires_grad_(True)
+    b = torch.randn(fout, device="cuda", requires_grad=True)
+    y = linear_f32.linear_f32(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xd, wd, bd = (t_.detach().double().requires_grad_(True) for t_ in (x, w, b))
+    yr = F.linear(xd, wd, bd)
+    yr.backward(g.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad.double(), xd.grad, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(w.grad.double(), wd.grad, rtol=1e-5, atol=1e-4 * (t * b_) ** 0.5)
+    torch.testing.assert_close(b.grad.double(), bd.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_conv2d_f32_auto_route_times_both_and_caches(monkeypatch):
+    from hyperion.ops import conv_f32
+
+    monkeypatch.setattr(conv_f32, "ROUTE", "auto")
+    conv_f32._ROUTE.clear()
+    conv = conv_f32.Conv2d(64, 64, 3, padding=1, bias=False).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 64, 28, 28, device="cuda").contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y1 = conv(x)
+    assert len(conv_f32._ROUTE) == 1
+    y2 = conv(x)
+    assert len(conv_f32._ROUTE) == 1
+    ref = F.conv2d(x.detach(), conv.weight.detach(), None, 1, 1)
+    torch.testing.assert_close(y1, ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y2, y1)
