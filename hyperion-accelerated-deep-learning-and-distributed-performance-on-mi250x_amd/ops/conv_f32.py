@@ -141,14 +141,15 @@ class _Conv2dF32Fn(torch.autograd.Function):
 # forces the native path (tests, traces), ROUTE=vendor the vendor one.
 ROUTE = os.environ.get("HYPERION_CONV_F32_ROUTE", "auto")
 _ROUTE: Dict[tuple, bool] = {}
+ROUTE_MS: Dict[tuple, Tuple[float, float]] = {}  # key -> (native, vendor) ms per fwd + bwd (records)
 
 
 def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     if ROUTE != "auto":
         return ROUTE == "native"
     w, b = conv.weight, conv.bias
-    key = (tuple(x.shape), tuple(w.shape), tuple(conv.stride), tuple(conv.padding), b is not None, x.requires_grad,
-           w.requires_grad)
+    # geometry only: a no-grad call (an inference loop after training warm-up) reuses the decision
+    key = (tuple(x.shape), tuple(w.shape), tuple(conv.stride), tuple(conv.padding), b is not None)
     c = _ROUTE.get(key)
     if c is None:
         if torch.cuda.is_current_stream_capturing():
@@ -170,8 +171,10 @@ def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 
         run(True)
         run(False)
-        c = _time(lambda: run(True), reps=3) < _time(lambda: run(False), reps=3)
+        tn, tv = _time(lambda: run(True), reps=3) / 3, _time(lambda: run(False), reps=3) / 3
+        c = tn < tv
         _ROUTE[key] = c
+        ROUTE_MS[key] = (tn, tv)
     return c
 
 

@@ -30,4 +30,5 @@ print(f"{name} native={native} {1e3 * (time.perf_counter() - t0) / steps:.3f} ms
 if native:
     print("routes (native faster):", sum(conv_f32._ROUTE.values()), "of", len(conv_f32._ROUTE))
     for k, v in conv_f32._ROUTE.items():
-        print("  ", k[0], k[1], k[2], k[3], "native" if v else "vendor")
+        tn, tv = conv_f32.ROUTE_MS.get(k, (0.0, 0.0))
+        print("  ", k[0], k[1], k[2], k[3], "native" if v else "vendor", f"native {tn * 1e3:.1f} us vendor {tv * 1e3:.1f} us")

@@ -18,6 +18,7 @@
 #   bash scripts/gpu_suite.sh llama_pmc                  PMC passes over the Llama-2-7B LoRA step (weight streaming)
 #   bash scripts/gpu_suite.sh steps                      graphed model steps (WL="vitgraph vitselgraph ..."), one JSON each
 #   bash scripts/gpu_suite.sh final                      bench x2 + every README step row (one box, one call)
+#   bash scripts/gpu_suite.sh refresh                    README micro rows: matmul / STREAM, attention, LM head, fused-vs-eager
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -152,6 +153,16 @@ final)
     timeout -k 10 400 python -u scripts/run_model_step.py fsdp $cfg >> "$out/fsdp_steps.jsonl" 2>> "$out/fsdp_steps.err" || { tail -5 "$out/fsdp_steps.err"; exit 1; }
     echo "fsdp $cfg $(tail -1 "$out/fsdp_steps.jsonl" | grep -o '"ms_per_step": [0-9.]*')"
   done
+  ;;
+refresh)
+  PYTHONPATH=$PWD timeout -k 10 500 python -u -m hyperion.cli.hardware_bench --out "$out/hardware" > "$out/hardware.log" 2>&1 || { tail -5 "$out/hardware.log"; exit 1; }
+  echo hardware ok
+  timeout -k 10 300 python -u scripts/attn_bench.py > "$out/attn_bench.jsonl" 2> "$out/attn_bench.err" || { tail -5 "$out/attn_bench.err"; exit 1; }
+  echo attn ok
+  timeout -k 10 300 python -u scripts/ce_bench.py --out "$out/ce_bench.json" > "$out/ce_bench.log" 2>&1 || { tail -5 "$out/ce_bench.log"; exit 1; }
+  echo ce ok
+  PYTHONPATH=$PWD timeout -k 10 400 python -u -m hyperion.cli.bench_models --out "$out/fusion/x" --only fusion > "$out/fusion.log" 2>&1 || { tail -5 "$out/fusion.log"; exit 1; }
+  ls "$out" "$out/hardware" "$out/fusion"
   ;;
 *)
   echo "unknown stage $stage"; exit 2
