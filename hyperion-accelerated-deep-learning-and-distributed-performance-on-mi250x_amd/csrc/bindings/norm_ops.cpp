@@ -3,6 +3,10 @@
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
+namespace hyp {
+void adam_set_streaming(int on);  // adam.hip
+}
+
 namespace hypbind {
 namespace {
 
@@ -239,6 +243,8 @@ void register_norm_ops(pybind11::module& m) {
         pybind11::arg("sums") = pybind11::none());
   m.def("bn_bwd_dx", &bn_bwd_dx, "BN backward dx pass from a pre-masked dz and its complete sums");
   m.def("adam_mt", &adam_mt, "multi-tensor fused Adam/AdamW");
+  m.def("adam_set_streaming", [](int64_t on) { hyp::adam_set_streaming((int)on); },
+        "A/B: non-temporal loads / stores of the fp32 optimizer state in adam_mt");
   m.def("mse_fwd_bwd", [](const at::Tensor& x, const at::Tensor& t) {
     HYP_CHECK_CUDA_TENSOR(x);
     TORCH_CHECK(x.is_contiguous() && t.is_contiguous() && t.scalar_type() == at::kFloat && x.numel() == t.numel() &&

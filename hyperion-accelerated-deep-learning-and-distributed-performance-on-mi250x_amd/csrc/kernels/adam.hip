@@ -40,7 +40,21 @@ struct AdamArgs {
   float lr, b1, b2, eps, wd;
   int adamw;
   int zero_grad;  // write zeros over the gradient once read (replaces a separate zero_grad pass)
+  int nt;         // streaming (non-temporal) loads / stores of the fp32 state (adam_set_streaming)
 };
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_state(const float* p, int nt) {
+  if (nt) {
+    const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(p));
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  return *reinterpret_cast<const float4*>(p);
+}
+__device__ __forceinline__ void st_state(float* p, const float4& v, int nt) {
+  if (nt) __builtin_nontemporal_store(f32x4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4v*>(p));
+  else *reinterpret_cast<float4*>(p) = v;
+}
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a, float lr,
                                           float bc1, float bc2_sqrt) {
@@ -107,9 +121,9 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
   // vector body: all of p/g/m/v are >=16B aligned at `start` (host checks base alignment; chunk % 4 == 0)
   const int64_t nvec_end = start + ((end - start) & ~int64_t(3));
   for (int64_t i = start + 4 * threadIdx.x; i < nvec_end; i += 4 * kThreads) {
-    float4 pv = *reinterpret_cast<float4*>(p + i);
-    float4 mv = *reinterpret_cast<float4*>(m + i);
-    float4 vv = *reinterpret_cast<float4*>(v + i);
+    float4 pv = ld_state(p + i, a.nt);
+    float4 mv = ld_state(m + i, a.nt);
+    float4 vv = ld_state(v + i, a.nt);
     float gv[4];
     load4<G>(g + i, gv);
     if (a.zero_grad) store4z<G>(g + i);
@@ -117,9 +131,9 @@ __global__ __launch_bounds__(kThreads) void adam_mt_k(const int64_t* __restrict_
     adam_elem(pv.y, gv[1] * gs, mv.y, vv.y, a, lr, bc1, bc2_sqrt);
     adam_elem(pv.z, gv[2] * gs, mv.z, vv.z, a, lr, bc1, bc2_sqrt);
     adam_elem(pv.w, gv[3] * gs, mv.w, vv.w, a, lr, bc1, bc2_sqrt);
-    *reinterpret_cast<float4*>(p + i) = pv;
-    *reinterpret_cast<float4*>(m + i) = mv;
-    *reinterpret_cast<float4*>(v + i) = vv;
+    st_state(p + i, pv, a.nt);
+    st_state(m + i, mv, a.nt);
+    st_state(v + i, vv, a.nt);
     if (MASTER) store4<PL>(pl + i, pv);
   }
   for (int64_t i = nvec_end + threadIdx.x; i < end; i += kThreads) {
@@ -224,12 +238,15 @@ __global__ void sum_partials_k(const float* __restrict__ part, int n, float* __r
 
 }  // namespace
 
+int g_adam_nt = 0;
+void adam_set_streaming(int on) { g_adam_nt = on; }
+
 hipError_t adam_multi_tensor(int grad_dtype, int param_dtype, const int64_t* ptrs, const int64_t* sizes,
                              const int* blocks, int nblocks, int T, int chunk, float lr, float b1, float b2, float eps,
                              float wd, int adamw, const float* lr_t, const float* step_t, const float* inv_scale,
                              const float* found_inf, hipStream_t stream, int zero_grad) {
   if (nblocks == 0) return hipSuccess;
-  AdamArgs a{lr, b1, b2, eps, wd, adamw, zero_grad};
+  AdamArgs a{lr, b1, b2, eps, wd, adamw, zero_grad, g_adam_nt};
   HYP_DISPATCH_FLOAT(grad_dtype, G, {
     if (param_dtype == kF32)
       hipLaunchKernelGGL((adam_mt_k<G, float, false>), dim3(nblocks), dim3(kThreads), 0, stream, ptrs, sizes, blocks,
