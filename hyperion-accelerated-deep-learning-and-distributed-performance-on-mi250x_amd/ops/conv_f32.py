@@ -137,7 +137,7 @@ class _Conv2dF32Fn(torch.autograd.Function):
 # Per-convolution routing: the native path and the vendor convolution are timed (forward + both
 # gradients, on operands of the call's shape) on the first eager call of each geometry and the faster
 # runs from then on — the fp32 MFMA GEMM wins some ResNet shapes and loses others to MIOpen
-# (profiles/r06/fp32_conv_*.json), so per-layer routing beats either side alone.  ROUTE=native
+# (profiles/r06/fp32_conv_routes_resnet50.txt), so per-layer routing beats either side alone.  ROUTE=native
 # forces the native path (tests, traces), ROUTE=vendor the vendor one.
 ROUTE = os.environ.get("HYPERION_CONV_F32_ROUTE", "auto")
 _ROUTE: Dict[tuple, bool] = {}
