@@ -57,7 +57,7 @@ at::Tensor gemm_f32(const at::Tensor& a, const at::Tensor& b, bool a_tr, bool b_
   TORCH_CHECK(hyp::gemm_f32_supported(M, N, K, a_tr, b_tr, (int)a.stride(0), (int)b.stride(0), (int)c.stride(0)),
               "gemm_f32: unsupported shape / layout (row-form K % 4, tr-form M / N % 4)");
   const at::DeviceGuard guard(a.device());
-  TORCH_CHECK(shape < 3, "gemm_f32: shape 0 (128x128), 1 (256x64), 2 (64x256) or < 0 (planned)");
+  TORCH_CHECK(shape < 5, "gemm_f32: shape 0 (128x128), 1 (256x64), 2 (64x256), 3 (256x128), 4 (128x256) or < 0 (planned)");
   const int sp = hyp::gemm_f32_splits(M, N, K, (int)splits, (int)shape);
   at::Tensor part;
   if (sp > 1) part = at::empty({(int64_t)sp * M * N}, a.options());

@@ -110,11 +110,13 @@ __device__ __forceinline__ f32x2 frag(const float* img, int row, int c, int h) {
   }
 }
 
-// WM x WN waves of 64 x 64 outputs: tiles 128x128 (2x2), 256x64 (4x1), 64x256 (1x4)
-template <int WM, int WN, bool ATR, bool BTR>
+// WM x WN waves, each FM x FN blocks of 32 x 32 outputs: 128x128 (2x2 waves of 2x2), 256x64, 64x256,
+// and the one-workgroup-per-CU 256x128 / 128x256 (2x2 waves of 4x2 / 2x4: twice the MFMA work per
+// fragment read and per barrier, one wave per SIMD)
+template <int WM, int WN, int FM, int FN, bool ATR, bool BTR>
 __global__ __launch_bounds__(kThreads) void gemm_f32_k(const F32Args p) {
   static_assert(WM * WN == 4, "4 waves");
-  constexpr int BM = 64 * WM, BN = 64 * WN, IA = BM * kBK, IB = BN * kBK;
+  constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN, IA = BM * kBK, IB = BN * kBK;
   __shared__ __attribute__((aligned(16))) float smem[2 * (IA + IB)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -139,11 +141,11 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_k(const F32Args p) {
   const int kend = min(p.K, kbeg + p.kper);
   const int nk = (kend - kbeg + kBK - 1) / kBK;
 
-  f32x16 acc[2][2];
+  f32x16 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
@@ -161,60 +163,66 @@ __global__ __launch_bounds__(kThreads) void gemm_f32_k(const F32Args p) {
     __syncthreads();
   }
   const int r32 = lane & 31, h = lane >> 5;
+  const int wr = wm * 32 * FM, wc = wn * 32 * FN;
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
     if (t + 1 < nk) stage(t + 1, smem + (cur ^ 1) * (IA + IB));
     const float* as = smem + cur * (IA + IB);
     const float* bs = as + IA;
     // fragments double-buffered in registers: chunk c + 1's LDS reads are in flight while chunk
-    // c's 8 MFMAs (512 cycles) run — one register set would serialize read latency and MFMAs
-    f32x2 a[2][2], b[2][2];
+    // c's 2·FM·FN MFMAs (64 cycles each) run — one register set would serialize read latency and MFMAs
+    f32x2 a[2][FM], b[2][FN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a[0][i] = frag<ATR, BM>(as, wm * 64 + i * 32 + r32, 0, h);
+    for (int i = 0; i < FM; ++i) a[0][i] = frag<ATR, BM>(as, wr + i * 32 + r32, 0, h);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[0][j] = frag<BTR, BN>(bs, wn * 64 + j * 32 + r32, 0, h);
+    for (int j = 0; j < FN; ++j) b[0][j] = frag<BTR, BN>(bs, wc + j * 32 + r32, 0, h);
 #pragma unroll
     for (int c = 0; c < kBK / 4; ++c) {
       const int q = c & 1;
       if (c + 1 < kBK / 4) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[q ^ 1][i] = frag<ATR, BM>(as, wm * 64 + i * 32 + r32, c + 1, h);
+        for (int i = 0; i < FM; ++i) a[q ^ 1][i] = frag<ATR, BM>(as, wr + i * 32 + r32, c + 1, h);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[q ^ 1][j] = frag<BTR, BN>(bs, wn * 64 + j * 32 + r32, c + 1, h);
+        for (int j = 0; j < FN; ++j) b[q ^ 1][j] = frag<BTR, BN>(bs, wc + j * 32 + r32, c + 1, h);
       }
+      // the .x k-step of every block, then the .y one: an accumulator's two MFMAs are FM·FN issues
+      // apart (back-to-back dependent MFMAs wait out the 64-cycle result latency)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][i].x, b[q][j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q][i].y, b[q][j].y, acc[i][j], 0, 0, 0);
-        }
       // interleave the next chunk's LDS reads between this chunk's MFMAs (hipcc otherwise issues
       // them after the last MFMA and waits on them before the next chunk: ~10 % MFMA idle)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < FM + FN; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // up to 2 DS reads
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN - (FM + FN), 0);
     }
     __builtin_amdgcn_s_waitcnt(0);  // next slice's LDS-DMA (this wave)
     __syncthreads();                // ... every wave's; everyone done with `cur`
   }
 
-  // acc[i][j][v] = C[m0 + wm*64 + i*32 + 8 (v / 4) + 4 h + (v % 4)][n0 + wn*64 + j*32 + r32]
+  // acc[i][j][v] = C[m0 + wr + i*32 + 8 (v / 4) + 4 h + (v % 4)][n0 + wc + j*32 + r32]
   const bool slab = p.splits > 1;
   float* part = slab ? p.part + (int64_t)split * p.M * p.N : nullptr;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 64 + j * 32 + r32;
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wc + j * 32 + r32;
     if (col >= p.N) continue;
     const float bv = (!slab && p.bias) ? p.bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int row = m0 + wm * 64 + i * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+        const int row = m0 + wr + i * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
         if (row >= p.M) continue;
         if (slab) {
           part[(int64_t)row * p.N + col] = acc[i][j][v];
@@ -343,7 +351,10 @@ bool gemm_f32_supported(int M, int N, int K, bool a_tr, bool b_tr, int lda, int 
 }
 
 namespace {
-constexpr int kShapes[3][2] = {{2, 2}, {4, 1}, {1, 4}};  // (WM, WN): 128x128, 256x64, 64x256
+// (BM, BN, workgroups per CU): 128x128, 256x64, 64x256 (2 per CU: 64-80 KiB of LDS), 256x128,
+// 128x256 (1 per CU: 96 KiB)
+constexpr int kNumShapes = 5;
+constexpr int kShapes[kNumShapes][3] = {{128, 128, 2}, {256, 64, 2}, {64, 256, 2}, {256, 128, 1}, {128, 256, 1}};
 
 // Launch plan: the tile shape and split count minimising a cost model of the MFMA-bound kernel —
 // 256 CUs each time-slice their resident workgroups, so the time is the number of 256-workgroup
@@ -353,17 +364,18 @@ constexpr int kShapes[3][2] = {{2, 2}, {4, 1}, {1, 4}};  // (WM, WN): 128x128, 2
 void plan(int M, int N, int K, int req, int req_shape, int* shape, int* splits, int* per_out) {
   const int nk = (K + kBK - 1) / kBK;
   double best = 1e30;
-  int bs = req_shape >= 0 && req_shape < 3 ? req_shape : 0, bsp = 1, bper = nk;
-  for (int t = 0; t < 3; ++t) {
+  int bs = req_shape >= 0 && req_shape < kNumShapes ? req_shape : 0, bsp = 1, bper = nk;
+  for (int t = 0; t < kNumShapes; ++t) {
     if (req_shape >= 0 && t != req_shape) continue;
-    const int bm = 64 * kShapes[t][0], bn = 64 * kShapes[t][1];
+    const int bm = kShapes[t][0], bn = kShapes[t][1], occ = kShapes[t][2];
     const int64_t tiles = (int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
     for (int s = 1; s <= std::min(nk, 128); ++s) {
       if (req > 0 && s != std::min(req, nk)) continue;
       const int per = (nk + s - 1) / s, se = (nk + per - 1) / per;
       if (se != s) continue;
-      const int64_t waves = (tiles * s + 255) / 256;
-      double est = (double)waves * (per + 1.5);
+      // a 1-per-CU tile does twice the MFMA work per slice of a 2-per-CU one in the same time slot
+      const int64_t waves = (tiles * s + 256 * occ - 1) / (256 * occ);
+      double est = (double)waves * (per + 1.5) * (occ == 1 ? 2.0 : 1.0);
       if (s > 1) est += ((double)M * N * 4.0 * (s + 1) / 4.0e6 + 3.0) / 1.7;
       if (est < best * 0.98) {
         best = est;
@@ -378,13 +390,13 @@ void plan(int M, int N, int K, int req, int req_shape, int* shape, int* splits, 
   *per_out = bper;
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int FM, int FN>
 void launch_shape(const F32Args& p, bool a_tr, bool b_tr, int nwg, hipStream_t st) {
   const dim3 grid(nwg), block(kThreads);
-  if (!a_tr && !b_tr) hipLaunchKernelGGL((gemm_f32_k<WM, WN, false, false>), grid, block, 0, st, p);
-  else if (!a_tr && b_tr) hipLaunchKernelGGL((gemm_f32_k<WM, WN, false, true>), grid, block, 0, st, p);
-  else if (a_tr && !b_tr) hipLaunchKernelGGL((gemm_f32_k<WM, WN, true, false>), grid, block, 0, st, p);
-  else hipLaunchKernelGGL((gemm_f32_k<WM, WN, true, true>), grid, block, 0, st, p);
+  if (!a_tr && !b_tr) hipLaunchKernelGGL((gemm_f32_k<WM, WN, FM, FN, false, false>), grid, block, 0, st, p);
+  else if (!a_tr && b_tr) hipLaunchKernelGGL((gemm_f32_k<WM, WN, FM, FN, false, true>), grid, block, 0, st, p);
+  else if (a_tr && !b_tr) hipLaunchKernelGGL((gemm_f32_k<WM, WN, FM, FN, true, false>), grid, block, 0, st, p);
+  else hipLaunchKernelGGL((gemm_f32_k<WM, WN, FM, FN, true, true>), grid, block, 0, st, p);
 }
 }  // namespace
 
@@ -402,11 +414,13 @@ hipError_t gemm_f32(const float* A, const float* B, float* C, float* part, const
   plan(M, N, K, splits, shape, &shape, &splits, &per);
   if (splits > 1 && part == nullptr) return hipErrorInvalidValue;
   F32Args p{A, B, C, part, bias, zero, M, N, K, lda, ldb, ldc, per * kBK, splits, alpha, beta, relu};
-  const int bm = 64 * kShapes[shape][0], bn = 64 * kShapes[shape][1];
+  const int bm = kShapes[shape][0], bn = kShapes[shape][1];
   const int nwg = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * splits;
-  if (shape == 0) launch_shape<2, 2>(p, a_tr, b_tr, nwg, st);
-  else if (shape == 1) launch_shape<4, 1>(p, a_tr, b_tr, nwg, st);
-  else launch_shape<1, 4>(p, a_tr, b_tr, nwg, st);
+  if (shape == 0) launch_shape<2, 2, 2, 2>(p, a_tr, b_tr, nwg, st);
+  else if (shape == 1) launch_shape<4, 1, 2, 2>(p, a_tr, b_tr, nwg, st);
+  else if (shape == 2) launch_shape<1, 4, 2, 2>(p, a_tr, b_tr, nwg, st);
+  else if (shape == 3) launch_shape<2, 2, 4, 2>(p, a_tr, b_tr, nwg, st);
+  else launch_shape<2, 2, 2, 4>(p, a_tr, b_tr, nwg, st);
   if (splits == 1) return hipGetLastError();
   const bool v4 = N % 4 == 0 && ldc % 4 == 0 && reinterpret_cast<uintptr_t>(C) % 16 == 0;
   const int64_t work = (int64_t)M * N / (v4 ? 4 : 1);

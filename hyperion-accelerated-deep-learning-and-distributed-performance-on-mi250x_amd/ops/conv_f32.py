@@ -44,7 +44,7 @@ def _tune(C, a, b, a_tr: bool, b_tr: bool, K: int) -> Tuple[int, int]:
 
     nk = (K + 31) // 32
     best, plan = _time(lambda: C.gemm_f32(a, b, a_tr=a_tr, b_tr=b_tr), reps=3), (-1, -1)
-    for shape in (0, 1, 2):
+    for shape in (0, 1, 2):  # 3 / 4 (one workgroup per CU) measured slower everywhere
         for sp in _SPLITS:
             if sp > 1 and nk // sp < 2:
                 break
