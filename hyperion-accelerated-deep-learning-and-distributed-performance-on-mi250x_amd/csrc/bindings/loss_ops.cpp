@@ -56,7 +56,10 @@ at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V,
   TORCH_CHECK(dy.is_contiguous() && dy.numel() == n * E && E % 8 == 0, "embedding_bwd: contiguous dy [..., E]");
   TORCH_CHECK(ids.is_contiguous() && ids.scalar_type() == at::kLong, "embedding_bwd: contiguous int64 ids");
   const at::DeviceGuard guard(dy.device());
-  auto dw32 = at::zeros({V, E}, dy.options().dtype(at::kFloat));
+  // fp32: the zeroed accumulator is the gradient; bf16 / f16: only the ids' rows are used (cleared
+  // in-kernel), the rest of the scratch accumulator is never touched
+  auto dw32 = dy.scalar_type() == at::kFloat ? at::zeros({V, E}, dy.options())
+                                             : at::empty({V, E}, dy.options().dtype(at::kFloat));
   at::Tensor dw = dy.scalar_type() == at::kFloat ? dw32 : at::empty({V, E}, dy.options());
   HYP_CHECK_HIP(hyp::embedding_backward(dtype_code(dy), ids.data_ptr<int64_t>(), dy.data_ptr(),
                                         dw32.data_ptr<float>(), dw.data_ptr(), n, (int)E, V, pad_idx, cur_stream()));

@@ -49,13 +49,31 @@ __global__ __launch_bounds__(256) void embed_bwd_atomic_k(const int64_t* __restr
   for (int c = lane; c < E; c += 64) atomicAdd(dst + c, ld1<T>(src + c));
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void cast_f32_k(const float* __restrict__ src, T* __restrict__ dst, int64_t n) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (i >= n) return;
-  float v[8];
-  Vec8<float>::load(src + i, v);
-  Vec8<T>::store(dst + i, v);
+// Touched rows only (one wave per token; a repeated id rewrites the same row with the same values):
+// ZERO = true clears the fp32 accumulator row before the atomics, ZERO = false rounds the finished
+// row into the weight-dtype gradient.  The accumulator's untouched rows are never initialized or
+// read, and the low-precision gradient is zero-filled by one memset — the two full [V, E] passes
+// of a dense fp32 buffer (zero fill + cast: ~55 us for GPT-2's 50257 x 768) become ~2 x 6 MB.
+template <typename T, bool ZERO>
+__global__ __launch_bounds__(256) void embed_rows_k(const int64_t* __restrict__ ids, float* __restrict__ dw32,
+                                                    T* __restrict__ dw, int64_t n, int E, int64_t V, int64_t pad_idx) {
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= n) return;
+  const int64_t id = ids[tok];
+  if (id < 0 || id >= V || id == pad_idx) return;
+  const int lane = threadIdx.x & 63;
+  float* row = dw32 + id * E;
+  for (int c = lane * 8; c < E; c += 64 * 8) {
+    float v[8];
+    if (ZERO) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      Vec8<float>::store(row + c, v);
+    } else {
+      Vec8<float>::load(row + c, v);
+      Vec8<T>::store(dw + id * E + c, v);
+    }
+  }
 }
 
 }  // namespace
@@ -71,20 +89,23 @@ hipError_t embedding_forward(int dtype, const int64_t* ids, const void* w, void*
   return hipGetLastError();
 }
 
-// dw32: [V, E] fp32 accumulator (ZEROED by the caller; it is the result itself when dtype is f32);
-// dw: the output in the weight dtype (ignored for f32)
+// dw32: [V, E] fp32 accumulator — for f32 it is the result itself and must be ZEROED by the caller;
+// for bf16 / f16 it may be uninitialized (only the rows of the ids are cleared, accumulated and
+// rounded into dw, which is zero-filled here)
 hipError_t embedding_backward(int dtype, const int64_t* ids, const void* dy, float* dw32, void* dw, int64_t n, int E,
                               int64_t V, int64_t pad_idx, hipStream_t st) {
   if (E % 8 != 0) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((n + 3) / 4)), block(256);
   HYP_DISPATCH_FLOAT(dtype, T, {
-    if (n > 0)
-      hipLaunchKernelGGL(embed_bwd_atomic_k<T>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, ids, (const T*)dy,
-                         dw32, n, E, V, pad_idx);
     if (dtype != kF32) {
-      const int64_t total = V * E;  // E % 8 == 0
-      hipLaunchKernelGGL(cast_f32_k<T>, dim3((unsigned)((total / 8 + 255) / 256)), dim3(256), 0, st, dw32, (T*)dw,
-                         total);
+      hipError_t e = hipMemsetAsync(dw, 0, (size_t)V * E * sizeof(T), st);
+      if (e != hipSuccess) return e;
+      if (n > 0) hipLaunchKernelGGL((embed_rows_k<T, true>), grid, block, 0, st, ids, dw32, (T*)dw, n, E, V, pad_idx);
     }
+    if (n > 0)
+      hipLaunchKernelGGL(embed_bwd_atomic_k<T>, grid, block, 0, st, ids, (const T*)dy, dw32, n, E, V, pad_idx);
+    if (dtype != kF32 && n > 0)
+      hipLaunchKernelGGL((embed_rows_k<T, false>), grid, block, 0, st, ids, dw32, (T*)dw, n, E, V, pad_idx);
   });
   return hipGetLastError();
 }
