@@ -5,6 +5,7 @@
 
 namespace hyp {
 void adam_set_streaming(int on);  // adam.hip
+void colsum_set_fin_lanes(int lanes);  // reduce.hip
 }
 
 namespace hypbind {
@@ -258,6 +259,8 @@ void register_norm_ops(pybind11::module& m) {
   }, "mean-squared error and its gradient 2(x - t)/n in one pass", pybind11::arg("x"), pybind11::arg("target"));
   m.def("colsum_set_fused", [](int64_t max_p) { hyp::colsum_set_fused((int)max_p); },
         "column sums: partial-row cap of the one-launch last-arriver combine (0 = two launches, the default)");
+  m.def("colsum_set_fin_lanes", [](int64_t lanes) { hyp::colsum_set_fin_lanes((int)lanes); },
+        "A/B: row lanes of the final column-sum combine (64 = 1024 threads, default; 16 = 256 threads)");
   m.def("colsum_set_act_wgs", [](int64_t wgs) { hyp::colsum_set_act_wgs((int)wgs); },
         "act_bwd_colsum: target workgroup count of the partial pass (A/B; default 1024)");
   m.def("column_sum", &column_sum, "column sums of a [.., N] matrix (bias gradients)", pybind11::arg("x"),

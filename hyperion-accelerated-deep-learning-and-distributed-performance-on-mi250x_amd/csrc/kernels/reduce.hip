@@ -123,7 +123,10 @@ __global__ __launch_bounds__(kThreads) void colsum_partial_k(const T* __restrict
 // round trips instead of P/8 (a thread-per-column combine over P = 256 partials was 11.5 us — 1.3 ms
 // per ViT-B/16 step over its ~100 bias / LayerNorm-parameter gradients), then a fixed-order LDS
 // sum over the 16 lanes (deterministic).
-constexpr int kFinLanes = 16;
+// row lanes of the final combine: 64 (1024 threads: four times the loads in flight of the original
+// 16, for combines whose N / 64 column blocks leave most CUs idle — a LayerNorm's dγ | dβ at
+// d = 768 is 24 workgroups); colsum_set_fin_lanes(16) restores the 256-thread kernel (A/B)
+int g_fin_lanes = 64;
 
 // Activation backward + bias-gradient partials in one pass (the FFN's first linear): dy = dh·act'(z)
 // is written once and its column sums are accumulated from registers — autograd ran the
@@ -209,10 +212,10 @@ __global__ __launch_bounds__(kThreads) void act_bwd_colsum_k(const T* __restrict
 
 // columns [0, split) go to out, [split, N) to out2 (its own dtype): a norm's dγ | dβ and the
 // producing linear's bias gradient (the linear's dtype) from one combine, no cast kernel after it
-template <typename O, typename O2 = O>
-__global__ __launch_bounds__(kThreads) void colsum_final_k(const float* __restrict__ part, int P, int N,
-                                                           O* __restrict__ out, int split = 1 << 30,
-                                                           O2* __restrict__ out2 = nullptr) {
+template <typename O, typename O2 = O, int kFinLanes = 64>
+__global__ __launch_bounds__(16 * kFinLanes) void colsum_final_k(const float* __restrict__ part, int P, int N,
+                                                                 O* __restrict__ out, int split = 1 << 30,
+                                                                 O2* __restrict__ out2 = nullptr) {
   __shared__ float red[kFinLanes][64];
   const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
   const int c = blockIdx.x * 64 + tx * 4;
@@ -291,15 +294,25 @@ void colsum_set_fused(int max_p) { g_colsum_fused_max_p = max_p < 0 ? 0 : (max_p
 
 int colsum_fused_max_p() { return g_colsum_fused_max_p; }
 
+void colsum_set_fin_lanes(int lanes) { g_fin_lanes = lanes == 16 ? 16 : 64; }
+
+template <typename O, typename O2>
+static void launch_final(const float* part, int P, int N, O* out, int split, O2* out2, hipStream_t st) {
+  const dim3 grid((N + 63) / 64);
+  if (g_fin_lanes == 16)
+    hipLaunchKernelGGL((colsum_final_k<O, O2, 16>), grid, dim3(256), 0, st, part, P, N, out, split, out2);
+  else
+    hipLaunchKernelGGL((colsum_final_k<O, O2, 64>), grid, dim3(1024), 0, st, part, P, N, out, split, out2);
+}
+
 hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dtype, hipStream_t st) {
   if (N % 4 != 0 || P < 1) return hipErrorInvalidValue;
-  const dim3 grid((N + 63) / 64);
   if (out_dtype == kF32)
-    hipLaunchKernelGGL(colsum_final_k<float>, grid, dim3(kThreads), 0, st, part, P, N, static_cast<float*>(out));
+    launch_final<float, float>(part, P, N, static_cast<float*>(out), 1 << 30, nullptr, st);
   else if (out_dtype == kBF16)
-    hipLaunchKernelGGL(colsum_final_k<bf16_t>, grid, dim3(kThreads), 0, st, part, P, N, static_cast<bf16_t*>(out));
+    launch_final<bf16_t, bf16_t>(part, P, N, static_cast<bf16_t*>(out), 1 << 30, nullptr, st);
   else if (out_dtype == kF16)
-    hipLaunchKernelGGL(colsum_final_k<f16_t>, grid, dim3(kThreads), 0, st, part, P, N, static_cast<f16_t*>(out));
+    launch_final<f16_t, f16_t>(part, P, N, static_cast<f16_t*>(out), 1 << 30, nullptr, st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -308,16 +321,12 @@ hipError_t colsum_combine(const float* part, int P, int N, void* out, int out_dt
 template <typename O>
 static hipError_t combine_split_to(const float* part, int P, int N, O* out, int split, void* out2, int dt2,
                                    hipStream_t st) {
-  const dim3 grid((N + 63) / 64);
   if (dt2 == kF32)
-    hipLaunchKernelGGL((colsum_final_k<O, float>), grid, dim3(kThreads), 0, st, part, P, N, out, split,
-                       static_cast<float*>(out2));
+    launch_final<O, float>(part, P, N, out, split, static_cast<float*>(out2), st);
   else if (dt2 == kBF16)
-    hipLaunchKernelGGL((colsum_final_k<O, bf16_t>), grid, dim3(kThreads), 0, st, part, P, N, out, split,
-                       static_cast<bf16_t*>(out2));
+    launch_final<O, bf16_t>(part, P, N, out, split, static_cast<bf16_t*>(out2), st);
   else if (dt2 == kF16)
-    hipLaunchKernelGGL((colsum_final_k<O, f16_t>), grid, dim3(kThreads), 0, st, part, P, N, out, split,
-                       static_cast<f16_t*>(out2));
+    launch_final<O, f16_t>(part, P, N, out, split, static_cast<f16_t*>(out2), st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

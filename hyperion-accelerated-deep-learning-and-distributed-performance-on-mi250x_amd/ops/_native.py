@@ -60,6 +60,8 @@ def _load():
         _MOD.conv_set_group(int(os.environ["HYPERION_CONV_GROUP"]))  # tile-order group sweep (A/B)
     if _MOD is not None and os.environ.get("HYPERION_ACT_COLSUM_WGS") and hasattr(_MOD, "colsum_set_act_wgs"):
         _MOD.colsum_set_act_wgs(int(os.environ["HYPERION_ACT_COLSUM_WGS"]))  # act_bwd_colsum grid (A/B)
+    if _MOD is not None and os.environ.get("HYPERION_COLSUM_FIN_LANES") and hasattr(_MOD, "colsum_set_fin_lanes"):
+        _MOD.colsum_set_fin_lanes(int(os.environ["HYPERION_COLSUM_FIN_LANES"]))  # final combine width (A/B)
     if _MOD is not None and os.environ.get("HYPERION_LN_WAVES") and hasattr(_MOD, "ln_set_waves"):
         _MOD.ln_set_waves(int(os.environ["HYPERION_LN_WAVES"]))  # LayerNorm grid sweep (A/B)
     if _MOD is not None and os.environ.get("HYPERION_ATTN_QSPLIT") and hasattr(_MOD, "attn_set_qsplit"):
