@@ -534,7 +534,24 @@ __global__ __launch_bounds__(256) void gemm_splitk_epi_k(const float* __restrict
     const int64_t off = i * 4;
     const int row = (int)(off / N), col = (int)(off % N);
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < splits; ++z) {
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {  // four slab loads in flight, summed in slice order (as before)
+      float4 q[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q[i] = *reinterpret_cast<const float4*>(part + (z + i) * slab + off);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[0] += q[i].x; v[1] += q[i].y; v[2] += q[i].z; v[3] += q[i].w;
+      }
+    }
+    if (splits - z >= 2) {
+      const float4 q0 = *reinterpret_cast<const float4*>(part + z * slab + off);
+      const float4 q1 = *reinterpret_cast<const float4*>(part + (z + 1) * slab + off);
+      v[0] += q0.x; v[1] += q0.y; v[2] += q0.z; v[3] += q0.w;
+      v[0] += q1.x; v[1] += q1.y; v[2] += q1.z; v[3] += q1.w;
+      z += 2;
+    }
+    if (z < splits) {
       const float4 q = *reinterpret_cast<const float4*>(part + z * slab + off);
       v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
     }
