@@ -9,6 +9,8 @@
 // 256-byte atomic runs), then one cast pass for bf16/f16 weights.  (A first, deterministic
 // sorted-run version serialized each id's run in one wave: the LM's pad token is ~1/3 of all
 // tokens, so one wave summed ~1300 rows — 1.35 ms per step; profiles/lm_r01.)
+#include <algorithm>
+
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -76,6 +78,13 @@ __global__ __launch_bounds__(256) void embed_rows_k(const int64_t* __restrict__ 
   }
 }
 
+// zero fill in 16-byte stores (a kernel rather than hipMemsetAsync: a memset issued while a stream
+// captures a segmented hipGraph was not replayed — the FSDP segmented step read stale gradient rows)
+__global__ __launch_bounds__(256) void zero16_k(uint4* __restrict__ p, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 }  // namespace
 
 hipError_t embedding_forward(int dtype, const int64_t* ids, const void* w, void* out, int64_t n, int E, int64_t V,
@@ -98,8 +107,9 @@ hipError_t embedding_backward(int dtype, const int64_t* ids, const void* dy, flo
   const dim3 grid((unsigned)((n + 3) / 4)), block(256);
   HYP_DISPATCH_FLOAT(dtype, T, {
     if (dtype != kF32) {
-      hipError_t e = hipMemsetAsync(dw, 0, (size_t)V * E * sizeof(T), st);
-      if (e != hipSuccess) return e;
+      const int64_t n16 = V * E * (int64_t)sizeof(T) / 16;  // E % 8 == 0: whole 16-byte chunks
+      hipLaunchKernelGGL(zero16_k, dim3((unsigned)std::min<int64_t>((n16 + 255) / 256, 8192)), block, 0, st,
+                         static_cast<uint4*>(dw), n16);
       if (n > 0) hipLaunchKernelGGL((embed_rows_k<T, true>), grid, block, 0, st, ids, dw32, (T*)dw, n, E, V, pad_idx);
     }
     if (n > 0)
