@@ -19,6 +19,7 @@
 #   bash scripts/gpu_suite.sh steps                      graphed model steps (WL="vitgraph vitselgraph ..."), one JSON each
 #   bash scripts/gpu_suite.sh final                      bench x2 + every README step row (one box, one call)
 #   bash scripts/gpu_suite.sh refresh                    README micro rows: matmul / STREAM, attention, LM head, fused-vs-eager
+#   bash scripts/gpu_suite.sh fp32                       fp32 path: three-loop rows native vs vendor, fp32 GEMM vs hipBLASLt, routes
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -163,6 +164,12 @@ refresh)
   echo ce ok
   PYTHONPATH=$PWD timeout -k 10 400 python -u -m hyperion.cli.bench_models --out "$out/fusion/x" --only fusion > "$out/fusion.log" 2>&1 || { tail -5 "$out/fusion.log"; exit 1; }
   ls "$out" "$out/hardware" "$out/fusion"
+  ;;
+fp32)
+  timeout -k 10 300 python -u scripts/fp32_step.py create_resnet50 1 10 > "$out/routes.txt" 2>&1 || { tail -5 "$out/routes.txt"; exit 1; }
+  timeout -k 10 600 python -u scripts/fp32_ab.py > "$out/three_loop_ab.jsonl" 2> "$out/three_loop_ab.err" || { tail -5 "$out/three_loop_ab.err"; exit 1; }
+  timeout -k 10 300 python -u scripts/f32_gemm_probe.py --short > "$out/gemm_probe.jsonl" 2> "$out/gemm_probe.err" || exit 1
+  head -3 "$out/routes.txt"; cut -c1-160 "$out/three_loop_ab.jsonl"
   ;;
 *)
   echo "unknown stage $stage"; exit 2
