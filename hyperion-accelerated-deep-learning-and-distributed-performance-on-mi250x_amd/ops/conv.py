@@ -715,6 +715,11 @@ def _conv_bn_eval(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor,
     dt = x.dtype
     if torch.is_autocast_enabled(x.device.type):
         dt = torch.get_autocast_dtype(x.device.type)
+    if dt == torch.float32:  # fp32: the BN folded into the fp32-MFMA GEMM (ops/conv_f32.py), when faster
+        from .conv_f32 import conv_bn_eval_f32
+
+        sc, sh = _eval_affine(bn, x.device)
+        return conv_bn_eval_f32(conv, bn, x, residual, sc, sh)
     if dt not in (torch.bfloat16, torch.float16):
         return None
     xc = x.to(dt) if x.dtype != dt else x

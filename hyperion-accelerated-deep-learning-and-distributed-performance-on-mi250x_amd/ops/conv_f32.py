@@ -201,3 +201,79 @@ class Conv2d(nn.Conv2d):
 def conv2d_f32_reference(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride, padding) -> torch.Tensor:
     """The oracle of the GPU tests (fp64 on the CPU)."""
     return F.conv2d(x.double().cpu(), w.double().cpu(), None if b is None else b.double().cpu(), stride, padding)
+
+
+# ---- inference: conv -> BN(running stats) -> (+ residual) -> (ReLU) with the BN folded -------------------
+# (the filter rows scaled by γ/σ, the shift as the GEMM's bias, ReLU in its epilogue when there is no
+# residual): one im2col + one GEMM per layer instead of a conv, a BN pass and a ReLU pass.  Routed
+# per geometry against the vendor conv + BN the same way as training (forward timing only).
+_EVAL_ROUTE: Dict[tuple, bool] = {}
+
+
+def _folded(conv: nn.Conv2d, sc: torch.Tensor, sh: torch.Tensor, kp: int):
+    w = conv.weight
+    key = (w.data_ptr(), w._version, sc.data_ptr(), sh.data_ptr(),
+           None if conv.bias is None else (conv.bias.data_ptr(), conv.bias._version))
+    cache = conv.__dict__.get("_hyp_f32_folded")
+    if cache is not None and cache[0] == key:
+        return cache[1], cache[2]
+    with torch.no_grad():
+        wm = _wmat(w * sc.view(-1, 1, 1, 1), kp)
+        b = sh + conv.bias.float() * sc if conv.bias is not None else sh
+        b = b.contiguous()
+    conv.__dict__["_hyp_f32_folded"] = (key, wm, b)
+    return wm, b
+
+
+def _eval_native(conv, x, residual, act, sc, sh):
+    C = _native.native()
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    nb, cin, h, wd = x.shape
+    co, _, r, s = conv.weight.shape
+    (sh_, sw), (ph, pw) = tuple(conv.stride), tuple(conv.padding)
+    ho, wo = (h + 2 * ph - r) // sh_ + 1, (wd + 2 * pw - s) // sw + 1
+    kp = (r * s * cin + 3) // 4 * 4
+    wm, bias = _folded(conv, sc, sh, kp)
+    direct = r == 1 and s == 1 and sh_ == 1 and sw == 1 and ph == 0 and pw == 0 and cin % 4 == 0
+    cols = x.permute(0, 2, 3, 1).reshape(nb * h * wd, cin) if direct else C.im2col_f32(x, r, s, sh_, sw, ph, pw, kp)
+    y = torch.empty((nb, co, ho, wo), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    gemm(cols, wm, bias=bias, relu=bool(act) and residual is None, out=y.permute(0, 2, 3, 1).view(nb * ho * wo, co))
+    if residual is not None:
+        y.add_(residual)
+        if act:
+            y.relu_()
+    return y
+
+
+def conv_bn_eval_f32(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor],
+                     sc: torch.Tensor, sh: torch.Tensor) -> Optional[torch.Tensor]:
+    """fp32 inference conv + BN (+ residual) (+ ReLU) with the BN folded (None: the caller's path)."""
+    if not f32_conv_ok(x, conv) or torch.is_grad_enabled():
+        return None
+    act = bool(getattr(bn, "act", False))
+    if residual is not None and (residual.dtype != x.dtype or residual.shape[0] != x.shape[0]):
+        return None
+    key = (tuple(x.shape), tuple(conv.weight.shape), tuple(conv.stride), tuple(conv.padding), residual is not None)
+    c = _EVAL_ROUTE.get(key) if ROUTE == "auto" else ROUTE == "native"
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            c = True
+        else:
+            from .gemm import _time
+
+            def vendor():
+                y = F.batch_norm(F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding), bn.running_mean,
+                                 bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+                if residual is not None:
+                    y = y + residual
+                return F.relu(y) if act else y
+
+            _eval_native(conv, x, residual, act, sc, sh)
+            vendor()
+            c = _time(lambda: _eval_native(conv, x, residual, act, sc, sh), reps=3) < _time(vendor, reps=3)
+            _EVAL_ROUTE[key] = c
+    if not c:
+        return None
+    _native.count("conv_bn_eval_f32")
+    return _eval_native(conv, x, residual, act, sc, sh)

@@ -172,3 +172,28 @@ def test_conv2d_f32_auto_route_times_both_and_caches(monkeypatch):
     ref = F.conv2d(x.detach(), conv.weight.detach(), None, 1, 1)
     torch.testing.assert_close(y1, ref, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(y2, y1)
+
+
+def test_resnet18_fp32_eval_bn_folded_matches_vendor():
+    """Inference with the BN folded into the fp32 GEMM (conv_bn_eval_f32) vs conv + BN on the vendor ops."""
+    from hyperion.models import resnet18
+    from hyperion.ops import _native, conv_f32
+
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    for mod in m.modules():  # non-trivial running statistics
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+    m.eval()
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv_f32.ENABLED = False
+        try:
+            ref = m(x)
+        finally:
+            conv_f32.ENABLED = True
+        _native.reset_counters()
+        out = m(x)
+    assert _native.counters().get("conv_bn_eval_f32", 0) >= 16, _native.counters()
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * ref.abs().max().item())
