@@ -63,8 +63,9 @@ def parse(argv=None):
                          "(the N>1 schedule's collectives at world 1)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--channels-last", type=int, default=1)
-    ap.add_argument("--loss", default="torch", choices=["torch", "fused"],
-                    help="MSE loss: torch's ops or Hyperion's one-pass kernel (ops.losses)")
+    ap.add_argument("--loss", default="torch", choices=["torch", "fused", "head"],
+                    help="MSE loss: torch's ops, Hyperion's one-pass kernel, or 'head': the classifier fc and "
+                         "the MSE as one fused native forward + one backward launch (ops.losses.LinearMSELoss)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--smi", type=int, default=0, help="sample amd-smi power / clocks during the timed steps")
     return ap.parse_args(argv)
@@ -148,6 +149,12 @@ def main(argv=None) -> int:
     from hyperion.ops.losses import MSELoss
 
     loss_fn = MSELoss() if (args.kernels != "torch" and args.loss == "fused") else nn.MSELoss()
+    if args.kernels != "torch" and args.loss == "head" and dev.type == "cuda":
+        from hyperion.ops.losses import LinearMSELoss
+
+        net = model.module if hasattr(model, "module") else model
+        net.head_in_loss = True  # the model returns pooled features; the loss applies fc (same math)
+        loss_fn = LinearMSELoss(net.fc)
 
     B = args.batch
     x = torch.rand(B, 3, args.image, args.image, device=dev).to(memory_format=mf)
@@ -221,7 +228,8 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "image": args.image,
                 "parallelism": f"dp{n_gpus}",
-                "loss": "MSE vs rand(B,1000) (reference benchmark_model)",
+                "loss": "MSE vs rand(B,1000) (reference benchmark_model)" + (
+                    "; fc + MSE fused (linear_mse.hip)" if args.loss == "head" else ""),
                 "optimizer": "Adam lr=1e-3 (hyperion FusedAdam, multi-tensor)",
                 "hipgraph": use_graph,
                 "ddp_schedule": (None if (n_gpus == 1 and not args.ddp_world1) else

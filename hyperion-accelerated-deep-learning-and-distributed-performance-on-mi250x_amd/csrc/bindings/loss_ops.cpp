@@ -1,4 +1,6 @@
 // Torch bindings: fused softmax cross-entropy (forward + in-place backward).
+#include <map>
+
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
@@ -32,6 +34,67 @@ std::vector<at::Tensor> ce_fwd_bwd(at::Tensor& logits, const at::Tensor& target,
                                            lse.data_ptr<float>(), ptr_or_null<float>(scale), (float)scale_mul,
                                            ignore_index, write_grad ? 1 : 0, cur_stream(), ptr_or_null<float>(bias)));
   return {loss, lse};
+}
+
+// ---- classifier head + MSE (linear_mse.hip) -----------------------------------------------------
+void check_head(const at::Tensor& x, const at::Tensor& w, const char* who) {
+  HYP_CHECK_CUDA_TENSOR(x);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.is_contiguous() && w.is_contiguous() && x.size(1) == w.size(1) &&
+                  x.scalar_type() == w.scalar_type() && w.device() == x.device() && x.size(0) >= 1 &&
+                  x.size(0) <= 64 && x.size(1) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              who, ": contiguous 16-byte aligned x [M <= 64, K % 8 == 0] and w [N, K] of one dtype and device");
+}
+
+// 4096 zeroed int32 tickets per device (forward / backward regions), reset by the kernels
+int* head_tickets(const at::Tensor& x) {
+  static std::map<int, at::Tensor> tickets;
+  auto& tk = tickets[x.get_device()];
+  if (!tk.defined()) tk = at::zeros({4096}, x.options().dtype(at::kInt));
+  return tk.data_ptr<int>();
+}
+
+// (loss fp32 scalar, dz fp32 [M, N])
+std::vector<at::Tensor> linear_mse_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                                       const at::Tensor& y) {
+  check_head(x, w, "linear_mse_fwd");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(y.scalar_type() == at::kFloat && y.is_contiguous() && y.dim() == 2 && y.size(0) == M && y.size(1) == N &&
+                  y.device() == x.device(), "linear_mse_fwd: y must be a contiguous fp32 [M, N]");
+  if (b.has_value() && b->defined())
+    TORCH_CHECK(b->scalar_type() == x.scalar_type() && b->is_contiguous() && b->numel() == N && b->device() == x.device(),
+                "linear_mse_fwd: bias must be a contiguous [N] of x's dtype");
+  const at::DeviceGuard guard(x.device());
+  auto fopt = x.options().dtype(at::kFloat);
+  auto loss = at::empty({}, fopt);
+  auto dz = at::empty({M, N}, fopt);
+  auto ws = at::empty({hyp::linear_mse_workspace((int)M, (int)N, (int)K)}, fopt);
+  HYP_CHECK_HIP(hyp::linear_mse_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), vptr_or_null(b), y.data_ptr<float>(),
+                                    (int)M, (int)N, (int)K, dz.data_ptr<float>(), ws.data_ptr<float>(),
+                                    head_tickets(x), loss.data_ptr<float>(), cur_stream()));
+  return {loss, dz};
+}
+
+// (dx [M, K], dw [N, K], db [N] or undefined) scaled by the fp32 device scalar go
+std::vector<at::Tensor> linear_mse_bwd(const at::Tensor& dz, const at::Tensor& go, const at::Tensor& x,
+                                       const at::Tensor& w, bool with_bias) {
+  check_head(x, w, "linear_mse_bwd");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(dz.scalar_type() == at::kFloat && dz.is_contiguous() && dz.numel() == M * N && go.numel() == 1 &&
+                  go.scalar_type() == at::kFloat && go.device() == x.device() && dz.device() == x.device(),
+              "linear_mse_bwd: fp32 dz [M, N] and a 1-element fp32 go");
+  const at::DeviceGuard guard(x.device());
+  auto goc = go.contiguous();
+  auto ws = at::empty({hyp::linear_mse_workspace((int)M, (int)N, (int)K)}, x.options().dtype(at::kFloat));
+  auto dx = at::empty_like(x);
+  auto dw = at::empty_like(w);
+  at::Tensor db;
+  if (with_bias) db = at::empty({N}, w.options());
+  HYP_CHECK_HIP(hyp::linear_mse_bwd(dtype_code(x), dz.data_ptr<float>(), goc.data_ptr<float>(), x.data_ptr(),
+                                    w.data_ptr(), (int)M, (int)N, (int)K, dx.data_ptr(), dw.data_ptr(),
+                                    with_bias ? db.data_ptr() : nullptr, ws.data_ptr<float>(), head_tickets(x),
+                                    cur_stream()));
+  return {dx, dw, db};
 }
 
 // ---- embedding ---------------------------------------------------------------------------------
@@ -70,6 +133,10 @@ at::Tensor embedding_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t V,
 
 void register_loss_ops(pybind11::module& m) {
   m.def("embedding_fwd", &embedding_fwd, "token embedding gather");
+  m.def("linear_mse_fwd", &linear_mse_fwd, "classifier head + MSE forward (loss, fp32 dz)", pybind11::arg("x"),
+        pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("y"));
+  m.def("linear_mse_bwd", &linear_mse_bwd, "classifier head + MSE backward (dx, dw, db) in one launch",
+        pybind11::arg("dz"), pybind11::arg("go"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("with_bias"));
   m.def("embedding_bwd", &embedding_bwd, "dense embedding gradient (fp32 atomic accumulate + cast)");
   m.def("ce_fwd_bwd", &ce_fwd_bwd, "in-place softmax cross-entropy forward+backward", pybind11::arg("logits"),
         pybind11::arg("target"), pybind11::arg("scale"), pybind11::arg("scale_mul"), pybind11::arg("ignore_index"),

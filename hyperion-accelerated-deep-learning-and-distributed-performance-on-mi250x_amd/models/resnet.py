@@ -113,6 +113,9 @@ class ResNet(nn.Module):
         # vs hipBLASLt's one — HYPERION_RESNET_FC=native opts in)
         fc_cls = Linear if os.environ.get("HYPERION_RESNET_FC", "torch") == "native" else nn.Linear
         self.fc = fc_cls(512 * block.expansion, num_classes)
+        # head_in_loss: forward returns the pooled features and the loss applies fc
+        # (ops.losses.LinearMSELoss: the fused classifier + MSE of the step benchmark)
+        self.head_in_loss = False
 
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
@@ -150,7 +153,7 @@ class ResNet(nn.Module):
         with _native.zero_scope(self, "forward", x.device):
             x = self.forward_features(x)
             x = torch.flatten(self.avgpool(x), 1)
-            return self.fc(x)
+            return x if self.head_in_loss else self.fc(x)
 
     def _bottom(self, x: torch.Tensor) -> torch.Tensor:
         with _native.zero_scope(self, "bottom", x.device):
@@ -159,7 +162,8 @@ class ResNet(nn.Module):
     def _top(self, h: torch.Tensor) -> torch.Tensor:
         with _native.zero_scope(self, "top", h.device):
             x = self.layer4(self.layer3(self.layer2(h)))
-            return self.fc(torch.flatten(self.avgpool(x), 1))
+            x = torch.flatten(self.avgpool(x), 1)
+            return x if self.head_in_loss else self.fc(x)
 
     def graph_stages(self):
         """``forward(x) == top(bottom(x))``, cut after layer1: 99% of the gradient bytes (layer2-4,
