@@ -63,7 +63,7 @@ def parse(argv=None):
                          "(the N>1 schedule's collectives at world 1)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--channels-last", type=int, default=1)
-    ap.add_argument("--loss", default="torch", choices=["torch", "fused", "head"],
+    ap.add_argument("--loss", default="head", choices=["torch", "fused", "head"],
                     help="MSE loss: torch's ops, Hyperion's one-pass kernel, or 'head': the classifier fc and "
                          "the MSE as one fused native forward + one backward launch (ops.losses.LinearMSELoss)")
     ap.add_argument("--json-out", default=None)

@@ -42,62 +42,71 @@ __device__ __forceinline__ float round_to(float v) {
   return ld1<T>(&t);
 }
 
-// last arriver of a group of `count` workgroups counting in on *ticket (release before, acquire
-// after); the caller resets the ticket
-__device__ __forceinline__ bool last_arriver(int* ticket, int count) {
-  __shared__ int s_last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1) == count - 1;
-  __syncthreads();
-  const bool last = s_last;
-  if (last) __threadfence();
-  return last;
-}
-
 template <typename T>
 __global__ __launch_bounds__(kLmT) void linear_mse_fwd_k(const T* __restrict__ X, const T* __restrict__ W,
                                                          const T* __restrict__ b, const float* __restrict__ y, int M,
-                                                         int N, int K, float* __restrict__ zp, float* __restrict__ dz,
-                                                         float* __restrict__ part, int* __restrict__ tickets,
-                                                         float* __restrict__ loss) {
+                                                         int N, int K, float* __restrict__ zp) {
   __shared__ float xs[kLmMaxM][kLmKC + 4];
   __shared__ float ws[kLmN][kLmKC + 4];
-  __shared__ float red[kLmT / 64];
   const int t = threadIdx.x, nl = t & (kLmN - 1), mg = t >> 4;
-  const int tile = blockIdx.x, n0 = tile * kLmN, nb = gridDim.x;
+  const int n0 = blockIdx.x * kLmN;
   const int kper = (K + kLmKS * 8 - 1) / (kLmKS * 8) * 8;
   const int kbeg = blockIdx.y * kper, kend = min(K, kbeg + kper);
   float acc[kLmMaxM / 16] = {0.f, 0.f, 0.f, 0.f};
+  // one chunk's global loads all in flight at once (<= 4 X vectors + 1 weight vector per thread),
+  // and the next chunk's issued before this chunk's FMAs: one exposed memory round trip per slice
+  float xr[kLmMaxM * kLmKC / 8 / kLmT][8], wr[8];
+  auto gload = [&](int k0) {
+    const int kv = min(kLmKC, kend - k0) / 8;
+#pragma unroll
+    for (int i = 0; i < kLmMaxM * kLmKC / 8 / kLmT; ++i) {
+      const int v = t + i * kLmT;
+      if (v < M * kv) {
+        const int m = v / kv, kk = (v - m * kv) * 8;
+        Vec8<T>::load(X + (int64_t)m * K + k0 + kk, xr[i]);
+      }
+    }
+    if (t < kLmN * kv) {
+      const int r = t / kv, kk = (t - r * kv) * 8;
+      if (n0 + r < N) Vec8<T>::load(W + (int64_t)(n0 + r) * K + k0 + kk, wr);
+      else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wr[e] = 0.f;
+    }
+  };
+  auto lstore = [&](int kv) {
+#pragma unroll
+    for (int i = 0; i < kLmMaxM * kLmKC / 8 / kLmT; ++i) {
+      const int v = t + i * kLmT;
+      if (v < M * kv) {
+        const int m = v / kv, kk = (v - m * kv) * 8;
+        *reinterpret_cast<float4*>(&xs[m][kk]) = make_float4(xr[i][0], xr[i][1], xr[i][2], xr[i][3]);
+        *reinterpret_cast<float4*>(&xs[m][kk + 4]) = make_float4(xr[i][4], xr[i][5], xr[i][6], xr[i][7]);
+      }
+    }
+    if (t < kLmN * kv) {
+      const int r = t / kv, kk = (t - r * kv) * 8;
+      *reinterpret_cast<float4*>(&ws[r][kk]) = make_float4(wr[0], wr[1], wr[2], wr[3]);
+      *reinterpret_cast<float4*>(&ws[r][kk + 4]) = make_float4(wr[4], wr[5], wr[6], wr[7]);
+    }
+  };
+  if (kbeg < kend) gload(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += kLmKC) {
     const int kv = min(kLmKC, kend - k0) / 8;  // 8-element vectors in this chunk (K % 8 == 0)
     __syncthreads();
-    for (int v = t; v < M * kv; v += kLmT) {
-      const int m = v / kv, kk = (v - m * kv) * 8;
-      float f[8];
-      Vec8<T>::load(X + (int64_t)m * K + k0 + kk, f);
-      *reinterpret_cast<float4*>(&xs[m][kk]) = make_float4(f[0], f[1], f[2], f[3]);
-      *reinterpret_cast<float4*>(&xs[m][kk + 4]) = make_float4(f[4], f[5], f[6], f[7]);
-    }
-    for (int v = t; v < kLmN * kv; v += kLmT) {
-      const int r = v / kv, kk = (v - r * kv) * 8;
-      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (n0 + r < N) Vec8<T>::load(W + (int64_t)(n0 + r) * K + k0 + kk, f);
-      *reinterpret_cast<float4*>(&ws[r][kk]) = make_float4(f[0], f[1], f[2], f[3]);
-      *reinterpret_cast<float4*>(&ws[r][kk + 4]) = make_float4(f[4], f[5], f[6], f[7]);
-    }
+    lstore(kv);
     __syncthreads();
+    if (k0 + kLmKC < kend) gload(k0 + kLmKC);
     const int kc = kv * 8;
 #pragma unroll 4
     for (int kk = 0; kk < kc; kk += 4) {
       const float4 w4 = *reinterpret_cast<const float4*>(&ws[nl][kk]);
 #pragma unroll
       for (int j = 0; j < kLmMaxM / 16; ++j) {
-        const int m = mg + 16 * j;
-        if (m < M) {
-          const float4 x4 = *reinterpret_cast<const float4*>(&xs[m][kk]);
-          acc[j] = fmaf(x4.x, w4.x, fmaf(x4.y, w4.y, fmaf(x4.z, w4.z, fmaf(x4.w, w4.w, acc[j]))));
-        }
+        // rows past M re-read row M - 1 (results dropped): no branch, so the LDS reads batch
+        const int m = min(mg + 16 * j, M - 1);
+        const float4 x4 = *reinterpret_cast<const float4*>(&xs[m][kk]);
+        acc[j] = fmaf(x4.x, w4.x, fmaf(x4.y, w4.y, fmaf(x4.z, w4.z, fmaf(x4.w, w4.w, acc[j]))));
       }
     }
   }
@@ -108,7 +117,16 @@ __global__ __launch_bounds__(kLmT) void linear_mse_fwd_k(const T* __restrict__ X
     const int m = mg + 16 * j;
     if (m < M && n < N) zp[((int64_t)blockIdx.y * M + m) * N + n] = acc[j];
   }
-  if (!last_arriver(tickets + tile, kLmKS)) return;
+}
+
+// the tile's K slices summed in order, bias, compute-dtype rounding, dz and the squared-error partial
+template <typename T>
+__global__ __launch_bounds__(kLmT) void linear_mse_epi_k(const float* __restrict__ zp, const T* __restrict__ b,
+                                                         const float* __restrict__ y, int M, int N,
+                                                         float* __restrict__ dz, float* __restrict__ part) {
+  __shared__ float red[kLmT / 64];
+  const int t = threadIdx.x, nl = t & (kLmN - 1), mg = t >> 4;
+  const int tile = blockIdx.x, n = tile * kLmN + nl;
   const float inv = 1.f / ((float)M * (float)N);
   const float bv = (b != nullptr && n < N) ? ld1<T>(b + n) : 0.f;
   float lp = 0.f;
@@ -129,29 +147,23 @@ __global__ __launch_bounds__(kLmT) void linear_mse_fwd_k(const T* __restrict__ X
   for (int o = 32; o > 0; o >>= 1) lp += __shfl_xor(lp, o, 64);
   if ((t & 63) == 0) red[t >> 6] = lp;
   __syncthreads();
-  if (t == 0) {
-    part[tile] = (red[0] + red[1]) + (red[2] + red[3]);
-    tickets[tile] = 0;
-  }
-  // the last tile sums the tiles' partials in order
-  if (!last_arriver(tickets + nb, nb)) return;
-  if (t < 64) {
-    float s = 0.f;
-    for (int p = t; p < nb; p += 64) s += part[p];
+  if (t == 0) part[tile] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// loss = sum of the tile partials (fixed order) / (M N); one wave
+__global__ __launch_bounds__(64) void linear_mse_loss_k(const float* __restrict__ part, int nb, float inv,
+                                                        float* __restrict__ loss) {
+  float s = 0.f;
+  for (int p = threadIdx.x; p < nb; p += 64) s += part[p];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (t == 0) {
-      *loss = s * inv;
-      tickets[nb] = 0;
-    }
-  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (threadIdx.x == 0) *loss = s * inv;
 }
 
 template <typename T>
 __global__ __launch_bounds__(kLmT) void linear_mse_bwd_k(const float* __restrict__ dz, const float* __restrict__ go,
                                                          const T* __restrict__ X, const T* __restrict__ W, int M,
                                                          int N, int K, int NBW, int NS, float* __restrict__ dxp,
-                                                         int* __restrict__ tickets, T* __restrict__ dX,
                                                          T* __restrict__ dW, T* __restrict__ db) {
   __shared__ float dzs[kLmMaxM][kLmNC + 1];
   __shared__ float ws[kLmNC][kLmDxK + 4];
@@ -244,23 +256,28 @@ __global__ __launch_bounds__(kLmT) void linear_mse_bwd_k(const float* __restrict
       if (m < M) Vec8<float>::store(dxp + ((int64_t)ns * M + m) * K + k0 + kg, acc[r]);
     }
   }
-  if (!last_arriver(tickets + kt, NS)) return;
-  if (kin) {
+}
+
+// dX[m, k] = sum of the N-slice partials in slice order (deterministic)
+template <typename T>
+__global__ __launch_bounds__(kLmT) void linear_mse_dx_k(const float* __restrict__ dxp, int M, int K, int NS,
+                                                        T* __restrict__ dX) {
+  const int t = threadIdx.x, kg = (t & 7) * 8, mg = t >> 3;
+  const int k0 = blockIdx.x * kLmDxK;
+  if (k0 + kg >= K) return;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int m = mg + 32 * r;
-      if (m >= M) continue;
-      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < NS; ++q) {  // slice order: deterministic
-        float v[8];
-        Vec8<float>::load(dxp + ((int64_t)q * M + m) * K + k0 + kg, v);
+  for (int r = 0; r < 2; ++r) {
+    const int m = mg + 32 * r;
+    if (m >= M) continue;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < NS; ++q) {
+      float v[8];
+      Vec8<float>::load(dxp + ((int64_t)q * M + m) * K + k0 + kg, v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s[e] += v[e];
-      }
-      Vec8<T>::store(dX + (int64_t)m * K + k0 + kg, s);
+      for (int e = 0; e < 8; ++e) s[e] += v[e];
     }
+    Vec8<T>::store(dX + (int64_t)m * K + k0 + kg, s);
   }
-  if (t == 0) tickets[kt] = 0;
 }
 
 }  // namespace
@@ -281,8 +298,12 @@ hipError_t linear_mse_fwd(int dtype, const void* X, const void* W, const void* b
   float* part = ws + (int64_t)kLmKS * M * N;
   HYP_DISPATCH_FLOAT(dtype, T, {
     hipLaunchKernelGGL(linear_mse_fwd_k<T>, dim3(nb, kLmKS), dim3(kLmT), 0, st, static_cast<const T*>(X),
-                       static_cast<const T*>(W), static_cast<const T*>(b), y, M, N, K, ws, dz, part, tickets, loss);
+                       static_cast<const T*>(W), static_cast<const T*>(b), y, M, N, K, ws);
+    hipLaunchKernelGGL(linear_mse_epi_k<T>, dim3(nb), dim3(kLmT), 0, st, ws, static_cast<const T*>(b), y, M, N, dz,
+                       part);
   });
+  hipLaunchKernelGGL(linear_mse_loss_k, dim3(1), dim3(64), 0, st, part, nb, 1.f / ((float)M * (float)N), loss);
+  (void)tickets;  // reserved: the in-kernel last-arriver combines measured slower (agent-scope fences)
   return hipGetLastError();
 }
 
@@ -293,9 +314,10 @@ hipError_t linear_mse_bwd(int dtype, const float* dz, const float* go, const voi
     return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     hipLaunchKernelGGL(linear_mse_bwd_k<T>, dim3(nbw + kt * ns), dim3(kLmT), 0, st, dz, go, static_cast<const T*>(X),
-                       static_cast<const T*>(W), M, N, K, nbw, ns, ws, tickets + kLmTicketRegion,
-                       static_cast<T*>(dX), static_cast<T*>(dW), static_cast<T*>(db));
+                       static_cast<const T*>(W), M, N, K, nbw, ns, ws, static_cast<T*>(dW), static_cast<T*>(db));
+    hipLaunchKernelGGL(linear_mse_dx_k<T>, dim3(kt), dim3(kLmT), 0, st, ws, M, K, ns, static_cast<T*>(dX));
   });
+  (void)tickets;
   return hipGetLastError();
 }
 
