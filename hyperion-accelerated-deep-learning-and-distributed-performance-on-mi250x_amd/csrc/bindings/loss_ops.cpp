@@ -1,6 +1,4 @@
 // Torch bindings: fused softmax cross-entropy (forward + in-place backward).
-#include <map>
-
 #include "bindings/common.h"
 #include "bindings/registry.h"
 
@@ -46,14 +44,6 @@ void check_head(const at::Tensor& x, const at::Tensor& w, const char* who) {
               who, ": contiguous 16-byte aligned x [M <= 64, K % 8 == 0] and w [N, K] of one dtype and device");
 }
 
-// 4096 zeroed int32 tickets per device (forward / backward regions), reset by the kernels
-int* head_tickets(const at::Tensor& x) {
-  static std::map<int, at::Tensor> tickets;
-  auto& tk = tickets[x.get_device()];
-  if (!tk.defined()) tk = at::zeros({4096}, x.options().dtype(at::kInt));
-  return tk.data_ptr<int>();
-}
-
 // (loss fp32 scalar, dz fp32 [M, N])
 std::vector<at::Tensor> linear_mse_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
                                        const at::Tensor& y) {
@@ -71,7 +61,7 @@ std::vector<at::Tensor> linear_mse_fwd(const at::Tensor& x, const at::Tensor& w,
   auto ws = at::empty({hyp::linear_mse_workspace((int)M, (int)N, (int)K)}, fopt);
   HYP_CHECK_HIP(hyp::linear_mse_fwd(dtype_code(x), x.data_ptr(), w.data_ptr(), vptr_or_null(b), y.data_ptr<float>(),
                                     (int)M, (int)N, (int)K, dz.data_ptr<float>(), ws.data_ptr<float>(),
-                                    head_tickets(x), loss.data_ptr<float>(), cur_stream()));
+                                    loss.data_ptr<float>(), cur_stream()));
   return {loss, dz};
 }
 
@@ -92,8 +82,7 @@ std::vector<at::Tensor> linear_mse_bwd(const at::Tensor& dz, const at::Tensor& g
   if (with_bias) db = at::empty({N}, w.options());
   HYP_CHECK_HIP(hyp::linear_mse_bwd(dtype_code(x), dz.data_ptr<float>(), goc.data_ptr<float>(), x.data_ptr(),
                                     w.data_ptr(), (int)M, (int)N, (int)K, dx.data_ptr(), dw.data_ptr(),
-                                    with_bias ? db.data_ptr() : nullptr, ws.data_ptr<float>(), head_tickets(x),
-                                    cur_stream()));
+                                    with_bias ? db.data_ptr() : nullptr, ws.data_ptr<float>(), cur_stream()));
   return {dx, dw, db};
 }
 

@@ -388,14 +388,14 @@ int colsum_fused_max_p();
 hipError_t mse_fwd_bwd(int dtype, const void* x, const float* t, int64_t n, float* loss, void* g, hipStream_t st);
 // classifier head + MSE (linear_mse.hip), M <= 64, K % 8 == 0.  Forward writes the fp32 gradient
 // dz [M, N] and the loss; backward writes dX [M, K], dW [N, K] and db [N] (optional) scaled by the
-// device scalar go.  ws: linear_mse_workspace(M, N, K) floats; tickets: 4096 zeroed int32 (reset
-// by the kernels: graph-replay safe)
+// device scalar go.  ws: linear_mse_workspace(M, N, K) floats (slice partials, combined by their
+// own launches in a fixed order: deterministic)
 int linear_mse_partials(int N);
 int64_t linear_mse_workspace(int M, int N, int K);
 hipError_t linear_mse_fwd(int dtype, const void* X, const void* W, const void* b, const float* y, int M, int N, int K,
-                          float* dz, float* ws, int* tickets, float* loss, hipStream_t st);
+                          float* dz, float* ws, float* loss, hipStream_t st);
 hipError_t linear_mse_bwd(int dtype, const float* dz, const float* go, const void* X, const void* W, int M, int N,
-                          int K, void* dX, void* dW, void* db, float* ws, int* tickets, hipStream_t st);
+                          int K, void* dX, void* dW, void* db, float* ws, hipStream_t st);
 // tickets (non-null): ceil(N / 512) zeroed int32 slots — the combine runs in the same launch (the
 // last-arriving block of each column slab; the slots are reset to zero on exit)
 hipError_t column_sum(int dtype, const void* x, int64_t M, int N, void* out, int out_dtype, float* part, int P,

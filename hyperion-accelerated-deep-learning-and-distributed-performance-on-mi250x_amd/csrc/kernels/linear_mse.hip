@@ -7,17 +7,20 @@
 // reduce) for only 0.4 GFLOP.  Here:
 //
 // * linear_mse_fwd_k: grid = (N / 16 column tiles, 4 K slices) — ~250 workgroups for the ResNet
-//   head; X and the tile's 16 weight rows staged through LDS as fp32 in 128-deep K chunks, 4 rows
-//   x 1 column per thread, fp32 slice partials.  The tile's last-arriving slice (agent-scope
-//   release / acquire ticket, reset on exit: graph-replay safe) sums the slices in order, rounds z
-//   to the compute dtype (the bf16 logits of the torch path), writes dz = 2 (z - y) / (M N) in
-//   fp32 and the tile's squared-error partial; the last tile sums those in order — deterministic.
+//   head; X and the tile's 16 weight rows staged through LDS as fp32 in 128-deep K chunks (the
+//   next chunk's loads in flight during this chunk's FMAs), 4 rows x 1 column per thread, fp32
+//   slice partials.  linear_mse_epi_k sums a tile's slices in order, rounds z to the compute dtype
+//   (the bf16 logits of the torch path), writes dz = 2 (z - y) / (M N) in fp32 and the tile's
+//   squared-error partial; linear_mse_loss_k sums those in order — deterministic.
 // * linear_mse_bwd_k: ONE launch for all three gradients, scaled by the incoming loss gradient
 //   (a device scalar, so a captured step replays with whatever the loss scaler holds):
 //   workgroups [0, N / 8) own 8 columns each and write dW (8 x K, 8 k per thread, 8 rows' loads
 //   in flight) and db directly; the other (K / 64) x (N / 112) workgroups each stage 112 weight
-//   rows x 64 columns and the matching dz block in LDS, write an fp32 dX partial, and the last
-//   N slice of each column block sums the partials in order.
+//   rows x 64 columns and the matching dz block in LDS and write an fp32 dX partial, which
+//   linear_mse_dx_k sums in slice order.
+// The combines are separate launches on purpose: an in-kernel last-arriver combine needs an
+// agent-scope release fence per workgroup (an L2 write-back on gfx950) and measured ~50 us slower
+// per step (fwd 72 + bwd 70 us vs 21 + 15 us + three ~5 us combines; profiles/r06/linear_mse/).
 #include "hyp_common.h"
 #include "hyp_kernels.h"
 
@@ -33,7 +36,6 @@ constexpr int kLmNW = 8;         // dW columns per backward workgroup
 constexpr int kLmDxK = 64;       // dX columns per backward workgroup
 constexpr int kLmNC = 112;       // dX: weight rows (dz columns) per N slice, staged in LDS
 constexpr int kLmMaxNS = 16;     // dX: N slices cap
-constexpr int kLmTicketRegion = 2048;  // tickets: [0, 2048) forward, [2048, 4096) backward
 
 template <typename T>
 __device__ __forceinline__ float round_to(float v) {
@@ -292,9 +294,9 @@ int64_t linear_mse_workspace(int M, int N, int K) {
 }
 
 hipError_t linear_mse_fwd(int dtype, const void* X, const void* W, const void* b, const float* y, int M, int N, int K,
-                          float* dz, float* ws, int* tickets, float* loss, hipStream_t st) {
+                          float* dz, float* ws, float* loss, hipStream_t st) {
   const int nb = linear_mse_partials(N);
-  if (M < 1 || M > kLmMaxM || N < 1 || K < 8 || K % 8 != 0 || nb + 1 > kLmTicketRegion) return hipErrorInvalidValue;
+  if (M < 1 || M > kLmMaxM || N < 1 || K < 8 || K % 8 != 0) return hipErrorInvalidValue;
   float* part = ws + (int64_t)kLmKS * M * N;
   HYP_DISPATCH_FLOAT(dtype, T, {
     hipLaunchKernelGGL(linear_mse_fwd_k<T>, dim3(nb, kLmKS), dim3(kLmT), 0, st, static_cast<const T*>(X),
@@ -303,21 +305,19 @@ hipError_t linear_mse_fwd(int dtype, const void* X, const void* W, const void* b
                        part);
   });
   hipLaunchKernelGGL(linear_mse_loss_k, dim3(1), dim3(64), 0, st, part, nb, 1.f / ((float)M * (float)N), loss);
-  (void)tickets;  // reserved: the in-kernel last-arriver combines measured slower (agent-scope fences)
   return hipGetLastError();
 }
 
 hipError_t linear_mse_bwd(int dtype, const float* dz, const float* go, const void* X, const void* W, int M, int N,
-                          int K, void* dX, void* dW, void* db, float* ws, int* tickets, hipStream_t st) {
+                          int K, void* dX, void* dW, void* db, float* ws, hipStream_t st) {
   const int nbw = (N + kLmNW - 1) / kLmNW, kt = (K + kLmDxK - 1) / kLmDxK, ns = (N + kLmNC - 1) / kLmNC;
-  if (M < 1 || M > kLmMaxM || N < 1 || K < 8 || K % 8 != 0 || ns > kLmMaxNS || kt > kLmTicketRegion)
+  if (M < 1 || M > kLmMaxM || N < 1 || K < 8 || K % 8 != 0 || ns > kLmMaxNS)
     return hipErrorInvalidValue;
   HYP_DISPATCH_FLOAT(dtype, T, {
     hipLaunchKernelGGL(linear_mse_bwd_k<T>, dim3(nbw + kt * ns), dim3(kLmT), 0, st, dz, go, static_cast<const T*>(X),
                        static_cast<const T*>(W), M, N, K, nbw, ns, ws, static_cast<T*>(dW), static_cast<T*>(db));
     hipLaunchKernelGGL(linear_mse_dx_k<T>, dim3(kt), dim3(kLmT), 0, st, ws, M, K, ns, static_cast<T*>(dX));
   });
-  (void)tickets;
   return hipGetLastError();
 }
 
